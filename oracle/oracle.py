@@ -1,0 +1,285 @@
+"""ctypes wrapper of the CPU oracle (``oracle/pdplqr_oracle.c``).
+
+TEST INFRASTRUCTURE ONLY: imported by ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg.  The product path (``pdp-lqr_amd``)
+never imports it.  Parity status: see the C file's header ("parity unpinned"
+w.r.t. reference outputs; pinned to the dense-KKT golden fixtures).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborcpdplqr.so")
+_lib = None
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        vp = C.c_void_p
+        L.orc_serial_create.restype = vp
+        L.orc_serial_create.argtypes = [C.c_int, C.c_int, C.c_int, _ip, _dp, _dp, _dp, _dp, _dp]
+        for nm in ["orc_serial_destroy", "orc_serial_clear_workspace"]:
+            getattr(L, nm).argtypes = [vp]
+        L.orc_serial_update_problem_data.argtypes = [vp, _dp, _dp, _dp, _dp, C.c_double]
+        L.orc_serial_backward.argtypes = [vp, _dp]
+        L.orc_serial_backward_without_factorization.argtypes = [vp, _dp]
+        L.orc_serial_forward.argtypes = [vp, _dp, _dp]
+        L.orc_serial_get_stage.argtypes = [vp, C.c_int, _dp, _dp]
+        L.orc_parallel_create.restype = vp
+        L.orc_parallel_create.argtypes = [C.c_int, C.c_int, C.c_int, _ip, _dp, _dp, _dp, _dp, _dp, C.c_int,
+                                          C.c_int, C.c_int]
+        L.orc_parallel_destroy.argtypes = [vp]
+        L.orc_parallel_update_problem_data.argtypes = [vp, _dp, _dp, _dp, _dp, C.c_double]
+        L.orc_parallel_backward.argtypes = [vp, _dp]
+        L.orc_parallel_backward_without_factorization.argtypes = [vp, _dp]
+        L.orc_parallel_forward.argtypes = [vp, _dp, _dp]
+        L.orc_parallel_backward_ok.argtypes = [vp]
+        L.orc_parallel_backward_ok.restype = C.c_int
+        L.orc_parallel_segments.argtypes = [vp, _ip, _ip]
+        L.orc_parallel_get_segment.argtypes = [vp, C.c_int, _dp, _dp, _dp, _dp]
+        L.orc_segmentation.argtypes = [C.c_int, C.c_int, C.c_int, _ip, _ip]
+        L.orc_segmentation.restype = C.c_int
+        L.orc_kkt_create.restype = vp
+        L.orc_kkt_create.argtypes = [C.c_int, C.c_int, C.c_int, _ip, _dp, _dp, _dp, _dp, _dp, C.c_double,
+                                     C.c_double]
+        L.orc_kkt_destroy.argtypes = [vp]
+        for nm in ["orc_kkt_dim", "orc_kkt_nnz", "orc_kkt_sumLnz"]:
+            getattr(L, nm).argtypes = [vp]
+            getattr(L, nm).restype = C.c_int
+        L.orc_kkt_update_problem_data.argtypes = [vp, _dp, _dp, _dp, _dp, C.c_double]
+        L.orc_kkt_backward.argtypes = [vp, _dp]
+        L.orc_kkt_backward.restype = C.c_int
+        L.orc_kkt_forward.argtypes = [vp, _dp, _dp]
+        L.orc_kkt_get_solution.argtypes = [vp, _dp]
+        L.orc_kkt_get_csc.argtypes = [vp, _ip, _ip, _dp]
+        L.orc_batched_serial_solve.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp,
+                                               C.c_double, _dp, C.c_int]
+        L.orc_batched_serial_solve.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _d(a: Optional[np.ndarray]):
+    if a is None:
+        return C.cast(0, _dp)
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_ip)
+
+
+def _flat(vecs) -> np.ndarray:
+    if isinstance(vecs, np.ndarray):
+        return np.ascontiguousarray(vecs, dtype=np.float64)
+    parts = [np.asarray(v, dtype=np.float64).reshape(-1) for v in vecs]
+    return np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros(0))
+
+
+class _Base:
+    def __init__(self, pm):
+        self.pm = pm
+        self._keep = [np.ascontiguousarray(x) for x in (pm.ncs.astype(np.int32), pm.E, pm.c, pm.H, pm.h, pm.D)]
+        self.n, self.m, self.N = pm.n, pm.m, pm.N
+        self.s = pm.n + pm.m
+
+    def _model_args(self):
+        ncs, E, c, H, h, D = self._keep
+        if D.size == 0:
+            D = np.zeros(1)
+            self._keep[5] = D
+        return [self.n, self.m, self.N, _i(ncs), _d(E), _d(c), _d(H), _d(h), _d(D)]
+
+    def _ws_len(self):
+        return self.N * self.s + self.n
+
+    def _ny(self):
+        return max(int(np.sum(self.pm.ncs)), 1)
+
+    def _vecs(self, v, size):
+        a = _flat(v) if v is not None else np.zeros(size)
+        if a.size == 0:
+            a = np.zeros(1)
+        return a
+
+
+class OracleSerial(_Base):
+    """``LQRSolver`` restatement (``lqr_solver.hpp:9-77``)."""
+
+    def __init__(self, pm):
+        super().__init__(pm)
+        self.h = lib().orc_serial_create(*self._model_args())
+        if not self.h:
+            raise RuntimeError("oracle serial create failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_serial_destroy(self.h)
+            self.h = None
+
+    def clear_workspace(self):
+        lib().orc_serial_clear_workspace(self.h)
+
+    def update_problem_data(self, ws, ys, zs, inv_rho, sigma):
+        a = [self._vecs(ws, self._ws_len()), self._vecs(ys, self._ny()), self._vecs(zs, self._ny()),
+             self._vecs(inv_rho, self._ny())]
+        lib().orc_serial_update_problem_data(self.h, *[_d(x) for x in a], float(sigma))
+
+    def backward(self, rho):
+        r = self._vecs(rho, self._ny())
+        lib().orc_serial_backward(self.h, _d(r))
+
+    def backward_without_factorization(self, rho):
+        r = self._vecs(rho, self._ny())
+        lib().orc_serial_backward_without_factorization(self.h, _d(r))
+
+    def forward(self, x0) -> np.ndarray:
+        out = np.zeros(self._ws_len())
+        lib().orc_serial_forward(self.h, _d(np.ascontiguousarray(x0, dtype=np.float64)), _d(out))
+        return out
+
+    def stage(self, k):
+        dim = self.s if k < self.N else self.n
+        L = np.zeros(dim * dim)
+        lp = np.zeros(dim)
+        lib().orc_serial_get_stage(self.h, k, _d(L), _d(lp))
+        return L.reshape(dim, dim, order="F"), lp
+
+    def value_function(self, k):
+        """(P_k, p_k) with P_k = Lxx Lxx^T (the reference's segment/condensed convention)."""
+        L, lp = self.stage(k)
+        Lxx = L[-self.n:, -self.n:]
+        return Lxx @ Lxx.T, lp[-self.n:].copy()
+
+
+class OracleParallel(_Base):
+    """``LQRParallelSolver`` restatement (``lqr_solver_parallel.hpp:19-238``)."""
+
+    def __init__(self, pm, num_segments, load_balancing=True, condensed="CHOLESKY"):
+        super().__init__(pm)
+        t = {"LU": 0, "CHOLESKY": 1}[condensed]
+        self.ns = num_segments
+        self.h = lib().orc_parallel_create(*self._model_args(), int(num_segments), int(bool(load_balancing)), t)
+        if not self.h:
+            raise RuntimeError("oracle parallel create failed (bad segmentation or CHOLESKY with 1 segment)")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_parallel_destroy(self.h)
+            self.h = None
+
+    def segments(self):
+        a = np.zeros(self.ns, dtype=np.int32)
+        b = np.zeros(self.ns, dtype=np.int32)
+        lib().orc_parallel_segments(self.h, _i(a), _i(b))
+        return a, b
+
+    def update_problem_data(self, ws, ys, zs, inv_rho, sigma):
+        a = [self._vecs(ws, self._ws_len()), self._vecs(ys, self._ny()), self._vecs(zs, self._ny()),
+             self._vecs(inv_rho, self._ny())]
+        lib().orc_parallel_update_problem_data(self.h, *[_d(x) for x in a], float(sigma))
+
+    def backward(self, rho):
+        r = self._vecs(rho, self._ny())
+        lib().orc_parallel_backward(self.h, _d(r))
+        return bool(lib().orc_parallel_backward_ok(self.h))
+
+    def backward_without_factorization(self, rho):
+        r = self._vecs(rho, self._ny())
+        lib().orc_parallel_backward_without_factorization(self.h, _d(r))
+
+    def forward(self, x0) -> np.ndarray:
+        out = np.zeros(self._ws_len())
+        lib().orc_parallel_forward(self.h, _d(np.ascontiguousarray(x0, dtype=np.float64)), _d(out))
+        return out
+
+    def segment_state(self, i):
+        n = self.n
+        P, p, xh, uh = np.zeros(n * n), np.zeros(n), np.zeros(n), np.zeros(n)
+        lib().orc_parallel_get_segment(self.h, i, _d(P), _d(p), _d(xh), _d(uh))
+        return P.reshape(n, n, order="F"), p, xh, uh
+
+
+class OracleKKT(_Base):
+    """``QDLDLSolver`` restatement (``qdldl_solver.hpp:14-151`` + ``kkt.hpp``)."""
+
+    def __init__(self, pm, rho_dyn=1e-6, sigma=1e-6):
+        super().__init__(pm)
+        self.h = lib().orc_kkt_create(*self._model_args(), float(rho_dyn), float(sigma))
+        if not self.h:
+            raise RuntimeError("oracle kkt create failed")
+        self.dim = lib().orc_kkt_dim(self.h)
+        self.nnz = lib().orc_kkt_nnz(self.h)
+        self.sumLnz = lib().orc_kkt_sumLnz(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_kkt_destroy(self.h)
+            self.h = None
+
+    def update_problem_data(self, ws, ys, zs, inv_rho, sigma):
+        a = [self._vecs(ws, self._ws_len()), self._vecs(ys, self._ny()), self._vecs(zs, self._ny()),
+             self._vecs(inv_rho, self._ny())]
+        lib().orc_kkt_update_problem_data(self.h, *[_d(x) for x in a], float(sigma))
+
+    def backward(self, inv_rho) -> int:
+        r = self._vecs(inv_rho, self._ny())
+        st = lib().orc_kkt_backward(self.h, _d(r))
+        if st < 0:
+            raise RuntimeError(f"QDLDL factorization failed with status: {st}")
+        return st
+
+    def forward(self, x0) -> np.ndarray:
+        out = np.zeros(self._ws_len())
+        lib().orc_kkt_forward(self.h, _d(np.ascontiguousarray(x0, dtype=np.float64)), _d(out))
+        return out
+
+    def solution(self):
+        x = np.zeros(self.dim)
+        lib().orc_kkt_get_solution(self.h, _d(x))
+        return x
+
+    def csc(self):
+        Ap = np.zeros(self.dim + 1, dtype=np.int32)
+        Ai = np.zeros(self.nnz, dtype=np.int32)
+        Ax = np.zeros(self.nnz)
+        lib().orc_kkt_get_csc(self.h, _i(Ap), _i(Ai), _d(Ax))
+        return Ap, Ai, Ax
+
+
+def batched_serial_solve(n, m, N, E, c, H, h, x0, sigma=1e-6, threads=0) -> np.ndarray:
+    """CPU baseline: independent serial (``LQRSolver``) solves over a batch, OpenMP
+    over problems.  Arrays are batch-major flat (see problems.random_batch_arrays)."""
+    batch = E.shape[0]
+    out = np.zeros((batch, N * (n + m) + n))
+    lib().orc_batched_serial_solve(n, m, N, batch, _d(np.ascontiguousarray(E)), _d(np.ascontiguousarray(c)),
+                                   _d(np.ascontiguousarray(H)), _d(np.ascontiguousarray(h)),
+                                   _d(np.ascontiguousarray(x0)), float(sigma), _d(out), int(threads))
+    return out
+
+
+def segmentation(N, ns, load_balancing=True):
+    a = np.zeros(ns, dtype=np.int32)
+    b = np.zeros(ns, dtype=np.int32)
+    ok = lib().orc_segmentation(N, ns, int(bool(load_balancing)), _i(a), _i(b))
+    return bool(ok), a, b
