@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- LQR stages/sec on MI355X (driver contract).
+
+Workload (north_star target): batch = 4096 independent
+synthetic LQRs per GPU, N = 1024, nx = 12, nu = 4, fp64, model resident in HBM.
+One step = backward + forward of the batched serial Riccati (the reference's
+timed region, examples/lqr_example.cpp:197-202).  value = N * batch * n_gpus /
+(time per step, max over ranks): weak scaling, no data-path collective (the
+problems are independent; a barrier and a max-reduce of the clock only).
+
+Roofline: the dominant kernel (k_riccati_bwd) timed with HIP events on the
+handle's stream; algorithmic bytes per stage = SURVEY.md 8(d)'s compulsory
+reads of E, c, H, h = 8 (n s + n + s^2 + s) (3,808 B at 12/4); the forward
+kernel owns the w write (128 B), 3,936 B per stage in all.  `traffic` comes
+from the committed rocprofv3 PMC summary (profiles/) when it matches.
+
+cpu_baseline: the Eigen-free C restatement (oracle/, "port"), batched serial
+solves with OpenMP on the host cores, rank 0 only, bounded sample.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+ N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pdp-lqr_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "LQR stages/sec (N*batch) at nx=12,nu=4; wall-clock/solve; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def gen_batch_device(n, m, N, batch, seed, device):
+    """Synthetic LQR batch (BASELINE.md section 3 distribution) generated on the
+    GPU directly in the boundary layout (include/pdplqr.h)."""
+    f64 = torch.float64
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    s = n + m
+    E = torch.empty(batch, N, s, n, dtype=f64, device=device)  # column-major n x s blocks
+    E[:, :, :m, :] = torch.randn(batch, N, m, n, dtype=f64, device=device, generator=g)
+    E[:, :, m:, :] = 0.1 * torch.randn(batch, N, n, n, dtype=f64, device=device, generator=g)
+    E[:, :, m:, :] += torch.eye(n, dtype=f64, device=device)
+    c = torch.randn(batch, N, n, dtype=f64, device=device, generator=g)
+    H = torch.empty(batch, N * s * s + n * n, dtype=f64, device=device)
+    chunk = max(1, (1 << 27) // (N * s * s))
+    for b0 in range(0, batch, chunk):
+        b1 = min(batch, b0 + chunk)
+        M = torch.randn(b1 - b0, N, s, s, dtype=f64, device=device, generator=g)
+        Hk = M @ M.transpose(-1, -2) / s + torch.eye(s, dtype=f64, device=device)
+        H[b0:b1, :N * s * s] = Hk.reshape(b1 - b0, N * s * s)
+        del M, Hk
+    MN = torch.randn(batch, n, n, dtype=f64, device=device, generator=g)
+    H[:, N * s * s:] = (MN @ MN.transpose(-1, -2) / n + torch.eye(n, dtype=f64, device=device)).reshape(batch, n * n)
+    h = torch.randn(batch, N * s + n, dtype=f64, device=device, generator=g)
+    x0 = torch.randn(batch, n, dtype=f64, device=device, generator=g)
+    return E.reshape(batch, -1).contiguous(), c.reshape(batch, -1).contiguous(), H, h, x0
+
+
+def load_pmc_traffic(workload_tag):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/*_pmc.json), or None."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir)):
+        if f.endswith("_pmc.json"):
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except Exception:
+                continue
+            if d.get("workload") == workload_tag and "bytes_per_launch" in d:
+                best = d
+    return best
+
+
+def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
+    """Oracle ("port") batched serial solves on host cores; bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import batched_serial_solve
+    from pdplqr.problems import random_batch_arrays
+
+    if threads is None:
+        try:
+            threads = len(os.sched_getaffinity(0))
+        except Exception:
+            threads = os.cpu_count() or 1
+        threads = max(1, min(16, threads))  # the GPU box grants a 16-CPU share per GPU
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, sample_batch, 7)
+    batched_serial_solve(n, m, N, E[:threads], c[:threads], H[:threads], h[:threads], x0[:threads],
+                         threads=threads)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        batched_serial_solve(n, m, N, E, c, H, h, x0, threads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    stages = reps * sample_batch * N
+    return {"value": stages / el, "unit": "stages/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {sample_batch} problems of N={N} nx={n} nu={m} (batched serial Riccati, "
+                      f"OpenMP over problems, {el:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--N", type=int, default=1024)
+    ap.add_argument("--nx", type=int, default=12)
+    ap.add_argument("--nu", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--keep-factors", action="store_true", help="also cache L_k (factor-reuse path)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, B = args.nx, args.nu, args.N, args.batch
+    s = n + m
+    E, c, H, h, x0 = gen_batch_device(n, m, N, B, seed=1234 + rank, device=dev)
+    ws0 = torch.zeros(B, N * s + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    bs = BatchedLQRSolver(n, m, N, B, keep_factors=args.keep_factors, device=local)
+    bs.set_model(E, c, H, h)
+    del H  # the handle holds its own copy
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.synchronize()
+    stream = torch.cuda.ExternalStream(bs.handle.stream(), device=dev)
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(stream)
+        bs.backward()
+        if evs:
+            evs[1].record(stream)
+        bs.forward(x0, out)
+        if evs:
+            evs[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    bs.synchronize()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    bs.synchronize()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    st = bs.status()
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms_bwd = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    ms_fwd = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    stages = N * B
+    value = stages * world * args.steps / el
+    bytes_bwd_stage = 8 * (n * s + n + s * s + s)  # SURVEY.md 8(d) compulsory reads
+    bytes_stage = bytes_bwd_stage + 8 * s  # + the w write = B of BASELINE.md section 2
+    achieved = bytes_bwd_stage * stages / (ms_bwd * 1e-3) / 1e9
+    tag = f"N{N}_n{n}_m{m}_b{B}_kf{int(args.keep_factors)}"
+    pmc = load_pmc_traffic(tag)
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "stages/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (BASELINE.md section 3 distribution, generated on device)",
+        "config": {"workload": f"batched serial Riccati backward+forward, N={N} nx={n} nu={m} batch={B} per GPU "
+                               "(north_star target config)",
+                   "N": N, "nx": n, "nu": m, "batch_per_gpu": B, "solver": "LQRSolver (batched)",
+                   "keep_factors": bool(args.keep_factors), "parallelism": f"batch-sharded x{world}"},
+        "roofline": {"kernel": "k_riccati_bwd<1>", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": (pmc["bytes_per_launch"] if pmc else None),
+                     "bytes_per_stage_algorithmic": bytes_bwd_stage, "ms_per_launch": ms_bwd},
+        "kernels_ms": {"backward": ms_bwd, "forward": ms_fwd},
+        "solve_hbm_frac": bytes_stage * stages / ((ms_bwd + ms_fwd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "status_ok": bool(np.all(st == 0)),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(n, m, N, seconds=args.cpu_seconds)
+    elif rank == 0:
+        res["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    bs.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+// internal.hpp -- shared declarations of libpdplqr (MI355X / gfx950, HIP).
+//
+// Device data layout (HBM), per handle.  Model arrays keep the boundary's
+// reference layout (include/pdplqr.h); the workspace is solver-owned:
+//   Hw  [b][N*ps + pn]   H~_k = H_k + sigma I (+ rho D^T D), packed lower, column-major
+//   hw  [b][N*s + n]     h~_k = h_k - sigma w_k (- D^T rho g)
+//   gw  [b][ny]          g_k = z_k - inv_rho o y_k
+//   KD  [b][N][m*n + m]  rollout gains K_k = -Luu^{-T} Lxu^T, d_k = -Luu^{-T} lu
+//   Lc  [b][N*ps + pn]   (keep_factors) Cholesky factor L_k, packed lower
+//   lpc [b][N*s + n]     (keep_factors) lp_k = [lu; p]
+// with ps = s(s+1)/2 and pn = n(n+1)/2.  One wavefront owns one problem in the
+// batched serial kernels (see DESIGN.md for the per-kernel roofline).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "pdplqr.h"
+
+namespace pdplqr {
+
+void set_error(const std::string &msg);
+
+#define PDPLQR_HIP_TRY(expr)                                                                        \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) {                                                                     \
+            ::pdplqr::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+            return PDPLQR_ERR_HIP;                                                                  \
+        }                                                                                           \
+    } while (0)
+
+struct Shape {
+    int n, m, N, batch;
+    int s, ps, pn;      // s = n + m, packed sizes
+    int ny;             // sum_k nc_k
+    int ndD;            // sum_k nc_k * dim_k
+    long long perE, perc, perH, perh, perHw, perKD;
+};
+
+// Riccati (serial, batched) kernels: kernels_riccati.hip
+struct RiccatiArgs {
+    Shape sh;
+    const double *E, *c;   // model
+    double *Hw, *hw;       // workspace (read by the backward)
+    double *KD;            // out: rollout gains
+    double *Lc, *lpc;      // factor cache (nullable)
+    int32_t *status;       // per-problem factorization status
+    const short2 *tab_s;   // packed-lower index tables (i, j)
+    const short2 *tab_n;
+};
+
+int launch_update_problem_data(const Shape &sh, const double *H, const double *hv, const double *ws,
+                               const double *ys, const double *zs, const double *irho, double sigma, double *Hw,
+                               double *hw, double *gw, const short2 *tab_s, const short2 *tab_n,
+                               hipStream_t st);
+int launch_penalty(const Shape &sh, const double *D, const double *rho, const double *gw, double *Hw,
+                   double *hw, const int32_t *d_off, const int32_t *y_off, const short2 *tab_s,
+                   const short2 *tab_n, int with_H, int max_nc, hipStream_t st);
+int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st);
+int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st);
+int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *KD, const double *x0,
+                           double *ws, hipStream_t st);
+
+}  // namespace pdplqr
+
+struct pdplqr_handle_s {
+    pdplqr_config cfg;
+    std::vector<int32_t> ncs;
+    std::vector<int32_t> d_off_h, y_off_h;
+    pdplqr::Shape sh;
+    int max_nc;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // model
+    double *E = nullptr, *c = nullptr, *H = nullptr, *h = nullptr, *D = nullptr;
+    // workspace
+    double *Hw = nullptr, *hw = nullptr, *gw = nullptr;
+    double *KD = nullptr, *Lc = nullptr, *lpc = nullptr;
+    int32_t *status = nullptr;
+    int32_t *d_off = nullptr, *y_off = nullptr;
+    short2 *tab_s = nullptr, *tab_n = nullptr;
+    // staging for host inputs / outputs
+    double *st_ws = nullptr, *st_y = nullptr, *st_z = nullptr, *st_ir = nullptr, *st_rho = nullptr;
+    double *st_x0 = nullptr;
+    bool model_set = false, updated = false, factored = false;
+    bool host_staged = false;  // a host->device copy is in flight on `stream`
+    std::vector<void *> allocs;
+};

@@ -1,0 +1,15 @@
+// solvers.hpp -- per-solver-kind implementation hooks behind the C ABI.
+#pragma once
+#include "internal.hpp"
+
+namespace pdplqr {
+int solver_init(pdplqr_handle h);      // allocate solver-specific state
+void solver_release(pdplqr_handle h);  // free it (device buffers are in h->allocs)
+int solver_on_model(pdplqr_handle h);  // after set_model (KKT: assemble + analyse)
+int solver_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
+                  double sigma);
+int solver_backward(pdplqr_handle h, const double *rho);
+int solver_backward_nofact(pdplqr_handle h, const double *rho);
+int solver_forward(pdplqr_handle h, const double *x0, double *ws);
+int solver_clear(pdplqr_handle h);
+}  // namespace pdplqr

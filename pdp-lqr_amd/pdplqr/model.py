@@ -171,3 +171,28 @@ def initialize_vectors(model: LQRModel, rho: float):
     rho_vecs = [np.full(model.ncs[k], rho) for k in range(N + 1)]
     inv_rho_vecs = [np.full(model.ncs[k], 1.0 / rho) for k in range(N + 1)]
     return ws, ys, zs, rho_vecs, inv_rho_vecs
+
+
+def unpack_model(pm: PackedModel) -> LQRModel:
+    """Inverse of ``pack_model`` (nodes in time order)."""
+    n, m, N = pm.n, pm.m, pm.N
+    s = n + m
+    model = LQRModel(n, m, N)
+    off = 0
+    for k in range(N + 1):
+        nc = int(pm.ncs[k])
+        model.add_node(n, m, nc, k, k == N)
+        nd = model.nodes[k]
+        if k < N:
+            nd.E[:] = pm.E[k * n * s:(k + 1) * n * s].reshape(n, s, order="F")
+            nd.c[:] = pm.c[k * n:(k + 1) * n]
+            nd.H[:] = pm.H[k * s * s:(k + 1) * s * s].reshape(s, s, order="F")
+            nd.h[:] = pm.h[k * s:(k + 1) * s]
+        else:
+            nd.H[:] = pm.H[N * s * s:].reshape(n, n, order="F")
+            nd.h[:] = pm.h[N * s:]
+        dim = s if k < N else n
+        if nc > 0:
+            nd.D_con[:] = pm.D[off:off + nc * dim].reshape(nc, dim, order="F")
+            off += nc * dim
+    return model

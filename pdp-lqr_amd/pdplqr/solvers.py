@@ -1,0 +1,311 @@
+"""Host-side mirror of the reference solver classes over the C ABI.
+
+Same names, arguments and protocol as the reference (C++ namespace ``lqr``):
+
+* ``LQRSolver(model)``                                   lqr_solver.hpp:9-77
+* ``LQRParallelSolver(model, num_segments, load_balancing=True,
+  solver_type=CondensedSystemSolverType.CHOLESKY)``      lqr_solver_parallel.hpp:19-238
+* ``QDLDLSolver(model)``                                 qdldl_solver.hpp:14-151
+
+each with ``update_problem_data(ws, ys, zs, inv_rho_vecs, sigma)``,
+``backward(rho_vecs)`` (``QDLDLSolver``: ``inv_rho_vecs``),
+``backward_without_factorization(rho_vecs)`` (Riccati solvers),
+``forward(x0, ws)`` (writes ``ws`` in place, as the reference's
+``std::vector<VectorXs>&``) and ``clear_workspace()``.  All compute runs in
+HIP kernels on the MI355X (libpdplqr.so); there is no CPU fallback.
+
+``BatchedLQRSolver`` is the batched entry point the reference lacks: ``batch``
+independent problems of one shape, host numpy or device (torch) buffers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import Config, check, lib
+from .model import LQRModel, pack_model, pack_stage_vectors, w_sizes
+
+
+class CondensedSystemSolverType(enum.IntEnum):
+    """lqr_solver_parallel.hpp:14-17"""
+
+    LU = _lib.PDPLQR_CONDENSED_LU
+    CHOLESKY = _lib.PDPLQR_CONDENSED_CHOLESKY
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
+
+
+def _ptr(x, what: str):
+    """(pointer, mem) for a float64 contiguous numpy array or torch tensor."""
+    if x is None:
+        return None, None
+    if _is_torch(x):
+        import torch
+
+        if x.dtype != torch.float64 or not x.is_contiguous():
+            raise TypeError(f"{what}: torch tensor must be float64 and contiguous")
+        mem = _lib.PDPLQR_MEM_DEVICE if x.is_cuda else _lib.PDPLQR_MEM_HOST
+        return C.c_void_p(x.data_ptr()), mem
+    a = x
+    if not isinstance(a, np.ndarray) or a.dtype != np.float64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError(f"{what}: expected a C-contiguous float64 numpy array")
+    return C.c_void_p(a.ctypes.data), _lib.PDPLQR_MEM_HOST
+
+
+def _mem_of(*ps):
+    mems = {m for (_, m) in ps if m is not None}
+    if len(mems) > 1:
+        raise TypeError("mixing host and device buffers in one call")
+    return mems.pop() if mems else _lib.PDPLQR_MEM_HOST
+
+
+class _Handle:
+    """Owns one pdplqr_handle."""
+
+    def __init__(self, nx, nu, N, batch=1, solver=_lib.PDPLQR_SOLVER_SERIAL, num_segments=1, load_balancing=True,
+                 condensed_type=_lib.PDPLQR_CONDENSED_CHOLESKY, device=0, keep_factors=True, ncs=None,
+                 rho_dyn=1e-6, kkt_sigma=1e-6):
+        L = lib()
+        cfg = Config()
+        L.pdplqr_config_init(C.byref(cfg))
+        cfg.nx, cfg.nu, cfg.N, cfg.batch = int(nx), int(nu), int(N), int(batch)
+        cfg.solver = int(solver)
+        cfg.num_segments = int(num_segments)
+        cfg.load_balancing = int(bool(load_balancing))
+        cfg.condensed_type = int(condensed_type)
+        cfg.device = int(device)
+        cfg.keep_factors = int(bool(keep_factors))
+        cfg.rho_dyn = float(rho_dyn)
+        cfg.kkt_sigma = float(kkt_sigma)
+        self._ncs = None
+        if ncs is not None:
+            self._ncs = np.ascontiguousarray(np.asarray(ncs, dtype=np.int32))
+            cfg.ncs = self._ncs.ctypes.data_as(C.POINTER(C.c_int32))
+        self.cfg = cfg
+        h = C.c_void_p()
+        check(L.pdplqr_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.nx, self.nu, self.N, self.batch = int(nx), int(nu), int(N), int(batch)
+        self.ncs = self._ncs if self._ncs is not None else np.zeros(N + 1, dtype=np.int32)
+        self.ny = int(np.sum(self.ncs))
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().pdplqr_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # raw protocol (pointers already validated) -----------------------------
+    def set_model(self, E, c, H, h, D=None):
+        ps = [_ptr(E, "E"), _ptr(c, "c"), _ptr(H, "H"), _ptr(h, "h"), _ptr(D, "D")]
+        mem = _mem_of(*ps)
+        check(lib().pdplqr_set_model(self.h, ps[0][0], ps[1][0], ps[2][0], ps[3][0], ps[4][0], mem))
+
+    def update_problem_data(self, ws, ys, zs, inv_rho, sigma):
+        ps = [_ptr(ws, "ws"), _ptr(ys, "ys"), _ptr(zs, "zs"), _ptr(inv_rho, "inv_rho")]
+        mem = _mem_of(*ps)
+        check(lib().pdplqr_update_problem_data(self.h, ps[0][0], ps[1][0], ps[2][0], ps[3][0], float(sigma), mem))
+
+    def backward(self, rho):
+        p = _ptr(rho, "rho")
+        check(lib().pdplqr_backward(self.h, p[0], _mem_of(p)))
+
+    def backward_without_factorization(self, rho):
+        p = _ptr(rho, "rho")
+        check(lib().pdplqr_backward_without_factorization(self.h, p[0], _mem_of(p)))
+
+    def forward(self, x0, ws_out):
+        ps = [_ptr(x0, "x0"), _ptr(ws_out, "ws")]
+        check(lib().pdplqr_forward(self.h, ps[0][0], ps[1][0], _mem_of(*ps)))
+
+    def clear_workspace(self):
+        check(lib().pdplqr_clear_workspace(self.h))
+
+    def synchronize(self):
+        check(lib().pdplqr_synchronize(self.h))
+
+    def stream(self) -> int:
+        return int(lib().pdplqr_get_stream(self.h) or 0)
+
+    def set_stream(self, stream_ptr: int):
+        check(lib().pdplqr_set_stream(self.h, C.c_void_p(stream_ptr)))
+
+    def status(self) -> np.ndarray:
+        out = np.zeros(self.batch, dtype=np.int32)
+        check(lib().pdplqr_get_status(self.h, out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
+
+    def value_function(self, b: int, k: int):
+        n = self.nx
+        P = np.zeros(n * n)
+        p = np.zeros(n)
+        check(lib().pdplqr_get_value_function(self.h, int(b), int(k), C.c_void_p(P.ctypes.data),
+                                              C.c_void_p(p.ctypes.data)))
+        return P.reshape(n, n, order="F"), p
+
+    def segments(self, ns: int):
+        a = np.zeros(ns, dtype=np.int32)
+        b = np.zeros(ns, dtype=np.int32)
+        check(lib().pdplqr_get_segments(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        b.ctypes.data_as(C.POINTER(C.c_int32))))
+        return a, b
+
+
+def _stage_vecs(model: LQRModel, vecs, what):
+    return pack_stage_vectors(vecs, [int(x) for x in model.ncs]) if model.ncs else np.zeros(0)
+
+
+class _ModelSolver:
+    """Shared body of the reference-mirroring single-problem solvers."""
+
+    _solver_kind = _lib.PDPLQR_SOLVER_SERIAL
+    _reupload_model = True  # Riccati solvers re-read model_ on every call (lqr_solver.hpp:25)
+
+    def _init_handle(self, model: LQRModel, device=0, keep_factors=True, **kw):
+        self.model_ = model  # non-owning in the reference: the model must outlive the solver
+        self._hd = _Handle(model.n, model.m, model.N, 1, self._solver_kind, device=device,
+                           keep_factors=keep_factors, ncs=[int(x) for x in model.ncs], **kw)
+        self._upload_model()
+
+    def _upload_model(self):
+        pm = pack_model(self.model_)
+        self._pm = pm
+        self._hd.set_model(pm.E, pm.c, pm.H, pm.h, pm.D if pm.D.size else None)
+
+    def _y(self, v):
+        if self._hd.ny == 0:
+            return None
+        return np.ascontiguousarray(pack_stage_vectors(v, [int(x) for x in self.model_.ncs]))
+
+    def clear_workspace(self):
+        self._hd.clear_workspace()
+
+    def update_problem_data(self, ws: Sequence[np.ndarray], ys, zs, inv_rho_vecs, sigma: float):
+        m = self.model_
+        if self._reupload_model:
+            self._upload_model()
+        w = np.ascontiguousarray(pack_stage_vectors(ws, w_sizes(m.n, m.m, m.N)))
+        self._hd.update_problem_data(w, self._y(ys), self._y(zs), self._y(inv_rho_vecs), sigma)
+
+    def backward(self, rho_vecs):
+        self._hd.backward(self._y(rho_vecs))
+
+    def forward(self, x0, ws: List[np.ndarray]):
+        m = self.model_
+        out = np.zeros(m.N * (m.n + m.m) + m.n)
+        self._hd.forward(np.ascontiguousarray(x0, dtype=np.float64), out)
+        s = m.n + m.m
+        for k in range(m.N):
+            ws[k][:] = out[k * s:(k + 1) * s]
+        ws[m.N][:] = out[m.N * s:]
+        return ws
+
+    def status(self) -> int:
+        return int(self._hd.status()[0])
+
+
+class LQRSolver(_ModelSolver):
+    """Serial square-root Riccati (lqr_solver.hpp:9-77), HIP backward/forward."""
+
+    _solver_kind = _lib.PDPLQR_SOLVER_SERIAL
+
+    def __init__(self, model: LQRModel, device: int = 0, keep_factors: bool = True):
+        self._init_handle(model, device=device, keep_factors=keep_factors)
+
+    def backward_without_factorization(self, rho_vecs):
+        self._hd.backward_without_factorization(self._y(rho_vecs))
+
+    def value_function(self, k: int):
+        """(P_k, p_k) with P_k = Lxx Lxx^T of the stage-k workspace."""
+        return self._hd.value_function(0, k)
+
+
+class LQRParallelSolver(_ModelSolver):
+    """Parallel DP over horizon segments (lqr_solver_parallel.hpp:19-238)."""
+
+    _solver_kind = _lib.PDPLQR_SOLVER_PARALLEL
+
+    def __init__(self, model: LQRModel, num_segments: int, load_balancing: bool = True,
+                 solver_type: CondensedSystemSolverType = CondensedSystemSolverType.CHOLESKY, device: int = 0):
+        self.num_segments = int(num_segments)
+        self._init_handle(model, device=device, keep_factors=True, num_segments=num_segments,
+                          load_balancing=load_balancing, condensed_type=int(solver_type))
+
+    def backward_without_factorization(self, rho_vecs):
+        self._hd.backward_without_factorization(self._y(rho_vecs))
+
+    def segments(self):
+        return self._hd.segments(self.num_segments)
+
+
+class QDLDLSolver(_ModelSolver):
+    """KKT + sparse LDL^T path (qdldl_solver.hpp:14-151).  The KKT matrix is
+    frozen at construction with rho_dyn = sigma = 1e-6 (qdldl_solver.hpp:38-42)."""
+
+    _solver_kind = _lib.PDPLQR_SOLVER_KKT
+    _reupload_model = False
+
+    def __init__(self, model: LQRModel, device: int = 0):
+        self._init_handle(model, device=device, keep_factors=False, rho_dyn=1e-6, kkt_sigma=1e-6)
+
+    def backward(self, inv_rho_vecs):  # NOTE: inverse rho, as the reference (qdldl_solver.hpp:24)
+        self._hd.backward(self._y(inv_rho_vecs))
+
+
+class BatchedLQRSolver:
+    """``batch`` independent LQ problems of one shape (n, m, N), solved by one
+    set of HIP launches.  Buffers are batch-major flat arrays in the boundary
+    layout (include/pdplqr.h): numpy (host) or torch CUDA tensors (device)."""
+
+    def __init__(self, n: int, m: int, N: int, batch: int, solver: str = "serial", num_segments: int = 1,
+                 load_balancing: bool = True, condensed: str = "CHOLESKY", keep_factors: bool = False,
+                 ncs=None, device: int = 0):
+        kind = {"serial": _lib.PDPLQR_SOLVER_SERIAL, "parallel": _lib.PDPLQR_SOLVER_PARALLEL,
+                "kkt": _lib.PDPLQR_SOLVER_KKT}[solver]
+        self.n, self.m, self.N, self.batch = n, m, N, batch
+        self._hd = _Handle(n, m, N, batch, kind, num_segments=num_segments, load_balancing=load_balancing,
+                           condensed_type=int(CondensedSystemSolverType[condensed]), device=device,
+                           keep_factors=keep_factors, ncs=ncs)
+
+    @property
+    def handle(self) -> _Handle:
+        return self._hd
+
+    def set_model(self, E, c, H, h, D=None):
+        self._hd.set_model(E, c, H, h, D)
+
+    def update_problem_data(self, ws, ys=None, zs=None, inv_rho=None, sigma: float = 0.0):
+        self._hd.update_problem_data(ws, ys, zs, inv_rho, sigma)
+
+    def backward(self, rho=None):
+        self._hd.backward(rho)
+
+    def backward_without_factorization(self, rho=None):
+        self._hd.backward_without_factorization(rho)
+
+    def forward(self, x0, ws_out):
+        self._hd.forward(x0, ws_out)
+        return ws_out
+
+    def synchronize(self):
+        self._hd.synchronize()
+
+    def status(self):
+        return self._hd.status()
+
+    def value_function(self, b, k):
+        return self._hd.value_function(b, k)
+
+    def close(self):
+        self._hd.close()

@@ -1,0 +1,216 @@
+"""GPU parity of the serial solver path (LQRSolver / batched serial Riccati)
+against the CPU oracle and the golden fixtures.
+
+Tolerance (north_star: "u* matching reference to 1e-6 rel"): every check
+below asserts the tighter bound 1e-9 relative (fp64 on both sides, different
+summation order; observed ~1e-14), and the headline 1e-6 on u*.
+All calls go through the C ABI (libpdplqr.so); no CPU fallback exists.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, rel_err, u_parts, x_parts
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
+
+
+def _oracle_serial(pm, d):
+    from oracle.oracle import OracleSerial
+
+    o = OracleSerial(pm)
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    return o, o.forward(d["x0"])
+
+
+def _lists(pm, d):
+    from pdplqr.model import unpack_model, unpack_ws
+
+    model = unpack_model(pm)
+    n, m, N = pm.n, pm.m, pm.N
+    ws = unpack_ws(d["ws"], n, m, N)
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    ys = [d["ys"][off[k]:off[k + 1]] for k in range(N + 1)]
+    zs = [d["zs"][off[k]:off[k + 1]] for k in range(N + 1)]
+    rho = [d["rho"][off[k]:off[k + 1]] for k in range(N + 1)]
+    irho = [d["inv_rho"][off[k]:off[k + 1]] for k in range(N + 1)]
+    return model, ws, ys, zs, rho, irho
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_lqrsolver_matches_oracle_and_golden(name):
+    from pdplqr import LQRSolver
+
+    pm, d = load_golden(name)
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRSolver(model)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    w = np.concatenate(out)
+    o, w_orc = _oracle_serial(pm, d)
+    n, m, N = pm.n, pm.m, pm.N
+    assert rel_err(w, w_orc) < TOL
+    assert rel_err(u_parts(w, n, m, N), u_parts(d["w_riccati"], n, m, N)) < 1e-6
+    assert rel_err(w, d["w_riccati"]) < TOL
+    assert sol.status() == 0
+    # value function P_k = Lxx Lxx^T, p_k (lqr_solver.hpp:24-26 workspace)
+    for i, k in enumerate(d["P_k"]):
+        P, p = sol.value_function(int(k))
+        Po, po = o.value_function(int(k))
+        assert rel_err(P, Po) < TOL and rel_err(p, po) < 1e-8
+        assert rel_err(P, d["P"][i]) < TOL
+
+
+@pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40"])
+def test_backward_without_factorization(name):
+    """lqr_solver.hpp:65-70 after a full backward, with new linear data."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import LQRSolver
+    from pdplqr.model import unpack_ws
+
+    pm, d = load_golden(name)
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRSolver(model)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    g = np.random.default_rng(1)
+    ws2 = d["ws"] + 0.2 * g.standard_normal(d["ws"].shape)
+    zs2 = d["zs"] + 0.2 * g.standard_normal(d["zs"].shape)
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    zs2l = [zs2[off[k]:off[k + 1]] for k in range(pm.N + 1)]
+    sol.update_problem_data(unpack_ws(ws2, pm.n, pm.m, pm.N), ys, zs2l, irho, float(d["sigma"]))
+    sol.backward_without_factorization(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    o = OracleSerial(pm)
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    o.update_problem_data(ws2, d["ys"], zs2, d["inv_rho"], float(d["sigma"]))
+    o.backward_without_factorization(d["rho"])
+    assert rel_err(np.concatenate(out), o.forward(d["x0"])) < TOL
+
+
+def _batched_case(n, m, N, batch, seed, device_buffers=False, keep=False):
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, seed)
+    ws0 = np.zeros((batch, N * (n + m) + n))
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+    if device_buffers:
+        import torch
+
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        bs.set_model(T(E), T(c), T(H), T(h))
+        bs.update_problem_data(T(ws0), sigma=1e-6)
+        bs.backward()
+        out = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device="cuda")
+        bs.forward(T(x0), out)
+        bs.synchronize()
+        out = out.cpu().numpy()
+    else:
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+        bs.backward()
+        out = np.zeros((batch, N * (n + m) + n))
+        bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    ref = []
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        ref.append(o.forward(x0[b]))
+    return out, np.stack(ref)
+
+
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 64, 37), (4, 2, 100, 9), (24, 8, 20, 5), (1, 1, 5, 3),
+                                         (6, 3, 1, 4), (13, 3, 17, 2), (10, 7, 9, 3)])
+def test_batched_serial_matches_oracle(n, m, N, batch):
+    out, ref = _batched_case(n, m, N, batch, seed=n * 100 + m)
+    for b in range(batch):
+        assert rel_err(out[b], ref[b]) < TOL, b
+        assert rel_err(u_parts(out[b], n, m, N), u_parts(ref[b], n, m, N)) < 1e-6
+
+
+def test_device_buffers_equal_host_buffers():
+    a, _ = _batched_case(12, 4, 32, 8, seed=5, device_buffers=False)
+    b, _ = _batched_case(12, 4, 32, 8, seed=5, device_buffers=True)
+    assert np.array_equal(a, b)
+
+
+def test_non_spd_sets_status_flag():
+    """The reference ignores Eigen's LLT info (lqr_kernel.hpp:89,126); this build
+    reports the first failing stage per problem instead."""
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 4, 2, 10, 3
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 3)
+    s = n + m
+    H = H.copy()
+    H[1, 7 * s * s:8 * s * s] = -np.eye(s).reshape(-1)  # stage 7 of problem 1 indefinite
+    bs = BatchedLQRSolver(n, m, N, batch)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(np.zeros((batch, N * s + n)), sigma=0.0)
+    bs.backward()
+    st = bs.status()
+    assert st[0] == 0 and st[2] == 0 and st[1] == 7 + 1
+
+
+def test_protocol_errors():
+    from pdplqr import BatchedLQRSolver, PdplqrError
+
+    bs = BatchedLQRSolver(4, 2, 5, 1)
+    with pytest.raises(PdplqrError):
+        bs.backward()  # before set_model / update_problem_data
+    with pytest.raises(PdplqrError):
+        bs.forward(np.zeros((1, 4)), np.zeros((1, 5 * 6 + 4)))
+
+
+def test_full_size_properties():
+    """BASELINE sizes (N=1024, 12/4) at a batch the oracle cannot cover:
+    size-independent properties -- every stage obeys the dynamics exactly
+    (x_{k+1} = A x_k + B u_k + c_k, lqr_kernel.hpp:201-203), and sampled
+    problems match the oracle."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 1024, 512
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 99)
+    bs = BatchedLQRSolver(n, m, N, batch)
+    bs.set_model(E, c, H, h)
+    ws0 = np.zeros((batch, N * s + n))
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws0)
+    bs.forward(x0, out)
+    assert np.all(np.isfinite(out))
+    Eb = E.reshape(batch, N, s, n).transpose(0, 1, 3, 2)  # (b, k, n, s)
+    w = out[:, :N * s].reshape(batch, N, s)
+    xnext = np.concatenate([w[:, 1:, m:], out[:, None, N * s:]], axis=1)
+    pred = np.einsum("bkij,bkj->bki", Eb, w) + c.reshape(batch, N, n)
+    assert np.max(np.abs(pred - xnext)) / max(1.0, np.max(np.abs(xnext))) < 1e-10
+    for b in [0, 211, batch - 1]:
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        assert rel_err(out[b], o.forward(x0[b])) < TOL
