@@ -144,7 +144,7 @@ int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out) {
     sh.perH = (long long)sh.N * sh.s * sh.s + (long long)sh.n * sh.n;
     sh.perh = (long long)sh.N * sh.s + sh.n;
     sh.perHw = (long long)sh.N * sh.ps + sh.pn;
-    sh.perKD = (long long)sh.N * (sh.m * sh.n + sh.m);
+    sh.perKD = (long long)sh.N * (sh.s * sh.m + sh.m);  // rollout record [L(:,0:m) | lu']
 
     int rc = PDPLQR_OK;
     hipError_t e = hipSetDevice(C.device);

@@ -5,7 +5,7 @@
 //   Hw  [b][N*ps + pn]   H~_k = H_k + sigma I (+ rho D^T D), packed lower, column-major
 //   hw  [b][N*s + n]     h~_k = h_k - sigma w_k (- D^T rho g)
 //   gw  [b][ny]          g_k = z_k - inv_rho o y_k
-//   KD  [b][N][m*n + m]  rollout gains K_k = -Luu^{-T} Lxu^T, d_k = -Luu^{-T} lu
+//   KD  [b][N][s*m + m]  rollout record FR_k = [L_k(:, 0:m) | lu'_k], lu' = Luu^{-1} lu
 //   Lc  [b][N*ps + pn]   (keep_factors) Cholesky factor L_k, packed lower
 //   lpc [b][N*s + n]     (keep_factors) lp_k = [lu; p]
 // with ps = s(s+1)/2 and pn = n(n+1)/2.  One wavefront owns one problem in the
@@ -46,7 +46,7 @@ struct RiccatiArgs {
     Shape sh;
     const double *E, *c;   // model
     double *Hw, *hw;       // workspace (read by the backward)
-    double *KD;            // out: rollout gains
+    double *KD;            // out: rollout records
     double *Lc, *lpc;      // factor cache (nullable)
     int32_t *status;       // per-problem factorization status
     const short2 *tab_s;   // packed-lower index tables (i, j)

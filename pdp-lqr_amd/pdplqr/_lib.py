@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpdplqr.so")
+LIB_PATH = os.environ.get("PDPLQR_LIB") or os.path.join(_HERE, "libpdplqr.so")  # override: diagnostics only
 
 PDPLQR_OK = 0
 PDPLQR_MEM_HOST = 0
@@ -56,6 +56,13 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Load torch first when it is installed so that
+    # libpdplqr.so binds to the runtime torch's tensors and streams live in.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libpdplqr.so not built at {LIB_PATH}: run `make -C pdp-lqr_amd/csrc` "
                           "or __graft_entry__.build() (no CPU fallback exists)")
