@@ -1,0 +1,40 @@
+"""Summarise rocprofv3 --pmc passes (scripts/collect_pmc.sh) per kernel.
+
+HBM bytes per launch = FETCH_SIZE * 1024 * 2 + WRITE_SIZE * 1024 for the
+dominant kernel: MI355X_MICROARCH.md section HBM -- on gfx950 FETCH_SIZE
+(= TCC_EA0_RDREQ x 64 B) reports half the bytes of a wide coalesced read, so
+it is doubled; WRITE_SIZE is exact.  The raw counters are kept alongside so
+the correction can be re-derived (RDREQ_32B shows the request size mix).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    root, tag = sys.argv[1], sys.argv[2]
+    per = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "?")
+                per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {"workload": tag, "kernels": {}}
+    for k, d in per.items():
+        short = k.split("(")[0].replace("void ", "")
+        if "pdplqr" not in short:
+            continue
+        out["kernels"][short] = {c: sum(v) / len(v) for c, v in d.items()}
+    bwd = [v for k, v in out["kernels"].items() if "k_riccati_bwd<" in k or k.endswith("k_riccati_bwd<1>")]
+    if bwd and "FETCH_SIZE" in bwd[0] and "WRITE_SIZE" in bwd[0]:
+        b = bwd[0]
+        out["bytes_per_launch"] = b["FETCH_SIZE"] * 1024 * 2 + b["WRITE_SIZE"] * 1024
+        out["correction"] = "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; units KB"
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
