@@ -84,6 +84,9 @@ typedef struct {
     const int32_t *ncs;      /* N+1 constraint counts or NULL                      */
     double rho_dyn;          /* KKT: lambda regularization, reference 1e-6 (:38)   */
     double kkt_sigma;        /* KKT: sigma frozen into the matrix, reference 1e-6 (:39) */
+    int32_t segment_len;     /* PARALLEL: device sub-segment length (0 = auto).  Every
+                                reference segment is refined into pieces of at most this
+                                many stages; results are identical up to rounding. */
 } pdplqr_config;
 
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,

@@ -416,8 +416,7 @@ int pdplqr_get_status(pdplqr_handle h, int32_t *flags) {
     if (!h || !flags) return invalid("null argument");
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
-    PDPLQR_HIP_TRY(hipMemcpy(flags, h->status, (size_t)h->sh.batch * sizeof(int32_t), hipMemcpyDeviceToHost));
-    return PDPLQR_OK;
+    return solver_status(h, flags);
 }
 
 }  // extern "C"

@@ -1,0 +1,329 @@
+// device_common.hpp -- device helpers shared by the Riccati kernels (gfx950).
+//
+// Everything here runs inside ONE wavefront that owns one problem (or one
+// horizon segment): stage matrices live in the f64 MFMA C/D layout
+// (v_mfma_f64_16x16x4_f64: lane l = 16 g + c holds rows g, g+4, g+8, g+12 of
+// column c of a 16x16 tile), padded to P = 16 T.
+#pragma once
+#include "internal.hpp"
+
+namespace pdplqr {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// packed lower (column-major) index of (i, j), i >= j, dimension d
+__device__ __forceinline__ int pidx(int i, int j, int d) { return j * d - ((j * (j - 1)) >> 1) + (i - j); }
+
+__device__ __forceinline__ double shfl_xor_f64(double v, int mask) { return __shfl_xor(v, mask, 64); }
+
+// Loads the padded stage matrix H~ into C/D-layout tiles.  Indices in
+// [lo, hi) map to the stored packed block (dimension dim, offset off);
+// everything else is the identity padding.
+template <int T>
+__device__ __forceinline__ void load_M(d4 (&M)[T][T], const double *__restrict__ Hp, int dim, int off, int lo, int hi,
+                                       int g, int c) {
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
+                double v;
+                if (i >= lo && i < hi && j >= lo && j < hi) {
+                    const int ii = i - off, jj = j - off;
+                    v = (ii >= jj) ? Hp[pidx(ii, jj, dim)] : Hp[pidx(jj, ii, dim)];
+                } else {
+                    v = (i == j) ? 1.0 : 0.0;
+                }
+                M[a][b][r] = v;
+            }
+}
+
+// Wave-scope ordering of LDS traffic between lanes of ONE wavefront: LDS
+// instructions of a wave retire in issue order, so a compiler-level barrier is
+// all that is needed (no s_barrier; the workgroup is a single wave).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(x): hardware estimate + two Newton steps (full fp64 accuracy).
+__device__ __forceinline__ double rsqrt_f64(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double e = __builtin_fma(-x * r, r, 1.0);
+    r = __builtin_fma(0.5 * r, e, r);
+    e = __builtin_fma(-x * r, r, 1.0);
+    return __builtin_fma(0.5 * r, e, r);
+}
+
+// Stage-k inputs of one lane, loaded one stage ahead (register prefetch).
+template <int T>
+struct StageIn {
+    double E[4 * T][T];  // MFMA B operand: E[4 cc + g][16 b + c]
+    d4 H[T][T];          // MFMA C input: H~[16 a + 4 r + g][16 b + c] (padded)
+    double c[4 * T];     // c[4 cc + g]
+    double h[T];         // h~[16 b + c]
+};
+
+template <int T>
+__device__ __forceinline__ void load_stage(StageIn<T> &in, const double *__restrict__ Ek, const double *__restrict__ ck,
+                                           const double *__restrict__ Hk, const double *__restrict__ hk, int n,
+                                           int s, int g, int c) {
+#pragma unroll
+    for (int cc = 0; cc < 4 * T; ++cc) {
+        const int t = 4 * cc + g;
+#pragma unroll
+        for (int b = 0; b < T; ++b) {
+            const int j = 16 * b + c;
+            in.E[cc][b] = (t < n && j < s) ? Ek[t + j * n] : 0.0;
+        }
+        in.c[cc] = (t < n) ? ck[t] : 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
+                double v;
+                if (i < s && j < s)
+                    v = (i >= j) ? Hk[pidx(i, j, s)] : Hk[pidx(j, i, s)];
+                else
+                    v = (i == j) ? 1.0 : 0.0;
+                in.H[a][b][r] = v;
+            }
+#pragma unroll
+    for (int b = 0; b < T; ++b) {
+        const int j = 16 * b + c;
+        in.h[b] = (j < s) ? hk[j] : 0.0;
+    }
+}
+
+// Right-looking Cholesky of the symmetric padded matrix in C/D layout, pivots
+// jbeg..jend-1.  Column j is broadcast through LDS from row j (the row group
+// that owns row j holds M[j][*] = M[*][j]; M stays exactly symmetric because
+// every update is applied to both triangles with the same products).  The
+// owners write zeros for columns <= j, so every lane can update
+// M -= raw_i raw_k / M[j][j] without masking; the pivot column itself is left
+// unscaled and finalised by finalize_L (L[i][j] = M[i][j] / sqrt(M[j][j])).
+// With `aug`, the first `m` pivots also eliminate the linear column lpr (the
+// lp_k of lqr_kernel.hpp:142-146): lpr_i -= l_ij lu'_j with lu'_j = lp_j / L_jj,
+// which is exactly lu <- Luu^{-1} lu followed by p -= Lxu lu.  All lanes of the
+// wave run in lock step and LDS ops of one wave retire in order, so no barrier
+// is needed between the owners' writes and the readers.
+template <int T>
+__device__ __forceinline__ int chol_tiles(d4 (&M)[T][T], double (&myinv)[T], double (&lpr)[T][4], double *cb,
+                                          double *luq, int jbeg, int jend, int m, bool aug, int g, int c) {
+    int fail = -1;
+    const bool lane0 = (g == 0) && (c == 0);
+#pragma unroll
+    for (int j = 0; j < 16 * T; ++j) {
+        if (j >= jbeg && j < jend) {
+            const int tr = j >> 4, rr = (j >> 2) & 3, gj = j & 3, bj = j >> 4, cj = j & 15;
+            if (g == gj) {
+#pragma unroll
+                for (int b = 0; b < T; ++b) {
+                    const int jc = 16 * b + c;
+                    cb[jc] = (jc > j) ? M[tr][b][rr] : 0.0;
+                }
+            }
+            wave_sync();
+            const double djj = readlane_f64(M[tr][bj][rr], (gj << 4) + cj);
+            if (!(djj > 0.0) && fail < 0) fail = j;
+            const double inv = rsqrt_f64(djj);
+            const double inv2 = inv * inv;
+            if (c == cj) myinv[bj] = inv;
+            double lc[T];
+#pragma unroll
+            for (int b = 0; b < T; ++b) lc[b] = cb[16 * b + c] * inv2;
+            const bool augj = aug && j < m;
+            const double lpj = augj ? readlane_f64(lpr[tr][rr], gj << 4) : 0.0;
+            const double qj = lpj * inv2;
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double li = cb[16 * a + 4 * r + g];
+#pragma unroll
+                    for (int b = 0; b < T; ++b) M[a][b][r] = __builtin_fma(-li, lc[b], M[a][b][r]);
+                    // q = lp_j / M[j][j]; lpr_i -= raw_i * q  (raw_i = 0 for i <= j)
+                    if (augj) lpr[a][r] = __builtin_fma(-li, qj, lpr[a][r]);
+                }
+            if (augj && lane0) luq[j] = lpj * inv;
+            wave_sync();
+        }
+    }
+    return fail;
+}
+
+// L[i][jc] = M[i][jc] / sqrt(M[jc][jc]) below the diagonal, 0 above, for the
+// factored columns jc < jend; identity padding elsewhere is left as is.
+template <int T>
+__device__ __forceinline__ void finalize_L(d4 (&M)[T][T], const double (&myinv)[T], int jbeg, int jend, int g,
+                                           int c) {
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b) {
+            const int jc = 16 * b + c;
+            if (jc >= jbeg && jc < jend) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    M[a][b][r] = (i >= jc) ? M[a][b][r] * myinv[b] : 0.0;
+                }
+            }
+        }
+}
+
+template <int T>
+struct BwdSmem {
+    static constexpr int P = 16 * T;
+    static constexpr int LD = P + 1;  // odd leading dimension: conflict-free column reads
+    double L[P * LD];                 // L_{k+1} then L_k (padded, column-major, lower, zero upper)
+    double col[P];                    // Cholesky column broadcast
+    double pbt[P];                    // Pb_tmp = Lxx_next^T c
+    double pv[P];                     // p_{k+1}, then p_k
+    double lp[P];                     // lp_k (column -> row redistribution)
+    double luq[P];                    // lu'_k = Luu^{-1} lu
+};
+
+template <int T>
+__device__ __forceinline__ void store_L_lds(const d4 (&M)[T][T], double *L, int g, int c) {
+    constexpr int LD = 16 * T + 1;
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L[(16 * a + 4 * r + g) + (16 * b + c) * LD] = M[a][b][r];
+}
+
+
+// One backward stage k (LQRKernel::step_with_factorization, lqr_kernel.hpp:104-147)
+// on the padded tiles.  Consumes L_{k+1} (sm.L) and p_{k+1} (sm.pv); produces
+// L_k in M (finalised) and sm.L, p_k in sm.pv, lu'_k = Luu^{-1} lu in sm.luq,
+// lp_k in lpr (rows of the lane).  Returns the failing pivot or -1.
+template <int T>
+__device__ __forceinline__ int riccati_stage(BwdSmem<T> &sm, const StageIn<T> &cur, d4 (&M)[T][T],
+                                             double (&lpr)[T][4], int n, int m, int s, int g, int c) {
+    constexpr int LD = 16 * T + 1;
+    const int nch = (n + 3) >> 2;
+        // ---- A operand: Lxx_next^T, read from LDS (L_{k+1}) ----
+        double av[4 * T][T];
+#pragma unroll
+        for (int cc = 0; cc < 4 * T; ++cc) {
+            const int t = 4 * cc + g;
+#pragma unroll
+            for (int a = 0; a < T; ++a) {
+                const int tp = 16 * a + c;
+                av[cc][a] = (cc < nch && t < n && tp < n) ? sm.L[(m + t) + (m + tp) * LD] : 0.0;
+            }
+        }
+        // ---- W = Lxx_next^T E  (= V^T, V = E^T Lxx_next, lqr_kernel.hpp:121) ----
+        d4 W[T][T];
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) W[a][bt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int cc = 0; cc < 4 * T; ++cc)
+            if (cc < nch)
+#pragma unroll
+                for (int a = 0; a < T; ++a)
+#pragma unroll
+                    for (int bt = 0; bt < T; ++bt) W[a][bt] = mfma_f64(av[cc][a], cur.E[cc][bt], W[a][bt]);
+        // ---- Pb_tmp = Lxx_next^T c (lqr_kernel.hpp:138), reduced over row groups ----
+#pragma unroll
+        for (int a = 0; a < T; ++a) {
+            double part = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 4 * T; ++cc)
+                if (cc < nch) part = __builtin_fma(av[cc][a], cur.c[cc], part);
+            part += shfl_xor_f64(part, 16);
+            part += shfl_xor_f64(part, 32);
+            if (g == 0) sm.pbt[16 * a + c] = part;
+        }
+        // ---- M = H~ + W^T W  (= H~ + V V^T, lqr_kernel.hpp:123-124) ----
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) M[a][bt] = cur.H[a][bt];
+#pragma unroll
+        for (int kc = 0; kc < 4 * T; ++kc)
+            if (kc < nch) {
+                const int ka = kc >> 2, r = kc & 3;
+#pragma unroll
+                for (int a = 0; a < T; ++a)
+#pragma unroll
+                    for (int bt = 0; bt < T; ++bt) M[a][bt] = mfma_f64(W[ka][a][r], W[ka][bt][r], M[a][bt]);
+            }
+        // ---- lp = h~ + E^T (Lxx_next Pb_tmp + p_next) = h~ + W^T Pb_tmp + E^T p_next
+        //      (lqr_kernel.hpp:139-143; E^T Lxx_next = W^T) ----
+        wave_sync();
+        {
+            double part[T];
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) part[bt] = 0.0;
+#pragma unroll
+            for (int kc = 0; kc < 4 * T; ++kc)
+                if (kc < nch) {
+                    const int t = 4 * kc + g;
+                    const double pb = (t < n) ? sm.pbt[t] : 0.0;
+                    const double pn = (t < n) ? sm.pv[t] : 0.0;
+#pragma unroll
+                    for (int bt = 0; bt < T; ++bt) {
+                        part[bt] = __builtin_fma(W[kc >> 2][bt][kc & 3], pb, part[bt]);
+                        part[bt] = __builtin_fma(cur.E[kc][bt], pn, part[bt]);
+                    }
+                }
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                part[bt] += shfl_xor_f64(part[bt], 16);
+                part[bt] += shfl_xor_f64(part[bt], 32);
+                if (g == 0) sm.lp[16 * bt + c] = cur.h[bt] + part[bt];
+            }
+            wave_sync();
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    lpr[a][r] = (i < s) ? sm.lp[i] : 0.0;
+                }
+        }
+        // ---- L = chol(M) (lqr_kernel.hpp:126) with lu <- Luu^{-1} lu, p -= Lxu lu (:145-146) ----
+        double myinv[T];
+#pragma unroll
+        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
+        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, 0, s, m, true, g, c);
+        finalize_L<T>(M, myinv, 0, s, g, c);
+        store_L_lds<T>(M, sm.L, g, c);
+        // p_k -> LDS (next stage's p_next)
+        if (c == 0) {
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    if (i >= m && i < s) sm.pv[i - m] = lpr[a][r];
+                }
+        }
+        wave_sync();
+        return f;
+}
+
+}  // namespace pdplqr

@@ -67,6 +67,8 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 }  // namespace pdplqr
 
+namespace pdplqr { struct ParallelState; }
+
 struct pdplqr_handle_s {
     pdplqr_config cfg;
     std::vector<int32_t> ncs;
@@ -89,4 +91,6 @@ struct pdplqr_handle_s {
     bool model_set = false, updated = false, factored = false;
     bool host_staged = false;  // a host->device copy is in flight on `stream`
     std::vector<void *> allocs;
+    pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)
+    double *suf_bufs[2] = {nullptr, nullptr};
 };

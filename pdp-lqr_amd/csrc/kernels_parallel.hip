@@ -1,0 +1,632 @@
+// kernels_parallel.hip -- LQRParallelSolver on MI355X: horizon segments,
+// associative segment combine, segment rollout.
+//
+// Restates reference lqr_solver_parallel.hpp:64-238, lqr_kernel_parallel.hpp:52-218
+// and condensed_system.hpp:8-299:
+//   * k_seg_bwd<T>: one wavefront per (problem, segment) runs the segment's
+//     Riccati recursion from a zero terminal (the real terminal for the last
+//     segment, lqr_kernel_parallel.hpp:52-67) and accumulates the segment
+//     element (F, C, f) plus G_k (step_with_factorization, :88-136).  It exports
+//     e = (F, C, f, P = Lxx Lxx^T, p) as update_segment_data does
+//     (lqr_solver_parallel.hpp:182-187, condensed_system.hpp:64-74).
+//   * k_seg_scan: one Hillis-Steele round of the prefix and suffix scans of the
+//     elements under the associative operator
+//         Z = (I + C_a P_b)^{-1}, F = F_b Z F_a, C = F_b Z C_a F_b^T + C_b,
+//         f = F_b Z (f_a - C_a p_b) + f_b, P = P_a + F_a^T P_b Z F_a,
+//         p = p_a + F_a^T Z^T (p_b + P_b f_a).
+//     The reference folds the same operator serially on the master thread
+//     (condensed_system.hpp:82-137 LU form, :203-290 Cholesky form); here
+//     P_b Z = Y = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b), an SPD solve.
+//   * k_seg_boundary: x_hat_i = (I + C_pre P_suf)^{-1}(F_pre x0 + f_pre - C_pre p_suf)
+//     and u_hat_i = p_suf(i+1) + P_suf(i+1) x_hat_{i+1} (condensed forward).
+//   * the rollout reuses k_riccati_fwd with the G_k u_hat coupling
+//     (lqr_kernel_parallel.hpp:195-198).
+#include "device_common.hpp"
+#include "parallel.hpp"
+
+namespace pdplqr {
+
+// ---------------------------------------------------------------------------
+// Wave-level dense helpers on n x n (n <= 32) column-major matrices in LDS.
+// Every lane of the (single-wave) workgroup participates; callers separate
+// dependent phases with wave_sync().
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wm_gemm(double *C, const double *A, bool tA, const double *B, bool tB, int n,
+                                        double alpha, const double *Cadd, int lane) {
+    for (int idx = lane; idx < n * n; idx += 64) {
+        const int i = idx % n, j = idx / n;
+        double acc = 0.0;
+        for (int k = 0; k < n; ++k) {
+            const double a = tA ? A[k + i * n] : A[i + k * n];
+            const double b = tB ? B[j + k * n] : B[k + j * n];
+            acc = __builtin_fma(a, b, acc);
+        }
+        C[idx] = alpha * acc + (Cadd ? Cadd[idx] : 0.0);
+    }
+}
+
+// y = op(A) x (+ yadd), n-vector
+__device__ __forceinline__ void wm_gemv(double *y, const double *A, bool tA, const double *x, int n, double alpha,
+                                        const double *yadd, int lane) {
+    for (int i = lane; i < n; i += 64) {
+        double acc = 0.0;
+        for (int k = 0; k < n; ++k) acc = __builtin_fma(tA ? A[k + i * n] : A[i + k * n], x[k], acc);
+        y[i] = alpha * acc + (yadd ? yadd[i] : 0.0);
+    }
+}
+
+// L = chol(A) (lower, zero upper); returns false if a pivot is not positive.
+__device__ __forceinline__ bool wm_chol(double *L, const double *A, int n, int lane) {
+    for (int idx = lane; idx < n * n; idx += 64) L[idx] = A[idx];
+    wave_sync();
+    bool ok = true;
+    for (int j = 0; j < n; ++j) {
+        const double djj = L[j + j * n];
+        ok = ok && (djj > 0.0);
+        const double d = sqrt(djj);
+        wave_sync();
+        for (int i = j + 1 + lane; i < n; i += 64) L[i + j * n] /= d;
+        if (lane == 0) L[j + j * n] = d;
+        wave_sync();
+        const int r = n - j - 1;
+        for (int q = lane; q < r * r; q += 64) {
+            const int i = j + 1 + q % r, k = j + 1 + q / r;
+            if (i >= k) L[i + k * n] -= L[i + j * n] * L[k + j * n];
+        }
+        wave_sync();
+    }
+    for (int idx = lane; idx < n * n; idx += 64) {
+        const int i = idx % n, j = idx / n;
+        if (i < j) L[idx] = 0.0;
+    }
+    wave_sync();
+    return ok;
+}
+
+// X = L^{-1} B (L lower), columns of B in parallel; X may alias B.
+__device__ __forceinline__ void wm_trsm_lower(double *X, const double *L, const double *B, int n, int lane) {
+    for (int j = lane; j < n; j += 64) {
+        for (int i = 0; i < n; ++i) {
+            double v = B[i + j * n];
+            for (int k = 0; k < i; ++k) v -= L[i + k * n] * X[k + j * n];
+            X[i + j * n] = v / L[i + i * n];
+        }
+    }
+}
+
+// Element views: [F | C | f | P | p] packed contiguously (3 n^2 + 2 n doubles)
+struct Elem {
+    double *F, *C, *f, *P, *p;
+};
+
+__device__ __forceinline__ Elem elem_view(double *base, int n) {
+    Elem e;
+    e.F = base;
+    e.C = base + n * n;
+    e.f = base + 2 * n * n;
+    e.P = base + 2 * n * n + n;
+    e.p = base + 3 * n * n + n;
+    return e;
+}
+
+__device__ __forceinline__ void elem_copy(double *dst, const double *src, int n, int lane) {
+    const int sz = 3 * n * n + 2 * n;
+    for (int q = lane; q < sz; q += 64) dst[q] = src[q];
+}
+
+// Workspace of one combine: 8 n x n matrices + 4 n-vectors in LDS.
+struct CombineWs {
+    double *R, *X1, *X2, *X3, *Y, *Z, *X4, *X5, *v1, *v2, *v3, *v4;
+};
+
+__device__ __forceinline__ CombineWs combine_ws(double *base, int n) {
+    CombineWs w;
+    const int nn = n * n;
+    w.R = base; w.X1 = base + nn; w.X2 = base + 2 * nn; w.X3 = base + 3 * nn;
+    w.Y = base + 4 * nn; w.Z = base + 5 * nn; w.X4 = base + 6 * nn; w.X5 = base + 7 * nn;
+    w.v1 = base + 8 * nn; w.v2 = w.v1 + n; w.v3 = w.v2 + n; w.v4 = w.v3 + n;
+    return w;
+}
+static constexpr int kCombineWsDoubles(int n) { return 8 * n * n + 4 * n; }
+
+// Y = P_b Z = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b); Z = I - C_a Y.
+// Returns false when P_b or the SPD core is not positive definite.
+__device__ __forceinline__ bool combine_core(const double *Ca, const double *Pb, CombineWs &w, int n, int lane) {
+    bool ok = wm_chol(w.R, Pb, n, lane);                 // R
+    wm_gemm(w.X1, Ca, false, w.R, false, n, 1.0, nullptr, lane);  // X1 = C_a R
+    wave_sync();
+    wm_gemm(w.X2, w.R, true, w.X1, false, n, 1.0, nullptr, lane);  // X2 = R^T C_a R
+    wave_sync();
+    for (int i = lane; i < n; i += 64) w.X2[i + i * n] += 1.0;     // S = I + R^T C_a R
+    wave_sync();
+    ok = wm_chol(w.X3, w.X2, n, lane) && ok;             // Ls = chol(S)
+    // U = Ls^{-1} R^T
+    for (int idx = lane; idx < n * n; idx += 64) {
+        const int i = idx % n, j = idx / n;
+        w.X1[idx] = w.R[j + i * n];
+    }
+    wave_sync();
+    wm_trsm_lower(w.X1, w.X3, w.X1, n, lane);
+    wave_sync();
+    wm_gemm(w.Y, w.X1, true, w.X1, false, n, 1.0, nullptr, lane);  // Y = U^T U
+    wave_sync();
+    wm_gemm(w.Z, Ca, false, w.Y, false, n, -1.0, nullptr, lane);   // Z = -C_a Y
+    wave_sync();
+    for (int i = lane; i < n; i += 64) w.Z[i + i * n] += 1.0;       // Z = I - C_a Y
+    wave_sync();
+    return ok;
+}
+
+// out = a (x) b, a earlier, b later.  `need_Pp` = compute P, p; `need_FCf` = compute F, C, f.
+__device__ __forceinline__ bool elem_combine(double *out, const double *ab, const double *bb, CombineWs &w, int n,
+                                             bool need_FCf, bool need_Pp, int lane) {
+    Elem a = elem_view(const_cast<double *>(ab), n), b = elem_view(const_cast<double *>(bb), n),
+         o = elem_view(out, n);
+    const bool ok = combine_core(a.C, b.P, w, n, lane);
+    if (need_FCf) {
+        wm_gemm(w.X4, w.Z, false, a.F, false, n, 1.0, nullptr, lane);     // Z F_a
+        wm_gemm(w.X5, w.Z, false, a.C, false, n, 1.0, nullptr, lane);     // Z C_a
+        for (int i = lane; i < n; i += 64) {                               // v1 = f_a - C_a p_b
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc = __builtin_fma(a.C[i + k * n], b.p[k], acc);
+            w.v1[i] = a.f[i] - acc;
+        }
+        wave_sync();
+        wm_gemm(o.F, b.F, false, w.X4, false, n, 1.0, nullptr, lane);     // F = F_b Z F_a
+        wm_gemm(w.X1, w.X5, false, b.F, true, n, 1.0, nullptr, lane);     // Z C_a F_b^T
+        wm_gemv(w.v2, w.Z, false, w.v1, n, 1.0, nullptr, lane);           // Z (f_a - C_a p_b)
+        wave_sync();
+        wm_gemm(w.X3, b.F, false, w.X1, false, n, 1.0, b.C, lane);        // C = F_b Z C_a F_b^T + C_b
+        wm_gemv(o.f, b.F, false, w.v2, n, 1.0, b.f, lane);                // f = F_b v2 + f_b
+        wave_sync();
+        for (int idx = lane; idx < n * n; idx += 64) {                    // symmetrise C
+            const int i = idx % n, j = idx / n;
+            o.C[idx] = 0.5 * (w.X3[idx] + w.X3[j + i * n]);
+        }
+    }
+    if (need_Pp) {
+        wm_gemm(w.X4, w.Y, false, a.F, false, n, 1.0, nullptr, lane);     // Y F_a
+        wm_gemv(w.v3, b.P, false, a.f, n, 1.0, b.p, lane);                // v3 = p_b + P_b f_a
+        wave_sync();
+        wm_gemm(w.X5, a.F, true, w.X4, false, n, 1.0, a.P, lane);         // P = P_a + F_a^T Y F_a
+        wm_gemv(w.v4, w.Z, true, w.v3, n, 1.0, nullptr, lane);            // Z^T v3
+        wave_sync();
+        wm_gemv(o.p, a.F, true, w.v4, n, 1.0, a.p, lane);                 // p = p_a + F_a^T Z^T v3
+        for (int idx = lane; idx < n * n; idx += 64) {
+            const int i = idx % n, j = idx / n;
+            o.P[idx] = 0.5 * (w.X5[idx] + w.X5[j + i * n]);
+        }
+    }
+    wave_sync();
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// Segment backward: the reference's reduction_per_thread (lqr_solver_parallel.hpp:164-188)
+// ---------------------------------------------------------------------------
+template <int T>
+struct SegSmem {
+    static constexpr int P = 16 * T, NM = P * P;
+    double F[NM], C[NM], Ft[NM], Ct[NM], Acl[NM];  // n x n (ld n)
+    double Es[NM], FB[NM], K[NM], G[NM];           // E (n x s), F_next B (n x m), K, G (m x n)
+    double f[P], ft[P], cv[P], dv[P];
+};
+
+template <int T>
+__global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
+    constexpr int LD = 16 * T + 1;
+    __shared__ BwdSmem<T> sm;
+    __shared__ SegSmem<T> ss;
+    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
+    const long long b = blockIdx.x / S;
+    const int seg = blockIdx.x % S;
+    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
+    const bool last = (seg == S - 1) && A.last_is_terminal;
+    const long long frs = (long long)s * m + m;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.FR + b * sh.perKD;
+    double *Gb = A.G + b * (long long)sh.N * m * n;
+    double *Lcb = A.Lc ? A.Lc + b * sh.perHw : nullptr;
+    double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
+    int fail_stage = -1;
+
+    // ---- segment terminal (lqr_kernel_parallel.hpp:52-67) ----
+    if (last) {
+        d4 M[T][T];
+        load_M<T>(M, Hb + (long long)sh.N * sh.ps, n, m, m, s, g, c);
+        double myinv[T], lpr[T][4];
+#pragma unroll
+        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
+        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, m, s, m, false, g, c);
+        finalize_L<T>(M, myinv, m, s, g, c);
+        if (f >= 0) fail_stage = sh.N;
+        store_L_lds<T>(M, sm.L, g, c);
+        if (lane < n) {
+            const double v = hb[(long long)sh.N * s + lane];
+            sm.pv[lane] = v;
+            if (lpb) lpb[(long long)sh.N * s + lane] = v;
+        }
+        if (Lcb)
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                        if (j >= m && i >= j && i < s)
+                            Lcb[(long long)sh.N * sh.ps + pidx(i - m, j - m, n)] = M[a][bt][r];
+                    }
+    } else {  // dummy: L = 0, lp = 0, F = I, C = 0, f = 0
+        for (int q = lane; q < (16 * T) * LD; q += 64) sm.L[q] = 0.0;
+        for (int q = lane; q < 16 * T; q += 64) sm.pv[q] = 0.0;
+        for (int q = lane; q < n * n; q += 64) {
+            ss.F[q] = (q % n == q / n) ? 1.0 : 0.0;
+            ss.C[q] = 0.0;
+        }
+        for (int q = lane; q < n; q += 64) ss.f[q] = 0.0;
+    }
+    wave_sync();
+
+    for (int k = N1 - 1; k >= N0; --k) {
+        StageIn<T> cur;
+        load_stage<T>(cur, Eb + (long long)k * n * s, cb + (long long)k * n, Hb + (long long)k * sh.ps,
+                      hb + (long long)k * s, n, s, g, c);
+        d4 M[T][T];
+        double lpr[T][4];
+        const int f = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
+        if (f >= 0 && fail_stage < 0) fail_stage = k;
+        double *FRk = FRb + (long long)k * frs;
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                const int jc = 16 * bt + c;
+                if (jc < m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g;
+                        if (i < s) FRk[jc * s + i] = M[a][bt][r];
+                    }
+            }
+        if (lane < m) FRk[(long long)s * m + lane] = sm.luq[lane];
+        if (lpb) {
+            if (lane < m) lpb[(long long)k * s + lane] = sm.luq[lane];
+            if (lane < n) lpb[(long long)k * s + m + lane] = sm.pv[lane];
+        }
+        if (Lcb)
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                        if (i >= j && i < s) Lcb[(long long)k * sh.ps + pidx(i, j, s)] = M[a][bt][r];
+                    }
+        if (last) continue;
+        // ---- segment element recursion (lqr_kernel_parallel.hpp:97-135) ----
+        const double *Ek = Eb + (long long)k * n * s;
+        const double *L = sm.L;  // L_k, padded, ld LD
+        for (int q = lane; q < n * s; q += 64) ss.Es[q] = Ek[q];
+        if (lane < n) ss.cv[lane] = cb[(long long)k * n + lane];
+        wave_sync();
+        // K = -Luu^{-T} Lxu^T (:105,107) and d = -Luu^{-T} lu (:106,108)
+        if (lane <= n) {
+            for (int i = m - 1; i >= 0; --i) {
+                double v = (lane < n) ? -L[(m + lane) + i * LD] : -sm.luq[i];
+                for (int j = i + 1; j < m; ++j)
+                    v -= L[j + i * LD] * ((lane < n) ? ss.K[j + lane * m] : ss.dv[j]);
+                v /= L[i + i * LD];
+                if (lane < n) ss.K[i + lane * m] = v;
+                else ss.dv[i] = v;
+            }
+        }
+        // FB = F_next B (n x m): B^T F_next^T of :126 transposed
+        for (int q = lane; q < n * m; q += 64) {
+            const int t = q % n, i = q / n;
+            double acc = 0.0;
+            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[t + r * n], ss.Es[r + i * n], acc);
+            ss.FB[t + i * n] = acc;
+        }
+        wave_sync();
+        // G = -Luu^{-1} B^T F_next^T (:127-128): column t of G from row t of FB
+        if (lane < n) {
+            for (int i = 0; i < m; ++i) {
+                double v = -ss.FB[lane + i * n];
+                for (int j = 0; j < i; ++j) v -= L[i + j * LD] * ss.G[j + lane * m];
+                v /= L[i + i * LD];
+                ss.G[i + lane * m] = v;
+                Gb[(long long)k * m * n + i + lane * m] = v;
+            }
+        }
+        // Acl = A + B K (:129) ; ft = c + B d (:132)
+        for (int q = lane; q < n * n; q += 64) {
+            const int t = q % n, j = q / n;
+            double acc = ss.Es[t + (m + j) * n];
+            for (int i = 0; i < m; ++i) acc = __builtin_fma(ss.Es[t + i * n], ss.K[i + j * m], acc);
+            ss.Acl[q] = acc;
+        }
+        if (lane < n) {
+            double acc = ss.cv[lane];
+            for (int i = 0; i < m; ++i) acc = __builtin_fma(ss.Es[lane + i * n], ss.dv[i], acc);
+            ss.ft[lane] = acc;
+        }
+        wave_sync();
+        // F = F_next Acl (:130); f = F_next ft + f_next (:133); C = C_next + G^T G (:134)
+        for (int q = lane; q < n * n; q += 64) {
+            const int t = q % n, j = q / n;
+            double acc = 0.0;
+            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[t + r * n], ss.Acl[r + j * n], acc);
+            ss.Ft[q] = acc;
+            double cc = 0.0;
+            for (int i = 0; i < m; ++i) cc = __builtin_fma(ss.G[i + t * m], ss.G[i + j * m], cc);
+            ss.Ct[q] = ss.C[q] + cc;
+        }
+        double fnew = 0.0;
+        if (lane < n) {
+            double acc = 0.0;
+            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[lane + r * n], ss.ft[r], acc);
+            fnew = acc + ss.f[lane];
+        }
+        wave_sync();
+        for (int q = lane; q < n * n; q += 64) {
+            ss.F[q] = ss.Ft[q];
+            ss.C[q] = ss.Ct[q];
+        }
+        if (lane < n) ss.f[lane] = fnew;
+        wave_sync();
+    }
+    // ---- export the element (update_segment_data, lqr_solver_parallel.hpp:182-187) ----
+    double *eo = A.elem + (b * S + seg) * (long long)(3 * n * n + 2 * n);
+    Elem e = elem_view(eo, n);
+    for (int q = lane; q < n * n; q += 64) {
+        const int i = q % n, j = q / n;
+        double acc = 0.0;
+        for (int t = 0; t < n; ++t) acc = __builtin_fma(sm.L[(m + i) + (m + t) * LD], sm.L[(m + j) + (m + t) * LD], acc);
+        e.P[q] = acc;  // P = Lxx Lxx^T (condensed_system.hpp:69,188)
+        e.F[q] = last ? 0.0 : ss.F[q];
+        e.C[q] = last ? 0.0 : ss.C[q];
+    }
+    if (lane < n) {
+        e.f[lane] = last ? 0.0 : ss.f[lane];
+        e.p[lane] = sm.pv[lane];
+    }
+    if (lane == 0) A.seg_status[b * S + seg] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+// ---------------------------------------------------------------------------
+// One Hillis-Steele round: inclusive prefix (dir 0) or suffix (dir 1) scan.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    const int lane = threadIdx.x;
+    const int n = A.n, S = A.S, d = A.dist;
+    const int es = 3 * n * n + 2 * n;
+    const long long b = blockIdx.x / (2 * S);
+    const int rem = blockIdx.x % (2 * S);
+    const int dir = rem / S, i = rem % S;
+    const double *in = (dir == 0 ? A.pre_in : A.suf_in) + b * (long long)S * es;
+    double *out = (dir == 0 ? A.pre_out : A.suf_out) + b * (long long)S * es;
+    double *ea = dyn, *eb = dyn + es, *eo = dyn + 2 * es;
+    CombineWs w = combine_ws(dyn + 3 * es, n);
+    int ia, ib;
+    if (dir == 0) {  // pre_i = pre_{i-d} (x) pre_i
+        if (i - d < 0) {
+            elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
+            return;
+        }
+        ia = i - d; ib = i;
+    } else {  // suf_i = suf_i (x) suf_{i+d}
+        if (i + d >= S) {
+            elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
+            return;
+        }
+        ia = i; ib = i + d;
+    }
+    elem_copy(ea, in + (long long)ia * es, n, lane);
+    elem_copy(eb, in + (long long)ib * es, n, lane);
+    wave_sync();
+    // a suffix ending at the real terminal has F = C = f = 0; a zero-P right
+    // operand (never produced here) would need the identity rule instead.
+    const bool ok = elem_combine(eo, ea, eb, w, n, true, dir == 1, lane);
+    if (!ok && lane == 0) atomicOr(A.flag, 1);
+    elem_copy(out + (long long)i * es, eo, n, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Boundary states: x_hat_i from the exclusive prefix (optionally left-folded
+// with a global prefix) and the suffix (optionally right-folded with a global
+// suffix); u_hat_i in a second pass.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    const int lane = threadIdx.x;
+    const int n = A.n, S = A.S;
+    const int es = 3 * n * n + 2 * n;
+    const long long b = blockIdx.x / (S + 1);
+    const int i = blockIdx.x % (S + 1);  // i == S: state after the last segment (shard mode)
+    double *pre = dyn, *suf = dyn + es, *tmp = dyn + 2 * es;  // tmp + es: combine output
+    CombineWs w = combine_ws(dyn + 4 * es, n);
+    const double *preb = A.pre + b * (long long)S * es;
+    const double *sufb = A.suf + b * (long long)S * es;
+    // prefix before segment i: global_left (x) pre_{i-1}
+    if (i == 0) {
+        if (A.left) elem_copy(pre, A.left + b * (long long)es, n, lane);
+        else {
+            Elem e = elem_view(pre, n);
+            for (int q = lane; q < n * n; q += 64) {
+                e.F[q] = (q % n == q / n) ? 1.0 : 0.0;
+                e.C[q] = 0.0;
+                e.P[q] = 0.0;
+            }
+            for (int q = lane; q < n; q += 64) { e.f[q] = 0.0; e.p[q] = 0.0; }
+        }
+        wave_sync();
+    } else {
+        if (A.left) {
+            elem_copy(tmp, A.left + b * (long long)es, n, lane);
+            elem_copy(suf, preb + (long long)(i - 1) * es, n, lane);  // scratch
+            wave_sync();
+            elem_combine(pre, tmp, suf, w, n, true, false, lane);
+        } else {
+            elem_copy(pre, preb + (long long)(i - 1) * es, n, lane);
+            wave_sync();
+        }
+    }
+    // suffix from segment i: suf_i (x) global_right ; for i == S only global_right
+    bool have_suf = true;
+    if (i < S) {
+        if (A.right) {
+            elem_copy(tmp, sufb + (long long)i * es, n, lane);
+            elem_copy(suf, A.right + b * (long long)es, n, lane);
+            wave_sync();
+            double *o = tmp + es;  // scratch beyond tmp: pre | suf | tmp | tmp2 fit in 4 es (see launcher)
+            elem_combine(o, tmp, suf, w, n, false, true, lane);
+            elem_copy(suf, o, n, lane);
+            wave_sync();
+        } else {
+            elem_copy(suf, sufb + (long long)i * es, n, lane);
+            wave_sync();
+        }
+    } else {
+        if (A.right) {
+            elem_copy(suf, A.right + b * (long long)es, n, lane);
+            wave_sync();
+        } else {
+            have_suf = false;
+        }
+    }
+    Elem P = elem_view(pre, n), Sf = elem_view(suf, n);
+    double *x0 = tmp;  // reuse
+    if (lane < n) x0[lane] = A.x0[b * n + lane];
+    wave_sync();
+    // rhs = F_pre x0 + f_pre - C_pre p_suf
+    double *rhs = w.v1;
+    for (int r = lane; r < n; r += 64) {
+        double acc = P.f[r];
+        for (int k = 0; k < n; ++k) acc = __builtin_fma(P.F[r + k * n], x0[k], acc);
+        if (have_suf)
+            for (int k = 0; k < n; ++k) acc = __builtin_fma(-P.C[r + k * n], Sf.p[k], acc);
+        rhs[r] = acc;
+    }
+    wave_sync();
+    double *xh = A.xhat + (b * (long long)(S + 1) + i) * n;
+    if (have_suf) {
+        // x = (I + C_pre P_suf)^{-1} rhs = Z rhs with Z from combine_core(C_pre, P_suf)
+        const bool ok = combine_core(P.C, Sf.P, w, n, lane);
+        if (!ok && lane == 0) atomicOr(A.flag, 2);
+        wm_gemv(w.v2, w.Z, false, rhs, n, 1.0, nullptr, lane);
+        wave_sync();
+        if (lane < n) xh[lane] = w.v2[lane];
+        // costate at the start of segment i: lambda = P_suf x + p_suf (stored for u_hat_{i-1})
+        double *lam = A.lam + (b * (long long)(S + 1) + i) * n;
+        wave_sync();
+        for (int r = lane; r < n; r += 64) {
+            double acc = Sf.p[r];
+            for (int k = 0; k < n; ++k) acc = __builtin_fma(Sf.P[r + k * n], w.v2[k], acc);
+            lam[r] = acc;
+        }
+    } else {
+        if (lane < n) xh[lane] = rhs[lane];
+    }
+}
+
+int launch_seg_backward(const SegArgs &a, hipStream_t st) {
+    const dim3 grid((unsigned)(a.sh.batch * a.S)), blk(64);
+    if (a.sh.s <= 16) hipLaunchKernelGGL(k_seg_bwd<1>, grid, blk, 0, st, a);
+    else if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd<2>, grid, blk, 0, st, a);
+    else {
+        set_error("parallel solver: n + m > 32 is not supported by this build");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+static size_t combine_smem(int n, int elems) {
+    return (size_t)(elems * (3 * n * n + 2 * n) + kCombineWsDoubles(n)) * sizeof(double);
+}
+
+int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
+    const dim3 grid((unsigned)(batch * 2 * a.S)), blk(64);
+    hipLaunchKernelGGL(k_seg_scan, grid, blk, combine_smem(a.n, 3), st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st) {
+    const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
+    hipLaunchKernelGGL(k_seg_xhat, grid, blk, combine_smem(a.n, 4), st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// Combine a short list of elements on one wave (the per-rank fold of the
+// horizon-sharded solve): out_pre = e_0 (x) ... (x) e_{r-1} (identity if r = 0),
+// out_suf = e_{r+1} (x) ... (x) e_{R-1} (P = p = 0 marker when r = R-1).
+__global__ __launch_bounds__(64) void k_fold_shards(const double *elems, int R, int r, int n, double *out_pre,
+                                                    double *out_suf, int *has_suf, int *flag) {
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    const int lane = threadIdx.x;
+    const int es = 3 * n * n + 2 * n;
+    double *acc = dyn, *nx = dyn + es, *o = dyn + 2 * es;
+    CombineWs w = combine_ws(dyn + 3 * es, n);
+    // prefix
+    {
+        Elem e = elem_view(acc, n);
+        for (int q = lane; q < n * n; q += 64) {
+            e.F[q] = (q % n == q / n) ? 1.0 : 0.0;
+            e.C[q] = 0.0;
+            e.P[q] = 0.0;
+        }
+        for (int q = lane; q < n; q += 64) { e.f[q] = 0.0; e.p[q] = 0.0; }
+        wave_sync();
+        for (int j = 0; j < r; ++j) {
+            elem_copy(nx, elems + (long long)j * es, n, lane);
+            wave_sync();
+            if (j == 0) {
+                elem_copy(acc, nx, n, lane);
+            } else {
+                if (!elem_combine(o, acc, nx, w, n, true, false, lane) && lane == 0) atomicOr(flag, 4);
+                elem_copy(acc, o, n, lane);
+            }
+            wave_sync();
+        }
+        elem_copy(out_pre, acc, n, lane);
+    }
+    // suffix (right fold from the end: e_{R-1}, then e_j (x) acc)
+    if (r + 1 >= R) {
+        if (lane == 0) *has_suf = 0;
+        return;
+    }
+    elem_copy(acc, elems + (long long)(R - 1) * es, n, lane);
+    wave_sync();
+    for (int j = R - 2; j > r; --j) {
+        elem_copy(nx, elems + (long long)j * es, n, lane);
+        wave_sync();
+        if (!elem_combine(o, nx, acc, w, n, true, true, lane) && lane == 0) atomicOr(flag, 8);
+        elem_copy(acc, o, n, lane);
+        wave_sync();
+    }
+    elem_copy(out_suf, acc, n, lane);
+    if (lane == 0) *has_suf = 1;
+}
+
+int launch_fold_shards(const double *elems, int R, int r, int n, double *out_pre, double *out_suf, int *has_suf,
+                       int *flag, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_shards, dim3(1), dim3(64), combine_smem(n, 3), st, elems, R, r, n, out_pre, out_suf,
+                       has_suf, flag);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// Local total element of a shard = suffix scan entry 0 (already computed):
+// copied out by the caller.
+
+}  // namespace pdplqr

@@ -20,20 +20,10 @@
 //     M = H~ + W^T W            (MFMA, both operands = W's registers, no data movement)
 //     L = chol(M)               (right-looking, column broadcast through LDS)
 // i.e. M = H~ + V V^T with V = E^T Lxx_next exactly as lqr_kernel.hpp:121-126.
-#include "internal.hpp"
+#include "device_common.hpp"
+#include "parallel.hpp"
 
 namespace pdplqr {
-
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// packed lower (column-major) index of (i, j), i >= j, dimension d
-__device__ __forceinline__ int pidx(int i, int j, int d) { return j * d - ((j * (j - 1)) >> 1) + (i - j); }
-
-__device__ __forceinline__ double shfl_xor_f64(double v, int mask) { return __shfl_xor(v, mask, 64); }
 
 // ---------------------------------------------------------------------------
 // update_problem_data (lqr_solver.hpp:41-56)
@@ -162,198 +152,6 @@ int launch_penalty(const Shape &sh, const double *D, const double *rho, const do
 // ---------------------------------------------------------------------------
 // Backward with factorization: one wavefront per problem, f64 MFMA tiles.
 // ---------------------------------------------------------------------------
-// Loads the padded stage matrix H~ into C/D-layout tiles.  Indices in
-// [lo, hi) map to the stored packed block (dimension dim, offset off);
-// everything else is the identity padding.
-template <int T>
-__device__ __forceinline__ void load_M(d4 (&M)[T][T], const double *__restrict__ Hp, int dim, int off, int lo, int hi,
-                                       int g, int c) {
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
-                double v;
-                if (i >= lo && i < hi && j >= lo && j < hi) {
-                    const int ii = i - off, jj = j - off;
-                    v = (ii >= jj) ? Hp[pidx(ii, jj, dim)] : Hp[pidx(jj, ii, dim)];
-                } else {
-                    v = (i == j) ? 1.0 : 0.0;
-                }
-                M[a][b][r] = v;
-            }
-}
-
-// Wave-scope ordering of LDS traffic between lanes of ONE wavefront: LDS
-// instructions of a wave retire in issue order, so a compiler-level barrier is
-// all that is needed (no s_barrier; the workgroup is a single wave).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-    return __hiloint2double(hi, lo);
-}
-
-// 1/sqrt(x): hardware estimate + two Newton steps (full fp64 accuracy).
-__device__ __forceinline__ double rsqrt_f64(double x) {
-    double r = __builtin_amdgcn_rsq(x);
-    double e = __builtin_fma(-x * r, r, 1.0);
-    r = __builtin_fma(0.5 * r, e, r);
-    e = __builtin_fma(-x * r, r, 1.0);
-    return __builtin_fma(0.5 * r, e, r);
-}
-
-// Stage-k inputs of one lane, loaded one stage ahead (register prefetch).
-template <int T>
-struct StageIn {
-    double E[4 * T][T];  // MFMA B operand: E[4 cc + g][16 b + c]
-    d4 H[T][T];          // MFMA C input: H~[16 a + 4 r + g][16 b + c] (padded)
-    double c[4 * T];     // c[4 cc + g]
-    double h[T];         // h~[16 b + c]
-};
-
-template <int T>
-__device__ __forceinline__ void load_stage(StageIn<T> &in, const double *__restrict__ Ek, const double *__restrict__ ck,
-                                           const double *__restrict__ Hk, const double *__restrict__ hk, int n,
-                                           int s, int g, int c) {
-#pragma unroll
-    for (int cc = 0; cc < 4 * T; ++cc) {
-        const int t = 4 * cc + g;
-#pragma unroll
-        for (int b = 0; b < T; ++b) {
-            const int j = 16 * b + c;
-            in.E[cc][b] = (t < n && j < s) ? Ek[t + j * n] : 0.0;
-        }
-        in.c[cc] = (t < n) ? ck[t] : 0.0;
-    }
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
-                double v;
-                if (i < s && j < s)
-                    v = (i >= j) ? Hk[pidx(i, j, s)] : Hk[pidx(j, i, s)];
-                else
-                    v = (i == j) ? 1.0 : 0.0;
-                in.H[a][b][r] = v;
-            }
-#pragma unroll
-    for (int b = 0; b < T; ++b) {
-        const int j = 16 * b + c;
-        in.h[b] = (j < s) ? hk[j] : 0.0;
-    }
-}
-
-// Right-looking Cholesky of the symmetric padded matrix in C/D layout, pivots
-// jbeg..jend-1.  Column j is broadcast through LDS from row j (the row group
-// that owns row j holds M[j][*] = M[*][j]; M stays exactly symmetric because
-// every update is applied to both triangles with the same products).  The
-// owners write zeros for columns <= j, so every lane can update
-// M -= raw_i raw_k / M[j][j] without masking; the pivot column itself is left
-// unscaled and finalised by finalize_L (L[i][j] = M[i][j] / sqrt(M[j][j])).
-// With `aug`, the first `m` pivots also eliminate the linear column lpr (the
-// lp_k of lqr_kernel.hpp:142-146): lpr_i -= l_ij lu'_j with lu'_j = lp_j / L_jj,
-// which is exactly lu <- Luu^{-1} lu followed by p -= Lxu lu.  All lanes of the
-// wave run in lock step and LDS ops of one wave retire in order, so no barrier
-// is needed between the owners' writes and the readers.
-template <int T>
-__device__ __forceinline__ int chol_tiles(d4 (&M)[T][T], double (&myinv)[T], double (&lpr)[T][4], double *cb,
-                                          double *luq, int jbeg, int jend, int m, bool aug, int g, int c) {
-    int fail = -1;
-    const bool lane0 = (g == 0) && (c == 0);
-#pragma unroll
-    for (int j = 0; j < 16 * T; ++j) {
-        if (j >= jbeg && j < jend) {
-            const int tr = j >> 4, rr = (j >> 2) & 3, gj = j & 3, bj = j >> 4, cj = j & 15;
-            if (g == gj) {
-#pragma unroll
-                for (int b = 0; b < T; ++b) {
-                    const int jc = 16 * b + c;
-                    cb[jc] = (jc > j) ? M[tr][b][rr] : 0.0;
-                }
-            }
-            wave_sync();
-            const double djj = readlane_f64(M[tr][bj][rr], (gj << 4) + cj);
-            if (!(djj > 0.0) && fail < 0) fail = j;
-            const double inv = rsqrt_f64(djj);
-            const double inv2 = inv * inv;
-            if (c == cj) myinv[bj] = inv;
-            double lc[T];
-#pragma unroll
-            for (int b = 0; b < T; ++b) lc[b] = cb[16 * b + c] * inv2;
-            const bool augj = aug && j < m;
-            const double lpj = augj ? readlane_f64(lpr[tr][rr], gj << 4) : 0.0;
-            const double qj = lpj * inv2;
-#pragma unroll
-            for (int a = 0; a < T; ++a)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const double li = cb[16 * a + 4 * r + g];
-#pragma unroll
-                    for (int b = 0; b < T; ++b) M[a][b][r] = __builtin_fma(-li, lc[b], M[a][b][r]);
-                    // q = lp_j / M[j][j]; lpr_i -= raw_i * q  (raw_i = 0 for i <= j)
-                    if (augj) lpr[a][r] = __builtin_fma(-li, qj, lpr[a][r]);
-                }
-            if (augj && lane0) luq[j] = lpj * inv;
-            wave_sync();
-        }
-    }
-    return fail;
-}
-
-// L[i][jc] = M[i][jc] / sqrt(M[jc][jc]) below the diagonal, 0 above, for the
-// factored columns jc < jend; identity padding elsewhere is left as is.
-template <int T>
-__device__ __forceinline__ void finalize_L(d4 (&M)[T][T], const double (&myinv)[T], int jbeg, int jend, int g,
-                                           int c) {
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b) {
-            const int jc = 16 * b + c;
-            if (jc >= jbeg && jc < jend) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * a + 4 * r + g;
-                    M[a][b][r] = (i >= jc) ? M[a][b][r] * myinv[b] : 0.0;
-                }
-            }
-        }
-}
-
-template <int T>
-struct BwdSmem {
-    static constexpr int P = 16 * T;
-    static constexpr int LD = P + 1;  // odd leading dimension: conflict-free column reads
-    double L[P * LD];                 // L_{k+1} then L_k (padded, column-major, lower, zero upper)
-    double col[P];                    // Cholesky column broadcast
-    double pbt[P];                    // Pb_tmp = Lxx_next^T c
-    double pv[P];                     // p_{k+1}, then p_k
-    double lp[P];                     // lp_k (column -> row redistribution)
-    double luq[P];                    // lu'_k = Luu^{-1} lu
-};
-
-template <int T>
-__device__ __forceinline__ void store_L_lds(const d4 (&M)[T][T], double *L, int g, int c) {
-    constexpr int LD = 16 * T + 1;
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) L[(16 * a + 4 * r + g) + (16 * b + c) * LD] = M[a][b][r];
-}
-
 // Per-stage rollout record FR_k = [L(:, 0:m) (s x m, column-major) | lu'_k (m)]:
 // exactly what LQRKernel::forward_step reads (Luu, Lxu, lu; lqr_kernel.hpp:190-198).
 #ifndef PDPLQR_BWD_WAVES
@@ -361,13 +159,11 @@ __device__ __forceinline__ void store_L_lds(const d4 (&M)[T][T], double *L, int 
 #endif
 template <int T>
 __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati_bwd(RiccatiArgs A) {
-    constexpr int P = 16 * T, LD = P + 1;
     __shared__ BwdSmem<T> sm;
     const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
-    const int nch = (n + 3) >> 2;
     const long long frs = (long long)s * m + m;
     const double *Eb = A.E + b * sh.perE;
     const double *cb = A.c + b * sh.perc;
@@ -416,110 +212,18 @@ __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati
         if (k > 0)
             load_stage<T>(nxt, Eb + (long long)(k - 1) * n * s, cb + (long long)(k - 1) * n,
                           Hb + (long long)(k - 1) * sh.ps, hb + (long long)(k - 1) * s, n, s, g, c);
-        // ---- A operand: Lxx_next^T, read from LDS (L_{k+1}) ----
-        double av[4 * T][T];
-#pragma unroll
-        for (int cc = 0; cc < 4 * T; ++cc) {
-            const int t = 4 * cc + g;
-#pragma unroll
-            for (int a = 0; a < T; ++a) {
-                const int tp = 16 * a + c;
-                av[cc][a] = (cc < nch && t < n && tp < n) ? sm.L[(m + t) + (m + tp) * LD] : 0.0;
-            }
-        }
-        // ---- W = Lxx_next^T E  (= V^T, V = E^T Lxx_next, lqr_kernel.hpp:121) ----
-        d4 W[T][T];
-#pragma unroll
-        for (int a = 0; a < T; ++a)
-#pragma unroll
-            for (int bt = 0; bt < T; ++bt) W[a][bt] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int cc = 0; cc < 4 * T; ++cc)
-            if (cc < nch)
-#pragma unroll
-                for (int a = 0; a < T; ++a)
-#pragma unroll
-                    for (int bt = 0; bt < T; ++bt) W[a][bt] = mfma_f64(av[cc][a], cur.E[cc][bt], W[a][bt]);
-        // ---- Pb_tmp = Lxx_next^T c (lqr_kernel.hpp:138), reduced over row groups ----
-#pragma unroll
-        for (int a = 0; a < T; ++a) {
-            double part = 0.0;
-#pragma unroll
-            for (int cc = 0; cc < 4 * T; ++cc)
-                if (cc < nch) part = __builtin_fma(av[cc][a], cur.c[cc], part);
-            part += shfl_xor_f64(part, 16);
-            part += shfl_xor_f64(part, 32);
-            if (g == 0) sm.pbt[16 * a + c] = part;
-        }
-        // ---- M = H~ + W^T W  (= H~ + V V^T, lqr_kernel.hpp:123-124) ----
         d4 M[T][T];
-#pragma unroll
-        for (int a = 0; a < T; ++a)
-#pragma unroll
-            for (int bt = 0; bt < T; ++bt) M[a][bt] = cur.H[a][bt];
-#pragma unroll
-        for (int kc = 0; kc < 4 * T; ++kc)
-            if (kc < nch) {
-                const int ka = kc >> 2, r = kc & 3;
-#pragma unroll
-                for (int a = 0; a < T; ++a)
-#pragma unroll
-                    for (int bt = 0; bt < T; ++bt) M[a][bt] = mfma_f64(W[ka][a][r], W[ka][bt][r], M[a][bt]);
-            }
-        // ---- lp = h~ + E^T (Lxx_next Pb_tmp + p_next) = h~ + W^T Pb_tmp + E^T p_next
-        //      (lqr_kernel.hpp:139-143; E^T Lxx_next = W^T) ----
-        wave_sync();
         double lpr[T][4];
-        {
-            double part[T];
-#pragma unroll
-            for (int bt = 0; bt < T; ++bt) part[bt] = 0.0;
-#pragma unroll
-            for (int kc = 0; kc < 4 * T; ++kc)
-                if (kc < nch) {
-                    const int t = 4 * kc + g;
-                    const double pb = (t < n) ? sm.pbt[t] : 0.0;
-                    const double pn = (t < n) ? sm.pv[t] : 0.0;
-#pragma unroll
-                    for (int bt = 0; bt < T; ++bt) {
-                        part[bt] = __builtin_fma(W[kc >> 2][bt][kc & 3], pb, part[bt]);
-                        part[bt] = __builtin_fma(cur.E[kc][bt], pn, part[bt]);
-                    }
-                }
-#pragma unroll
-            for (int bt = 0; bt < T; ++bt) {
-                part[bt] += shfl_xor_f64(part[bt], 16);
-                part[bt] += shfl_xor_f64(part[bt], 32);
-                if (g == 0) sm.lp[16 * bt + c] = cur.h[bt] + part[bt];
-            }
-            wave_sync();
-#pragma unroll
-            for (int a = 0; a < T; ++a)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * a + 4 * r + g;
-                    lpr[a][r] = (i < s) ? sm.lp[i] : 0.0;
-                }
-        }
-        // ---- L = chol(M) (lqr_kernel.hpp:126) with lu <- Luu^{-1} lu, p -= Lxu lu (:145-146) ----
-        double myinv[T];
-#pragma unroll
-        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
-        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, 0, s, m, true, g, c);
+        const int f = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
         if (f >= 0 && fail_stage < 0) fail_stage = k;
-        finalize_L<T>(M, myinv, 0, s, g, c);
-        store_L_lds<T>(M, sm.L, g, c);
-        // p_k -> LDS (next stage's p_next) and the factor cache
-        if (c == 0) {
+        // p_k -> factor cache
+        if (lpb && c == 0) {
 #pragma unroll
             for (int a = 0; a < T; ++a)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int i = 16 * a + 4 * r + g;
-                    if (i >= m && i < s) {
-                        sm.pv[i - m] = lpr[a][r];
-                        if (lpb) lpb[(long long)k * s + i] = lpr[a][r];
-                    }
+                    if (i >= m && i < s) lpb[(long long)k * s + i] = lpr[a][r];
                 }
         }
         // rollout record: L(:, 0:m) and lu'
@@ -713,42 +417,81 @@ __device__ __forceinline__ void fwd_load(FwdIn<R, MM> &in, const double *__restr
     in.lu = own ? Fk[s * m + cl] : 0.0;
 }
 
-template <int R, int MM>
+template <int R, int MM, bool SEG>
 __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
-                                                    const double *__restrict__ x0, double *__restrict__ ws) {
+                                                    const double *__restrict__ x0, double *__restrict__ ws, SegFwd sf) {
     constexpr int NJ = 4 * R;
     __shared__ double sw[64];  // w_k = [u; x]
+    __shared__ double suh[64]; // u_hat of this segment
     const int lane = threadIdx.x, g = lane >> 4, cl = lane & 15;
-    const long long b = blockIdx.x;
-    const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
+    const int n = sh.n, m = sh.m, s = sh.s;
+    long long b;
+    int N0, N1;
+    bool last;
+    if (SEG) {
+        b = blockIdx.x / sf.S;
+        const int seg = blockIdx.x % sf.S;
+        N0 = sf.seg_start[seg];
+        N1 = N0 + sf.seg_len[seg];
+        last = (seg == sf.S - 1) && sf.last_is_terminal;
+        const double *xh = sf.xhat + (b * (sf.S + 1) + seg) * n;
+        if (lane < n) {
+            sw[m + lane] = xh[lane];
+            suh[lane] = last ? 0.0 : sf.lam[(b * (sf.S + 1) + seg + 1) * n + lane];
+        }
+        if (!last && seg == sf.S - 1 && lane < n)  // shard slice end: x after the slice
+            ws[b * sh.perh + (long long)N1 * s + lane] = sf.xhat[(b * (sf.S + 1) + sf.S) * n + lane];
+    } else {
+        b = blockIdx.x;
+        N0 = 0;
+        N1 = sh.N;
+        last = true;
+        if (lane < n) sw[m + lane] = x0[b * n + lane];
+    }
+    const int N = sh.N;
     const long long frs = (long long)s * m + m;
     const double *Eb = E + b * sh.perE;
     const double *cb = c + b * sh.perc;
     const double *Fb = FR + b * sh.perKD;
+    const double *Gb = SEG ? sf.G + b * (long long)N * m * n : nullptr;
     double *wb = ws + b * sh.perh;
-    if (lane < n) {
-        const double v = x0[b * n + lane];
-        sw[m + lane] = v;
-        wb[m + lane] = v;  // ws[0].tail(n) = x0 (lqr_solver.hpp:73)
-    }
+    if (lane < n) wb[(long long)N0 * s + m + lane] = sw[m + lane];  // ws[N0].tail(n) = x_hat (lqr_solver_parallel.hpp:224)
     wave_sync();
+    // G u_hat term per stage: lanes (g, cl < m) own G[cl][4 qq + g]
+    double uh[NJ];
+#pragma unroll
+    for (int qq = 0; qq < NJ; ++qq) {
+        const int t = 4 * qq + g;
+        uh[qq] = (SEG && !last && t < n) ? suh[t] : 0.0;
+    }
     FwdIn<R, MM> cur, nxt;
-    fwd_load<R, MM>(cur, Eb, cb, Fb, n, m, s, g, cl);
-    for (int k = 0; k < N; ++k) {
-        if (k + 1 < N)
+    double gq[NJ], gqn[NJ];
+    fwd_load<R, MM>(cur, Eb + (long long)N0 * n * s, cb + (long long)N0 * n, Fb + (long long)N0 * frs, n, m, s, g, cl);
+#pragma unroll
+    for (int qq = 0; qq < NJ; ++qq) {
+        const int t = 4 * qq + g;
+        gq[qq] = (SEG && !last && cl < m && t < n) ? Gb[(long long)N0 * m * n + cl + t * m] : 0.0;
+    }
+    for (int k = N0; k < N1; ++k) {
+        if (k + 1 < N1) {
             fwd_load<R, MM>(nxt, Eb + (long long)(k + 1) * n * s, cb + (long long)(k + 1) * n,
                             Fb + (long long)(k + 1) * frs, n, m, s, g, cl);
-        // v = lu' + Lxu^T x (lanes cl < m), x-part of E w
-        double xv[NJ];
+#pragma unroll
+            for (int qq = 0; qq < NJ; ++qq) {
+                const int t = 4 * qq + g;
+                gqn[qq] = (SEG && !last && cl < m && t < n) ? Gb[(long long)(k + 1) * m * n + cl + t * m] : 0.0;
+            }
+        }
+        // v = lu' + Lxu^T x - G u_hat  (lqr_kernel_parallel.hpp:195-197 / lqr_kernel.hpp:197)
+        double v = 0.0;
 #pragma unroll
         for (int qq = 0; qq < NJ; ++qq) {
             const int t = 4 * qq + g;
-            xv[qq] = (t < n) ? sw[m + t] : 0.0;
+            const double xt = (t < n) ? sw[m + t] : 0.0;
+            v = __builtin_fma(cur.lxu[qq], xt, v);
+            if (SEG) v = __builtin_fma(-gq[qq], uh[qq], v);
         }
-        double v = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < NJ; ++qq) v = __builtin_fma(cur.lxu[qq], xv[qq], v);
         v += shfl_xor_f64(v, 16);
         v += shfl_xor_f64(v, 32);
         v += cur.lu;
@@ -776,7 +519,7 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
             }
         }
         wave_sync();
-        // x+ = c + A x + B u  (lqr_kernel.hpp:201-203), reduced over row groups
+        const bool upd = last || (k < N1 - 1);  // update_x_next (lqr_solver_parallel.hpp:231)
         double xn[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -792,7 +535,7 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
         }
         wave_sync();
         if (g == 0 && cl < m) wb[(long long)k * s + cl] = myu;
-        if (g == 0) {
+        if (g == 0 && upd) {
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 const int t = cl + 16 * q;
@@ -803,29 +546,45 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
             }
         }
         wave_sync();
-        if (k + 1 < N) cur = nxt;
+        if (k + 1 < N1) {
+            cur = nxt;
+#pragma unroll
+            for (int qq = 0; qq < NJ; ++qq) gq[qq] = gqn[qq];
+        }
     }
 }
 
-int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
-                           double *ws, hipStream_t st) {
-    const dim3 grid(sh.batch), blk(64);
+template <bool SEG>
+static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                      double *ws, const SegFwd &sf, hipStream_t st) {
+    const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
     if (sh.s > 32) {
         set_error("forward: n + m > 32 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     const int R = sh.s <= 16 ? 1 : 2;
     if (R == 1) {
-        if (sh.m <= 4) hipLaunchKernelGGL((k_riccati_fwd<1, 4>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
-        else if (sh.m <= 8) hipLaunchKernelGGL((k_riccati_fwd<1, 8>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
-        else hipLaunchKernelGGL((k_riccati_fwd<1, 16>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
+        if (sh.m <= 4) hipLaunchKernelGGL((k_riccati_fwd<1, 4, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
+        else if (sh.m <= 8) hipLaunchKernelGGL((k_riccati_fwd<1, 8, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
+        else hipLaunchKernelGGL((k_riccati_fwd<1, 16, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
     } else {
-        if (sh.m <= 8) hipLaunchKernelGGL((k_riccati_fwd<2, 8>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
-        else if (sh.m <= 16) hipLaunchKernelGGL((k_riccati_fwd<2, 16>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
-        else hipLaunchKernelGGL((k_riccati_fwd<2, 32>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
+        if (sh.m <= 8) hipLaunchKernelGGL((k_riccati_fwd<2, 8, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
+        else if (sh.m <= 16) hipLaunchKernelGGL((k_riccati_fwd<2, 16, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
+        else hipLaunchKernelGGL((k_riccati_fwd<2, 32, SEG>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
     }
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
+}
+
+int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                           double *ws, hipStream_t st) {
+    SegFwd none{};
+    return launch_fwd<false>(sh, E, c, FR, x0, ws, none, st);
+}
+
+int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
+                               double *ws, hipStream_t st) {
+    return launch_fwd<true>(sh, E, c, FR, nullptr, ws, sf, st);
 }
 
 }  // namespace pdplqr

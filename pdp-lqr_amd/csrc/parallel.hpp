@@ -1,0 +1,54 @@
+// parallel.hpp -- argument blocks of the parallel (segmented) solver kernels.
+#pragma once
+#include "internal.hpp"
+
+namespace pdplqr {
+
+struct SegArgs {
+    Shape sh;
+    int S;                    // device segments per problem
+    const int32_t *seg_start;  // [S]
+    const int32_t *seg_len;    // [S]
+    int last_is_terminal;      // 1: the last segment ends at the real terminal node N
+    const double *E, *c, *Hw, *hw;
+    double *FR, *G;            // rollout records [b][N][s m + m], coupling gains [b][N][m n]
+    double *Lc, *lpc;          // factor cache (nullable)
+    double *elem;              // [b][S][3 n^2 + 2 n]
+    int32_t *seg_status;       // [b][S]
+};
+
+struct ScanArgs {
+    int n, S, dist;
+    const double *pre_in, *suf_in;
+    double *pre_out, *suf_out;
+    int *flag;
+};
+
+struct BoundaryArgs {
+    int n, S;
+    const double *pre, *suf;   // inclusive prefix / suffix scans [b][S][es]
+    const double *left;        // optional global prefix element [b][es] (horizon shards)
+    const double *right;       // optional global suffix element [b][es]
+    const double *x0;          // [b][n]
+    double *xhat;              // [b][S+1][n]
+    double *lam;               // [b][S+1][n]  costate at segment starts
+    int *flag;
+};
+
+struct SegFwd {
+    int S;
+    const int32_t *seg_start, *seg_len;
+    int last_is_terminal;
+    const double *G;           // [b][N][m n]
+    const double *xhat, *lam;  // [b][S+1][n]
+};
+
+int launch_seg_backward(const SegArgs &a, hipStream_t st);
+int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
+int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st);
+int launch_fold_shards(const double *elems, int R, int r, int n, double *out_pre, double *out_suf, int *has_suf,
+                       int *flag, hipStream_t st);
+int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
+                               double *ws, hipStream_t st);
+
+}  // namespace pdplqr

@@ -1,4 +1,8 @@
 // solvers.hip -- dispatch of the protocol calls to the three solver kinds.
+#include <algorithm>
+#include <vector>
+
+#include "parallel.hpp"
 #include "solvers.hpp"
 
 namespace pdplqr {
@@ -6,6 +10,51 @@ namespace pdplqr {
 static int unsupported(const char *what) {
     set_error(std::string(what) + ": not implemented in this build");
     return PDPLQR_ERR_UNSUPPORTED;
+}
+
+// ---------------------------------------------------------------------------
+// PARALLEL solver state (LQRParallelSolver, lqr_solver_parallel.hpp:19-238)
+// ---------------------------------------------------------------------------
+struct ParallelState {
+    std::vector<int32_t> ref_start, ref_len;  // the reference's segmentation (:64-88)
+    std::vector<int32_t> seg_start_h, seg_len_h;  // device segments (each reference segment refined)
+    int S = 0;
+    int32_t *seg_start = nullptr, *seg_len = nullptr, *seg_status = nullptr;
+    double *G = nullptr, *elem = nullptr, *bufA = nullptr, *bufB = nullptr, *xhat = nullptr, *lam = nullptr;
+    const double *pre_final = nullptr, *suf_final = nullptr;
+    int *flag = nullptr;
+    // horizon shards
+    double *left = nullptr, *right = nullptr, *gathered = nullptr;
+    int *has_suf = nullptr;
+};
+
+template <typename X>
+static int palloc(pdplqr_handle h, X **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, count * sizeof(X));
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc: ") + hipGetErrorString(e));
+        return PDPLQR_ERR_ALLOC;
+    }
+    h->allocs.push_back(q);
+    *p = reinterpret_cast<X *>(q);
+    return PDPLQR_OK;
+}
+
+// Reference segmentation (lqr_solver_parallel.hpp:70-81): Nseg_i = int(N/(scale+ns-1))
+// for i < ns-1, scale = 1.55 under load balancing; the last takes the remainder.
+static bool ref_segmentation(int N, int ns, bool lb, std::vector<int32_t> &st, std::vector<int32_t> &len) {
+    const double alpha = 1.55, scale = lb ? alpha : 1.0;
+    st.assign(ns, 0);
+    len.assign(ns, 0);
+    for (int i = 0; i < ns; ++i) {
+        st[i] = (i == 0) ? 0 : st[i - 1] + len[i - 1];
+        len[i] = (i < ns - 1) ? (int)((double)N / (scale + ns - 1)) : N - st[i];
+        if (len[i] < 1) return false;
+    }
+    return true;
 }
 
 static RiccatiArgs riccati_args(pdplqr_handle h) {
@@ -24,15 +73,154 @@ static RiccatiArgs riccati_args(pdplqr_handle h) {
     return a;
 }
 
-int solver_init(pdplqr_handle h) {
-    if (h->cfg.solver == PDPLQR_SOLVER_SERIAL) {
-        if (h->sh.s > 32) return unsupported("SERIAL solver with n + m > 32");
-        return PDPLQR_OK;
+static int parallel_init(pdplqr_handle h) {
+    const Shape &sh = h->sh;
+    if (sh.s > 32) return unsupported("PARALLEL solver with n + m > 32");
+    ParallelState *ps = new ParallelState();
+    h->par = ps;
+    const int ns = h->cfg.num_segments;
+    if (h->cfg.condensed_type == PDPLQR_CONDENSED_CHOLESKY && ns < 2) {
+        // condensed_system.hpp:230-236 reads workspace_[1] out of bounds for ns = 1
+        set_error("CHOLESKY condensed system needs num_segments >= 2 (the reference reads out of bounds)");
+        return PDPLQR_ERR_INVALID;
     }
-    return unsupported(h->cfg.solver == PDPLQR_SOLVER_PARALLEL ? "PARALLEL solver" : "KKT solver");
+    if (!ref_segmentation(sh.N, ns, h->cfg.load_balancing != 0, ps->ref_start, ps->ref_len)) {
+        set_error("segmentation yields an empty segment (N < num_segments + 0.55, lqr_solver_parallel.hpp:77-78)");
+        return PDPLQR_ERR_INVALID;
+    }
+    // device refinement: split every reference segment into pieces of <= Lsub
+    // stages so that the GPU sees enough independent segment waves.
+    int Lsub = h->cfg.segment_len;
+    if (Lsub <= 0) {
+        const long long work = (long long)sh.N * sh.batch;
+        Lsub = (int)std::max<long long>(8, (work + 2047) / 2048);
+    }
+    for (int i = 0; i < ns; ++i) {
+        const int pieces = (ps->ref_len[i] + Lsub - 1) / Lsub;
+        const int base = ps->ref_len[i] / pieces, extra = ps->ref_len[i] % pieces;
+        int st = ps->ref_start[i];
+        for (int q = 0; q < pieces; ++q) {
+            const int len = base + (q < extra ? 1 : 0);
+            ps->seg_start_h.push_back(st);
+            ps->seg_len_h.push_back(len);
+            st += len;
+        }
+    }
+    ps->S = (int)ps->seg_start_h.size();
+    const long long B = sh.batch, S = ps->S, es = 3LL * sh.n * sh.n + 2LL * sh.n;
+    int rc;
+    if ((rc = palloc(h, &ps->seg_start, S)) || (rc = palloc(h, &ps->seg_len, S)) ||
+        (rc = palloc(h, &ps->seg_status, B * S)) || (rc = palloc(h, &ps->G, B * sh.N * sh.m * sh.n)) ||
+        (rc = palloc(h, &ps->elem, B * S * es)) || (rc = palloc(h, &ps->bufA, B * S * es)) ||
+        (rc = palloc(h, &ps->bufB, B * S * es)) || (rc = palloc(h, &ps->xhat, B * (S + 1) * sh.n)) ||
+        (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, 1)) ||
+        (rc = palloc(h, &ps->left, B * es)) || (rc = palloc(h, &ps->right, B * es)) ||
+        (rc = palloc(h, &ps->has_suf, 1)))
+        return rc;
+    PDPLQR_HIP_TRY(hipMemcpy(ps->seg_start, ps->seg_start_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ps->seg_len, ps->seg_len_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemset(ps->flag, 0, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemset(ps->seg_status, 0, B * S * sizeof(int32_t)));
+    return PDPLQR_OK;
 }
 
-void solver_release(pdplqr_handle) {}
+// segment backward + prefix/suffix scans; `last_is_terminal` = 0 for a
+// non-final horizon shard.
+static int parallel_backward(pdplqr_handle h, int last_is_terminal) {
+    ParallelState *ps = h->par;
+    const Shape &sh = h->sh;
+    SegArgs a;
+    a.sh = sh;
+    a.S = ps->S;
+    a.seg_start = ps->seg_start;
+    a.seg_len = ps->seg_len;
+    a.last_is_terminal = last_is_terminal;
+    a.E = h->E;
+    a.c = h->c;
+    a.Hw = h->Hw;
+    a.hw = h->hw;
+    a.FR = h->KD;
+    a.G = ps->G;
+    a.Lc = h->Lc;
+    a.lpc = h->lpc;
+    a.elem = ps->elem;
+    a.seg_status = ps->seg_status;
+    PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, sizeof(int), h->stream));
+    int rc = launch_seg_backward(a, h->stream);
+    if (rc) return rc;
+    const double *pin = ps->elem, *sin = ps->elem;
+    double *preo[2] = {ps->bufA, ps->bufB};
+    if (!h->suf_bufs[0]) {  // suffix ping-pong buffers, allocated on first use
+        const long long es = 3LL * sh.n * sh.n + 2LL * sh.n;
+        if ((rc = palloc(h, &h->suf_bufs[0], (long long)sh.batch * ps->S * es)) ||
+            (rc = palloc(h, &h->suf_bufs[1], (long long)sh.batch * ps->S * es)))
+            return rc;
+    }
+    int round = 0;
+    for (int d = 1; d < ps->S; d <<= 1, ++round) {
+        ScanArgs s;
+        s.n = sh.n;
+        s.S = ps->S;
+        s.dist = d;
+        s.pre_in = pin;
+        s.suf_in = sin;
+        s.pre_out = preo[round & 1];
+        s.suf_out = h->suf_bufs[round & 1];
+        s.flag = ps->flag;
+        if ((rc = launch_seg_scan(s, sh.batch, h->stream))) return rc;
+        pin = s.pre_out;
+        sin = s.suf_out;
+    }
+    ps->pre_final = pin;
+    ps->suf_final = sin;
+    return PDPLQR_OK;
+}
+
+static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const double *left, const double *right,
+                            int last_is_terminal) {
+    ParallelState *ps = h->par;
+    const Shape &sh = h->sh;
+    BoundaryArgs ba;
+    ba.n = sh.n;
+    ba.S = ps->S;
+    ba.pre = ps->pre_final;
+    ba.suf = ps->suf_final;
+    ba.left = left;
+    ba.right = right;
+    ba.x0 = x0;
+    ba.xhat = ps->xhat;
+    ba.lam = ps->lam;
+    ba.flag = ps->flag;
+    int rc = launch_seg_xhat(ba, sh.batch, h->stream);
+    if (rc) return rc;
+    SegFwd sf;
+    sf.S = ps->S;
+    sf.seg_start = ps->seg_start;
+    sf.seg_len = ps->seg_len;
+    sf.last_is_terminal = last_is_terminal;
+    sf.G = ps->G;
+    sf.xhat = ps->xhat;
+    sf.lam = ps->lam;
+    return launch_riccati_forward_seg(sh, h->E, h->c, h->KD, sf, ws, h->stream);
+}
+
+// ---------------------------------------------------------------------------
+int solver_init(pdplqr_handle h) {
+    switch (h->cfg.solver) {
+        case PDPLQR_SOLVER_SERIAL:
+            if (h->sh.s > 32) return unsupported("SERIAL solver with n + m > 32");
+            return PDPLQR_OK;
+        case PDPLQR_SOLVER_PARALLEL:
+            return parallel_init(h);
+        default:
+            return unsupported("KKT solver");
+    }
+}
+
+void solver_release(pdplqr_handle h) {
+    delete h->par;
+    h->par = nullptr;
+}
 
 int solver_on_model(pdplqr_handle) { return PDPLQR_OK; }
 
@@ -46,10 +234,12 @@ int solver_backward(pdplqr_handle h, const double *rho) {
     int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                             h->max_nc, h->stream);
     if (rc) return rc;
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1);
     return launch_riccati_backward(riccati_args(h), h->stream);
 }
 
 int solver_backward_nofact(pdplqr_handle h, const double *rho) {
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return unsupported("PARALLEL backward_without_factorization");
     int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 0,
                             h->max_nc, h->stream);
     if (rc) return rc;
@@ -57,10 +247,32 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho) {
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
     return launch_riccati_forward(h->sh, h->E, h->c, h->KD, x0, ws, h->stream);
 }
 
 int solver_clear(pdplqr_handle) { return PDPLQR_OK; }
+
+int solver_status(pdplqr_handle h, int32_t *flags) {
+    const Shape &sh = h->sh;
+    if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL) {
+        PDPLQR_HIP_TRY(hipMemcpy(flags, h->status, (size_t)sh.batch * sizeof(int32_t), hipMemcpyDeviceToHost));
+        return PDPLQR_OK;
+    }
+    ParallelState *ps = h->par;
+    std::vector<int32_t> st((size_t)sh.batch * ps->S);
+    int flag = 0;
+    PDPLQR_HIP_TRY(hipMemcpy(st.data(), ps->seg_status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(&flag, ps->flag, sizeof(int), hipMemcpyDeviceToHost));
+    for (int b = 0; b < sh.batch; ++b) {
+        int v = 0;
+        for (int i = 0; i < ps->S; ++i) v = std::max(v, (int)st[(size_t)b * ps->S + i]);
+        // a failed condensed (segment) combine is reported as N + 2, the
+        // analogue of the condensed backward returning false (condensed_system.hpp:217-226)
+        flags[b] = v ? v : (flag ? sh.N + 2 : 0);
+    }
+    return PDPLQR_OK;
+}
 
 }  // namespace pdplqr
 
@@ -68,9 +280,17 @@ using namespace pdplqr;
 
 extern "C" {
 
-int pdplqr_get_segments(pdplqr_handle h, int32_t *, int32_t *) {
-    if (!h) return PDPLQR_ERR_INVALID;
-    return unsupported("get_segments");
+int pdplqr_get_segments(pdplqr_handle h, int32_t *idx_start, int32_t *Nseg) {
+    if (!h || !idx_start || !Nseg) return PDPLQR_ERR_INVALID;
+    if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL || !h->par) {
+        set_error("get_segments needs a PARALLEL handle");
+        return PDPLQR_ERR_INVALID;
+    }
+    for (size_t i = 0; i < h->par->ref_start.size(); ++i) {
+        idx_start[i] = h->par->ref_start[i];
+        Nseg[i] = h->par->ref_len[i];
+    }
+    return PDPLQR_OK;
 }
 
 int pdplqr_shard_element_size(pdplqr_handle h) {

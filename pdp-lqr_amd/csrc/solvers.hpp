@@ -12,4 +12,5 @@ int solver_backward(pdplqr_handle h, const double *rho);
 int solver_backward_nofact(pdplqr_handle h, const double *rho);
 int solver_forward(pdplqr_handle h, const double *x0, double *ws);
 int solver_clear(pdplqr_handle h);
+int solver_status(pdplqr_handle h, int32_t *flags);  // per-problem status (host)
 }  // namespace pdplqr

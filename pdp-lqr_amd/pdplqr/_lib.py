@@ -45,6 +45,7 @@ class Config(C.Structure):
         ("solver", C.c_int32), ("num_segments", C.c_int32), ("load_balancing", C.c_int32),
         ("condensed_type", C.c_int32), ("device", C.c_int32), ("keep_factors", C.c_int32),
         ("ncs", C.POINTER(C.c_int32)), ("rho_dyn", C.c_double), ("kkt_sigma", C.c_double),
+        ("segment_len", C.c_int32),
     ]
 
 

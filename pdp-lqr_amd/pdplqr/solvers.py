@@ -70,7 +70,7 @@ class _Handle:
 
     def __init__(self, nx, nu, N, batch=1, solver=_lib.PDPLQR_SOLVER_SERIAL, num_segments=1, load_balancing=True,
                  condensed_type=_lib.PDPLQR_CONDENSED_CHOLESKY, device=0, keep_factors=True, ncs=None,
-                 rho_dyn=1e-6, kkt_sigma=1e-6):
+                 rho_dyn=1e-6, kkt_sigma=1e-6, segment_len=0):
         L = lib()
         cfg = Config()
         L.pdplqr_config_init(C.byref(cfg))
@@ -83,6 +83,7 @@ class _Handle:
         cfg.keep_factors = int(bool(keep_factors))
         cfg.rho_dyn = float(rho_dyn)
         cfg.kkt_sigma = float(kkt_sigma)
+        cfg.segment_len = int(segment_len)
         self._ncs = None
         if ncs is not None:
             self._ncs = np.ascontiguousarray(np.asarray(ncs, dtype=np.int32))
@@ -237,10 +238,11 @@ class LQRParallelSolver(_ModelSolver):
     _solver_kind = _lib.PDPLQR_SOLVER_PARALLEL
 
     def __init__(self, model: LQRModel, num_segments: int, load_balancing: bool = True,
-                 solver_type: CondensedSystemSolverType = CondensedSystemSolverType.CHOLESKY, device: int = 0):
+                 solver_type: CondensedSystemSolverType = CondensedSystemSolverType.CHOLESKY, device: int = 0,
+                 segment_len: int = 0):
         self.num_segments = int(num_segments)
         self._init_handle(model, device=device, keep_factors=True, num_segments=num_segments,
-                          load_balancing=load_balancing, condensed_type=int(solver_type))
+                          load_balancing=load_balancing, condensed_type=int(solver_type), segment_len=segment_len)
 
     def backward_without_factorization(self, rho_vecs):
         self._hd.backward_without_factorization(self._y(rho_vecs))
@@ -270,13 +272,13 @@ class BatchedLQRSolver:
 
     def __init__(self, n: int, m: int, N: int, batch: int, solver: str = "serial", num_segments: int = 1,
                  load_balancing: bool = True, condensed: str = "CHOLESKY", keep_factors: bool = False,
-                 ncs=None, device: int = 0):
+                 ncs=None, device: int = 0, segment_len: int = 0):
         kind = {"serial": _lib.PDPLQR_SOLVER_SERIAL, "parallel": _lib.PDPLQR_SOLVER_PARALLEL,
                 "kkt": _lib.PDPLQR_SOLVER_KKT}[solver]
         self.n, self.m, self.N, self.batch = n, m, N, batch
         self._hd = _Handle(n, m, N, batch, kind, num_segments=num_segments, load_balancing=load_balancing,
                            condensed_type=int(CondensedSystemSolverType[condensed]), device=device,
-                           keep_factors=keep_factors, ncs=ncs)
+                           keep_factors=keep_factors, ncs=ncs, segment_len=segment_len)
 
     @property
     def handle(self) -> _Handle:

@@ -1,0 +1,121 @@
+"""GPU parity of LQRParallelSolver (segment Riccati + associative segment
+combine + segment rollout) against the CPU oracle's restatement of the
+reference parallel solver (lqr_solver_parallel.hpp) and the golden fixtures.
+
+Tolerance: 1e-9 relative on w = [u; x] (north_star bound 1e-6 on u*).  The
+device refines every reference segment into sub-segments (segment_len);
+results must not depend on that refinement beyond rounding.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, rel_err, u_parts
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0, "no HIP device visible"
+
+
+def _lists(pm, d):
+    from pdplqr.model import unpack_model, unpack_ws
+
+    model = unpack_model(pm)
+    N = pm.N
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    sl = lambda v: [v[off[k]:off[k + 1]] for k in range(N + 1)]
+    return model, unpack_ws(d["ws"], pm.n, pm.m, N), sl(d["ys"]), sl(d["zs"]), sl(d["rho"]), sl(d["inv_rho"])
+
+
+def _oracle_par(pm, d, ns, condensed):
+    from oracle.oracle import OracleParallel
+
+    o = OracleParallel(pm, ns, True, condensed)
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    return o.forward(d["x0"])
+
+
+@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("ns,condensed,seglen", [(4, "CHOLESKY", 0), (2, "LU", 0), (8, "CHOLESKY", 3), (4, "LU", 1)])
+def test_parallel_matches_oracle(name, ns, condensed, seglen):
+    from oracle.oracle import segmentation
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+
+    pm, d = load_golden(name)
+    if not segmentation(pm.N, ns, True)[0]:
+        pytest.skip("empty segment")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRParallelSolver(model, ns, True, CondensedSystemSolverType[condensed], segment_len=seglen)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    w = np.concatenate(out)
+    ref = _oracle_par(pm, d, ns, condensed)
+    assert rel_err(w, ref) < TOL
+    assert rel_err(w, d["w_riccati"]) < TOL
+    n, m, N = pm.n, pm.m, pm.N
+    assert rel_err(u_parts(w, n, m, N), u_parts(d["w_riccati"], n, m, N)) < 1e-6
+    assert sol.status() == 0
+    st, ln = sol.segments()
+    ost, oln = segmentation(pm.N, ns, True)[1:]
+    assert list(st) == list(ost) and list(ln) == list(oln)
+
+
+def test_quadrotor_example_parallel_kat():
+    """lqr_example.cpp:212-221: 4 segments, load balancing, CHOLESKY."""
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+    from pdplqr.model import initialize_vectors
+    from pdplqr.problems import quadrotor_model
+
+    model, x0 = quadrotor_model(100)
+    ws, ys, zs, rho, irho = initialize_vectors(model, 0.01)
+    sol = LQRParallelSolver(model, 4, True, CondensedSystemSolverType.CHOLESKY)
+    sol.update_problem_data(ws, ys, zs, irho, 1e-6)
+    sol.backward(rho)
+    sol.forward(x0, ws)
+    assert np.allclose(ws[0][:4], [-2.8980566697, 2.8980566697, -2.8980566697, 2.8980566697], atol=5e-10)
+    assert abs(ws[100][2] - 0.9999999000) < 5e-10
+
+
+def test_cholesky_single_segment_rejected():
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver, PdplqrError
+    from pdplqr.problems import random_model
+
+    model, _ = random_model(4, 2, 10, seed=1)
+    with pytest.raises(PdplqrError):
+        LQRParallelSolver(model, 1, True, CondensedSystemSolverType.CHOLESKY)
+    LQRParallelSolver(model, 1, True, CondensedSystemSolverType.LU)  # LU with one segment is valid
+
+
+@pytest.mark.parametrize("n,m,N,batch,seglen", [(12, 4, 1024, 1, 0), (12, 4, 96, 6, 5), (24, 8, 64, 2, 8),
+                                                (4, 2, 33, 3, 2)])
+def test_batched_parallel_matches_oracle(n, m, N, batch, seglen):
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, n * 7 + m)
+    s = n + m
+    ws0 = np.zeros((batch, N * s + n))
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=True,
+                          segment_len=seglen)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws0)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
