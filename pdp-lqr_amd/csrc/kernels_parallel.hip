@@ -432,9 +432,10 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     elem_copy(ea, in + (long long)ia * es, n, lane);
     elem_copy(eb, in + (long long)ib * es, n, lane);
     wave_sync();
-    // a suffix ending at the real terminal has F = C = f = 0; a zero-P right
-    // operand (never produced here) would need the identity rule instead.
-    const bool ok = elem_combine(eo, ea, eb, w, n, true, dir == 1, lane);
+    // Both directions need full elements: the next round's combine reads the
+    // right operand's P, p (Z = (I + C_a P_b)^{-1}).  A suffix ending at the
+    // real terminal has F = C = f = 0.
+    const bool ok = elem_combine(eo, ea, eb, w, n, true, true, lane);
     if (!ok && lane == 0) atomicOr(A.flag, 1);
     elem_copy(out + (long long)i * es, eo, n, lane);
 }

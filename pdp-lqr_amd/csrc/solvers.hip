@@ -309,3 +309,31 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *, const double *, int32_
 }
 
 }  // extern "C"
+
+// Internal diagnostics (not part of include/pdplqr.h): copy a PARALLEL
+// handle's segment buffers to host.  which: 0 elem, 1 prefix scan, 2 suffix
+// scan, 3 xhat [b][S+1][n], 4 lam, 5 device segment starts/lengths (int32 pairs).
+extern "C" int pdplqr_debug_parallel(pdplqr_handle h, int which, void *out, long long bytes) {
+    if (!h || !h->par) return PDPLQR_ERR_INVALID;
+    ParallelState *ps = h->par;
+    PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+    const void *src = nullptr;
+    switch (which) {
+        case 0: src = ps->elem; break;
+        case 1: src = ps->pre_final; break;
+        case 2: src = ps->suf_final; break;
+        case 3: src = ps->xhat; break;
+        case 4: src = ps->lam; break;
+        case 5: {
+            int32_t *o = reinterpret_cast<int32_t *>(out);
+            for (int i = 0; i < ps->S && (long long)(2 * i + 1) * 4 < bytes; ++i) {
+                o[2 * i] = ps->seg_start_h[i];
+                o[2 * i + 1] = ps->seg_len_h[i];
+            }
+            return ps->S;
+        }
+        default: return PDPLQR_ERR_INVALID;
+    }
+    PDPLQR_HIP_TRY(hipMemcpy(out, src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return ps->S;
+}
