@@ -93,4 +93,5 @@ struct pdplqr_handle_s {
     std::vector<void *> allocs;
     pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)
     double *suf_bufs[2] = {nullptr, nullptr};
+    int shard_last = 1;  // last shard_backward's is_last_shard
 };

@@ -571,11 +571,16 @@ int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st) {
 // Combine a short list of elements on one wave (the per-rank fold of the
 // horizon-sharded solve): out_pre = e_0 (x) ... (x) e_{r-1} (identity if r = 0),
 // out_suf = e_{r+1} (x) ... (x) e_{R-1} (P = p = 0 marker when r = R-1).
-__global__ __launch_bounds__(64) void k_fold_shards(const double *elems, int R, int r, int n, double *out_pre,
-                                                    double *out_suf, int *has_suf, int *flag) {
+__global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int R, int r, int n, int batch,
+                                                    double *out_pre_all, double *out_suf_all, int *has_suf, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     const int lane = threadIdx.x;
     const int es = 3 * n * n + 2 * n;
+    const long long b = blockIdx.x;
+    // element j of problem b: elems_all[(j * batch + b) * es]; outputs [b][es]
+    const double *elems = elems_all + b * es;
+    const long long stride = (long long)batch * es;
+    double *out_pre = out_pre_all + b * es, *out_suf = out_suf_all + b * es;
     double *acc = dyn, *nx = dyn + es, *o = dyn + 2 * es;
     CombineWs w = combine_ws(dyn + 3 * es, n);
     // prefix
@@ -589,7 +594,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems, int R, 
         for (int q = lane; q < n; q += 64) { e.f[q] = 0.0; e.p[q] = 0.0; }
         wave_sync();
         for (int j = 0; j < r; ++j) {
-            elem_copy(nx, elems + (long long)j * es, n, lane);
+            elem_copy(nx, elems + (long long)j * stride, n, lane);
             wave_sync();
             if (j == 0) {
                 elem_copy(acc, nx, n, lane);
@@ -603,26 +608,26 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems, int R, 
     }
     // suffix (right fold from the end: e_{R-1}, then e_j (x) acc)
     if (r + 1 >= R) {
-        if (lane == 0) *has_suf = 0;
+        if (lane == 0 && b == 0) *has_suf = 0;
         return;
     }
-    elem_copy(acc, elems + (long long)(R - 1) * es, n, lane);
+    elem_copy(acc, elems + (long long)(R - 1) * stride, n, lane);
     wave_sync();
     for (int j = R - 2; j > r; --j) {
-        elem_copy(nx, elems + (long long)j * es, n, lane);
+        elem_copy(nx, elems + (long long)j * stride, n, lane);
         wave_sync();
         if (!elem_combine(o, nx, acc, w, n, true, true, lane) && lane == 0) atomicOr(flag, 8);
         elem_copy(acc, o, n, lane);
         wave_sync();
     }
     elem_copy(out_suf, acc, n, lane);
-    if (lane == 0) *has_suf = 1;
+    if (lane == 0 && b == 0) *has_suf = 1;
 }
 
-int launch_fold_shards(const double *elems, int R, int r, int n, double *out_pre, double *out_suf, int *has_suf,
-                       int *flag, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_shards, dim3(1), dim3(64), combine_smem(n, 3), st, elems, R, r, n, out_pre, out_suf,
-                       has_suf, flag);
+int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
+                       int *has_suf, int *flag, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_shards, dim3(batch), dim3(64), combine_smem(n, 3), st, elems, R, r, n, batch, out_pre,
+                       out_suf, has_suf, flag);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

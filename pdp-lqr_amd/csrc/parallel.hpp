@@ -46,8 +46,8 @@ struct SegFwd {
 int launch_seg_backward(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st);
-int launch_fold_shards(const double *elems, int R, int r, int n, double *out_pre, double *out_suf, int *has_suf,
-                       int *flag, hipStream_t st);
+int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
+                       int *has_suf, int *flag, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st);
 

@@ -25,6 +25,7 @@ struct ParallelState {
     int *flag = nullptr;
     // horizon shards
     double *left = nullptr, *right = nullptr, *gathered = nullptr;
+    int gathered_cap = 0;
     int *has_suf = nullptr;
 };
 
@@ -298,14 +299,97 @@ int pdplqr_shard_element_size(pdplqr_handle h) {
     return 3 * h->sh.n * h->sh.n + 2 * h->sh.n;
 }
 
-int pdplqr_shard_backward(pdplqr_handle h, const double *, int, double *, int) {
-    if (!h) return PDPLQR_ERR_INVALID;
-    return unsupported("shard_backward");
+// Horizon shards: this handle holds one slice of the
+// horizon.  Backward = segment recursion + local scans; the slice element is the
+// suffix-scan entry 0 (e_0 (x) ... (x) e_{S-1}).  Elements: [batch][3n^2+2n].
+int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem) {
+    if (!h || !elem_out) return PDPLQR_ERR_INVALID;
+    if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL || !h->par) {
+        set_error("shard_backward needs a PARALLEL handle");
+        return PDPLQR_ERR_INVALID;
+    }
+    if (!h->updated) {
+        set_error("shard_backward before update_problem_data");
+        return PDPLQR_ERR_STATE;
+    }
+    PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
+    const Shape &sh = h->sh;
+    const double *drho = h->st_rho;
+    if (sh.ny > 0) {
+        if (!rho) return PDPLQR_ERR_INVALID;
+        if (mem == PDPLQR_MEM_DEVICE) drho = rho;
+        else PDPLQR_HIP_TRY(hipMemcpyAsync(h->st_rho, rho, (size_t)sh.batch * sh.ny * sizeof(double),
+                                           hipMemcpyHostToDevice, h->stream));
+    }
+    int rc = launch_penalty(sh, h->D, drho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
+                            h->max_nc, h->stream);
+    if (rc) return rc;
+    if ((rc = parallel_backward(h, is_last_shard ? 1 : 0))) return rc;
+    h->shard_last = is_last_shard ? 1 : 0;
+    ParallelState *ps = h->par;
+    const long long es = 3LL * sh.n * sh.n + 2LL * sh.n;
+    // suffix entry 0 of every problem: suf_final[b][0]
+    for (int b = 0; b < sh.batch; ++b) {
+        const double *src = ps->suf_final + (long long)b * ps->S * es;
+        PDPLQR_HIP_TRY(hipMemcpyAsync(elem_out + b * es, src, es * sizeof(double),
+                                      mem == PDPLQR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                      h->stream));
+    }
+    if (mem != PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+    h->factored = true;
+    return PDPLQR_OK;
 }
 
-int pdplqr_shard_forward(pdplqr_handle h, const double *, const double *, int32_t, int32_t, double *, int) {
-    if (!h) return PDPLQR_ERR_INVALID;
-    return unsupported("shard_forward");
+// elems_all: [num_shards][batch][3n^2+2n] (rank-major, the all-gather output).
+int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_all, int32_t num_shards,
+                         int32_t shard_id, double *ws, int mem) {
+    if (!h || !x0 || !elems_all || !ws) return PDPLQR_ERR_INVALID;
+    if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL || !h->par) {
+        set_error("shard_forward needs a PARALLEL handle");
+        return PDPLQR_ERR_INVALID;
+    }
+    if (num_shards < 1 || shard_id < 0 || shard_id >= num_shards) {
+        set_error("shard_forward: bad shard index");
+        return PDPLQR_ERR_INVALID;
+    }
+    if (!h->factored) {
+        set_error("shard_forward before shard_backward");
+        return PDPLQR_ERR_STATE;
+    }
+    PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
+    const Shape &sh = h->sh;
+    ParallelState *ps = h->par;
+    const long long es = 3LL * sh.n * sh.n + 2LL * sh.n;
+    const double *dx0 = x0, *delems = elems_all;
+    if (mem != PDPLQR_MEM_DEVICE) {
+        if (!ps->gathered) {
+            int rc = palloc(h, &ps->gathered, (long long)num_shards * sh.batch * es);
+            if (rc) return rc;
+            ps->gathered_cap = num_shards;
+        } else if (ps->gathered_cap < num_shards) {
+            set_error("shard_forward: number of shards grew between calls");
+            return PDPLQR_ERR_INVALID;
+        }
+        PDPLQR_HIP_TRY(hipMemcpyAsync(ps->gathered, elems_all, (size_t)num_shards * sh.batch * es * sizeof(double),
+                                      hipMemcpyHostToDevice, h->stream));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(h->st_x0, x0, (size_t)sh.batch * sh.n * sizeof(double), hipMemcpyHostToDevice,
+                                      h->stream));
+        delems = ps->gathered;
+        dx0 = h->st_x0;
+    }
+    int rc = launch_fold_shards(delems, num_shards, shard_id, sh.n, sh.batch, ps->left, ps->right, ps->has_suf,
+                                ps->flag, h->stream);
+    if (rc) return rc;
+    const double *left = shard_id > 0 ? ps->left : nullptr;
+    const double *right = shard_id + 1 < num_shards ? ps->right : nullptr;
+    double *dws = mem == PDPLQR_MEM_DEVICE ? ws : h->st_ws;
+    if ((rc = parallel_forward(h, dx0, dws, left, right, h->shard_last))) return rc;
+    if (mem != PDPLQR_MEM_DEVICE) {
+        PDPLQR_HIP_TRY(hipMemcpyAsync(ws, dws, (size_t)sh.batch * sh.perh * sizeof(double), hipMemcpyDeviceToHost,
+                                      h->stream));
+        PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return PDPLQR_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,148 @@
+"""Horizon sharding across GPUs (one process per GPU), DESIGN.md section 6.
+
+Rank r owns stages [N0_r, N1_r) of one long horizon (config C4: N = 65536,
+nx = 24, nu = 8 over 8 x MI355X).  Each rank
+  1. solves its slice as a PARALLEL handle (segments + local scans) and exports
+     its slice element e_r = (F, C, f, P, p)           -> pdplqr_shard_backward
+  2. all-gathers the R elements (3n^2 + 2n doubles each) over RCCL/xGMI
+  3. folds the global prefix (ranks < r) and suffix (ranks > r), computes the
+     boundary states of its segments and rolls out      -> pdplqr_shard_forward
+This is the multi-GPU form of the reference's condensed segment system
+(condensed_system.hpp:8-299), whose serial fold over OpenMP segments is
+replaced by the associative combine.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .solvers import _Handle, _mem_of, _ptr
+
+
+def split_horizon(N: int, R: int) -> List[Tuple[int, int]]:
+    """Contiguous, balanced slices [N0, N1) of the horizon, one per rank."""
+    base, extra = divmod(N, R)
+    out, st = [], 0
+    for r in range(R):
+        ln = base + (1 if r < extra else 0)
+        out.append((st, st + ln))
+        st += ln
+    return out
+
+
+def slice_arrays(E, c, H, h, n, m, N, N0, N1, last):
+    """Local boundary arrays of the slice [N0, N1) from batch-major full arrays.
+    Non-final slices get a zero terminal block (unused: their last segment uses
+    the dummy zero terminal, lqr_kernel_parallel.hpp:60-66)."""
+    s = n + m
+    xp = _xp(E)
+    B = E.shape[0]
+    El = E[:, N0 * n * s:N1 * n * s]
+    cl = c[:, N0 * n:N1 * n]
+    Hs = H[:, N0 * s * s:N1 * s * s]
+    hs = h[:, N0 * s:N1 * s]
+    if last:
+        HN, hN = H[:, N * s * s:], h[:, N * s:]
+    else:
+        HN = xp.zeros((B, n * n), dtype=H.dtype, **_dev(H))
+        hN = xp.zeros((B, n), dtype=h.dtype, **_dev(h))
+    cat = xp.concatenate if xp is np else xp.cat
+    return (_contig(El), _contig(cl), _contig(cat([Hs, HN], 1)), _contig(cat([hs, hN], 1)))
+
+
+def _xp(a):
+    if isinstance(a, np.ndarray):
+        return np
+    import torch
+
+    return torch
+
+
+def _dev(a):
+    return {} if isinstance(a, np.ndarray) else {"device": a.device}
+
+
+def _contig(a):
+    return np.ascontiguousarray(a) if isinstance(a, np.ndarray) else a.contiguous()
+
+
+class HorizonShard:
+    """One rank's slice of a horizon-sharded solve (batch problems share the split)."""
+
+    def __init__(self, n: int, m: int, N_local: int, batch: int = 1, device: int = 0, segment_len: int = 0,
+                 ncs=None):
+        self.n, self.m, self.N, self.batch = n, m, N_local, batch
+        self.es = 3 * n * n + 2 * n
+        self._hd = _Handle(n, m, N_local, batch, _lib.PDPLQR_SOLVER_PARALLEL, num_segments=1,
+                           condensed_type=_lib.PDPLQR_CONDENSED_LU, device=device, keep_factors=True, ncs=ncs,
+                           segment_len=segment_len)
+
+    @property
+    def handle(self):
+        return self._hd
+
+    def set_model(self, E, c, H, h, D=None):
+        self._hd.set_model(E, c, H, h, D)
+
+    def update_problem_data(self, ws, ys=None, zs=None, inv_rho=None, sigma: float = 0.0):
+        self._hd.update_problem_data(ws, ys, zs, inv_rho, sigma)
+
+    def backward(self, elem_out, is_last: bool, rho=None):
+        """Slice backward; writes the slice element(s) [batch, 3n^2+2n] into elem_out."""
+        pr, pe = _ptr(rho, "rho"), _ptr(elem_out, "elem")
+        mem = pe[1]
+        check(lib().pdplqr_shard_backward(self._hd.h, pr[0], int(bool(is_last)), pe[0], mem))
+        return elem_out
+
+    def forward(self, x0, elems_all, num_shards: int, shard_id: int, ws_out):
+        """elems_all: [num_shards, batch, 3n^2+2n] (rank-major all-gather output)."""
+        p0, pe, pw = _ptr(x0, "x0"), _ptr(elems_all, "elems"), _ptr(ws_out, "ws")
+        check(lib().pdplqr_shard_forward(self._hd.h, p0[0], pe[0], int(num_shards), int(shard_id), pw[0],
+                                         _mem_of(p0, pe, pw)))
+        return ws_out
+
+    def synchronize(self):
+        self._hd.synchronize()
+
+    def stream(self) -> int:
+        return self._hd.stream()
+
+    def close(self):
+        self._hd.close()
+
+
+def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
+    """backward -> all-gather of slice elements -> forward, on the current
+    torch.distributed process group.  With the nccl backend (RCCL) the
+    elements stay on the GPU; with gloo they are gathered through host memory."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    elem = torch.empty(shard.batch, shard.es, dtype=torch.float64, device=dev)
+    if on_gpu:
+        shard.backward(elem, rank == world - 1, rho)
+        # the element is produced on the handle's stream: order it before RCCL's
+        shard.synchronize()
+        gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(gathered, elem, group=group)
+        torch.cuda.current_stream().synchronize()
+    else:
+        e_np = np.zeros((shard.batch, shard.es))
+        shard.backward(e_np, rank == world - 1, None if rho is None else rho)
+        elem = torch.from_numpy(e_np)
+        parts = [torch.empty_like(elem) for _ in range(world)]
+        dist.all_gather(parts, elem, group=group)
+        gathered = torch.stack(parts).contiguous()
+        if isinstance(ws_out, np.ndarray):
+            gathered = gathered.numpy()
+        elif getattr(ws_out, "is_cuda", False):
+            gathered = gathered.to(ws_out.device)
+    return shard.forward(x0, gathered, world, rank, ws_out)

@@ -1,0 +1,131 @@
+"""GPU tests of horizon sharding (pdplqr_shard_backward / pdplqr_shard_forward):
+R virtual ranks in one process (host-side all-gather), and 2 real processes
+exchanging elements with torch.distributed (gloo) on one GPU.  Compared with
+the serial oracle on the full horizon; tolerance 1e-9 relative."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0
+
+
+def _full(n, m, N, batch, seed):
+    from pdplqr.problems import random_batch_arrays
+
+    return random_batch_arrays(n, m, N, batch, seed)
+
+
+def _oracle(n, m, N, E, c, H, h, x0):
+    from oracle.oracle import OracleSerial
+    from pdplqr.model import PackedModel
+
+    outs = []
+    for b in range(E.shape[0]):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(np.zeros(N * (n + m) + n), None, None, None, 1e-6)
+        o.backward(None)
+        outs.append(o.forward(x0[b]))
+    return np.stack(outs)
+
+
+def _run_virtual(n, m, N, batch, R, seglen, seed=3):
+    from pdplqr.horizon import HorizonShard, slice_arrays, split_horizon
+
+    E, c, H, h, x0 = _full(n, m, N, batch, seed)
+    s = n + m
+    sl = split_horizon(N, R)
+    shards, elems = [], []
+    for r, (N0, N1) in enumerate(sl):
+        last = r == R - 1
+        Nl = N1 - N0
+        sh = HorizonShard(n, m, Nl, batch, segment_len=seglen)
+        sh.set_model(*slice_arrays(E, c, H, h, n, m, N, N0, N1, last))
+        sh.update_problem_data(np.zeros((batch, Nl * s + n)), sigma=1e-6)
+        e = np.zeros((batch, 3 * n * n + 2 * n))
+        sh.backward(e, last)
+        shards.append(sh)
+        elems.append(e)
+    gathered = np.ascontiguousarray(np.stack(elems))
+    full = np.zeros((batch, N * s + n))
+    ends = []
+    for r, (N0, N1) in enumerate(sl):
+        Nl = N1 - N0
+        loc = np.zeros((batch, Nl * s + n))
+        shards[r].forward(x0, gathered, R, r, loc)
+        full[:, N0 * s:N1 * s] = loc[:, :Nl * s]
+        if r == R - 1:
+            full[:, N * s:] = loc[:, Nl * s:]
+        else:
+            ends.append((N1, loc[:, Nl * s:].copy()))
+    for N1, xe in ends:  # each slice-end state is the next slice's first state
+        assert rel_err(xe, full[:, N1 * s + m:(N1 + 1) * s]) < TOL
+    return full, _oracle(n, m, N, E, c, H, h, x0)
+
+
+@pytest.mark.parametrize("n,m,N,batch,R,seglen", [(12, 4, 256, 1, 1, 0), (12, 4, 256, 1, 2, 0),
+                                                  (12, 4, 200, 2, 3, 7), (24, 8, 96, 1, 4, 8),
+                                                  (4, 2, 50, 3, 5, 2)])
+def test_virtual_ranks_match_oracle(n, m, N, batch, R, seglen):
+    got, ref = _run_virtual(n, m, N, batch, R, seglen)
+    for b in range(batch):
+        assert rel_err(got[b], ref[b]) < TOL, b
+
+
+def _dist_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pdplqr.horizon import HorizonShard, slice_arrays, solve_distributed, split_horizon
+
+        n, m, N = 12, 4, 160
+        E, c, H, h, x0 = _full(n, m, N, 1, 11)
+        N0, N1 = split_horizon(N, world)[rank]
+        last = rank == world - 1
+        sh = HorizonShard(n, m, N1 - N0, 1, segment_len=8)
+        sh.set_model(*slice_arrays(E, c, H, h, n, m, N, N0, N1, last))
+        sh.update_problem_data(np.zeros((1, (N1 - N0) * (n + m) + n)), sigma=1e-6)
+        loc = np.zeros((1, (N1 - N0) * (n + m) + n))
+        solve_distributed(sh, x0, loc)
+        q.put((rank, N0, N1, loc))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_gloo_exchange():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 500)
+    ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, m, N = 12, 4, 160
+    s = n + m
+    E, c, H, h, x0 = _full(n, m, N, 1, 11)
+    ref = _oracle(n, m, N, E, c, H, h, x0)[0]
+    full = np.zeros(N * s + n)
+    for rank, N0, N1, loc in res:
+        full[N0 * s:N1 * s] = loc[0, :(N1 - N0) * s]
+        if N1 == N:
+            full[N * s:] = loc[0, (N1 - N0) * s:]
+    assert rel_err(full, ref) < TOL
