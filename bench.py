@@ -111,6 +111,90 @@ def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
                       f"OpenMP over problems, {el:.1f} s)"}
 
 
+def _timed(fn, steps, warmup, dev, dist):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el / steps
+
+
+def bench_single(local, dev, dist, steps=10, warmup=3):
+    """C2: one N = 1024, 12/4 problem, LQRParallelSolver path (segments + scans).
+    Latency-bound; stages/s = N / time of backward + forward (every rank runs a
+    replica)."""
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N = 12, 4, 1024
+    E, c, H, h, x0 = gen_batch_device(n, m, N, 1, seed=77, device=dev)
+    ws0 = torch.zeros(1, N * (n + m) + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    res = {}
+    for solver in ("parallel", "serial"):
+        bs = BatchedLQRSolver(n, m, N, 1, solver=solver, num_segments=8, keep_factors=(solver == "parallel"),
+                              device=local)
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+
+        def step():
+            bs.backward()
+            bs.forward(x0, out)
+
+        t = _timed(step, steps, warmup, dev, dist)
+        res[solver] = {"ms_per_solve": t * 1e3, "stages_per_s": N / t, "status_ok": bool(np.all(bs.status() == 0))}
+        bs.close()
+    return res
+
+
+def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
+    """C4: one N = Ntot, 24/8 problem, horizon-sharded over the ranks (strong
+    scaling): shard backward -> all-gather of slice elements (RCCL when nccl)
+    -> shard forward.  value = Ntot / time per solve (max over ranks)."""
+    from pdplqr.horizon import HorizonShard, solve_distributed, split_horizon
+
+    n, m = 24, 8
+    s = n + m
+    N0, N1 = split_horizon(Ntot, world)[rank]
+    Nl = N1 - N0
+    last = rank == world - 1
+    E, c, H, h, x0 = gen_batch_device(n, m, Nl, 1, seed=4242 + rank, device=dev)
+    if not last:
+        H[:, Nl * s * s:] = 0.0
+        h[:, Nl * s:] = 0.0
+    x0 = gen_batch_device(n, m, 1, 1, seed=4242, device=dev)[4]  # the same x0 on every rank
+    sh = HorizonShard(n, m, Nl, 1, device=local)
+    sh.set_model(E, c, H, h)
+    ws0 = torch.zeros(1, Nl * s + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    sh.update_problem_data(ws0, sigma=1e-6)
+    del E, H
+    if dist:
+        step = lambda: solve_distributed(sh, x0, out)
+    else:
+        elem = torch.empty(1, 1, sh.es, dtype=torch.float64, device=dev)
+
+        def step():
+            sh.backward(elem[0], True)
+            sh.forward(x0, elem, 1, 0, out)
+    t = _timed(step, steps, warmup, dev, dist)
+    ok = bool(torch.isfinite(out).all().item())
+    sh.close()
+    return {"N": Ntot, "nx": n, "nu": m, "n_gpus": world, "ms_per_solve": t * 1e3, "stages_per_s": Ntot / t,
+            "scaling": "strong", "finite": ok, "exchange": "all-gather of 3n^2+2n doubles per rank"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +207,8 @@ def main():
     ap.add_argument("--keep-factors", action="store_true", help="also cache L_k (factor-reuse path)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 secondary lines")
+    ap.add_argument("--c4-N", type=int, default=65536)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,13 +303,18 @@ def main():
         "solve_hbm_frac": bytes_stage * stages / ((ms_bwd + ms_fwd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "status_ok": bool(np.all(st == 0)),
     }
+    bs.close()
+    del E, c, h, x0, ws0, out
+    torch.cuda.empty_cache()
+    if not args.no_secondary:
+        res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
+                            "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(n, m, N, seconds=args.cpu_seconds)
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(res), flush=True)
-    bs.close()
     if dist:
         dist.destroy_process_group()
 
