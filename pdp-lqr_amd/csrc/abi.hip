@@ -143,7 +143,7 @@ int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out) {
     sh.perc = (long long)sh.N * sh.n;
     sh.perH = (long long)sh.N * sh.s * sh.s + (long long)sh.n * sh.n;
     sh.perh = (long long)sh.N * sh.s + sh.n;
-    sh.perHw = (long long)sh.N * sh.ps + sh.pn;
+    sh.perHw = ((long long)sh.N * sh.ps + sh.pn + 1) / 2 * 2;  // 16-byte aligned per problem
     sh.perKD = (long long)sh.N * (sh.s * sh.m + sh.m);  // rollout record [L(:,0:m) | lu']
 
     int rc = PDPLQR_OK;

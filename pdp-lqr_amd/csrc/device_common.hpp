@@ -112,81 +112,105 @@ __device__ __forceinline__ void load_stage(StageIn<T> &in, const double *__restr
     }
 }
 
+// Position of row/column index i in the pivot broadcast buffer: the 4T rows a
+// lane owns (16 a + 4 r + g) are contiguous, so a lane fetches them with
+// 128-bit LDS reads.
+template <int T>
+__device__ __forceinline__ constexpr int colpos(int i) {
+    return (i & 3) * (4 * T) + ((i >> 4) << 2) + ((i >> 2) & 3);
+}
+
 // Right-looking Cholesky of the symmetric padded matrix in C/D layout, pivots
 // jbeg..jend-1.  Column j is broadcast through LDS from row j (the row group
 // that owns row j holds M[j][*] = M[*][j]; M stays exactly symmetric because
 // every update is applied to both triangles with the same products).  The
 // owners write zeros for columns <= j, so every lane can update
 // M -= raw_i raw_k / M[j][j] without masking; the pivot column itself is left
-// unscaled and finalised by finalize_L (L[i][j] = M[i][j] / sqrt(M[j][j])).
-// With `aug`, the first `m` pivots also eliminate the linear column lpr (the
-// lp_k of lqr_kernel.hpp:142-146): lpr_i -= l_ij lu'_j with lu'_j = lp_j / L_jj,
-// which is exactly lu <- Luu^{-1} lu followed by p -= Lxu lu.  All lanes of the
-// wave run in lock step and LDS ops of one wave retire in order, so no barrier
-// is needed between the owners' writes and the readers.
+// unscaled and finalised by finalize_L (L[i][j] = M[i][j] / sqrt(M[j][j]),
+// the reciprocal square roots are kept in sinv).  With `aug`, the first `m`
+// pivots also eliminate the linear column lpr (the lp_k of
+// lqr_kernel.hpp:142-146): lpr_i -= l_ij lu'_j with lu'_j = lp_j / L_jj, which
+// is exactly lu <- Luu^{-1} lu followed by p -= Lxu lu.  All lanes of the
+// wave run in lock step and LDS ops of one wave retire in order, so no
+// barrier is needed between the owners' writes and the readers.
+// Returns true if every pivot was positive.
 template <int T>
-__device__ __forceinline__ int chol_tiles(d4 (&M)[T][T], double (&myinv)[T], double (&lpr)[T][4], double *cb,
-                                          double *luq, int jbeg, int jend, int m, bool aug, int g, int c) {
-    int fail = -1;
+__device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], double *cb, double *sinv, double *luq,
+                                           int jbeg, int jend, int m, bool aug, int g, int c) {
+    bool ok = true;
     const bool lane0 = (g == 0) && (c == 0);
+    const double2 *rows = reinterpret_cast<const double2 *>(cb + g * 4 * T);
+    // pivot j = 16 tr + 4 rr + gj: (tr, rr) unrolled so register indices stay
+    // compile-time, the row group gj is a runtime loop (keeps the scheduler
+    // from hoisting work across all pivots, which would exhaust registers)
 #pragma unroll
-    for (int j = 0; j < 16 * T; ++j) {
-        if (j >= jbeg && j < jend) {
-            const int tr = j >> 4, rr = (j >> 2) & 3, gj = j & 3, bj = j >> 4, cj = j & 15;
-            if (g == gj) {
+    for (int tr = 0; tr < T; ++tr)
 #pragma unroll
-                for (int b = 0; b < T; ++b) {
-                    const int jc = 16 * b + c;
-                    cb[jc] = (jc > j) ? M[tr][b][rr] : 0.0;
+        for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll 1
+            for (int gj = 0; gj < 4; ++gj) {
+                const int j = 16 * tr + 4 * rr + gj;
+                if (j < jbeg || j >= jend) continue;
+                if (g == gj) {
+#pragma unroll
+                    for (int b = 0; b < T; ++b) {
+                        const int jc = 16 * b + c;
+                        cb[colpos<T>(jc)] = (jc > j) ? M[tr][b][rr] : 0.0;
+                    }
                 }
-            }
-            wave_sync();
-            const double djj = readlane_f64(M[tr][bj][rr], (gj << 4) + cj);
-            if (!(djj > 0.0) && fail < 0) fail = j;
-            const double inv = rsqrt_f64(djj);
-            const double inv2 = inv * inv;
-            if (c == cj) myinv[bj] = inv;
-            double lc[T];
+                wave_sync();
+                const double djj = readlane_f64(M[tr][tr][rr], (gj << 4) + (j & 15));
+                ok = ok && (djj > 0.0);
+                const double inv = rsqrt_f64(djj);
+                const double inv2 = inv * inv;
+                if (lane0) sinv[j] = inv;
+                double lc[T];
 #pragma unroll
-            for (int b = 0; b < T; ++b) lc[b] = cb[16 * b + c] * inv2;
-            const bool augj = aug && j < m;
-            const double lpj = augj ? readlane_f64(lpr[tr][rr], gj << 4) : 0.0;
-            const double qj = lpj * inv2;
+                for (int b = 0; b < T; ++b) lc[b] = cb[colpos<T>(16 * b + c)] * inv2;
+                const bool augj = aug && j < m;
+                const double lpj = augj ? readlane_f64(lpr[tr][rr], gj << 4) : 0.0;
+                const double qj = lpj * inv2;
+                double li[T][4];
+#pragma unroll
+                for (int q = 0; q < 2 * T; ++q) {
+                    const double2 v = rows[q];
+                    li[q >> 1][(q & 1) * 2] = v.x;
+                    li[q >> 1][(q & 1) * 2 + 1] = v.y;
+                }
+#pragma unroll
+                for (int a = 0; a < T; ++a)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                        for (int b = 0; b < T; ++b) M[a][b][r] = __builtin_fma(-li[a][r], lc[b], M[a][b][r]);
+                        // q = lp_j / M[j][j]; lpr_i -= raw_i * q  (raw_i = 0 for i <= j)
+                        if (augj) lpr[a][r] = __builtin_fma(-li[a][r], qj, lpr[a][r]);
+                    }
+                if (augj && lane0) luq[j] = lpj * inv;
+                wave_sync();
+            }
+        }
+    return ok;
+}
+
+// L[i][jc] = M[i][jc] / sqrt(M[jc][jc]) below the diagonal, 0 above, for the
+// factored columns jbeg <= jc < jend; identity padding elsewhere is left as is.
+template <int T>
+__device__ __forceinline__ void finalize_L(d4 (&M)[T][T], const double *sinv, int jbeg, int jend, int g, int c) {
+#pragma unroll
+    for (int b = 0; b < T; ++b) {
+        const int jc = 16 * b + c;
+        if (jc >= jbeg && jc < jend) {
+            const double iv = sinv[jc];
 #pragma unroll
             for (int a = 0; a < T; ++a)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const double li = cb[16 * a + 4 * r + g];
-#pragma unroll
-                    for (int b = 0; b < T; ++b) M[a][b][r] = __builtin_fma(-li, lc[b], M[a][b][r]);
-                    // q = lp_j / M[j][j]; lpr_i -= raw_i * q  (raw_i = 0 for i <= j)
-                    if (augj) lpr[a][r] = __builtin_fma(-li, qj, lpr[a][r]);
+                    const int i = 16 * a + 4 * r + g;
+                    M[a][b][r] = (i >= jc) ? M[a][b][r] * iv : 0.0;
                 }
-            if (augj && lane0) luq[j] = lpj * inv;
-            wave_sync();
         }
     }
-    return fail;
-}
-
-// L[i][jc] = M[i][jc] / sqrt(M[jc][jc]) below the diagonal, 0 above, for the
-// factored columns jc < jend; identity padding elsewhere is left as is.
-template <int T>
-__device__ __forceinline__ void finalize_L(d4 (&M)[T][T], const double (&myinv)[T], int jbeg, int jend, int g,
-                                           int c) {
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b) {
-            const int jc = 16 * b + c;
-            if (jc >= jbeg && jc < jend) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * a + 4 * r + g;
-                    M[a][b][r] = (i >= jc) ? M[a][b][r] * myinv[b] : 0.0;
-                }
-            }
-        }
 }
 
 template <int T>
@@ -194,7 +218,8 @@ struct BwdSmem {
     static constexpr int P = 16 * T;
     static constexpr int LD = P + 1;  // odd leading dimension: conflict-free column reads
     double L[P * LD];                 // L_{k+1} then L_k (padded, column-major, lower, zero upper)
-    double col[P];                    // Cholesky column broadcast
+    alignas(16) double col[P];        // Cholesky pivot-row broadcast (colpos order)
+    double inv[P];                    // 1 / sqrt(pivot) per column
     double pbt[P];                    // Pb_tmp = Lxx_next^T c
     double pv[P];                     // p_{k+1}, then p_k
     double lp[P];                     // lp_k (column -> row redistribution)
@@ -216,9 +241,9 @@ __device__ __forceinline__ void store_L_lds(const d4 (&M)[T][T], double *L, int 
 // One backward stage k (LQRKernel::step_with_factorization, lqr_kernel.hpp:104-147)
 // on the padded tiles.  Consumes L_{k+1} (sm.L) and p_{k+1} (sm.pv); produces
 // L_k in M (finalised) and sm.L, p_k in sm.pv, lu'_k = Luu^{-1} lu in sm.luq,
-// lp_k in lpr (rows of the lane).  Returns the failing pivot or -1.
+// lp_k in lpr (rows of the lane).  Returns false on a non-positive pivot.
 template <int T>
-__device__ __forceinline__ int riccati_stage(BwdSmem<T> &sm, const StageIn<T> &cur, d4 (&M)[T][T],
+__device__ __forceinline__ bool riccati_stage(BwdSmem<T> &sm, const StageIn<T> &cur, d4 (&M)[T][T],
                                              double (&lpr)[T][4], int n, int m, int s, int g, int c) {
     constexpr int LD = 16 * T + 1;
     const int nch = (n + 3) >> 2;
@@ -306,11 +331,8 @@ __device__ __forceinline__ int riccati_stage(BwdSmem<T> &sm, const StageIn<T> &c
                 }
         }
         // ---- L = chol(M) (lqr_kernel.hpp:126) with lu <- Luu^{-1} lu, p -= Lxu lu (:145-146) ----
-        double myinv[T];
-#pragma unroll
-        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
-        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, 0, s, m, true, g, c);
-        finalize_L<T>(M, myinv, 0, s, g, c);
+        const bool ok = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, 0, s, m, true, g, c);
+        finalize_L<T>(M, sm.inv, 0, s, g, c);
         store_L_lds<T>(M, sm.L, g, c);
         // p_k -> LDS (next stage's p_next)
         if (c == 0) {
@@ -323,7 +345,7 @@ __device__ __forceinline__ int riccati_stage(BwdSmem<T> &sm, const StageIn<T> &c
                 }
         }
         wave_sync();
-        return f;
+        return ok;
 }
 
 }  // namespace pdplqr

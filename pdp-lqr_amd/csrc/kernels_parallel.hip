@@ -239,12 +239,10 @@ __global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
     if (last) {
         d4 M[T][T];
         load_M<T>(M, Hb + (long long)sh.N * sh.ps, n, m, m, s, g, c);
-        double myinv[T], lpr[T][4];
-#pragma unroll
-        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
-        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, m, s, m, false, g, c);
-        finalize_L<T>(M, myinv, m, s, g, c);
-        if (f >= 0) fail_stage = sh.N;
+        double lpr[T][4];
+        const bool okN = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, m, s, m, false, g, c);
+        finalize_L<T>(M, sm.inv, m, s, g, c);
+        if (!okN) fail_stage = sh.N;
         store_L_lds<T>(M, sm.L, g, c);
         if (lane < n) {
             const double v = hb[(long long)sh.N * s + lane];
@@ -279,8 +277,8 @@ __global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
                       hb + (long long)k * s, n, s, g, c);
         d4 M[T][T];
         double lpr[T][4];
-        const int f = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
-        if (f >= 0 && fail_stage < 0) fail_stage = k;
+        const bool okk = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
+        if (!okk && fail_stage < 0) fail_stage = k;
         double *FRk = FRb + (long long)k * frs;
 #pragma unroll
         for (int a = 0; a < T; ++a)

@@ -23,6 +23,9 @@
 #include "device_common.hpp"
 #include "parallel.hpp"
 
+#include <stdint.h>
+#include <stdlib.h>
+
 namespace pdplqr {
 
 // ---------------------------------------------------------------------------
@@ -52,6 +55,10 @@ __global__ void k_update_problem_data(Shape sh, const double *__restrict__ H, co
                 v = Hb[(long long)k * s * s + i + j * s];
             } else {
                 const int q = (int)(r - (long long)sh.N * sh.ps);
+                if (q >= sh.pn) {  // 16-byte alignment pad of the problem
+                    Hw[t] = 0.0;
+                    continue;
+                }
                 const short2 ij = tab_n[q];
                 i = ij.x; j = ij.y;
                 v = Hb[(long long)sh.N * s * s + i + j * sh.n];
@@ -105,7 +112,9 @@ __global__ void k_penalty(Shape sh, const double *__restrict__ D, const double *
                 i = ij.x; j = ij.y;
             } else {
                 k = N;
-                const short2 ij = tab_n[(int)(r - (long long)N * sh.ps)];
+                const int q = (int)(r - (long long)N * sh.ps);
+                if (q >= sh.pn) continue;  // alignment pad
+                const short2 ij = tab_n[q];
                 i = ij.x; j = ij.y;
             }
             const int nc = y_off[k + 1] - y_off[k];
@@ -178,12 +187,10 @@ __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati
     {
         d4 M[T][T];
         load_M<T>(M, Hb + (long long)N * sh.ps, n, m, m, s, g, c);
-        double myinv[T], lpr[T][4];
-#pragma unroll
-        for (int q = 0; q < T; ++q) myinv[q] = 1.0;
-        const int f = chol_tiles<T>(M, myinv, lpr, sm.col, sm.luq, m, s, m, false, g, c);
-        finalize_L<T>(M, myinv, m, s, g, c);
-        if (f >= 0) fail_stage = N;
+        double lpr[T][4];
+        const bool okN = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, m, s, m, false, g, c);
+        finalize_L<T>(M, sm.inv, m, s, g, c);
+        if (!okN) fail_stage = N;
         store_L_lds<T>(M, sm.L, g, c);
         if (lane < n) {
             const double v = hb[(long long)N * s + lane];
@@ -214,8 +221,8 @@ __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati
                           Hb + (long long)(k - 1) * sh.ps, hb + (long long)(k - 1) * s, n, s, g, c);
         d4 M[T][T];
         double lpr[T][4];
-        const int f = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
-        if (f >= 0 && fail_stage < 0) fail_stage = k;
+        const bool okk = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
+        if (!okk && fail_stage < 0) fail_stage = k;
         // p_k -> factor cache
         if (lpb && c == 0) {
 #pragma unroll
@@ -261,8 +268,183 @@ __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati
     if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
 }
 
+// ---------------------------------------------------------------------------
+// Shape-specialised backward (n = NN, m = MM known at compile time) with the
+// stage inputs streamed by LDS-DMA (global_load_lds_dwordx4, no VGPRs): the
+// record of stage k-1 -- E (n s), c (n), h~ (s), packed H~ (s(s+1)/2) -- lands
+// in the other half of a double buffer while stage k computes.  Requires every
+// section to be a whole number of 16-byte chunks (even double counts).
+// ---------------------------------------------------------------------------
+template <int NN, int MM>
+struct FastShape {
+    static constexpr int n = NN, m = MM, s = NN + MM;
+    static constexpr int ps = s * (s + 1) / 2;
+    static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, Q = OP + ps;
+    static constexpr int CH = Q / 2, NI = (CH + 63) / 64;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && s % 2 == 0 && ps % 2 == 0;
+};
+
+template <int T, int NN, int MM, bool KEEP>
+__global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati_bwd_fast(RiccatiArgs A) {
+    using SH = FastShape<NN, MM>;
+    constexpr int n = SH::n, m = SH::m, s = SH::s, ps = SH::ps, NI = SH::NI, CH = SH::CH;
+    static_assert(SH::ok, "fast path needs 16-byte stage sections");
+    __shared__ BwdSmem<T> sm;
+    __shared__ __attribute__((aligned(16))) double stg[2][NI * 128];
+    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const Shape &sh = A.sh;
+    const int N = sh.N;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.KD + b * sh.perKD;
+    double *Lcb = KEEP ? A.Lc + b * sh.perHw : nullptr;
+    double *lpb = KEEP ? A.lpc + b * sh.perh : nullptr;
+    int fail_stage = -1;
+
+    // per-lane DMA source offsets (section, offset) for each of the NI chunks
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            int ch = q * 64 + lane;
+            ch = ch < CH ? ch : CH - 1;  // surplus lanes re-load the last chunk into an unused slot
+            const int d = 2 * ch;
+            const double *src = d < SH::OC   ? Eb + (long long)k * n * s + d
+                                : d < SH::OH ? cb + (long long)k * n + (d - SH::OC)
+                                : d < SH::OP ? hb + (long long)k * s + (d - SH::OH)
+                                             : Hb + (long long)k * ps + (d - SH::OP);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(&stg[slot][q * 128]), 16, 0,
+                                             0);
+        }
+    };
+
+    // ---- terminal (lqr_kernel.hpp:80-91) ----
+    {
+        d4 M[T][T];
+        load_M<T>(M, Hb + (long long)N * ps, n, m, m, s, g, c);
+        double lpr[T][4];
+        const bool okN = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, m, s, m, false, g, c);
+        finalize_L<T>(M, sm.inv, m, s, g, c);
+        if (!okN) fail_stage = N;
+        store_L_lds<T>(M, sm.L, g, c);
+        if (lane < n) {
+            const double v = hb[(long long)N * s + lane];
+            sm.pv[lane] = v;
+            if (KEEP) lpb[(long long)N * s + lane] = v;
+        }
+        if (KEEP)
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                        if (j >= m && i >= j && i < s)
+                            Lcb[(long long)N * ps + pidx(i - m, j - m, n)] = M[a][bt][r];
+                    }
+        wave_sync();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma(N - 1, (N - 1) & 1);
+    for (int k = N - 1; k >= 0; --k) {
+        if (k > 0) {
+            dma(k - 1, (k - 1) & 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // stage k's record has landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const double *R = stg[k & 1];
+        StageIn<T> cur;
+#pragma unroll
+        for (int cc = 0; cc < 4 * T; ++cc) {
+            const int t = 4 * cc + g;
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                const int j = 16 * bt + c;
+                cur.E[cc][bt] = (t < n && j < s) ? R[SH::OE + j * n + t] : 0.0;
+            }
+            cur.c[cc] = (t < n) ? R[SH::OC + t] : 0.0;
+        }
+#pragma unroll
+        for (int bt = 0; bt < T; ++bt) {
+            const int j = 16 * bt + c;
+            cur.h[bt] = (j < s) ? R[SH::OH + j] : 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                    cur.H[a][bt][r] = (i < s && j < s) ? R[SH::OP + (i >= j ? pidx(i, j, s) : pidx(j, i, s))]
+                                                       : (i == j ? 1.0 : 0.0);
+                }
+        d4 M[T][T];
+        double lpr[T][4];
+        const bool okk = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
+        if (!okk && fail_stage < 0) fail_stage = k;
+        // rollout record FR_k = [L(:, 0:m) | lu']
+        double *FRk = FRb + (long long)k * (s * m + m);
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                const int jc = 16 * bt + c;
+                if (jc < m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g;
+                        if (i < s) FRk[jc * s + i] = M[a][bt][r];
+                    }
+            }
+        if (lane < m) FRk[s * m + lane] = sm.luq[lane];
+        if (KEEP) {
+            if (lane < m) lpb[(long long)k * s + lane] = sm.luq[lane];
+            if (lane < n) lpb[(long long)k * s + m + lane] = sm.pv[lane];
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                        if (i >= j && i < s) Lcb[(long long)k * ps + pidx(i, j, s)] = M[a][bt][r];
+                    }
+        }
+    }
+    if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+template <int T, int NN, int MM>
+static void launch_fast(const RiccatiArgs &a, hipStream_t st) {
+    if (a.Lc) hipLaunchKernelGGL((k_riccati_bwd_fast<T, NN, MM, true>), dim3(a.sh.batch), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((k_riccati_bwd_fast<T, NN, MM, false>), dim3(a.sh.batch), dim3(64), 0, st, a);
+}
+
+// 16-byte alignment of every per-problem / per-stage block (fast path).
+static bool fast_aligned(const RiccatiArgs &a) {
+    const Shape &sh = a.sh;
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return al(a.E) && al(a.c) && al(a.Hw) && al(a.hw) && sh.perE % 2 == 0 && sh.perc % 2 == 0 &&
+           sh.perHw % 2 == 0 && sh.perh % 2 == 0;
+}
+
 int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
-    if (a.sh.s <= 16) {
+    {
+        const int rc = launch_riccati_backward_schur(a, st);  // keep_factors = 0, n + m <= 16
+        if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
+    }
+    const bool fast_ok = fast_aligned(a) && !getenv("PDPLQR_NO_FAST");
+    if (fast_ok && a.sh.n == 12 && a.sh.m == 4) {
+        launch_fast<1, 12, 4>(a, st);
+    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 8) {
+        launch_fast<2, 24, 8>(a, st);
+    } else if (a.sh.s <= 16) {
         hipLaunchKernelGGL(k_riccati_bwd<1>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (a.sh.s <= 32) {
         hipLaunchKernelGGL(k_riccati_bwd<2>, dim3(a.sh.batch), dim3(64), 0, st, a);

@@ -72,6 +72,55 @@ def test_lqrsolver_matches_oracle_and_golden(name):
         assert rel_err(P, d["P"][i]) < TOL
 
 
+@pytest.mark.parametrize("name", golden_names())
+def test_value_form_backward_matches_golden(name):
+    """keep_factors = 0 takes the value-matrix kernel for n + m <= 16
+    (kernels_schur.hip: only the u-pivots are factored, P_k is the Schur
+    complement) -- same rollout as the square-root recursion."""
+    from pdplqr import LQRSolver
+
+    pm, d = load_golden(name)
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRSolver(model, keep_factors=False)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    w = np.concatenate(out)
+    _, w_orc = _oracle_serial(pm, d)
+    n, m, N = pm.n, pm.m, pm.N
+    assert sol.status() == 0
+    assert rel_err(w, w_orc) < TOL
+    assert rel_err(u_parts(w, n, m, N), u_parts(d["w_riccati"], n, m, N)) < 1e-6
+
+
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 200, 5), (12, 4, 7, 3), (5, 3, 40, 4), (1, 1, 30, 2), (13, 3, 25, 3),
+                                         (8, 8, 20, 2), (3, 5, 17, 3)])
+def test_value_form_batched_shapes(n, m, N, batch):
+    """Both value-form variants (LDS-DMA 12/4 and runtime shape) against the oracle."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 101 + n + m)
+    s = n + m
+    ws0 = np.zeros((batch, N * s + n))
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws0)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+
+
 @pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40"])
 def test_backward_without_factorization(name):
     """lqr_solver.hpp:65-70 after a full backward, with new linear data."""
@@ -153,7 +202,8 @@ def test_device_buffers_equal_host_buffers():
     assert np.array_equal(a, b)
 
 
-def test_non_spd_sets_status_flag():
+@pytest.mark.parametrize("keep", [True, False])
+def test_non_spd_sets_status_flag(keep):
     """The reference ignores Eigen's LLT info (lqr_kernel.hpp:89,126); this build
     reports the first failing stage per problem instead."""
     from pdplqr import BatchedLQRSolver
@@ -164,7 +214,7 @@ def test_non_spd_sets_status_flag():
     s = n + m
     H = H.copy()
     H[1, 7 * s * s:8 * s * s] = -np.eye(s).reshape(-1)  # stage 7 of problem 1 indefinite
-    bs = BatchedLQRSolver(n, m, N, batch)
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
     bs.set_model(E, c, H, h)
     bs.update_problem_data(np.zeros((batch, N * s + n)), sigma=0.0)
     bs.backward()
