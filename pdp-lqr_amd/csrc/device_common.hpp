@@ -53,11 +53,55 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Sum over the four row groups g of a column (lanes c, c+16, c+32, c+48),
+// returned on all of them, with gfx950's v_permlane16/32_swap (VALU, no LDS
+// round trip like ds_bpermute).  Each swap of two copies of v yields
+// (v[l], v[l ^ 16]) in some order per lane; the fp add is commutative, so all
+// four groups end with bit-identical sums.
+__device__ __forceinline__ double sum_groups(double v) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+    lo = __double2loint(v);
+    hi = __double2hiint(v);
+    a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
     return __hiloint2double(hi, lo);
 }
+
+// LDS-DMA of 16 bytes per lane: LDS[lds_base + 16 lane] <- *src
+// (global_load_lds_dwordx4; lds_base is the wave-uniform LDS byte address).
+// Issued through inline asm on purpose: the compiler's waitcnt insertion
+// treats every later ds_read of the same LDS object as aliasing an in-flight
+// builtin DMA and puts s_waitcnt vmcnt(0) in front of it, which serialises the
+// prefetch.  Callers own the vmcnt accounting (loads retire in issue order).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; it is only live inside this asm
+__device__ __forceinline__ void dma16(const void *src, const void *lds_dst) {
+    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)lds_dst;
+    asm volatile(
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %0, off" ::"v"(src),
+        "s"(__builtin_amdgcn_readfirstlane(base))
+        : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// Stores through an explicit global (addrspace 1) pointer.  A store through a
+// generic pointer keeps a flat memory operand, and the waitcnt pass then puts
+// s_waitcnt vmcnt(0) before every later ds_read (the store "may write LDS"),
+// which drains the DMA prefetch queue.
+__device__ __forceinline__ void gstore(double *p, double v) { *(__attribute__((address_space(1))) double *)p = v; }
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gstore2(double *p, d2v v) { *(__attribute__((address_space(1))) d2v *)p = v; }
 
 // 1/sqrt(x): hardware estimate + two Newton steps (full fp64 accuracy).
 __device__ __forceinline__ double rsqrt_f64(double x) {

@@ -62,6 +62,8 @@ int launch_penalty(const Shape &sh, const double *D, const double *rho, const do
                    const short2 *tab_n, int with_H, int max_nc, hipStream_t st);
 int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
+int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                       double *ws, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
 int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *KD, const double *x0,
                            double *ws, hipStream_t st);

@@ -760,6 +760,8 @@ static int launch_fwd(const Shape &sh, const double *E, const double *c, const d
 
 int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                            double *ws, hipStream_t st) {
+    const int rc = launch_rollout_dma(sh, E, c, FR, x0, ws, st);  // kernels_rollout.hip
+    if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
     SegFwd none{};
     return launch_fwd<false>(sh, E, c, FR, x0, ws, none, st);
 }

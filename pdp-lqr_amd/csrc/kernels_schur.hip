@@ -60,7 +60,10 @@ struct SchurSmem {
     alignas(16) double lpt[16];  // lp_k, column -> row redistribution (colpos order)
     double inv[16];              // 1 / sqrt(pivot), u columns
     double luq[16];              // lu' = Luu^{-1} lu
-    double tp[16 * 17];          // transpose of P_k (odd leading dimension: conflict-free)
+    union {
+        double tp[16 * 17];           // transpose of P_k (odd leading dimension: conflict-free)
+        alignas(16) double rec[128];  // rollout record staging (one coalesced store per stage)
+    };
 };
 
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
@@ -84,8 +87,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
             part = __builtin_fma(G[kk], in.ct[kk], part);
             part = __builtin_fma(in.E[kk], prow[kk], part);
         }
-    part += shfl_xor_f64(part, 16);
-    part += shfl_xor_f64(part, 32);
+    part = sum_groups(part);
     if (g == 0) sm.lpt[colpos<1>(c)] = in.h + part;
     wave_sync();
     double lpr[1][4];
@@ -130,11 +132,31 @@ __device__ __forceinline__ void schur_store_record(double *FRk, const d4 &Pm, co
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 4 * r + g;
-            if (i < s) FRk[c * s + i] = (i >= c) ? Pm[r] * iv : 0.0;
+            if (i < s) gstore(FRk + c * s + i, (i >= c) ? Pm[r] * iv : 0.0);
         }
     }
     const int lane = 16 * g + c;
-    if (lane < m) FRk[s * m + lane] = sm.luq[lane];
+    if (lane < m) gstore(FRk + s * m + lane, sm.luq[lane]);
+}
+
+// Same record, staged in LDS and written with one dwordx4 store instruction
+// (lanes < FS/2): coalesced, and a fixed vm-op count for the DMA accounting.
+template <int M, int S>
+__device__ __forceinline__ void schur_store_record_staged(double *FRk, const d4 &Pm, SchurSmem &sm, int g, int c) {
+    constexpr int FS = S * M + M;
+    static_assert(FS % 2 == 0 && FS <= 128, "record staging");
+    const int lane = 16 * g + c;
+    if (c < M) {
+        const double iv = sm.inv[c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            if (i < S) sm.rec[c * S + i] = (i >= c) ? Pm[r] * iv : 0.0;
+        }
+    }
+    if (lane < M) sm.rec[S * M + lane] = sm.luq[lane];
+    wave_sync();
+    if (lane < FS / 2) gstore2(FRk + 2 * lane, reinterpret_cast<const d2v *>(sm.rec)[lane]);
 }
 
 // Stage-record layout of the LDS-DMA variant (compile-time shapes).
@@ -185,9 +207,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
                                 : d < SH::OH ? cb + (long long)k * SH::n + (d - SH::OC)
                                 : d < SH::OP ? hb + (long long)k * SH::s + (d - SH::OH)
                                              : Hb + (long long)k * SH::ps + (d - SH::OP);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)(&stg[slot][q * 128]), 16, 0,
-                                             0);
+            dma16(src, &stg[slot][q * 128]);
         }
     };
 
@@ -210,11 +230,16 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     }
 
     if constexpr (CT) {
+        // vm ops per iteration: NI DMA (stage k-1) + 1 record store, so after
+        // issuing DMA(k-1) "DMA(k) has landed" is vmcnt(NI + 1); the first
+        // iteration has no store behind DMA(N-1) yet.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // terminal loads
         dma(N - 1, (N - 1) & 1);
         for (int k = N - 1; k >= 0; --k) {
             if (k > 0) {
                 dma(k - 1, (k - 1) & 1);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // stage k's record has landed
+                if (k == N - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 1) : "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
@@ -223,7 +248,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
             const bool ok = schur_stage(Pm, prow, in, sm, m, s, g, c);
             if (!ok && fail_stage < 0) fail_stage = k;
-            schur_store_record(FRb + (long long)k * frs, Pm, sm, m, s, g, c);
+            schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
             wave_sync();  // the record's LDS reads retire before the next DMA overwrites the slot
         }
     } else {

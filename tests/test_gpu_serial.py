@@ -94,7 +94,7 @@ def test_value_form_backward_matches_golden(name):
     assert rel_err(u_parts(w, n, m, N), u_parts(d["w_riccati"], n, m, N)) < 1e-6
 
 
-@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 200, 5), (12, 4, 7, 3), (5, 3, 40, 4), (1, 1, 30, 2), (13, 3, 25, 3),
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 200, 5), (12, 4, 7, 3), (12, 4, 1, 2), (12, 4, 2, 3), (12, 4, 3, 2), (5, 3, 40, 4), (1, 1, 30, 2), (13, 3, 25, 3),
                                          (8, 8, 20, 2), (3, 5, 17, 3)])
 def test_value_form_batched_shapes(n, m, N, batch):
     """Both value-form variants (LDS-DMA 12/4 and runtime shape) against the oracle."""
