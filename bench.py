@@ -65,9 +65,10 @@ def gen_batch_device(n, m, N, batch, seed, device):
     return E.reshape(batch, -1).contiguous(), c.reshape(batch, -1).contiguous(), H, h, x0
 
 
-def load_pmc_traffic(workload_tag):
+def load_pmc_traffic(workload_tag, kernel=None):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/*_pmc.json), or None."""
+    PMC summary (profiles/*_pmc.json), or None.  Only a summary collected on the
+    same workload AND the same backward kernel counts."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     if not os.path.isdir(pdir):
@@ -78,7 +79,8 @@ def load_pmc_traffic(workload_tag):
                 d = json.load(open(os.path.join(pdir, f)))
             except Exception:
                 continue
-            if d.get("workload") == workload_tag and "bytes_per_launch" in d:
+            if (d.get("workload") == workload_tag and "bytes_per_launch" in d
+                    and (kernel is None or d.get("dominant_kernel", "").endswith(kernel))):
                 best = d
     return best
 
@@ -195,6 +197,17 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
             "scaling": "strong", "finite": ok, "exchange": "all-gather of 3n^2+2n doubles per rank"}
 
 
+def bwd_kernel_name(n, m, keep):
+    """The backward kernel the C ABI dispatches for this shape (kernels_schur.hip /
+    kernels_riccati.hip launch_riccati_backward)."""
+    s = n + m
+    if not keep and s <= 16:
+        return "k_riccati_bwd_schur<12, 4>" if (n, m) == (12, 4) else "k_riccati_bwd_schur<0, 0>"
+    if (n, m) == (12, 4):
+        return f"k_riccati_bwd_fast<1, 12, 4, {str(bool(keep)).lower()}>"
+    return "k_riccati_bwd<1>" if s <= 16 else "k_riccati_bwd<2>"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,7 +290,7 @@ def main():
     bytes_stage = bytes_bwd_stage + 8 * s  # + the w write = B of BASELINE.md section 2
     achieved = bytes_bwd_stage * stages / (ms_bwd * 1e-3) / 1e9
     tag = f"N{N}_n{n}_m{m}_b{B}_kf{int(args.keep_factors)}"
-    pmc = load_pmc_traffic(tag)
+    pmc = load_pmc_traffic(tag, bwd_kernel_name(n, m, args.keep_factors))
     res = {
         "metric": METRIC,
         "value": value,
@@ -295,7 +308,7 @@ def main():
                                "(north_star target config)",
                    "N": N, "nx": n, "nu": m, "batch_per_gpu": B, "solver": "LQRSolver (batched)",
                    "keep_factors": bool(args.keep_factors), "parallelism": f"batch-sharded x{world}"},
-        "roofline": {"kernel": "k_riccati_bwd<1>", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": bwd_kernel_name(n, m, args.keep_factors), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": (pmc["bytes_per_launch"] if pmc else None),
                      "bytes_per_stage_algorithmic": bytes_bwd_stage, "ms_per_launch": ms_bwd},

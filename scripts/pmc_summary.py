@@ -28,7 +28,11 @@ def main():
         if "pdplqr" not in short:
             continue
         out["kernels"][short] = {c: sum(v) / len(v) for c, v in d.items()}
-    bwd = [v for k, v in out["kernels"].items() if "k_riccati_bwd<" in k or k.endswith("k_riccati_bwd<1>")]
+    # dominant kernel of the bench step: the value-form backward when present
+    names = sorted(out["kernels"], key=lambda k: ("bwd_schur" not in k, "k_riccati_bwd" not in k))
+    bwd = [out["kernels"][k] for k in names if "k_riccati_bwd" in k]
+    if bwd:
+        out["dominant_kernel"] = [k for k in names if "k_riccati_bwd" in k][0]
     if bwd and "FETCH_SIZE" in bwd[0] and "WRITE_SIZE" in bwd[0]:
         b = bwd[0]
         out["bytes_per_launch"] = b["FETCH_SIZE"] * 1024 * 2 + b["WRITE_SIZE"] * 1024
