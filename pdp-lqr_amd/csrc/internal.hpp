@@ -70,7 +70,8 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 }  // namespace pdplqr
 
-namespace pdplqr { struct ParallelState; }
+namespace pdplqr { struct ParallelState;
+struct KKTState; }
 
 struct pdplqr_handle_s {
     pdplqr_config cfg;
@@ -95,6 +96,7 @@ struct pdplqr_handle_s {
     bool host_staged = false;  // a host->device copy is in flight on `stream`
     std::vector<void *> allocs;
     pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)
+    pdplqr::KKTState *kkt = nullptr;       // KKT solver state (kkt.hip)
     double *suf_bufs[2] = {nullptr, nullptr};
     int shard_last = 1;  // last shard_backward's is_last_shard
 };

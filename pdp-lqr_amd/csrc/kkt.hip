@@ -1,0 +1,611 @@
+// kkt.hip -- QDLDLSolver on MI355X: the KKT system of kkt.hpp solved by a
+// block LDL^T in QDLDL's elimination order.
+//
+// The reference (qdldl_solver.hpp:36-151, kkt.hpp:45-331) assembles the KKT
+// matrix in the natural order [u0, x1,u1, ..., xN | y0, lambda1,y1, ...,
+// lambdaN,yN] and factors it with QDLDL's up-looking LDL^T.  In that order
+// every primal pivot comes first, so the factorisation is
+//     K = [H  C^T; C  -Reg],   H = blockdiag(H_k + sigma I),
+//     S = -Reg - C H^{-1} C^T  (the condensed dual system),
+// and S is block tridiagonal over the dual groups [y0], [lambda_k; y_k]
+// (group k couples to k +- 1 through the shared primal block z_k).  Only the
+// y diagonal (-inv_rho, update_rho_vecs kkt.hpp:105-122) changes between
+// factorisations, so the work splits into
+//   k_kkt_stage  (once per model, parallel over (problem, stage)):
+//                L_k = chol(H_k + sigma I), V_k = L_k^{-1} C_kk^T,
+//                U_k = L_k^{-1} C_{k+1,k}^T and the dual blocks V^T V, U^T U, U^T V
+//   k_kkt_factor (backward, serial over groups, one wave per problem):
+//                block Cholesky of -S = Reg + C H^{-1} C^T
+//   k_kkt_rhs    (update_problem_data, form_rhs kkt.hpp:224-300)
+//   k_kkt_x0     (forward: update_rhs_initial_stage kkt.hpp:207-222, accumulating +=)
+//   k_kkt_solve1/2/3 (forward, QDLDL_solve): w = L^{-1} r_p, dual condense,
+//                block forward/back substitution on -S, z = L^{-T}(w - V lam - U lam+).
+// Stage-0 state constraints are ignored by the KKT (kkt.hpp:218-221): C_00 has
+// only the u columns of D_0 and x0 enters only through S0 x0 and A0 x0.
+#include "device_common.hpp"
+#include "solvers.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace pdplqr {
+
+struct KKTArgs {
+    Shape sh;
+    int P;          // padded block size (16 or 32), leading dimension of every block
+    int dim;        // KKT dimension per problem
+    double sigma;   // frozen primal regularisation (kkt_sigma)
+    double rho_dyn; // frozen dynamics regularisation
+    const double *E, *c, *H, *h, *D;
+    const int32_t *d_off, *y_off, *ncs;
+    const int32_t *prim_off, *prim_dim, *dual_off, *gdim;
+    double *blk;    // [b][N+1][6][P*P]: L, V, U, VtV, UtU, UtV
+    double *fac;    // [b][N+1][2][P*P]: Lkk, L_{k+1,k}
+    double *rhs;    // [b][dim]
+    double *wv;     // [b][N+1][4][P]: w, t, t1, lam
+    int32_t *status;
+    int32_t *pstat;  // per problem: a primal block H_k + sigma I was not positive definite
+};
+
+// ---------------------------------------------------------------------------
+// wave-level helpers on column-major blocks in LDS (leading dimension ld)
+// ---------------------------------------------------------------------------
+// C (r x c) (+)= alpha op(A) op(B), inner dimension kd
+__device__ __forceinline__ void kgemm(double *C, int ldc, const double *A, int lda, bool tA, const double *B, int ldb,
+                                      bool tB, int r, int c, int kd, double alpha, bool acc, int lane) {
+    for (int idx = lane; idx < r * c; idx += 64) {
+        const int i = idx % r, j = idx / r;
+        double s = 0.0;
+        for (int k = 0; k < kd; ++k) {
+            const double a = tA ? A[k + i * lda] : A[i + k * lda];
+            const double b = tB ? B[j + k * ldb] : B[k + j * ldb];
+            s = __builtin_fma(a, b, s);
+        }
+        C[i + j * ldc] = (acc ? C[i + j * ldc] : 0.0) + alpha * s;
+    }
+}
+
+// in-place lower Cholesky of the n x n block (upper part zeroed)
+__device__ __forceinline__ bool kchol(double *A, int ld, int n, int lane) {
+    bool ok = true;
+    for (int j = 0; j < n; ++j) {
+        const double d = A[j + j * ld];
+        ok = ok && (d > 0.0);
+        const double r = sqrt(d), ir = 1.0 / r;
+        wave_sync();
+        for (int i = j + 1 + lane; i < n; i += 64) A[i + j * ld] *= ir;
+        if (lane == 0) A[j + j * ld] = r;
+        wave_sync();
+        const int t = n - j - 1;
+        for (int q = lane; q < t * t; q += 64) {
+            const int i = j + 1 + q % t, k = j + 1 + q / t;
+            if (i >= k) A[i + k * ld] -= A[i + j * ld] * A[k + j * ld];
+        }
+        wave_sync();
+    }
+    for (int idx = lane; idx < n * n; idx += 64) {
+        const int i = idx % n, j = idx / n;
+        if (i < j) A[i + j * ld] = 0.0;
+    }
+    wave_sync();
+    return ok;
+}
+
+// B (n x c) <- L^{-1} B, lanes over columns
+__device__ __forceinline__ void ktrsm(const double *L, int ldl, double *B, int ldb, int n, int c, int lane) {
+    for (int j = lane; j < c; j += 64)
+        for (int i = 0; i < n; ++i) {
+            double v = B[i + j * ldb];
+            for (int k = 0; k < i; ++k) v -= L[i + k * ldl] * B[k + j * ldb];
+            B[i + j * ldb] = v / L[i + i * ldl];
+        }
+}
+
+// x (n) <- L^{-1} x or L^{-T} x, column-oriented with the lanes over rows
+__device__ __forceinline__ void ktrsv(const double *L, int ldl, double *x, int n, bool trans, int lane) {
+    if (!trans) {
+        for (int j = 0; j < n; ++j) {
+            const double xj = x[j] / L[j + j * ldl];
+            wave_sync();
+            if (lane == 0) x[j] = xj;
+            for (int i = j + 1 + lane; i < n; i += 64) x[i] -= L[i + j * ldl] * xj;
+            wave_sync();
+        }
+    } else {
+        for (int j = n - 1; j >= 0; --j) {
+            const double xj = x[j] / L[j + j * ldl];
+            wave_sync();
+            if (lane == 0) x[j] = xj;
+            for (int i = lane; i < j; i += 64) x[i] -= L[j + i * ldl] * xj;  // (L^T)[i][j] = L[j][i]
+            wave_sync();
+        }
+    }
+}
+
+__device__ __forceinline__ void kcopy_out(double *dst, const double *src, int n, int lane) {
+    for (int q = lane; q < n; q += 64) dst[q] = src[q];
+}
+
+// reference column of KKT-ordered primal index a of stage k ((x, u) order
+// for 0 < k < N; u for k = 0; x for k = N)
+__device__ __forceinline__ int kref(int k, int N, int n, int m, int a) {
+    if (k == 0 || k == N) return a;
+    return a < n ? m + a : a - n;
+}
+
+// ---------------------------------------------------------------------------
+// k_kkt_stage: primal factor and dual blocks of stage k (once per model)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_kkt_stage(KKTArgs A) {
+    extern __shared__ double lds[];
+    const int P = A.P, PP = P * P;
+    double *L = lds, *V = lds + PP, *U = lds + 2 * PP, *T = lds + 3 * PP;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
+    const int nck = A.ncs[k];
+    const double *Hk = A.H + b * sh.perH + (long long)k * s * s;  // terminal: n x n at N s^2
+    const int ldH = k < N ? s : n;
+    const double *Ek = A.E + b * sh.perE + (long long)k * n * s;
+    const double *Dk = A.D + b * sh.ndD + A.d_off[k];
+    for (int q = lane; q < 4 * PP; q += 64) lds[q] = 0.0;
+    wave_sync();
+    for (int idx = lane; idx < p * p; idx += 64) {
+        const int a = idx % p, c = idx / p;
+        const double v = Hk[kref(k, N, n, m, a) + kref(k, N, n, m, c) * ldH];
+        L[a + c * P] = (a == c) ? v + A.sigma : v;
+    }
+    // V <- C_kk^T (p x g), U <- C_{k+1,k}^T (p x g1)
+    for (int idx = lane; idx < p * g; idx += 64) {
+        const int a = idx % p, r = idx / p;
+        double v;
+        if (k == 0) v = Dk[r + a * nck];  // y0 rows: D0 u-columns
+        else if (r < n) v = (a == r) ? -1.0 : 0.0;  // lambda_k rows: -x_k
+        else v = Dk[(r - n) + kref(k, N, n, m, a) * nck];
+        V[a + r * P] = v;
+    }
+    for (int idx = lane; idx < p * g1; idx += 64) {
+        const int a = idx % p, r = idx / p;
+        U[a + r * P] = (r < n) ? Ek[r + kref(k, N, n, m, a) * n] : 0.0;  // lambda_{k+1} rows: E_k
+    }
+    wave_sync();
+    const bool ok = kchol(L, P, p, lane);
+    ktrsm(L, P, V, P, p, g, lane);
+    ktrsm(L, P, U, P, p, g1, lane);
+    wave_sync();
+    double *out = A.blk + (b * (N + 1) + k) * 6LL * PP;
+    kcopy_out(out, L, PP, lane);
+    kcopy_out(out + PP, V, PP, lane);
+    kcopy_out(out + 2 * PP, U, PP, lane);
+    kgemm(T, P, V, P, true, V, P, false, g, g, p, 1.0, false, lane);  // V^T V
+    wave_sync();
+    kcopy_out(out + 3 * PP, T, PP, lane);
+    wave_sync();
+    kgemm(T, P, U, P, true, U, P, false, g1, g1, p, 1.0, false, lane);  // U^T U
+    wave_sync();
+    kcopy_out(out + 4 * PP, T, PP, lane);
+    wave_sync();
+    for (int q = lane; q < PP; q += 64) T[q] = 0.0;
+    wave_sync();
+    kgemm(T, P, U, P, true, V, P, false, g1, g, p, 1.0, false, lane);  // U^T V
+    wave_sync();
+    kcopy_out(out + 5 * PP, T, PP, lane);
+    if (!ok && lane == 0) A.pstat[b] = 1;  // primal block not positive definite
+}
+
+// ---------------------------------------------------------------------------
+// k_kkt_factor: block Cholesky of -S (backward; QDLDL_factor's dual part)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_kkt_factor(KKTArgs A, const double *__restrict__ inv_rho) {
+    extern __shared__ double lds[];
+    const int P = A.P, PP = P * P;
+    double *M = lds, *Lp = lds + PP, *X = lds + 2 * PP;
+    const Shape &sh = A.sh;
+    const int n = sh.n, N = sh.N, lane = threadIdx.x;
+    const long long b = blockIdx.x;
+    const double *ir = inv_rho + b * sh.ny;
+    int fail = 0;
+    for (int q = lane; q < 3 * PP; q += 64) lds[q] = 0.0;
+    wave_sync();
+    int gp = 0;
+    for (int k = 0; k <= N; ++k) {
+        const int g = A.gdim[k];
+        const double *bk = A.blk + (b * (N + 1) + k) * 6LL * PP;
+        const double *bp = A.blk + (b * (N + 1) + k - 1) * 6LL * PP;
+        for (int idx = lane; idx < PP; idx += 64) {
+            const int i = idx % P, j = idx / P;
+            double v = 0.0;
+            if (i < g && j < g) {
+                v = bk[3 * PP + idx];
+                if (k > 0) v += bp[4 * PP + idx];
+                if (i == j) v += (k == 0) ? ir[A.y_off[0] + i] : (i < n ? A.rho_dyn : ir[A.y_off[k] + i - n]);
+            }
+            M[idx] = v;
+        }
+        wave_sync();
+        if (k > 0) kgemm(M, P, Lp, P, false, Lp, P, true, g, g, gp, -1.0, true, lane);  // -= L_{k,k-1} L_{k,k-1}^T
+        wave_sync();
+        const bool ok = kchol(M, P, g, lane);
+        if (!ok && !fail) fail = k + 1;
+        double *fk = A.fac + (b * (N + 1) + k) * 2LL * PP;
+        kcopy_out(fk, M, PP, lane);
+        if (k < N) {
+            const int g1 = A.gdim[k + 1];
+            // L_{k+1,k} = (U^T V)_k Lkk^{-T}:  X = Lkk^{-1} (U^T V)^T  (g x g1), then transpose
+            for (int idx = lane; idx < PP; idx += 64) {
+                const int i = idx % P, j = idx / P;
+                X[idx] = (i < g && j < g1) ? bk[5 * PP + j + i * P] : 0.0;
+            }
+            wave_sync();
+            ktrsm(M, P, X, P, g, g1, lane);
+            wave_sync();
+            for (int idx = lane; idx < PP; idx += 64) {
+                const int i = idx % P, j = idx / P;
+                Lp[idx] = (i < g1 && j < g) ? X[j + i * P] : 0.0;
+            }
+            wave_sync();
+            kcopy_out(fk + PP, Lp, PP, lane);
+            wave_sync();
+        }
+        gp = g;
+    }
+    // status: first failing dual group + 1, or N + 2 when a primal block failed
+    if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
+}
+
+// ---------------------------------------------------------------------------
+// k_kkt_rhs: form_rhs (kkt.hpp:224-300) -- one thread per (problem, KKT row)
+// row descriptors: kind 0 = primal (stage, KKT index), 1 = y (stage, q),
+// 2 = lambda_{k+1} (k, i)
+// ---------------------------------------------------------------------------
+__global__ void k_kkt_rhs(KKTArgs A, const int4 *__restrict__ rows, const double *__restrict__ ws,
+                          const double *__restrict__ ys, const double *__restrict__ zs,
+                          const double *__restrict__ irho, double sigma) {
+    const Shape &sh = A.sh;
+    const long long total = (long long)A.dim * sh.batch;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const long long b = t / A.dim;
+        const int r = (int)(t - b * A.dim);
+        const int4 d = rows[r];
+        double v;
+        if (d.x == 0) {
+            const long long o = b * sh.perh + (long long)d.y * sh.s + kref(d.y, sh.N, sh.n, sh.m, d.z);
+            v = -A.h[o] + sigma * ws[o];
+        } else if (d.x == 1) {
+            const long long o = b * sh.ny + A.y_off[d.y] + d.z;
+            v = zs[o] - irho[o] * ys[o];
+        } else {
+            v = -A.c[b * sh.perc + (long long)d.y * sh.n + d.z];
+        }
+        A.rhs[b * A.dim + r] = v;
+    }
+}
+
+// update_rhs_initial_stage (kkt.hpp:207-222): rhs_u0 += -S0 x0, rhs_lambda1 += -A0 x0
+__global__ __launch_bounds__(64) void k_kkt_x0(KKTArgs A, const double *__restrict__ x0) {
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, lane = threadIdx.x;
+    const long long b = blockIdx.x;
+    const double *H0 = A.H + b * sh.perH, *E0 = A.E + b * sh.perE, *x = x0 + b * n;
+    double *r = A.rhs + b * A.dim;
+    if (lane < m) {
+        double a = 0.0;
+        for (int j = 0; j < n; ++j) a += H0[lane + (m + j) * s] * x[j];
+        r[lane] += -a;
+    } else if (lane >= 32 && lane - 32 < n) {
+        const int i = lane - 32;
+        double a = 0.0;
+        for (int j = 0; j < n; ++j) a += E0[i + (m + j) * n] * x[j];
+        r[A.dual_off[1] + i] += -a;
+    }
+}
+
+// forward phase 1 (parallel over stages): w = L^{-1} r_p, t = V^T w, t1 = U^T w
+__global__ __launch_bounds__(64) void k_kkt_solve1(KKTArgs A) {
+    extern __shared__ double lds[];
+    const int P = A.P, PP = P * P;
+    double *L = lds, *w = lds + PP;
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
+    const double *bk = A.blk + (b * (N + 1) + k) * 6LL * PP;
+    for (int q = lane; q < PP; q += 64) L[q] = bk[q];
+    const double *r = A.rhs + b * A.dim + A.prim_off[k];
+    for (int q = lane; q < P; q += 64) w[q] = q < p ? r[q] : 0.0;
+    wave_sync();
+    ktrsv(L, P, w, p, false, lane);
+    double *o = A.wv + (b * (N + 1) + k) * 4LL * P;
+    for (int j = lane; j < P; j += 64) {
+        double t = 0.0, t1 = 0.0;
+        for (int a = 0; a < p; ++a) {
+            t = __builtin_fma(bk[PP + a + j * P], w[a], t);        // V^T w
+            t1 = __builtin_fma(bk[2 * PP + a + j * P], w[a], t1);  // U^T w
+        }
+        o[j] = w[j];
+        o[P + j] = j < g ? t : 0.0;
+        o[2 * P + j] = j < g1 ? t1 : 0.0;
+    }
+}
+
+// forward phase 2 (serial over groups): (-S) lam = -(r_d - C H^{-1} r_p)
+__global__ __launch_bounds__(64) void k_kkt_solve2(KKTArgs A) {
+    extern __shared__ double lds[];
+    const int P = A.P, PP = P * P;
+    double *Lk = lds, *Lo = lds + PP, *v = lds + 2 * PP, *yp = v + P;
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x;
+    const long long b = blockIdx.x;
+    const double *rd = A.rhs + b * A.dim;
+    double *wvb = A.wv + b * (N + 1) * 4LL * P;
+    const double *fb = A.fac + b * (N + 1) * 2LL * PP;
+    for (int q = lane; q < P; q += 64) yp[q] = 0.0;
+    wave_sync();
+    for (int k = 0; k <= N; ++k) {  // L y = b
+        const int g = A.gdim[k];
+        for (int q = lane; q < PP; q += 64) {
+            Lk[q] = fb[(long long)k * 2 * PP + q];
+            Lo[q] = k > 0 ? fb[(long long)(k - 1) * 2 * PP + PP + q] : 0.0;  // L_{k,k-1}
+        }
+        wave_sync();
+        for (int i = lane; i < P; i += 64) {
+            double bi = 0.0;
+            if (i < g) {
+                const double t1 = k > 0 ? wvb[(long long)(k - 1) * 4 * P + 2 * P + i] : 0.0;
+                bi = -(rd[A.dual_off[k] + i] - wvb[(long long)k * 4 * P + P + i] - t1);
+                if (k > 0)
+                    for (int j = 0; j < P; ++j) bi -= Lo[i + j * P] * yp[j];
+            }
+            v[i] = bi;
+        }
+        wave_sync();
+        ktrsv(Lk, P, v, g, false, lane);
+        for (int i = lane; i < P; i += 64) {
+            wvb[(long long)k * 4 * P + 3 * P + i] = v[i];
+            yp[i] = v[i];
+        }
+        wave_sync();
+    }
+    for (int q = lane; q < P; q += 64) yp[q] = 0.0;
+    wave_sync();
+    for (int k = N; k >= 0; --k) {  // L^T lam = y
+        const int g = A.gdim[k];
+        for (int q = lane; q < PP; q += 64) {
+            Lk[q] = fb[(long long)k * 2 * PP + q];
+            Lo[q] = k < N ? fb[(long long)k * 2 * PP + PP + q] : 0.0;  // L_{k+1,k}
+        }
+        wave_sync();
+        for (int i = lane; i < P; i += 64) {
+            double vi = 0.0;
+            if (i < g) {
+                vi = wvb[(long long)k * 4 * P + 3 * P + i];
+                if (k < N)
+                    for (int j = 0; j < P; ++j) vi -= Lo[j + i * P] * yp[j];  // (L_{k+1,k}^T lam_{k+1})_i
+            }
+            v[i] = vi;
+        }
+        wave_sync();
+        ktrsv(Lk, P, v, g, true, lane);
+        for (int i = lane; i < P; i += 64) {
+            wvb[(long long)k * 4 * P + 3 * P + i] = v[i];
+            yp[i] = v[i];
+        }
+        wave_sync();
+    }
+}
+
+// forward phase 3 (parallel): z_k = L^{-T}(w - V lam_k - U lam_{k+1}), unpacked into ws
+__global__ __launch_bounds__(64) void k_kkt_solve3(KKTArgs A, const double *__restrict__ x0, double *__restrict__ ws) {
+    extern __shared__ double lds[];
+    const int P = A.P, PP = P * P;
+    double *L = lds, *z = lds + PP;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
+    const double *bk = A.blk + (b * (N + 1) + k) * 6LL * PP;
+    const double *wk = A.wv + (b * (N + 1) + k) * 4LL * P;
+    const double *wn = wk + 4LL * P;  // stage k+1 (lam_{k+1})
+    for (int q = lane; q < PP; q += 64) L[q] = bk[q];
+    for (int a = lane; a < P; a += 64) {
+        double v = 0.0;
+        if (a < p) {
+            v = wk[a];
+            for (int j = 0; j < g; ++j) v -= bk[PP + a + j * P] * wk[3 * P + j];
+            for (int j = 0; j < g1; ++j) v -= bk[2 * PP + a + j * P] * wn[3 * P + j];
+        }
+        z[a] = v;
+    }
+    wave_sync();
+    ktrsv(L, P, z, p, true, lane);
+    double *wb = ws + b * sh.perh;
+    if (k == 0) {  // ws[0] = [u0; x0] (qdldl_solver.hpp:133-134)
+        if (lane < m) wb[lane] = z[lane];
+        else if (lane < s) wb[lane] = x0[b * n + lane - m];
+    } else if (k < N) {
+        if (lane < n) wb[(long long)k * s + m + lane] = z[lane];
+        else if (lane < s) wb[(long long)k * s + lane - n] = z[lane];
+    } else {
+        if (lane < n) wb[(long long)N * s + lane] = z[lane];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host state
+// ---------------------------------------------------------------------------
+struct KKTState {
+    int P = 16, dim = 0;
+    std::vector<int32_t> prim_off, prim_dim, dual_off, gdim;
+    int32_t *d_prim_off = nullptr, *d_prim_dim = nullptr, *d_dual_off = nullptr, *d_gdim = nullptr, *d_ncs = nullptr;
+    int4 *rows = nullptr;
+    int32_t *pstat = nullptr;
+    double *blk = nullptr, *fac = nullptr, *rhs = nullptr, *wv = nullptr;
+    bool formed = false;
+};
+
+template <typename X>
+static int kalloc(pdplqr_handle h, X **p, size_t count) {
+    *p = nullptr;
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(X));
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc: ") + hipGetErrorString(e));
+        return PDPLQR_ERR_ALLOC;
+    }
+    h->allocs.push_back(q);
+    *p = reinterpret_cast<X *>(q);
+    return PDPLQR_OK;
+}
+
+static KKTArgs kkt_args(pdplqr_handle h) {
+    KKTState *ks = h->kkt;
+    KKTArgs a;
+    a.sh = h->sh;
+    a.P = ks->P;
+    a.dim = ks->dim;
+    a.sigma = h->cfg.kkt_sigma;
+    a.rho_dyn = h->cfg.rho_dyn;
+    a.E = h->E;
+    a.c = h->c;
+    a.H = h->H;
+    a.h = h->h;
+    a.D = h->D;
+    a.d_off = h->d_off;
+    a.y_off = h->y_off;
+    a.ncs = ks->d_ncs;
+    a.prim_off = ks->d_prim_off;
+    a.prim_dim = ks->d_prim_dim;
+    a.dual_off = ks->d_dual_off;
+    a.gdim = ks->d_gdim;
+    a.blk = ks->blk;
+    a.fac = ks->fac;
+    a.rhs = ks->rhs;
+    a.wv = ks->wv;
+    a.status = h->status;
+    a.pstat = ks->pstat;
+    return a;
+}
+
+int kkt_init(pdplqr_handle h) {
+    const Shape &sh = h->sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N;
+    KKTState *ks = new (std::nothrow) KKTState();
+    if (!ks) return PDPLQR_ERR_ALLOC;
+    h->kkt = ks;
+    ks->prim_off.resize(N + 1);
+    ks->prim_dim.resize(N + 1);
+    ks->dual_off.resize(N + 1);
+    ks->gdim.resize(N + 1);
+    int po = 0, dmax = s;
+    for (int k = 0; k <= N; ++k) {
+        ks->prim_off[k] = po;
+        ks->prim_dim[k] = k == 0 ? m : (k < N ? s : n);
+        po += ks->prim_dim[k];
+    }
+    int dof = po;  // = N s
+    for (int k = 0; k <= N; ++k) {
+        ks->dual_off[k] = dof;
+        ks->gdim[k] = (k == 0 ? 0 : n) + h->ncs[k];
+        dof += ks->gdim[k];
+        dmax = std::max(dmax, ks->gdim[k]);
+    }
+    ks->dim = dof;
+    if (dmax > 32) {
+        set_error("KKT solver with n + m > 32 or n + nc > 32 is not supported by this build");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    ks->P = dmax <= 16 ? 16 : 32;
+    // row descriptors (kind, stage, index)
+    std::vector<int4> rows(ks->dim);
+    for (int k = 0; k <= N; ++k) {
+        for (int a = 0; a < ks->prim_dim[k]; ++a) rows[ks->prim_off[k] + a] = make_int4(0, k, a, 0);
+        const int base = ks->dual_off[k];
+        if (k == 0) {
+            for (int q = 0; q < h->ncs[0]; ++q) rows[base + q] = make_int4(1, 0, q, 0);
+        } else {
+            for (int i = 0; i < n; ++i) rows[base + i] = make_int4(2, k - 1, i, 0);
+            for (int q = 0; q < h->ncs[k]; ++q) rows[base + n + q] = make_int4(1, k, q, 0);
+        }
+    }
+    const long long B = sh.batch, PP = (long long)ks->P * ks->P;
+    int rc;
+    if ((rc = kalloc(h, &ks->d_prim_off, N + 1)) || (rc = kalloc(h, &ks->d_prim_dim, N + 1)) ||
+        (rc = kalloc(h, &ks->d_dual_off, N + 1)) || (rc = kalloc(h, &ks->d_gdim, N + 1)) ||
+        (rc = kalloc(h, &ks->d_ncs, N + 1)) || (rc = kalloc(h, &ks->rows, ks->dim)) || (rc = kalloc(h, &ks->pstat, B)) ||
+        (rc = kalloc(h, &ks->blk, B * (N + 1) * 6 * PP)) || (rc = kalloc(h, &ks->fac, B * (N + 1) * 2 * PP)) ||
+        (rc = kalloc(h, &ks->rhs, B * ks->dim)) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
+        return rc;
+    PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_off, ks->prim_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_dim, ks->prim_dim.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ks->d_dual_off, ks->dual_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ks->d_gdim, ks->gdim.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ks->d_ncs, h->ncs.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy(ks->rows, rows.data(), rows.size() * sizeof(int4), hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemset(ks->wv, 0, B * (N + 1) * 4 * ks->P * sizeof(double)));
+    PDPLQR_HIP_TRY(hipMemset(ks->pstat, 0, B * sizeof(int32_t)));
+    return PDPLQR_OK;
+}
+
+void kkt_release(pdplqr_handle h) {
+    delete h->kkt;
+    h->kkt = nullptr;
+}
+
+// The reference forms the KKT matrix once, in the QDLDLSolver constructor
+// (qdldl_solver.hpp:36-45): the first model upload plays that role here.
+int kkt_on_model(pdplqr_handle h) {
+    KKTState *ks = h->kkt;
+    if (ks->formed) return PDPLQR_OK;
+    const Shape &sh = h->sh;
+    KKTArgs a = kkt_args(h);
+    const size_t smem = 4 * (size_t)ks->P * ks->P * sizeof(double);
+    hipLaunchKernelGGL(k_kkt_stage, dim3((unsigned)(sh.batch * (sh.N + 1))), dim3(64), smem, h->stream, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    ks->formed = true;
+    return PDPLQR_OK;
+}
+
+int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
+               double sigma) {
+    KKTState *ks = h->kkt;
+    const Shape &sh = h->sh;
+    KKTArgs a = kkt_args(h);
+    const long long total = (long long)ks->dim * sh.batch;
+    const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_kkt_rhs, dim3(grid), dim3(256), 0, h->stream, a, ks->rows, ws, ys, zs, irho, sigma);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int kkt_backward(pdplqr_handle h, const double *inv_rho) {
+    KKTState *ks = h->kkt;
+    const Shape &sh = h->sh;
+    KKTArgs a = kkt_args(h);
+    const size_t smem = 3 * (size_t)ks->P * ks->P * sizeof(double);
+    hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
+    KKTState *ks = h->kkt;
+    const Shape &sh = h->sh;
+    KKTArgs a = kkt_args(h);
+    const size_t P = ks->P, PP = P * P;
+    const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
+    hipLaunchKernelGGL(k_kkt_x0, probs, wave, 0, h->stream, a, x0);
+    hipLaunchKernelGGL(k_kkt_solve1, stages, wave, (PP + P) * sizeof(double), h->stream, a);
+    hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
+    hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int kkt_dim(pdplqr_handle h) { return h->kkt ? h->kkt->dim : 0; }
+
+}  // namespace pdplqr

@@ -214,24 +214,29 @@ int solver_init(pdplqr_handle h) {
         case PDPLQR_SOLVER_PARALLEL:
             return parallel_init(h);
         default:
-            return unsupported("KKT solver");
+            return kkt_init(h);
     }
 }
 
 void solver_release(pdplqr_handle h) {
     delete h->par;
     h->par = nullptr;
+    kkt_release(h);
 }
 
-int solver_on_model(pdplqr_handle) { return PDPLQR_OK; }
+int solver_on_model(pdplqr_handle h) {
+    return h->cfg.solver == PDPLQR_SOLVER_KKT ? kkt_on_model(h) : PDPLQR_OK;
+}
 
 int solver_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
                   double sigma) {
+    if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_update(h, ws, ys, zs, irho, sigma);
     return launch_update_problem_data(h->sh, h->H, h->h, ws, ys, zs, irho, sigma, h->Hw, h->hw, h->gw, h->tab_s,
                                       h->tab_n, h->stream);
 }
 
 int solver_backward(pdplqr_handle h, const double *rho) {
+    if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
     int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                             h->max_nc, h->stream);
     if (rc) return rc;
@@ -248,6 +253,7 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho) {
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {
+    if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_forward(h, x0, ws);
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
     return launch_riccati_forward(h->sh, h->E, h->c, h->KD, x0, ws, h->stream);
 }

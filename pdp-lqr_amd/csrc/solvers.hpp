@@ -13,4 +13,14 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho);
 int solver_forward(pdplqr_handle h, const double *x0, double *ws);
 int solver_clear(pdplqr_handle h);
 int solver_status(pdplqr_handle h, int32_t *flags);  // per-problem status (host)
+
+// KKT solver (kkt.hip)
+int kkt_init(pdplqr_handle h);
+void kkt_release(pdplqr_handle h);
+int kkt_on_model(pdplqr_handle h);
+int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
+               double sigma);
+int kkt_backward(pdplqr_handle h, const double *inv_rho);
+int kkt_forward(pdplqr_handle h, const double *x0, double *ws);
+int kkt_dim(pdplqr_handle h);
 }  // namespace pdplqr

@@ -256,7 +256,10 @@ class QDLDLSolver(_ModelSolver):
     frozen at construction with rho_dyn = sigma = 1e-6 (qdldl_solver.hpp:38-42)."""
 
     _solver_kind = _lib.PDPLQR_SOLVER_KKT
-    _reupload_model = False
+    # form_rhs / update_rhs_initial_stage read model_ on every call
+    # (kkt.hpp:207-300); the matrix itself stays the one formed at construction
+    # (the C ABI forms it on the first model upload only).
+    _reupload_model = True
 
     def __init__(self, model: LQRModel, device: int = 0):
         self._init_handle(model, device=device, keep_factors=False, rho_dyn=1e-6, kkt_sigma=1e-6)

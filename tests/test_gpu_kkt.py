@@ -1,0 +1,166 @@
+"""GPU parity of the QDLDLSolver path (kkt.hip) against the CPU oracle's
+restatement of kkt.hpp + QDLDL (oracle/pdplqr_oracle.c) and the golden
+QDLDL-equivalent fixtures (dense KKT solve, tests/golden/make_golden.py).
+
+Tolerance: 1e-8 relative on the full primal trajectory (the KKT system is
+conditioned ~1/rho_dyn; the oracle-vs-dense pin uses the same bound), and
+u* to 1e-6 (north_star).  The GPU path factors the same matrix in QDLDL's
+elimination order (all primal pivots first, then the dual groups) with a
+block Cholesky of the condensed dual system.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, rel_err, u_parts
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-8
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0, "no HIP device visible: GPU tests must run on an MI355X"
+
+
+def _lists(pm, d):
+    from pdplqr.model import unpack_model, unpack_ws
+
+    model = unpack_model(pm)
+    n, m, N = pm.n, pm.m, pm.N
+    ws = unpack_ws(d["ws"], n, m, N)
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    cut = lambda v: [v[off[k]:off[k + 1]] for k in range(N + 1)]
+    return model, ws, cut(d["ys"]), cut(d["zs"]), cut(d["rho"]), cut(d["inv_rho"])
+
+
+def _oracle(pm, d, x0=None, forwards=1):
+    from oracle.oracle import OracleKKT
+
+    o = OracleKKT(pm)
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["inv_rho"])
+    w = None
+    for _ in range(forwards):
+        w = o.forward(d["x0"] if x0 is None else x0)
+    return w
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_qdldl_solver_matches_oracle(name):
+    from pdplqr import QDLDLSolver
+
+    pm, d = load_golden(name)
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = QDLDLSolver(model)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(irho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    w = np.concatenate(out)
+    wo = _oracle(pm, d)
+    n, m, N = pm.n, pm.m, pm.N
+    assert sol.status() == 0
+    assert rel_err(w, wo) < TOL
+    assert rel_err(u_parts(w, n, m, N), u_parts(wo, n, m, N)) < 1e-6
+    if "w_qdldl" in d:
+        assert rel_err(w, d["w_qdldl"]) < TOL
+
+
+def test_qdldl_known_answer():
+    """Quadrotor example (lqr_example.cpp): QDLDL u0[0]."""
+    from pdplqr import QDLDLSolver
+
+    pm, d = load_golden("quadrotor_N100")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = QDLDLSolver(model)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(irho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    assert abs(out[0][0] - (-2.8980026778)) < 5e-9
+
+
+def test_forward_accumulates_initial_stage_rhs():
+    """update_rhs_initial_stage adds -S0 x0, -A0 x0 into the stored rhs on
+    every forward (kkt.hpp:207-222): a second forward without a new
+    update_problem_data solves a different system -- as the reference does."""
+    from pdplqr import QDLDLSolver
+
+    pm, d = load_golden("random_n12_m4_N64_nc4")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = QDLDLSolver(model)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(irho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    sol.forward(d["x0"], out)
+    w2 = np.concatenate(out)
+    wo2 = _oracle(pm, d, forwards=2)
+    assert rel_err(w2, wo2) < TOL
+    assert rel_err(w2, _oracle(pm, d)) > 1e-6  # really a different answer
+
+
+def test_refactor_with_new_inv_rho():
+    """backward re-writes -inv_rho on the y diagonal and refactors
+    (qdldl_solver.hpp:88-109); the rest of the matrix stays frozen."""
+    from pdplqr import QDLDLSolver
+
+    pm, d = load_golden("ubox_n12_m4_N48_nc4")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = QDLDLSolver(model)
+    g = np.random.default_rng(3)
+    for it in range(3):
+        ir = [v * (0.5 + g.random(v.shape)) for v in irho]
+        sol.update_problem_data(ws, ys, zs, ir, float(d["sigma"]))
+        sol.backward(ir)
+        out = [w.copy() for w in ws]
+        sol.forward(d["x0"], out)
+        d2 = dict(d)
+        d2["inv_rho"] = np.concatenate(ir)
+        assert rel_err(np.concatenate(out), _oracle(pm, d2)) < TOL, it
+
+
+@pytest.mark.parametrize("n,m,N,batch,nc", [(12, 4, 64, 5, 4), (4, 2, 33, 3, 2), (6, 3, 20, 2, 0), (12, 4, 3, 2, 4),
+                                          (20, 6, 10, 2, 5)])
+def test_batched_kkt_matches_oracle(n, m, N, batch, nc):
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 7 * n + m + nc)
+    s = n + m
+    g = np.random.default_rng(11 + nc)
+    ncs = np.full(N + 1, nc, dtype=np.int32)
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, nc * dk)) for dk in dims], axis=1) if nc else np.zeros((batch, 0))
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+    bs.set_model(E, c, H, h, D if nc else None)
+    bs.update_problem_data(ws, ys if nc else None, zs if nc else None, irho if nc else None, sigma=1e-6)
+    bs.backward(irho if nc else None)
+    out = np.zeros((batch, N * s + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b] if nc else np.zeros(0))
+        o = OracleKKT(pm)
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        o.backward(irho[b])
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+
+
+def test_kkt_protocol():
+    from pdplqr import BatchedLQRSolver, PdplqrError
+
+    bs = BatchedLQRSolver(4, 2, 5, 1, solver="kkt")
+    with pytest.raises(PdplqrError):
+        bs.backward_without_factorization()  # QDLDLSolver has none
+    with pytest.raises(PdplqrError):
+        bs.forward(np.zeros((1, 4)), np.zeros((1, 5 * 6 + 4)))  # before backward
