@@ -160,6 +160,51 @@ def bench_single(local, dev, dist, steps=10, warmup=3):
     return res
 
 
+def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
+    """C5: conic (box-constrained u) LQ, N = 512, 12/4, nc = 4 (D = [I 0]) on
+    every stage but the terminal, batch 1024, rho = 0.1, random y, z, w-bar.
+    One ADMM inner solve = backward + forward, timed for the KKT path
+    (QDLDLSolver semantics, kkt.hip) and for the Riccati path on the same data.
+    KKT matrix formation (the QDLDLSolver constructor) is outside the timed region."""
+    from pdplqr import BatchedLQRSolver
+
+    n, m, nc = 12, 4, 4
+    s = n + m
+    E, c, H, h, x0 = gen_batch_device(n, m, N, batch, seed=555, device=dev)
+    ncs = np.array([nc] * N + [0], dtype=np.int32)
+    Dk = torch.zeros(nc, s, dtype=torch.float64, device=dev)
+    Dk[:, :m] = torch.eye(m, dtype=torch.float64, device=dev)
+    D = Dk.t().contiguous().reshape(-1).repeat(batch, N)  # column-major nc x s blocks
+    g = torch.Generator(device=dev)
+    g.manual_seed(556)
+    ny = nc * N
+    ws = torch.randn(batch, N * s + n, dtype=torch.float64, device=dev, generator=g)
+    ys = torch.randn(batch, ny, dtype=torch.float64, device=dev, generator=g)
+    zs = torch.randn(batch, ny, dtype=torch.float64, device=dev, generator=g)
+    rho = torch.full((batch, ny), 0.1, dtype=torch.float64, device=dev)
+    irho = 1.0 / rho
+    out = torch.empty(batch, N * s + n, dtype=torch.float64, device=dev)
+    res = {"N": N, "nx": n, "nu": m, "nc": nc, "batch": batch}
+    for solver in ("kkt", "serial"):
+        bs = BatchedLQRSolver(n, m, N, batch, solver=solver, ncs=ncs, device=local)
+        bs.set_model(E, c, H, h, D)
+        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+        r = irho if solver == "kkt" else rho
+
+        def step():
+            bs.backward(r)
+            bs.forward(x0, out)
+
+        t = _timed(step, steps, warmup, dev, dist)
+        ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
+        res["kkt" if solver == "kkt" else "riccati"] = {"ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
+                                                        "status_ok": ok}
+        bs.close()
+    del E, H, D
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     """C4: one N = Ntot, 24/8 problem, horizon-sharded over the ranks (strong
     scaling): shard backward -> all-gather of slice elements (RCCL when nccl)
@@ -321,6 +366,7 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_secondary:
         res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
+                            "C5_conic_kkt": bench_conic(local, dev, dist),
                             "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(n, m, N, seconds=args.cpu_seconds)
