@@ -399,6 +399,144 @@ __global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Segment backward without factorization: reduction_without_factorization
+// (lqr_solver_parallel.hpp:190-211) with ParallelLQRKernel::
+// step_without_factorization (lqr_kernel_parallel.hpp:139-168).  The cached
+// factors L_k of the last factorising backward are reused; only the linear
+// terms change: lp_k, lu'_k (into the rollout record) and the element vectors
+// p, f.  f = F_{k+1}(c + B d) + f_{k+1} (:160-165) is evaluated as what it
+// is -- the end state of the segment's closed-loop rollout from x = 0 under
+// the new feed-forward d = -Luu^{-T} lu' -- so no per-stage F_k is stored.
+// F, C, P of the element are unchanged (update_segment_data(p, f, id),
+// condensed_system.hpp:76-80).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
+    constexpr int P = 32;
+    __shared__ double Lk[P * P];  // this stage's L (dense, ld s)
+    __shared__ double Ln[P * P];  // next stage's Lxx (ld n)
+    __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P], xs[P], us[P];
+    const int lane = threadIdx.x;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
+    const long long b = blockIdx.x / S;
+    const int seg = blockIdx.x % S;
+    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
+    const bool last = (seg == S - 1) && A.last_is_terminal;
+    const long long frs = (long long)s * m + m;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.FR + b * sh.perKD;
+    const double *Lcb = A.Lc + b * sh.perHw;
+    double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
+    // segment terminal: the real one (lqr_kernel.hpp:94-101) or the dummy L = 0, lp = 0
+    if (lane < n) pn[lane] = last ? hb[(long long)sh.N * s + lane] : 0.0;
+    if (last && lpb && lane < n) lpb[(long long)sh.N * s + lane] = pn[lane];
+    for (int q = lane; q < n * n; q += 64) {
+        const int i = q % n, j = q / n;
+        Ln[q] = (last && i >= j) ? Lcb[(long long)sh.N * sh.ps + pidx(i, j, n)] : 0.0;
+    }
+    wave_sync();
+    for (int k = N1 - 1; k >= N0; --k) {
+        const double *Ek = Eb + (long long)k * n * s;
+        for (int q = lane; q < s * s; q += 64) {
+            const int i = q % s, j = q / s;
+            Lk[q] = (i >= j) ? Lcb[(long long)k * sh.ps + pidx(i, j, s)] : 0.0;
+        }
+        if (lane < n) cvec[lane] = cb[(long long)k * n + lane];
+        wave_sync();
+        if (lane < n) {  // Pb_tmp = Lxx_next^T c
+            double a = 0.0;
+            for (int t = lane; t < n; ++t) a += Ln[t + lane * n] * cvec[t];
+            va[lane] = a;
+        }
+        wave_sync();
+        if (lane < n) {  // Pb = Lxx_next Pb_tmp + p_next
+            double a = 0.0;
+            for (int t = 0; t <= lane; ++t) a += Ln[lane + t * n] * va[t];
+            vb[lane] = a + pn[lane];
+        }
+        wave_sync();
+        if (lane < s) {  // lp = h~ + E^T Pb
+            double a = 0.0;
+            for (int t = 0; t < n; ++t) a += Ek[t + lane * n] * vb[t];
+            lp[lane] = hb[(long long)k * s + lane] + a;
+        }
+        wave_sync();
+        if (lane == 0) {  // lu <- Luu^{-1} lu
+            for (int i = 0; i < m; ++i) {
+                double v = lp[i];
+                for (int j = 0; j < i; ++j) v -= Lk[i + j * s] * lp[j];
+                lp[i] = v / Lk[i + i * s];
+            }
+        }
+        wave_sync();
+        if (lane < n) {  // p -= Lxu lu
+            double a = 0.0;
+            for (int i = 0; i < m; ++i) a += Lk[(m + lane) + i * s] * lp[i];
+            const double pnew = lp[m + lane] - a;
+            lp[m + lane] = pnew;
+            pn[lane] = pnew;
+        }
+        wave_sync();
+        if (lane < m) FRb[(long long)k * frs + (long long)s * m + lane] = lp[lane];
+        if (lpb && lane < s) lpb[(long long)k * s + lane] = lp[lane];
+        for (int q = lane; q < n * n; q += 64) {
+            const int i = q % n, j = q / n;
+            Ln[q] = Lk[(m + i) + (m + j) * s];
+        }
+        wave_sync();
+    }
+    double *eo = A.elem + (b * S + seg) * (long long)(3 * n * n + 2 * n);
+    Elem e = elem_view(eo, n);
+    if (lane < n) e.p[lane] = pn[lane];
+    if (last) {
+        if (lane < n) e.f[lane] = 0.0;
+        return;
+    }
+    // f: closed-loop rollout of the segment from x = 0 (u = -Luu^{-T}(lu' + Lxu^T x))
+    if (lane < n) xs[lane] = 0.0;
+    wave_sync();
+    for (int k = N0; k < N1; ++k) {
+        const double *Ek = Eb + (long long)k * n * s;
+        const double *FRk = FRb + (long long)k * frs;  // [L(:, 0:m) | lu']
+        if (lane < m) {
+            double v = FRk[(long long)s * m + lane];
+            for (int t = 0; t < n; ++t) v += FRk[lane * s + m + t] * xs[t];
+            va[lane] = v;
+        }
+        wave_sync();
+        if (lane == 0)
+            for (int i = m - 1; i >= 0; --i) {
+                double v = va[i];
+                for (int j = i + 1; j < m; ++j) v += FRk[i * s + j] * us[j];  // Luu[j][i] u_j
+                us[i] = -v / FRk[i * s + i];
+            }
+        wave_sync();
+        double xn = 0.0;
+        if (lane < n) {
+            xn = cb[(long long)k * n + lane];
+            for (int j = 0; j < m; ++j) xn += Ek[lane + j * n] * us[j];
+            for (int t = 0; t < n; ++t) xn += Ek[lane + (m + t) * n] * xs[t];
+        }
+        wave_sync();
+        if (lane < n) xs[lane] = xn;
+        wave_sync();
+    }
+    if (lane < n) e.f[lane] = xs[lane];
+}
+
+int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
+    if (a.sh.s > 32 || !a.Lc) {
+        set_error("PARALLEL backward_without_factorization needs keep_factors = 1 and n + m <= 32");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL(k_seg_bwd_nofact, dim3((unsigned)(a.sh.batch * a.S)), dim3(64), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // One Hillis-Steele round: inclusive prefix (dir 0) or suffix (dir 1) scan.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {

@@ -44,6 +44,7 @@ struct SegFwd {
 };
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st);
+int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,

@@ -127,7 +127,9 @@ static int parallel_init(pdplqr_handle h) {
 
 // segment backward + prefix/suffix scans; `last_is_terminal` = 0 for a
 // non-final horizon shard.
-static int parallel_backward(pdplqr_handle h, int last_is_terminal) {
+static int parallel_scans(pdplqr_handle h);
+
+static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
     ParallelState *ps = h->par;
     const Shape &sh = h->sh;
     SegArgs a;
@@ -147,8 +149,16 @@ static int parallel_backward(pdplqr_handle h, int last_is_terminal) {
     a.elem = ps->elem;
     a.seg_status = ps->seg_status;
     PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, sizeof(int), h->stream));
-    int rc = launch_seg_backward(a, h->stream);
+    int rc = fact ? launch_seg_backward(a, h->stream) : launch_seg_backward_nofact(a, h->stream);
     if (rc) return rc;
+    return parallel_scans(h);
+}
+
+// inclusive prefix / suffix scans of the segment elements (log2 S rounds)
+static int parallel_scans(pdplqr_handle h) {
+    ParallelState *ps = h->par;
+    const Shape &sh = h->sh;
+    int rc;
     const double *pin = ps->elem, *sin = ps->elem;
     double *preo[2] = {ps->bufA, ps->bufB};
     if (!h->suf_bufs[0]) {  // suffix ping-pong buffers, allocated on first use
@@ -240,15 +250,19 @@ int solver_backward(pdplqr_handle h, const double *rho) {
     int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                             h->max_nc, h->stream);
     if (rc) return rc;
-    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1);
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) {
+        h->shard_last = 1;
+        return parallel_backward(h, 1);
+    }
     return launch_riccati_backward(riccati_args(h), h->stream);
 }
 
 int solver_backward_nofact(pdplqr_handle h, const double *rho) {
-    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return unsupported("PARALLEL backward_without_factorization");
     int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 0,
                             h->max_nc, h->stream);
     if (rc) return rc;
+    // LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154)
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, h->shard_last, false);
     return launch_riccati_backward_nofact(riccati_args(h), h->stream);
 }
 

@@ -119,3 +119,43 @@ def test_batched_parallel_matches_oracle(n, m, N, batch, seglen):
         o.update_problem_data(ws0[b], None, None, None, 1e-6)
         o.backward(None)
         assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+
+
+@pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40",
+                                  "ubox_n12_m4_N48_nc4"])
+@pytest.mark.parametrize("ns,condensed,seglen", [(4, "CHOLESKY", 0), (2, "LU", 5), (8, "CHOLESKY", 3)])
+def test_parallel_backward_without_factorization(name, ns, condensed, seglen):
+    """LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:
+    148-154,190-211): after a factorising backward, new linear data (w-bar, y, z)
+    with the same rho reuses the cached factors; the solution equals a fresh full
+    solve of the new data (oracle, serial refactor)."""
+    from oracle.oracle import OracleSerial, segmentation
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+    from pdplqr.model import unpack_ws
+
+    pm, d = load_golden(name)
+    if not segmentation(pm.N, ns, True)[0]:
+        pytest.skip("empty segment")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRParallelSolver(model, ns, True, CondensedSystemSolverType[condensed], segment_len=seglen)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    g = np.random.default_rng(5)
+    ws2 = d["ws"] + 0.1 * g.standard_normal(d["ws"].shape)
+    zs2 = d["zs"] + 0.1 * g.standard_normal(d["zs"].shape)
+    ys2 = d["ys"] + 0.1 * g.standard_normal(d["ys"].shape)
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    sl = lambda v: [v[off[k]:off[k + 1]] for k in range(pm.N + 1)]
+    for it in range(2):  # twice: the second reuse starts from a nofact state
+        sol.update_problem_data(unpack_ws(ws2, pm.n, pm.m, pm.N), sl(ys2), sl(zs2), irho, float(d["sigma"]))
+        sol.backward_without_factorization(rho)
+        out = [w.copy() for w in ws]
+        sol.forward(d["x0"], out)
+        o = OracleSerial(pm)
+        o.update_problem_data(ws2, ys2, zs2, d["inv_rho"], float(d["sigma"]))
+        o.backward(d["rho"])
+        ref = o.forward(d["x0"])
+        assert rel_err(np.concatenate(out), ref) < TOL, it
+        ws2 = ws2 + 0.05 * g.standard_normal(ws2.shape)
