@@ -1,0 +1,154 @@
+// clqr/detail/bridge.hpp -- glue between the C++ facade (clqr/lqr/*.hpp) and
+// the C ABI of libpdplqr (pdplqr.h): model packing into the boundary layout,
+// stage-vector flattening, RAII over pdplqr_handle, error translation.
+#pragma once
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "clqr/lqr_model.hpp"
+#include "pdplqr.h"
+
+namespace lqr {
+namespace detail {
+
+// C ABI status -> exception (the reference throws std::runtime_error)
+inline void check(int rc, const char *what) {
+    if (rc != PDPLQR_OK) {
+        const char *msg = pdplqr_last_error();
+        throw std::runtime_error(std::string(what) + ": " + (msg && *msg ? msg : "pdplqr error ") +
+                                 " (status " + std::to_string(rc) + ")");
+    }
+}
+
+template <typename Dense>
+inline void append(std::vector<double> &dst, const Dense &a) {
+    const size_t k = static_cast<size_t>(a.size());
+    if (k) dst.insert(dst.end(), a.data(), a.data() + k);
+}
+
+// The model in the boundary layout of pdplqr.h (Eigen column-major blocks,
+// stage-major): E [N][n s], c [N][n], H [N][s s] + [n n], h [N][s] + [n],
+// D ragged [nc_k x dim_k].  Node k of the model is nodes[k].
+struct PackedModel {
+    std::vector<double> E, c, H, h, D;
+
+    void pack(const LQRModel &model) {
+        const int N = model.N;
+        if (static_cast<int>(model.nodes.size()) != N + 1)
+            throw std::runtime_error("LQRModel: expected N + 1 nodes, got " + std::to_string(model.nodes.size()));
+        E.clear();
+        c.clear();
+        H.clear();
+        h.clear();
+        D.clear();
+        for (int k = 0; k <= N; ++k) {
+            const Node &nd = model.nodes[static_cast<size_t>(k)];
+            if (k < N) {
+                append(E, nd.E);
+                append(c, nd.c);
+            }
+            append(H, nd.H);
+            append(h, nd.h);
+            if (nd.n_con > 0) append(D, nd.D_con);
+        }
+    }
+};
+
+// stage vectors (ws: s per stage, n at N; ys / zs / rho: nc_k per stage) <-> flat
+inline void flatten(const std::vector<VectorXs> &v, std::vector<double> &out) {
+    out.clear();
+    for (const VectorXs &x : v) append(out, x);
+}
+
+inline void unflatten_ws(const std::vector<double> &flat, std::vector<VectorXs> &ws, int n, int m, int N) {
+    if (static_cast<int>(ws.size()) < N + 1) throw std::runtime_error("forward: ws must hold N + 1 vectors");
+    const int s = n + m;
+    for (int k = 0; k <= N; ++k) {
+        VectorXs &w = ws[static_cast<size_t>(k)];
+        const int len = k < N ? s : n;
+        if (w.size() != len) w.resize(len);
+        std::memcpy(w.data(), flat.data() + static_cast<size_t>(k) * s, sizeof(double) * static_cast<size_t>(len));
+    }
+}
+
+// One pdplqr_handle of the requested solver kind for this model (batch 1).
+class Handle {
+public:
+    Handle(const LQRModel &model, int solver, int num_segments = 1, bool load_balancing = true, int condensed = 1,
+           bool keep_factors = true) {
+        pdplqr_config cfg;
+        pdplqr_config_init(&cfg);
+        cfg.nx = model.n;
+        cfg.nu = model.m;
+        cfg.N = model.N;
+        cfg.solver = solver;
+        cfg.num_segments = num_segments;
+        cfg.load_balancing = load_balancing ? 1 : 0;
+        cfg.condensed_type = condensed;
+        cfg.keep_factors = keep_factors ? 1 : 0;
+        ncs_.assign(model.ncs.begin(), model.ncs.end());
+        cfg.ncs = ncs_.data();
+        check(pdplqr_create(&cfg, &h_), "pdplqr_create");
+        n_ = model.n;
+        m_ = model.m;
+        N_ = model.N;
+    }
+    ~Handle() { pdplqr_destroy(h_); }
+    Handle(const Handle &) = delete;
+    Handle &operator=(const Handle &) = delete;
+
+    void upload(const LQRModel &model) {
+        packed_.pack(model);
+        check(pdplqr_set_model(h_, packed_.E.data(), packed_.c.data(), packed_.H.data(), packed_.h.data(),
+                               packed_.D.empty() ? nullptr : packed_.D.data(), PDPLQR_MEM_HOST),
+              "set_model");
+    }
+
+    void update(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys, const std::vector<VectorXs> &zs,
+                const std::vector<VectorXs> &inv_rho, scalar sigma) {
+        flatten(ws, w_);
+        flatten(ys, y_);
+        flatten(zs, z_);
+        flatten(inv_rho, r_);
+        check(pdplqr_update_problem_data(h_, w_.data(), nz(y_), nz(z_), nz(r_), sigma, PDPLQR_MEM_HOST),
+              "update_problem_data");
+    }
+
+    void backward(const std::vector<VectorXs> &rho, bool factorize) {
+        flatten(rho, r_);
+        check(factorize ? pdplqr_backward(h_, nz(r_), PDPLQR_MEM_HOST)
+                        : pdplqr_backward_without_factorization(h_, nz(r_), PDPLQR_MEM_HOST),
+              factorize ? "backward" : "backward_without_factorization");
+    }
+
+    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) {
+        if (x0.size() != n_) throw std::runtime_error("forward: x0 has the wrong size");
+        w_.assign(static_cast<size_t>(N_) * (n_ + m_) + n_, 0.0);
+        check(pdplqr_forward(h_, x0.data(), w_.data(), PDPLQR_MEM_HOST), "forward");
+        unflatten_ws(w_, ws, n_, m_, N_);
+    }
+
+    void clear() { check(pdplqr_clear_workspace(h_), "clear_workspace"); }
+
+    int status() {
+        int32_t st = 0;
+        check(pdplqr_get_status(h_, &st), "get_status");
+        return st;
+    }
+
+    pdplqr_handle raw() const { return h_; }
+
+private:
+    static const double *nz(const std::vector<double> &v) { return v.empty() ? nullptr : v.data(); }
+    pdplqr_handle h_ = nullptr;
+    int n_ = 0, m_ = 0, N_ = 0;
+    std::vector<int32_t> ncs_;
+    PackedModel packed_;
+    std::vector<double> w_, y_, z_, r_;
+};
+
+}  // namespace detail
+}  // namespace lqr

@@ -1,0 +1,60 @@
+// clqr/lqr/lqr_solver_parallel.hpp -- parallel (segmented) Riccati facade (MI355X).
+//
+// Public surface of the reference's LQRParallelSolver
+// (include/clqr/lqr/lqr_solver_parallel.hpp:19-238): the horizon is cut into
+// num_segments segments (alpha = 1.55 with load_balancing), each segment is
+// summarised as an element (F, C, f, P, p) and the segments are coupled by the
+// condensed system.  On the GPU every reference segment is further split into
+// sub-segments and the condensed system becomes an associative prefix/suffix
+// scan; CondensedSystemSolverType is accepted and validated as in the
+// reference.  The OpenMP team / core pinning of the reference has no analogue.
+#pragma once
+
+#include <stdexcept>
+#include <vector>
+
+#include "clqr/detail/bridge.hpp"
+
+namespace lqr {
+
+enum class CondensedSystemSolverType { LU = PDPLQR_CONDENSED_LU, CHOLESKY = PDPLQR_CONDENSED_CHOLESKY };
+
+class LQRParallelSolver {
+public:
+    LQRParallelSolver(const LQRModel &model, int num_segments, bool load_balancing = true,
+                      CondensedSystemSolverType solver_type = CondensedSystemSolverType::CHOLESKY)
+        : model_(model),
+          hd_(model, PDPLQR_SOLVER_PARALLEL, num_segments, load_balancing, static_cast<int>(solver_type), true),
+          num_segments_(num_segments) {
+        hd_.upload(model_);
+    }
+
+    void update_problem_data(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys,
+                             const std::vector<VectorXs> &zs, const std::vector<VectorXs> &inv_rho_vecs,
+                             const scalar sigma) {
+        hd_.upload(model_);
+        hd_.update(ws, ys, zs, inv_rho_vecs, sigma);
+    }
+
+    void backward(const std::vector<VectorXs> &rho_vecs) { hd_.backward(rho_vecs, true); }
+    void backward_without_factorization(const std::vector<VectorXs> &rho_vecs) { hd_.backward(rho_vecs, false); }
+    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) { hd_.forward(x0, ws); }
+    void clear_workspace() { hd_.clear(); }
+
+    int num_segments() const { return num_segments_; }
+
+    // segment boundaries of the reference segmentation (idx_start, Nseg)
+    void segments(std::vector<int> &idx_start, std::vector<int> &Nseg) const {
+        std::vector<int32_t> a(static_cast<size_t>(num_segments_)), b(static_cast<size_t>(num_segments_));
+        detail::check(pdplqr_get_segments(hd_.raw(), a.data(), b.data()), "get_segments");
+        idx_start.assign(a.begin(), a.end());
+        Nseg.assign(b.begin(), b.end());
+    }
+
+private:
+    const LQRModel &model_;
+    detail::Handle hd_;
+    int num_segments_;
+};
+
+}  // namespace lqr

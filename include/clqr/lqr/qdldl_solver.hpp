@@ -1,0 +1,46 @@
+// clqr/lqr/qdldl_solver.hpp -- KKT + LDL^T solver facade (MI355X).
+//
+// Public surface of the reference's QDLDLSolver
+// (include/clqr/lqr/qdldl_solver.hpp:14-151).  The KKT matrix of kkt.hpp is
+// formed once, at construction, with rho_dyn = sigma = 1e-6; backward takes
+// the INVERSE rho vectors and refactors; forward adds -S0 x0, -A0 x0 to the
+// stored right-hand side (accumulating, as kkt.hpp:207-222) and solves.  The
+// factorisation is libpdplqr's block LDL^T in QDLDL's elimination order
+// (csrc/kkt.hip), not the QDLDL library.
+#pragma once
+
+#include <stdexcept>
+#include <vector>
+
+#include "clqr/detail/bridge.hpp"
+
+namespace lqr {
+
+class QDLDLSolver {
+public:
+    explicit QDLDLSolver(const LQRModel &model)
+        : model_(model), hd_(model, PDPLQR_SOLVER_KKT, 1, true, PDPLQR_CONDENSED_CHOLESKY, false) {
+        hd_.upload(model_);  // forms the KKT system (the reference's constructor)
+    }
+
+    void update_problem_data(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys,
+                             const std::vector<VectorXs> &zs, const std::vector<VectorXs> &inv_rho_vecs,
+                             const scalar sigma) {
+        hd_.upload(model_);  // form_rhs reads h, c of the current model; the matrix stays frozen
+        hd_.update(ws, ys, zs, inv_rho_vecs, sigma);
+    }
+
+    void backward(const std::vector<VectorXs> &inv_rho_vecs) {
+        hd_.backward(inv_rho_vecs, true);
+        if (hd_.status() != 0)
+            throw std::runtime_error("QDLDL factorization failed with status: " + std::to_string(hd_.status()));
+    }
+
+    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) { hd_.forward(x0, ws); }
+
+private:
+    const LQRModel &model_;
+    detail::Handle hd_;
+};
+
+}  // namespace lqr

@@ -1,0 +1,102 @@
+"""The C++ drop-in surface (include/clqr/...): a downstream CMake project
+(tests/cpp/CMakeLists.txt) finds the package with find_package(pdpLQR), builds
+facade_check.cpp -- which sets up an lqr::LQRModel node by node and drives
+LQRSolver / LQRParallelSolver / QDLDLSolver like reference user code -- and
+links libpdplqr.so.  The build is checked on CPU; the solves run on the GPU and
+are compared with the oracle (same tolerances as the Python-facade tests)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_golden, rel_err
+
+CPP = os.path.join(ROOT, "tests", "cpp")
+
+
+def _have_lib():
+    return os.path.exists(os.path.join(ROOT, "pdp-lqr_amd", "pdplqr", "libpdplqr.so"))
+
+
+@pytest.fixture(scope="module")
+def facade_bin(tmp_path_factory):
+    if shutil.which("cmake") is None or not _have_lib():
+        pytest.skip("cmake or libpdplqr.so missing")
+    bd = tmp_path_factory.mktemp("cpp_build")
+    cfg = subprocess.run(["cmake", "-S", CPP, "-B", str(bd), f"-DpdpLQR_DIR={ROOT}/cmake"], capture_output=True,
+                         text=True, timeout=300)
+    assert cfg.returncode == 0, cfg.stdout + cfg.stderr
+    bld = subprocess.run(["cmake", "--build", str(bd), "-j4"], capture_output=True, text=True, timeout=600)
+    assert bld.returncode == 0, bld.stdout + bld.stderr
+    exe = os.path.join(str(bd), "facade_check")
+    assert os.path.exists(exe)
+    return exe
+
+
+def test_facade_builds_with_find_package(facade_bin):
+    """find_package(pdpLQR) + pdpLQR::pdpLQR: headers compile without Eigen, the
+    executable links against libpdplqr.so (no GPU needed)."""
+    assert os.access(facade_bin, os.X_OK)
+
+
+def _write_problem(path, pm, d):
+    with open(path, "wb") as f:
+        np.array([pm.n, pm.m, pm.N], dtype="<i4").tofile(f)
+        np.asarray(pm.ncs, dtype="<i4").tofile(f)
+        for a in (pm.E, pm.c, pm.H, pm.h, pm.D, d["x0"], np.array([float(d["sigma"])]), d["ws"], d["ys"], d["zs"],
+                  d["rho"], d["inv_rho"]):
+            np.asarray(a, dtype="<f8").ravel().tofile(f)
+
+
+def _run(exe, tmp, name, args):
+    pm, d = load_golden(name)
+    prob, out = os.path.join(tmp, name + ".bin"), os.path.join(tmp, name + ".out")
+    _write_problem(prob, pm, d)
+    r = subprocess.run([exe, prob, out] + args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return pm, d, np.fromfile(out, dtype="<f8")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["quadrotor_N100", "random_n12_m4_N64_nc4", "random_n24_m8_N40",
+                                  "quadrotor_N30_constrained"])
+@pytest.mark.parametrize("args", [["serial"], ["parallel", "4", "CHOLESKY"], ["parallel", "2", "LU"], ["qdldl"]])
+def test_cpp_facade_matches_oracle(facade_bin, tmp_path, name, args):
+    from oracle.oracle import OracleKKT, OracleParallel, OracleSerial, segmentation
+
+    pm, d = load_golden(name)
+    if args[0] == "parallel" and not segmentation(pm.N, int(args[1]), True)[0]:
+        pytest.skip("empty segment")
+    pm, d, w = _run(facade_bin, str(tmp_path), name, args)
+    if args[0] == "qdldl":
+        o = OracleKKT(pm)
+        o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+        o.backward(d["inv_rho"])
+        tol = 1e-8
+    else:
+        o = OracleSerial(pm) if args[0] == "serial" else OracleParallel(pm, int(args[1]), True, args[2])
+        o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+        o.backward(d["rho"])
+        tol = 1e-9
+    assert rel_err(w, o.forward(d["x0"])) < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["serial", "nofact"], ["parallel", "4", "CHOLESKY", "nofact"]])
+def test_cpp_facade_backward_without_factorization(facade_bin, tmp_path, args):
+    from oracle.oracle import OracleSerial
+
+    pm, d, w = _run(facade_bin, str(tmp_path), "random_n12_m4_N64_nc4", args)
+    o = OracleSerial(pm)
+    o.update_problem_data(d["ws"] + 0.1, d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    assert rel_err(w, o.forward(d["x0"])) < 1e-9
+
+
+@pytest.mark.gpu
+def test_cpp_facade_example_kat(facade_bin, tmp_path):
+    """lqr_example.cpp's quadrotor through the C++ facade: u0 = -2.8980566697 (x4)."""
+    pm, d, w = _run(facade_bin, str(tmp_path), "quadrotor_N100", ["serial"])
+    assert np.allclose(w[:4], [-2.8980566697, 2.8980566697, -2.8980566697, 2.8980566697], rtol=0, atol=5e-10)
