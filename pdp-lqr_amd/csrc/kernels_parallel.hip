@@ -16,83 +16,17 @@
 //         p = p_a + F_a^T Z^T (p_b + P_b f_a).
 //     The reference folds the same operator serially on the master thread
 //     (condensed_system.hpp:82-137 LU form, :203-290 Cholesky form); here
-//     P_b Z = Y = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b), an SPD solve.
+//     P_b Z = Y = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b), an SPD solve,
+//     evaluated on MFMA tiles (combine_tiles.hpp).
 //   * k_seg_boundary: x_hat_i = (I + C_pre P_suf)^{-1}(F_pre x0 + f_pre - C_pre p_suf)
 //     and u_hat_i = p_suf(i+1) + P_suf(i+1) x_hat_{i+1} (condensed forward).
 //   * the rollout reuses k_riccati_fwd with the G_k u_hat coupling
 //     (lqr_kernel_parallel.hpp:195-198).
+#include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
 
 namespace pdplqr {
-
-// ---------------------------------------------------------------------------
-// Wave-level dense helpers on n x n (n <= 32) column-major matrices in LDS.
-// Every lane of the (single-wave) workgroup participates; callers separate
-// dependent phases with wave_sync().
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void wm_gemm(double *C, const double *A, bool tA, const double *B, bool tB, int n,
-                                        double alpha, const double *Cadd, int lane) {
-    for (int idx = lane; idx < n * n; idx += 64) {
-        const int i = idx % n, j = idx / n;
-        double acc = 0.0;
-        for (int k = 0; k < n; ++k) {
-            const double a = tA ? A[k + i * n] : A[i + k * n];
-            const double b = tB ? B[j + k * n] : B[k + j * n];
-            acc = __builtin_fma(a, b, acc);
-        }
-        C[idx] = alpha * acc + (Cadd ? Cadd[idx] : 0.0);
-    }
-}
-
-// y = op(A) x (+ yadd), n-vector
-__device__ __forceinline__ void wm_gemv(double *y, const double *A, bool tA, const double *x, int n, double alpha,
-                                        const double *yadd, int lane) {
-    for (int i = lane; i < n; i += 64) {
-        double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc = __builtin_fma(tA ? A[k + i * n] : A[i + k * n], x[k], acc);
-        y[i] = alpha * acc + (yadd ? yadd[i] : 0.0);
-    }
-}
-
-// L = chol(A) (lower, zero upper); returns false if a pivot is not positive.
-__device__ __forceinline__ bool wm_chol(double *L, const double *A, int n, int lane) {
-    for (int idx = lane; idx < n * n; idx += 64) L[idx] = A[idx];
-    wave_sync();
-    bool ok = true;
-    for (int j = 0; j < n; ++j) {
-        const double djj = L[j + j * n];
-        ok = ok && (djj > 0.0);
-        const double d = sqrt(djj);
-        wave_sync();
-        for (int i = j + 1 + lane; i < n; i += 64) L[i + j * n] /= d;
-        if (lane == 0) L[j + j * n] = d;
-        wave_sync();
-        const int r = n - j - 1;
-        for (int q = lane; q < r * r; q += 64) {
-            const int i = j + 1 + q % r, k = j + 1 + q / r;
-            if (i >= k) L[i + k * n] -= L[i + j * n] * L[k + j * n];
-        }
-        wave_sync();
-    }
-    for (int idx = lane; idx < n * n; idx += 64) {
-        const int i = idx % n, j = idx / n;
-        if (i < j) L[idx] = 0.0;
-    }
-    wave_sync();
-    return ok;
-}
-
-// X = L^{-1} B (L lower), columns of B in parallel; X may alias B.
-__device__ __forceinline__ void wm_trsm_lower(double *X, const double *L, const double *B, int n, int lane) {
-    for (int j = lane; j < n; j += 64) {
-        for (int i = 0; i < n; ++i) {
-            double v = B[i + j * n];
-            for (int k = 0; k < i; ++k) v -= L[i + k * n] * X[k + j * n];
-            X[i + j * n] = v / L[i + i * n];
-        }
-    }
-}
 
 // Element views: [F | C | f | P | p] packed contiguously (3 n^2 + 2 n doubles)
 struct Elem {
@@ -112,93 +46,6 @@ __device__ __forceinline__ Elem elem_view(double *base, int n) {
 __device__ __forceinline__ void elem_copy(double *dst, const double *src, int n, int lane) {
     const int sz = 3 * n * n + 2 * n;
     for (int q = lane; q < sz; q += 64) dst[q] = src[q];
-}
-
-// Workspace of one combine: 8 n x n matrices + 4 n-vectors in LDS.
-struct CombineWs {
-    double *R, *X1, *X2, *X3, *Y, *Z, *X4, *X5, *v1, *v2, *v3, *v4;
-};
-
-__device__ __forceinline__ CombineWs combine_ws(double *base, int n) {
-    CombineWs w;
-    const int nn = n * n;
-    w.R = base; w.X1 = base + nn; w.X2 = base + 2 * nn; w.X3 = base + 3 * nn;
-    w.Y = base + 4 * nn; w.Z = base + 5 * nn; w.X4 = base + 6 * nn; w.X5 = base + 7 * nn;
-    w.v1 = base + 8 * nn; w.v2 = w.v1 + n; w.v3 = w.v2 + n; w.v4 = w.v3 + n;
-    return w;
-}
-static constexpr int kCombineWsDoubles(int n) { return 8 * n * n + 4 * n; }
-
-// Y = P_b Z = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b); Z = I - C_a Y.
-// Returns false when P_b or the SPD core is not positive definite.
-__device__ __forceinline__ bool combine_core(const double *Ca, const double *Pb, CombineWs &w, int n, int lane) {
-    bool ok = wm_chol(w.R, Pb, n, lane);                 // R
-    wm_gemm(w.X1, Ca, false, w.R, false, n, 1.0, nullptr, lane);  // X1 = C_a R
-    wave_sync();
-    wm_gemm(w.X2, w.R, true, w.X1, false, n, 1.0, nullptr, lane);  // X2 = R^T C_a R
-    wave_sync();
-    for (int i = lane; i < n; i += 64) w.X2[i + i * n] += 1.0;     // S = I + R^T C_a R
-    wave_sync();
-    ok = wm_chol(w.X3, w.X2, n, lane) && ok;             // Ls = chol(S)
-    // U = Ls^{-1} R^T
-    for (int idx = lane; idx < n * n; idx += 64) {
-        const int i = idx % n, j = idx / n;
-        w.X1[idx] = w.R[j + i * n];
-    }
-    wave_sync();
-    wm_trsm_lower(w.X1, w.X3, w.X1, n, lane);
-    wave_sync();
-    wm_gemm(w.Y, w.X1, true, w.X1, false, n, 1.0, nullptr, lane);  // Y = U^T U
-    wave_sync();
-    wm_gemm(w.Z, Ca, false, w.Y, false, n, -1.0, nullptr, lane);   // Z = -C_a Y
-    wave_sync();
-    for (int i = lane; i < n; i += 64) w.Z[i + i * n] += 1.0;       // Z = I - C_a Y
-    wave_sync();
-    return ok;
-}
-
-// out = a (x) b, a earlier, b later.  `need_Pp` = compute P, p; `need_FCf` = compute F, C, f.
-__device__ __forceinline__ bool elem_combine(double *out, const double *ab, const double *bb, CombineWs &w, int n,
-                                             bool need_FCf, bool need_Pp, int lane) {
-    Elem a = elem_view(const_cast<double *>(ab), n), b = elem_view(const_cast<double *>(bb), n),
-         o = elem_view(out, n);
-    const bool ok = combine_core(a.C, b.P, w, n, lane);
-    if (need_FCf) {
-        wm_gemm(w.X4, w.Z, false, a.F, false, n, 1.0, nullptr, lane);     // Z F_a
-        wm_gemm(w.X5, w.Z, false, a.C, false, n, 1.0, nullptr, lane);     // Z C_a
-        for (int i = lane; i < n; i += 64) {                               // v1 = f_a - C_a p_b
-            double acc = 0.0;
-            for (int k = 0; k < n; ++k) acc = __builtin_fma(a.C[i + k * n], b.p[k], acc);
-            w.v1[i] = a.f[i] - acc;
-        }
-        wave_sync();
-        wm_gemm(o.F, b.F, false, w.X4, false, n, 1.0, nullptr, lane);     // F = F_b Z F_a
-        wm_gemm(w.X1, w.X5, false, b.F, true, n, 1.0, nullptr, lane);     // Z C_a F_b^T
-        wm_gemv(w.v2, w.Z, false, w.v1, n, 1.0, nullptr, lane);           // Z (f_a - C_a p_b)
-        wave_sync();
-        wm_gemm(w.X3, b.F, false, w.X1, false, n, 1.0, b.C, lane);        // C = F_b Z C_a F_b^T + C_b
-        wm_gemv(o.f, b.F, false, w.v2, n, 1.0, b.f, lane);                // f = F_b v2 + f_b
-        wave_sync();
-        for (int idx = lane; idx < n * n; idx += 64) {                    // symmetrise C
-            const int i = idx % n, j = idx / n;
-            o.C[idx] = 0.5 * (w.X3[idx] + w.X3[j + i * n]);
-        }
-    }
-    if (need_Pp) {
-        wm_gemm(w.X4, w.Y, false, a.F, false, n, 1.0, nullptr, lane);     // Y F_a
-        wm_gemv(w.v3, b.P, false, a.f, n, 1.0, b.p, lane);                // v3 = p_b + P_b f_a
-        wave_sync();
-        wm_gemm(w.X5, a.F, true, w.X4, false, n, 1.0, a.P, lane);         // P = P_a + F_a^T Y F_a
-        wm_gemv(w.v4, w.Z, true, w.v3, n, 1.0, nullptr, lane);            // Z^T v3
-        wave_sync();
-        wm_gemv(o.p, a.F, true, w.v4, n, 1.0, a.p, lane);                 // p = p_a + F_a^T Z^T v3
-        for (int idx = lane; idx < n * n; idx += 64) {
-            const int i = idx % n, j = idx / n;
-            o.P[idx] = 0.5 * (w.X5[idx] + w.X5[j + i * n]);
-        }
-    }
-    wave_sync();
-    return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -539,8 +386,9 @@ int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // One Hillis-Steele round: inclusive prefix (dir 0) or suffix (dir 1) scan.
 // ---------------------------------------------------------------------------
+template <int T>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
-    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    __shared__ CombSmem<T> sm;
     const int lane = threadIdx.x;
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
@@ -549,8 +397,6 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     const int dir = rem / S, i = rem % S;
     const double *in = (dir == 0 ? A.pre_in : A.suf_in) + b * (long long)S * es;
     double *out = (dir == 0 ? A.pre_out : A.suf_out) + b * (long long)S * es;
-    double *ea = dyn, *eb = dyn + es, *eo = dyn + 2 * es;
-    CombineWs w = combine_ws(dyn + 3 * es, n);
     int ia, ib;
     if (dir == 0) {  // pre_i = pre_{i-d} (x) pre_i
         if (i - d < 0) {
@@ -565,15 +411,12 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
         }
         ia = i; ib = i + d;
     }
-    elem_copy(ea, in + (long long)ia * es, n, lane);
-    elem_copy(eb, in + (long long)ib * es, n, lane);
-    wave_sync();
     // Both directions need full elements: the next round's combine reads the
     // right operand's P, p (Z = (I + C_a P_b)^{-1}).  A suffix ending at the
     // real terminal has F = C = f = 0.
-    const bool ok = elem_combine(eo, ea, eb, w, n, true, true, lane);
+    const bool ok = tcombine<T>(out + (long long)i * es, in + (long long)ia * es, in + (long long)ib * es, n, true,
+                                true, sm, lane);
     if (!ok && lane == 0) atomicOr(A.flag, 1);
-    elem_copy(out + (long long)i * es, eo, n, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -581,15 +424,16 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
 // with a global prefix) and the suffix (optionally right-folded with a global
 // suffix); u_hat_i in a second pass.
 // ---------------------------------------------------------------------------
+template <int T>
 __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
+    __shared__ CombSmem<T> sm;
     const int lane = threadIdx.x;
     const int n = A.n, S = A.S;
     const int es = 3 * n * n + 2 * n;
     const long long b = blockIdx.x / (S + 1);
     const int i = blockIdx.x % (S + 1);  // i == S: state after the last segment (shard mode)
     double *pre = dyn, *suf = dyn + es, *tmp = dyn + 2 * es;  // tmp + es: combine output
-    CombineWs w = combine_ws(dyn + 4 * es, n);
     const double *preb = A.pre + b * (long long)S * es;
     const double *sufb = A.suf + b * (long long)S * es;
     // prefix before segment i: global_left (x) pre_{i-1}
@@ -610,7 +454,7 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
             elem_copy(tmp, A.left + b * (long long)es, n, lane);
             elem_copy(suf, preb + (long long)(i - 1) * es, n, lane);  // scratch
             wave_sync();
-            elem_combine(pre, tmp, suf, w, n, true, false, lane);
+            tcombine<T>(pre, tmp, suf, n, true, false, sm, lane);
         } else {
             elem_copy(pre, preb + (long long)(i - 1) * es, n, lane);
             wave_sync();
@@ -624,7 +468,7 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
             elem_copy(suf, A.right + b * (long long)es, n, lane);
             wave_sync();
             double *o = tmp + es;  // scratch beyond tmp: pre | suf | tmp | tmp2 fit in 4 es (see launcher)
-            elem_combine(o, tmp, suf, w, n, false, true, lane);
+            tcombine<T>(o, tmp, suf, n, false, true, sm, lane);
             elem_copy(suf, o, n, lane);
             wave_sync();
         } else {
@@ -644,7 +488,7 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
     if (lane < n) x0[lane] = A.x0[b * n + lane];
     wave_sync();
     // rhs = F_pre x0 + f_pre - C_pre p_suf
-    double *rhs = w.v1;
+    double *rhs = tmp + es;  // scratch (the fold output is consumed)
     for (int r = lane; r < n; r += 64) {
         double acc = P.f[r];
         for (int k = 0; k < n; ++k) acc = __builtin_fma(P.F[r + k * n], x0[k], acc);
@@ -655,23 +499,40 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
     wave_sync();
     double *xh = A.xhat + (b * (long long)(S + 1) + i) * n;
     if (have_suf) {
-        // x = (I + C_pre P_suf)^{-1} rhs = Z rhs with Z from combine_core(C_pre, P_suf)
-        const bool ok = combine_core(P.C, Sf.P, w, n, lane);
+        // x = (I + C_pre P_suf)^{-1} rhs = Z rhs with Z from comb_core(C_pre, P_suf)
+        constexpr int PL = 16 * T + 1;
+        WM<T> Ca, Y, Z, Zt;
+        wm_load(Ca, P.C, n, n, false, 0.0, lane >> 4, lane & 15);
+        const bool ok = comb_core(Y, Z, Zt, Ca, Sf.P, n, sm, lane);
         if (!ok && lane == 0) atomicOr(A.flag, 2);
-        wm_gemv(w.v2, w.Z, false, rhs, n, 1.0, nullptr, lane);
+        wm_store(Z, sm.A, PL, n, lane >> 4, lane & 15);
         wave_sync();
-        if (lane < n) xh[lane] = w.v2[lane];
+        lds_mv(sm.v2, sm.A, PL, false, rhs, nullptr, 1.0, n, lane);
+        wave_sync();
+        if (lane < n) xh[lane] = sm.v2[lane];
         // costate at the start of segment i: lambda = P_suf x + p_suf (stored for u_hat_{i-1})
         double *lam = A.lam + (b * (long long)(S + 1) + i) * n;
         wave_sync();
         for (int r = lane; r < n; r += 64) {
             double acc = Sf.p[r];
-            for (int k = 0; k < n; ++k) acc = __builtin_fma(Sf.P[r + k * n], w.v2[k], acc);
+            for (int k = 0; k < n; ++k) acc = __builtin_fma(Sf.P[r + k * n], sm.v2[k], acc);
             lam[r] = acc;
         }
     } else {
         if (lane < n) xh[lane] = rhs[lane];
     }
+}
+
+// Resident segment waves the device can hold for this shape: CUs x the
+// segment backward's occupancy.  Refining the horizon beyond that adds scan
+// rounds without adding parallelism.
+int seg_backward_slots(const Shape &sh, int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    hipError_t e = sh.s <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<1>, 64, 0)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<2>, 64, 0);
+    if (e != hipSuccess || per <= 0) per = 1;
+    return cus * per;
 }
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st) {
@@ -686,20 +547,26 @@ int launch_seg_backward(const SegArgs &a, hipStream_t st) {
     return PDPLQR_OK;
 }
 
-static size_t combine_smem(int n, int elems) {
-    return (size_t)(elems * (3 * n * n + 2 * n) + kCombineWsDoubles(n)) * sizeof(double);
-}
+static size_t elems_smem(int n, int elems) { return (size_t)elems * (3 * n * n + 2 * n) * sizeof(double); }
+
+static int tile_order(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 0); }
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * 2 * a.S)), blk(64);
-    hipLaunchKernelGGL(k_seg_scan, grid, blk, combine_smem(a.n, 3), st, a);
+    const int T = tile_order(a.n);
+    if (T == 1) hipLaunchKernelGGL(k_seg_scan<1>, grid, blk, 0, st, a);
+    else if (T == 2) hipLaunchKernelGGL(k_seg_scan<2>, grid, blk, 0, st, a);
+    else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
 
 int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
-    hipLaunchKernelGGL(k_seg_xhat, grid, blk, combine_smem(a.n, 4), st, a);
+    const int T = tile_order(a.n);
+    if (T == 1) hipLaunchKernelGGL(k_seg_xhat<1>, grid, blk, elems_smem(a.n, 4), st, a);
+    else if (T == 2) hipLaunchKernelGGL(k_seg_xhat<2>, grid, blk, elems_smem(a.n, 4), st, a);
+    else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -707,9 +574,11 @@ int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st) {
 // Combine a short list of elements on one wave (the per-rank fold of the
 // horizon-sharded solve): out_pre = e_0 (x) ... (x) e_{r-1} (identity if r = 0),
 // out_suf = e_{r+1} (x) ... (x) e_{R-1} (P = p = 0 marker when r = R-1).
+template <int T>
 __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int R, int r, int n, int batch,
                                                     double *out_pre_all, double *out_suf_all, int *has_suf, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
+    __shared__ CombSmem<T> sm;
     const int lane = threadIdx.x;
     const int es = 3 * n * n + 2 * n;
     const long long b = blockIdx.x;
@@ -718,7 +587,6 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     const long long stride = (long long)batch * es;
     double *out_pre = out_pre_all + b * es, *out_suf = out_suf_all + b * es;
     double *acc = dyn, *nx = dyn + es, *o = dyn + 2 * es;
-    CombineWs w = combine_ws(dyn + 3 * es, n);
     // prefix
     {
         Elem e = elem_view(acc, n);
@@ -735,7 +603,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
             if (j == 0) {
                 elem_copy(acc, nx, n, lane);
             } else {
-                if (!elem_combine(o, acc, nx, w, n, true, false, lane) && lane == 0) atomicOr(flag, 4);
+                if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag, 4);
                 elem_copy(acc, o, n, lane);
             }
             wave_sync();
@@ -752,7 +620,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     for (int j = R - 2; j > r; --j) {
         elem_copy(nx, elems + (long long)j * stride, n, lane);
         wave_sync();
-        if (!elem_combine(o, nx, acc, w, n, true, true, lane) && lane == 0) atomicOr(flag, 8);
+        if (!tcombine<T>(o, nx, acc, n, true, true, sm, lane) && lane == 0) atomicOr(flag, 8);
         elem_copy(acc, o, n, lane);
         wave_sync();
     }
@@ -762,8 +630,15 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
 
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_shards, dim3(batch), dim3(64), combine_smem(n, 3), st, elems, R, r, n, batch, out_pre,
-                       out_suf, has_suf, flag);
+    const int T = tile_order(n);
+    if (T == 1)
+        hipLaunchKernelGGL(k_fold_shards<1>, dim3(batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
+                           out_pre, out_suf, has_suf, flag);
+    else if (T == 2)
+        hipLaunchKernelGGL(k_fold_shards<2>, dim3(batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
+                           out_pre, out_suf, has_suf, flag);
+    else
+        return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

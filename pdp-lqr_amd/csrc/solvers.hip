@@ -90,11 +90,13 @@ static int parallel_init(pdplqr_handle h) {
         return PDPLQR_ERR_INVALID;
     }
     // device refinement: split every reference segment into pieces of <= Lsub
-    // stages so that the GPU sees enough independent segment waves.
+    // stages so that the GPU sees one segment wave per resident wave slot
+    // (more pieces only lengthen the scans, fewer leave CUs idle).
     int Lsub = h->cfg.segment_len;
     if (Lsub <= 0) {
         const long long work = (long long)sh.N * sh.batch;
-        Lsub = (int)std::max<long long>(8, (work + 2047) / 2048);
+        const long long slots = seg_backward_slots(sh, h->cfg.device);
+        Lsub = (int)std::max<long long>(8, (work + slots - 1) / slots);
     }
     for (int i = 0; i < ns; ++i) {
         const int pieces = (ps->ref_len[i] + Lsub - 1) / Lsub;
