@@ -15,7 +15,8 @@
 //     F = F_b Z F_a,  C = F_b Z C_a F_b^T + C_b,  f = F_b Z (f_a - C_a p_b) + f_b,
 //     P = P_a + F_a^T Y F_a,  p = p_a + F_a^T Z^T (p_b + P_b f_a).
 // Cholesky factors come from chol_tiles (device_common.hpp); the triangular
-// solve for U and the matrix-vector products go through LDS.
+// solve for U runs with the column in registers (Q staged in LDS); the
+// matrix-vector products are single-column MFMAs on the same operands.
 #pragma once
 
 #include "device_common.hpp"
@@ -27,12 +28,27 @@ struct WM {
     d4 t[T][T];
 };
 
+// Phase timestamps of the combines (debug builds with -DPDPLQR_COMB_PROFILE:
+// lane 0 of every block records wall_clock64() at each mark into slot
+// blockIdx % 1024; read back with pdplqr_debug_comb_times).
+#if defined(PDPLQR_COMB_PROFILE) && defined(PDPLQR_COMB_PROFILE_TU)  // kernels_parallel.hip only
+extern __device__ unsigned long long g_comb_t[1024 * 16];
+#define COMB_MARK(k)                                                                     \
+    do {                                                                                 \
+        if (threadIdx.x == 0) g_comb_t[(blockIdx.x % 1024) * 16 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define COMB_MARK(k) \
+    do {             \
+    } while (0)
+#endif
+
 template <int T>
 struct CombSmem {
     static constexpr int P = 16 * T, PL = P + 1;
-    double A[P * PL];  // Q, then Z (vector products)
+    alignas(16) double A[P * (P + 2)];  // Q^T (row stride P + 2), then Z (vector products)
     double B[P * PL];  // R -> U in place, then output staging (symmetrisation)
-    alignas(16) double cb[P];
+    alignas(16) double cb[P];  // pivot-row broadcast of chol_tiles
     double sinv[P], luq[P];
     double v1[P], v2[P], v3[P], v4[P];
 };
@@ -99,7 +115,7 @@ __device__ __forceinline__ bool wm_chol(WM<T> &M, int n, CombSmem<T> &sm, int g,
 #pragma unroll
         for (int r = 0; r < 4; ++r) lpr[a][r] = 0.0;
     const bool ok = chol_tiles<T>(M.t, lpr, sm.cb, sm.sinv, sm.luq, 0, n, 0, false, g, c);
-    finalize_L<T>(M.t, sm.sinv, 0, n, g, c);
+    finalize_L<T>(M.t, sm.sinv, 0, n, g, c);  // sinv[i] = 1 / L[i][i]
     wave_sync();
     return ok;
 }
@@ -112,36 +128,114 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     constexpr int P = 16 * T, PL = P + 1;
     const int g = lane >> 4, c = lane & 15;
     WM<T> R, S;
+    COMB_MARK(1);
     wm_load(R, Pb, n, n, false, 1.0, g, c);
     bool ok = wm_chol(R, n, sm, g, c);
+    COMB_MARK(2);
     {
         WM<T> T1;
         wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
         wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
     }
+    COMB_MARK(3);
     ok = wm_chol(S, n, sm, g, c) && ok;  // Q
-    wm_store(S, sm.A, PL, P, g, c);
-    wm_store(R, sm.B, PL, P, g, c);
+    COMB_MARK(4);
+    // U = Q^{-1} R^T by forward substitution, column j on lane j with the
+    // column in registers (loops unrolled over the padded size P).  Q is
+    // staged transposed (row i of Q contiguous: 128-bit broadcast reads),
+    // R as is (lane j reads its row j = column j of R^T).
+    constexpr int PQ = P + 2;  // even row stride keeps the 16-byte alignment
+    double *Qt = sm.A, *Rs = sm.B;
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
+                Qt[j + i * PQ] = S.t[a][b][r];  // Qt[k + i PQ] = Q[i][k]
+                Rs[i + j * PL] = R.t[a][b][r];
+            }
     wave_sync();
-    // U = Q^{-1} R^T, column j on lane j, in place over R: lane j reads only
-    // R[j][i] with i <= j (the lower triangle; R^T[i][j] = 0 for i > j) and
-    // writes U[i][j] = B[i + j PL], an entry no other lane reads later.
-    if (lane < n) {
-        const int j = lane;
-        for (int i = 0; i < n; ++i) {
-            double v = (i <= j) ? sm.B[j + i * PL] : 0.0;
-            for (int k = 0; k < i; ++k) v -= sm.A[i + k * PL] * sm.B[k + j * PL];
-            sm.B[i + j * PL] = v * sm.sinv[i];  // sinv[i] = 1 / Q[i][i]
+    double u[P];
+    const int j = lane < P ? lane : P - 1;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        if (i < n) {
+            double v0 = (i <= j) ? Rs[j + i * PL] : 0.0, v1 = 0.0;
+            const double2 *qrow = reinterpret_cast<const double2 *>(Qt + i * PQ);
+#pragma unroll
+            for (int k2 = 0; k2 < (i + 1) / 2; ++k2) {
+                const double2 q = qrow[k2];
+                v0 = __builtin_fma(-q.x, u[2 * k2], v0);
+                if (2 * k2 + 1 < i) v1 = __builtin_fma(-q.y, u[2 * k2 + 1], v1);
+            }
+            u[i] = (v0 + v1) * sm.sinv[i];  // sinv[i] = 1 / Q[i][i]
+        } else {
+            u[i] = (i == j) ? 1.0 : 0.0;  // identity padding
         }
     }
+    wave_sync();  // all reads of Qt / Rs done
+    // U (column j on lane j) -> C/D layout through LDS
+    if (lane < P)
+#pragma unroll
+        for (int i = 0; i < P; ++i) Rs[i + lane * PL] = u[i];
     wave_sync();
+    COMB_MARK(5);
     WM<T> U;
-    wm_load(U, sm.B, PL, n, false, 1.0, g, c);
+    wm_load(U, Rs, PL, P, false, 1.0, g, c);
     wm_tn(Y, U, U, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Y = U^T U
     wm_tn(Z, Ca, Y, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z = I - C_a Y
     wm_tn(Zt, Y, Ca, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z^T = I - Y C_a
     wave_sync();
+    COMB_MARK(6);
     return ok;
+}
+
+// n-vectors in the B-operand / C-layout column 0 of the tiles: lane (g, 0)
+// holds x[16 kt + 4 r + g] in t[kt][r]; other lanes hold 0.
+template <int T>
+struct WV {
+    d4 t[T];
+};
+
+template <int T>
+__device__ __forceinline__ void wv_load(WV<T> &x, const double *p, int n, int g, int c) {
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * a + 4 * r + g;
+            x.t[a][r] = (c == 0 && i < n) ? p[i] : 0.0;
+        }
+}
+
+template <int T>
+__device__ __forceinline__ void wv_store(const WV<T> &x, double *p, int n, int g, int c) {
+    if (c == 0)
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g;
+                if (i < n) p[i] = x.t[a][r];
+            }
+}
+
+// y = sgn X^T x (+ add): the single-column form of wm_tn
+template <int T>
+__device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, int n, double sgn,
+                                      const WV<T> *add) {
+#pragma unroll
+    for (int a = 0; a < T; ++a) {
+        d4 acc = add ? add->t[a] : d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kt = 0; kt < T; ++kt)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                if (16 * kt + 4 * kk < n) acc = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc);
+        y.t[a] = acc;
+    }
 }
 
 // y = add + op(M) x  (n-vectors, M column-major ld), lanes over rows
@@ -172,13 +266,13 @@ __device__ __forceinline__ void wm_store_sym(const WM<T> &M, double *out, int n,
 template <int T>
 __device__ __forceinline__ bool tcombine(double *out, const double *ea, const double *eb, int n, bool need_FCf,
                                          bool need_Pp, CombSmem<T> &sm, int lane) {
-    constexpr int PL = 16 * T + 1;
     const int g = lane >> 4, c = lane & 15;
     const int nn = n * n;
     const double *aF = ea, *aC = ea + nn, *af = ea + 2 * nn, *aP = ea + 2 * nn + n, *ap = ea + 3 * nn + n;
     const double *bF = eb, *bC = eb + nn, *bf = eb + 2 * nn, *bP = eb + 2 * nn + n, *bp = eb + 3 * nn + n;
     double *oF = out, *oC = out + nn, *of = out + 2 * nn, *oP = out + 2 * nn + n, *op = out + 3 * nn + n;
     WM<T> Ca, Y, Z, Zt;
+    COMB_MARK(0);
     wm_load(Ca, aC, n, n, false, 0.0, g, c);
     const bool ok = comb_core(Y, Z, Zt, Ca, bP, n, sm, lane);
     WM<T> Fa;
@@ -190,6 +284,7 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
         wm_tn(Pn, Fa, W, n, 1.0, 0.0, &Pa, g, c);
         wm_store_sym(Pn, oP, n, sm, lane);
     }
+    COMB_MARK(7);
     if (need_FCf) {
         WM<T> Fbt, W, Fn;
         wm_load(Fbt, bF, n, n, true, 0.0, g, c);                     // F_b^T
@@ -203,24 +298,34 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
         wm_tn(Cn, Fbt, W3, n, 1.0, 0.0, &Cb, g, c);                     // F_b Z C_a F_b^T + C_b
         wm_store_sym(Cn, oC, n, sm, lane);
     }
-    // vectors, with Z in LDS
-    wm_store(Z, sm.A, PL, n, g, c);
-    wave_sync();
+    COMB_MARK(8);
+    // vectors on the same tiles (single-column MFMAs; x in column 0)
     if (need_FCf) {
-        lds_mv(sm.v1, aC, n, false, bp, af, -1.0, n, lane);   // v1 = f_a - C_a p_b
-        wave_sync();
-        lds_mv(sm.v2, sm.A, PL, false, sm.v1, nullptr, 1.0, n, lane);  // Z v1
-        wave_sync();
-        lds_mv(of, bF, n, false, sm.v2, bf, 1.0, n, lane);    // f = F_b Z v1 + f_b
+        WV<T> pb, fa, v1, v2, fb, fo;
+        wv_load(pb, bp, n, g, c);
+        wv_load(fa, af, n, g, c);
+        wv_tn(v1, Ca, pb, n, -1.0, &fa);        // v1 = f_a - C_a p_b  (C_a symmetric)
+        wv_tn(v2, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z v1
+        WM<T> Fbt;
+        wm_load(Fbt, bF, n, n, true, 0.0, g, c);
+        wv_load(fb, bf, n, g, c);
+        wv_tn(fo, Fbt, v2, n, 1.0, &fb);        // f = F_b Z v1 + f_b
+        wv_store(fo, of, n, g, c);
     }
     if (need_Pp) {
-        lds_mv(sm.v3, bP, n, false, af, bp, 1.0, n, lane);     // v3 = p_b + P_b f_a
-        wave_sync();
-        lds_mv(sm.v4, sm.A, PL, true, sm.v3, nullptr, 1.0, n, lane);  // Z^T v3
-        wave_sync();
-        lds_mv(op, aF, n, true, sm.v4, ap, 1.0, n, lane);      // p = p_a + F_a^T Z^T v3
+        WM<T> Pb;
+        WV<T> fa, pb, v3, v4, pa, po;
+        wm_load(Pb, bP, n, n, false, 0.0, g, c);
+        wv_load(fa, af, n, g, c);
+        wv_load(pb, bp, n, g, c);
+        wv_tn(v3, Pb, fa, n, 1.0, &pb);         // v3 = p_b + P_b f_a  (P_b symmetric)
+        wv_tn(v4, Z, v3, n, 1.0, (const WV<T> *)nullptr);   // Z^T v3
+        wv_load(pa, ap, n, g, c);
+        wv_tn(po, Fa, v4, n, 1.0, &pa);         // p = p_a + F_a^T Z^T v3
+        wv_store(po, op, n, g, c);
     }
     wave_sync();
+    COMB_MARK(9);
     return ok;
 }
 

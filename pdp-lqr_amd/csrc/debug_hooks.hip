@@ -1,0 +1,71 @@
+// debug_hooks.hip -- test-only entry points (not part of include/pdplqr.h):
+// device kernels exercised directly by the GPU unit tests
+// (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
+#include "combine_tiles.hpp"
+
+// out = a (x) b on the device (one wave), elements in host memory.
+template <int T>
+__global__ __launch_bounds__(64) void k_debug_combine(const double *a, const double *b, double *out, int n, int *ok) {
+    __shared__ pdplqr::CombSmem<T> sm;
+    const bool good = pdplqr::tcombine<T>(out, a, b, n, true, true, sm, threadIdx.x);
+    if (threadIdx.x == 0) *ok = good ? 1 : 0;
+}
+
+extern "C" int pdplqr_debug_combine(int n, const double *a, const double *b, double *out) {
+    using namespace pdplqr;
+    const int T = n <= 16 ? 1 : (n <= 32 ? 2 : 0);
+    if (!T) return PDPLQR_ERR_UNSUPPORTED;
+    const size_t es = (size_t)(3 * n * n + 2 * n) * sizeof(double);
+    double *d = nullptr;
+    int *dok = nullptr, okh = 0;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 3 * es));
+    PDPLQR_HIP_TRY(hipMalloc(&dok, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, a, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
+    const double *da = d, *db = (const double *)((char *)d + es);
+    double *dout = (double *)((char *)d + 2 * es);
+    if (T == 1) hipLaunchKernelGGL(k_debug_combine<1>, dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    else hipLaunchKernelGGL(k_debug_combine<2>, dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    (void)hipFree(dok);
+    return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
+}
+
+
+// Raw v_rsq_f64 (no Newton refinement) over an array: the accuracy that
+// decides how many Newton steps rsqrt_f64 needs.
+__global__ void k_debug_rsq(const double *x, double *y, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = __builtin_amdgcn_rsq(x[i]);
+}
+
+extern "C" int pdplqr_debug_rsq(int n, const double *x, double *y) {
+    double *d = nullptr;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 2 * (size_t)n * sizeof(double)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_rsq, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n, n);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(y, d + n, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return PDPLQR_OK;
+}
+
+// rsqrt_f64 (device_common.hpp) over an array: the refined reciprocal square root.
+__global__ void k_debug_rsqrt(const double *x, double *y, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = pdplqr::rsqrt_f64(x[i]);
+}
+
+extern "C" int pdplqr_debug_rsqrt(int n, const double *x, double *y) {
+    double *d = nullptr;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 2 * (size_t)n * sizeof(double)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_rsqrt, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n, n);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(y, d + n, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return PDPLQR_OK;
+}

@@ -22,11 +22,16 @@
 //     and u_hat_i = p_suf(i+1) + P_suf(i+1) x_hat_{i+1} (condensed forward).
 //   * the rollout reuses k_riccati_fwd with the G_k u_hat coupling
 //     (lqr_kernel_parallel.hpp:195-198).
+#define PDPLQR_COMB_PROFILE_TU 1  // the combine phase marks live in this translation unit
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
 
 namespace pdplqr {
+
+#ifdef PDPLQR_COMB_PROFILE
+__device__ unsigned long long g_comb_t[1024 * 16];
+#endif
 
 // Element views: [F | C | f | P | p] packed contiguously (3 n^2 + 2 n doubles)
 struct Elem {
@@ -386,9 +391,24 @@ int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // One Hillis-Steele round: inclusive prefix (dir 0) or suffix (dir 1) scan.
 // ---------------------------------------------------------------------------
+// Both operand elements are prefetched into LDS with one LDS-DMA burst (a
+// single HBM/L2 latency) before the combine reads them.
+// (es = 3 n^2 + 2 n is odd for odd n: the last double goes by a plain copy;
+// the caller waits on vmcnt and then wave_sync()s.)
+template <int T>
+__device__ __forceinline__ void elem_prefetch(double *dst, const double *src, int es, int lane) {
+    const int chunks = es / 2;
+    for (int q = 0; q * 64 < chunks; ++q) {
+        const int ch = q * 64 + lane;
+        if (ch < chunks) dma16(src + 2 * ch, dst + 2 * q * 64);
+    }
+    if ((es & 1) && lane == 0) dst[es - 1] = src[es - 1];
+}
+
 template <int T>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
+    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 elements (launcher: elems_smem(n, 2))
     const int lane = threadIdx.x;
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
@@ -414,8 +434,12 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     // Both directions need full elements: the next round's combine reads the
     // right operand's P, p (Z = (I + C_a P_b)^{-1}).  A suffix ending at the
     // real terminal has F = C = f = 0.
-    const bool ok = tcombine<T>(out + (long long)i * es, in + (long long)ia * es, in + (long long)ib * es, n, true,
-                                true, sm, lane);
+    const int esp = (es + 1) & ~1;  // 16-byte aligned second buffer
+    elem_prefetch<T>(ebuf, in + (long long)ia * es, es, lane);
+    elem_prefetch<T>(ebuf + esp, in + (long long)ib * es, es, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    const bool ok = tcombine<T>(out + (long long)i * es, ebuf, ebuf + esp, n, true, true, sm, lane);
     if (!ok && lane == 0) atomicOr(A.flag, 1);
 }
 
@@ -554,8 +578,9 @@ static int tile_order(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 0); }
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * 2 * a.S)), blk(64);
     const int T = tile_order(a.n);
-    if (T == 1) hipLaunchKernelGGL(k_seg_scan<1>, grid, blk, 0, st, a);
-    else if (T == 2) hipLaunchKernelGGL(k_seg_scan<2>, grid, blk, 0, st, a);
+    const size_t smem = 2 * (size_t)((3 * a.n * a.n + 2 * a.n + 1) & ~1) * sizeof(double);
+    if (T == 1) hipLaunchKernelGGL(k_seg_scan<1>, grid, blk, smem, st, a);
+    else if (T == 2) hipLaunchKernelGGL(k_seg_scan<2>, grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -647,3 +672,9 @@ int launch_fold_shards(const double *elems, int R, int r, int n, int batch, doub
 // copied out by the caller.
 
 }  // namespace pdplqr
+
+#ifdef PDPLQR_COMB_PROFILE
+extern "C" int pdplqr_debug_comb_times(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_comb_t), sizeof(unsigned long long) * 1024 * 16) == hipSuccess ? 0 : -2;
+}
+#endif

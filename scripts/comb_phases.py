@@ -1,0 +1,42 @@
+"""Phase breakdown of the segment combine (debug build libpdplqr_combprof.so,
+-DPDPLQR_COMB_PROFILE): runs one horizon-slice backward (segments + scans) and
+prints the median duration of each combine phase over the recorded blocks."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("PDPLQR_LIB", os.path.join(ROOT, "pdp-lqr_amd", "build", "variants", "libpdplqr_combprof.so"))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pdp-lqr_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from pdplqr import _lib  # noqa: E402
+from pdplqr.horizon import HorizonShard  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+n, m = 24, 8
+dev = torch.device("cuda", 0)
+E, c, H, h, x0 = bench.gen_batch_device(n, m, N, 1, seed=1, device=dev)
+sh = HorizonShard(n, m, N, 1, device=0)
+sh.set_model(E, c, H, h)
+sh.update_problem_data(torch.zeros(1, N * (n + m) + n, dtype=torch.float64, device=dev), sigma=1e-6)
+elem = torch.empty(1, sh.es, dtype=torch.float64, device=dev)
+sh.backward(elem, True)
+sh.synchronize()
+L = _lib.lib()
+buf = np.zeros(1024 * 16, dtype=np.uint64)
+L.pdplqr_debug_comb_times.argtypes = [C.c_void_p]
+assert L.pdplqr_debug_comb_times(C.c_void_p(buf.ctypes.data)) == 0
+t = buf.reshape(1024, 16).astype(np.int64)
+ok = (t[:, 0] > 0) & (t[:, 9] > t[:, 0])
+for k in range(1, 10):
+    ok &= t[:, k] >= t[:, k - 1]
+t = t[ok]
+names = ["load Ca", "load Pb+chol R", "T1,S products", "chol Q", "U solve (LDS)", "Y,Z,Zt products", "P path",
+         "F,C path", "vectors"]
+d = np.diff(t[:, :10], axis=1)
+print(f"blocks={len(t)}  wall_clock64 ticks (100 MHz): total median {np.median(t[:, 9] - t[:, 0]):.0f}")
+for k, nm in enumerate(names):
+    print(f"  {nm:18s} {np.median(d[:, k]):8.0f}")

@@ -1,0 +1,88 @@
+"""Unit parity of the device segment combine (combine_tiles.hpp: MFMA tiles,
+blocked Cholesky, register triangular solve) against the numpy restatement of
+SURVEY.md 0.1 (tests/seg_ref.py), through the pdplqr_debug_combine test hook.
+Tolerance 1e-12 relative per block (fp64, well-conditioned random elements)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from seg_ref import combine
+
+pytestmark = pytest.mark.gpu
+
+
+def _elem(n, rng, zero_fcf=False):
+    F = np.eye(n) + 0.2 * rng.standard_normal((n, n))
+    G = rng.standard_normal((n, n))
+    Cm = G @ G.T / n
+    f = rng.standard_normal(n)
+    H = rng.standard_normal((n, n))
+    P = H @ H.T / n + np.eye(n)
+    p = rng.standard_normal(n)
+    if zero_fcf:
+        F, Cm, f = np.zeros((n, n)), np.zeros((n, n)), np.zeros(n)
+    return F, Cm, f, P, p
+
+
+def _pack(e):
+    F, Cm, f, P, p = e
+    return np.concatenate([F.ravel(order="F"), Cm.ravel(order="F"), f, P.ravel(order="F"), p])
+
+
+def _unpack(v, n):
+    nn = n * n
+    return (v[:nn].reshape(n, n, order="F"), v[nn:2 * nn].reshape(n, n, order="F"), v[2 * nn:2 * nn + n],
+            v[2 * nn + n:3 * nn + n].reshape(n, n, order="F"), v[3 * nn + n:])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 8, 12, 13, 16, 17, 20, 24, 31, 32])
+@pytest.mark.parametrize("zero_b", [False, True])
+def test_device_combine_matches_numpy(n, zero_b):
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(100 + n)
+    a, b = _elem(n, rng), _elem(n, rng, zero_fcf=zero_b)
+    va, vb = _pack(a), _pack(b)
+    out = np.zeros_like(va)
+    rc = L.pdplqr_debug_combine(n, va.ctypes.data, vb.ctypes.data, out.ctypes.data)
+    assert rc == 0
+    got, ref = _unpack(out, n), combine(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        assert np.linalg.norm(x - y) <= 1e-12 * max(1.0, np.linalg.norm(y)), name
+
+
+def test_rsq_f64_accuracy_allows_one_newton_step():
+    """rsqrt_f64 (device_common.hpp) refines v_rsq_f64 by Newton steps; record
+    the hardware estimate's accuracy (one step squares the relative error)."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_rsq.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(7)
+    x = np.concatenate([10.0 ** rng.uniform(-30, 30, 200000), rng.uniform(0.5, 2.0, 200000)])
+    y = np.zeros_like(x)
+    assert L.pdplqr_debug_rsq(x.size, x.ctypes.data, y.ctypes.data) == 0
+    rel = np.abs(y * np.sqrt(x) - 1.0)
+    print(f"v_rsq_f64 max rel err {rel.max():.3e} (2^{np.log2(rel.max()):.1f})")
+    assert rel.max() < 2.0 ** -22
+
+
+def test_rsqrt_f64_full_precision():
+    """The refined rsqrt_f64 is within 2 ulp of the correctly rounded 1/sqrt(x)."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_rsqrt.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(8)
+    x = np.concatenate([10.0 ** rng.uniform(-300, 300, 200000), rng.uniform(0.5, 2.0, 200000),
+                        np.array([1.0, 4.0, 2.0, 1e-300, 1e300])])
+    y = np.zeros_like(x)
+    assert L.pdplqr_debug_rsqrt(x.size, x.ctypes.data, y.ctypes.data) == 0
+    ref = 1.0 / np.sqrt(x)
+    ulp = np.spacing(ref)
+    err = np.abs(y - ref) / ulp
+    print(f"rsqrt_f64 max error {err.max():.2f} ulp")
+    assert err.max() <= 2.0
