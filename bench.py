@@ -113,6 +113,15 @@ def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
                       f"OpenMP over problems, {el:.1f} s)"}
 
 
+BACKEND = os.environ.get("PDPLQR_BENCH_BACKEND", "nccl")
+
+
+def _max_over_ranks(dist, value, dev):
+    t = torch.tensor([value], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _timed(fn, steps, warmup, dev, dist):
     for _ in range(warmup):
         fn()
@@ -127,9 +136,7 @@ def _timed(fn, steps, warmup, dev, dist):
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = _max_over_ranks(dist, el, dev)
     return el / steps
 
 
@@ -272,13 +279,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if BACKEND != "nccl":  # rehearsal: more ranks than GPUs share the devices
+        local %= max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        # nccl = RCCL over xGMI; PDPLQR_BENCH_BACKEND=gloo rehearses the
+        # multi-rank flow on a box with fewer GPUs than ranks
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(BACKEND, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -324,9 +338,7 @@ def main():
     el = time.perf_counter() - t0
     st = bs.status()
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = _max_over_ranks(dist, el, dev)
     ms_bwd = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     ms_fwd = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     stages = N * B
