@@ -56,22 +56,48 @@ __device__ __forceinline__ void elem_copy(double *dst, const double *src, int n,
 // ---------------------------------------------------------------------------
 // Segment backward: the reference's reduction_per_thread (lqr_solver_parallel.hpp:164-188)
 // ---------------------------------------------------------------------------
-template <int T>
-struct SegSmem {
-    static constexpr int P = 16 * T, NM = P * P;
-    double F[NM], C[NM], Ft[NM], Ct[NM], Acl[NM];  // n x n (ld n)
-    double Es[NM], FB[NM], K[NM], G[NM];           // E (n x s), F_next B (n x m), K, G (m x n)
-    double f[P], ft[P], cv[P], dv[P];
+// Element-recursion scratch of one segment wave, carved from dynamic LDS and
+// sized by the actual n, m (fixed 16T x 16T arrays would cap T = 2 at one wave
+// per CU).
+struct SegView {
+    double *F, *C, *Ft, *Ct, *Acl;  // n x n (ld n)
+    double *Es, *FB, *K, *G;        // E (n x s), F_next B (n x m), K, G (m x n)
+    double *f, *ft, *cv, *dv;       // n, n, n, m
 };
+
+__host__ __device__ inline size_t seg_smem_doubles(int n, int m) {
+    const int s = n + m;
+    return 5 * (size_t)n * n + (size_t)n * s + 3 * (size_t)n * m + 3 * (size_t)n + m;
+}
+
+__device__ __forceinline__ SegView seg_view(double *dyn, int n, int m) {
+    const int s = n + m, nn = n * n;
+    SegView v;
+    v.F = dyn;
+    v.C = v.F + nn;
+    v.Ft = v.C + nn;
+    v.Ct = v.Ft + nn;
+    v.Acl = v.Ct + nn;
+    v.Es = v.Acl + nn;
+    v.FB = v.Es + n * s;
+    v.K = v.FB + n * m;
+    v.G = v.K + m * n;
+    v.f = v.G + m * n;
+    v.ft = v.f + n;
+    v.cv = v.ft + n;
+    v.dv = v.cv + n;
+    return v;
+}
 
 template <int T>
 __global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
     constexpr int LD = 16 * T + 1;
     __shared__ BwdSmem<T> sm;
-    __shared__ SegSmem<T> ss;
+    extern __shared__ double seg_dyn[];
     const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
+    const SegView ss = seg_view(seg_dyn, n, m);
     const long long b = blockIdx.x / S;
     const int seg = blockIdx.x % S;
     const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
@@ -553,16 +579,29 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
 int seg_backward_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    hipError_t e = sh.s <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<1>, 64, 0)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<2>, 64, 0);
+    const size_t smem = seg_smem_doubles(sh.n, sh.m) * sizeof(double);
+    hipError_t e = sh.s <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<1>, 64, smem)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<2>, 64, smem);
+    if (e != hipSuccess || per <= 0) per = 1;
+    return cus * per;
+}
+
+// Resident scan waves (one combine each) the device holds for this shape.
+int seg_scan_slots(const Shape &sh, int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    const size_t smem = 2 * (size_t)((3 * sh.n * sh.n + 2 * sh.n + 1) & ~1) * sizeof(double);
+    hipError_t e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1>, 64, smem)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2>, 64, smem);
     if (e != hipSuccess || per <= 0) per = 1;
     return cus * per;
 }
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st) {
     const dim3 grid((unsigned)(a.sh.batch * a.S)), blk(64);
-    if (a.sh.s <= 16) hipLaunchKernelGGL(k_seg_bwd<1>, grid, blk, 0, st, a);
-    else if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd<2>, grid, blk, 0, st, a);
+    const size_t smem = seg_smem_doubles(a.sh.n, a.sh.m) * sizeof(double);
+    if (a.sh.s <= 16) hipLaunchKernelGGL(k_seg_bwd<1>, grid, blk, smem, st, a);
+    else if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd<2>, grid, blk, smem, st, a);
     else {
         set_error("parallel solver: n + m > 32 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;

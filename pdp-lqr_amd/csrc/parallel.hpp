@@ -45,6 +45,7 @@ struct SegFwd {
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st);
 int seg_backward_slots(const Shape &sh, int device);
+int seg_scan_slots(const Shape &sh, int device);
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st);

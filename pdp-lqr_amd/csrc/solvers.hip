@@ -90,13 +90,37 @@ static int parallel_init(pdplqr_handle h) {
         return PDPLQR_ERR_INVALID;
     }
     // device refinement: split every reference segment into pieces of <= Lsub
-    // stages so that the GPU sees one segment wave per resident wave slot
-    // (more pieces only lengthen the scans, fewer leave CUs idle).
+    // stages.  The number of device segments S per problem trades the serial
+    // segment backward (N/S stages per wave, batch S waves over the resident
+    // slots) against the scans (log2 S rounds of 2 batch S combines):
+    //     t(S) = a ceil(N/S) ceil(batch S / slots_bwd) + b ceil(log2 S) ceil(2 batch S / slots_scan)
+    // with a, b the per-stage and per-combine latencies of one wave
+    // (profiles/r01: ~10 / 15 us for s <= 16, ~50 / 45 us for 24/8).
     int Lsub = h->cfg.segment_len;
     if (Lsub <= 0) {
-        const long long work = (long long)sh.N * sh.batch;
-        const long long slots = seg_backward_slots(sh, h->cfg.device);
-        Lsub = (int)std::max<long long>(8, (work + slots - 1) / slots);
+        const double a = sh.s <= 16 ? 10.0 : 50.0, b = sh.s <= 16 ? 15.0 : 45.0;
+        const long long sb = seg_backward_slots(sh, h->cfg.device), ss = seg_scan_slots(sh, h->cfg.device);
+        const long long B = sh.batch;
+        auto cost = [&](long long S) {
+            const long long per = (sh.N + S - 1) / S, rb = (B * S + sb - 1) / sb, rs = (2 * B * S + ss - 1) / ss;
+            int lg = 0;
+            while ((1LL << lg) < S) ++lg;
+            return a * per * rb + b * lg * rs;
+        };
+        long long best = 1;
+        double bc = cost(1);
+        std::vector<long long> cand;
+        for (long long S = 2; S <= sh.N; S <<= 1) cand.push_back(S);
+        if (sb / B >= 1 && sb / B <= sh.N) cand.push_back(sb / B);
+        for (long long S : cand)
+            if (sh.N / S >= 4 || S == 1) {
+                const double cS = cost(S);
+                if (cS < bc) {
+                    bc = cS;
+                    best = S;
+                }
+            }
+        Lsub = (int)((sh.N + best - 1) / best);
     }
     for (int i = 0; i < ns; ++i) {
         const int pieces = (ps->ref_len[i] + Lsub - 1) / Lsub;
