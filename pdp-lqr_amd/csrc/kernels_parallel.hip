@@ -3,12 +3,9 @@
 //
 // Restates reference lqr_solver_parallel.hpp:64-238, lqr_kernel_parallel.hpp:52-218
 // and condensed_system.hpp:8-299:
-//   * k_seg_bwd<T>: one wavefront per (problem, segment) runs the segment's
-//     Riccati recursion from a zero terminal (the real terminal for the last
-//     segment, lqr_kernel_parallel.hpp:52-67) and accumulates the segment
-//     element (F, C, f) plus G_k (step_with_factorization, :88-136).  It exports
-//     e = (F, C, f, P = Lxx Lxx^T, p) as update_segment_data does
-//     (lqr_solver_parallel.hpp:182-187, condensed_system.hpp:64-74).
+//   * the segment backward (element e = (F, C, f, P, p) of every segment) is
+//     k_seg_bwd_aug in kernels_segment.hip; k_seg_bwd_nofact below is its
+//     linear-terms-only counterpart.
 //   * k_seg_scan: one Hillis-Steele round of the prefix and suffix scans of the
 //     elements under the associative operator
 //         Z = (I + C_a P_b)^{-1}, F = F_b Z F_a, C = F_b Z C_a F_b^T + C_b,
@@ -54,234 +51,12 @@ __device__ __forceinline__ void elem_copy(double *dst, const double *src, int n,
 }
 
 // ---------------------------------------------------------------------------
-// Segment backward: the reference's reduction_per_thread (lqr_solver_parallel.hpp:164-188)
-// ---------------------------------------------------------------------------
-// Element-recursion scratch of one segment wave, carved from dynamic LDS and
-// sized by the actual n, m (fixed 16T x 16T arrays would cap T = 2 at one wave
-// per CU).
-struct SegView {
-    double *F, *C, *Ft, *Ct, *Acl;  // n x n (ld n)
-    double *Es, *FB, *K, *G;        // E (n x s), F_next B (n x m), K, G (m x n)
-    double *f, *ft, *cv, *dv;       // n, n, n, m
-};
-
-__host__ __device__ inline size_t seg_smem_doubles(int n, int m) {
-    const int s = n + m;
-    return 5 * (size_t)n * n + (size_t)n * s + 3 * (size_t)n * m + 3 * (size_t)n + m;
-}
-
-__device__ __forceinline__ SegView seg_view(double *dyn, int n, int m) {
-    const int s = n + m, nn = n * n;
-    SegView v;
-    v.F = dyn;
-    v.C = v.F + nn;
-    v.Ft = v.C + nn;
-    v.Ct = v.Ft + nn;
-    v.Acl = v.Ct + nn;
-    v.Es = v.Acl + nn;
-    v.FB = v.Es + n * s;
-    v.K = v.FB + n * m;
-    v.G = v.K + m * n;
-    v.f = v.G + m * n;
-    v.ft = v.f + n;
-    v.cv = v.ft + n;
-    v.dv = v.cv + n;
-    return v;
-}
-
-template <int T>
-__global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
-    constexpr int LD = 16 * T + 1;
-    __shared__ BwdSmem<T> sm;
-    extern __shared__ double seg_dyn[];
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
-    const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
-    const SegView ss = seg_view(seg_dyn, n, m);
-    const long long b = blockIdx.x / S;
-    const int seg = blockIdx.x % S;
-    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
-    const bool last = (seg == S - 1) && A.last_is_terminal;
-    const long long frs = (long long)s * m + m;
-    const double *Eb = A.E + b * sh.perE;
-    const double *cb = A.c + b * sh.perc;
-    const double *Hb = A.Hw + b * sh.perHw;
-    const double *hb = A.hw + b * sh.perh;
-    double *FRb = A.FR + b * sh.perKD;
-    double *Gb = A.G + b * (long long)sh.N * m * n;
-    double *Lcb = A.Lc ? A.Lc + b * sh.perHw : nullptr;
-    double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
-    int fail_stage = -1;
-
-    // ---- segment terminal (lqr_kernel_parallel.hpp:52-67) ----
-    if (last) {
-        d4 M[T][T];
-        load_M<T>(M, Hb + (long long)sh.N * sh.ps, n, m, m, s, g, c);
-        double lpr[T][4];
-        const bool okN = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, m, s, m, false, g, c);
-        finalize_L<T>(M, sm.inv, m, s, g, c);
-        if (!okN) fail_stage = sh.N;
-        store_L_lds<T>(M, sm.L, g, c);
-        if (lane < n) {
-            const double v = hb[(long long)sh.N * s + lane];
-            sm.pv[lane] = v;
-            if (lpb) lpb[(long long)sh.N * s + lane] = v;
-        }
-        if (Lcb)
-#pragma unroll
-            for (int a = 0; a < T; ++a)
-#pragma unroll
-                for (int bt = 0; bt < T; ++bt)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
-                        if (j >= m && i >= j && i < s)
-                            Lcb[(long long)sh.N * sh.ps + pidx(i - m, j - m, n)] = M[a][bt][r];
-                    }
-    } else {  // dummy: L = 0, lp = 0, F = I, C = 0, f = 0
-        for (int q = lane; q < (16 * T) * LD; q += 64) sm.L[q] = 0.0;
-        for (int q = lane; q < 16 * T; q += 64) sm.pv[q] = 0.0;
-        for (int q = lane; q < n * n; q += 64) {
-            ss.F[q] = (q % n == q / n) ? 1.0 : 0.0;
-            ss.C[q] = 0.0;
-        }
-        for (int q = lane; q < n; q += 64) ss.f[q] = 0.0;
-    }
-    wave_sync();
-
-    for (int k = N1 - 1; k >= N0; --k) {
-        StageIn<T> cur;
-        load_stage<T>(cur, Eb + (long long)k * n * s, cb + (long long)k * n, Hb + (long long)k * sh.ps,
-                      hb + (long long)k * s, n, s, g, c);
-        d4 M[T][T];
-        double lpr[T][4];
-        const bool okk = riccati_stage<T>(sm, cur, M, lpr, n, m, s, g, c);
-        if (!okk && fail_stage < 0) fail_stage = k;
-        double *FRk = FRb + (long long)k * frs;
-#pragma unroll
-        for (int a = 0; a < T; ++a)
-#pragma unroll
-            for (int bt = 0; bt < T; ++bt) {
-                const int jc = 16 * bt + c;
-                if (jc < m)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = 16 * a + 4 * r + g;
-                        if (i < s) FRk[jc * s + i] = M[a][bt][r];
-                    }
-            }
-        if (lane < m) FRk[(long long)s * m + lane] = sm.luq[lane];
-        if (lpb) {
-            if (lane < m) lpb[(long long)k * s + lane] = sm.luq[lane];
-            if (lane < n) lpb[(long long)k * s + m + lane] = sm.pv[lane];
-        }
-        if (Lcb)
-#pragma unroll
-            for (int a = 0; a < T; ++a)
-#pragma unroll
-                for (int bt = 0; bt < T; ++bt)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
-                        if (i >= j && i < s) Lcb[(long long)k * sh.ps + pidx(i, j, s)] = M[a][bt][r];
-                    }
-        if (last) continue;
-        // ---- segment element recursion (lqr_kernel_parallel.hpp:97-135) ----
-        const double *Ek = Eb + (long long)k * n * s;
-        const double *L = sm.L;  // L_k, padded, ld LD
-        for (int q = lane; q < n * s; q += 64) ss.Es[q] = Ek[q];
-        if (lane < n) ss.cv[lane] = cb[(long long)k * n + lane];
-        wave_sync();
-        // K = -Luu^{-T} Lxu^T (:105,107) and d = -Luu^{-T} lu (:106,108)
-        if (lane <= n) {
-            for (int i = m - 1; i >= 0; --i) {
-                double v = (lane < n) ? -L[(m + lane) + i * LD] : -sm.luq[i];
-                for (int j = i + 1; j < m; ++j)
-                    v -= L[j + i * LD] * ((lane < n) ? ss.K[j + lane * m] : ss.dv[j]);
-                v /= L[i + i * LD];
-                if (lane < n) ss.K[i + lane * m] = v;
-                else ss.dv[i] = v;
-            }
-        }
-        // FB = F_next B (n x m): B^T F_next^T of :126 transposed
-        for (int q = lane; q < n * m; q += 64) {
-            const int t = q % n, i = q / n;
-            double acc = 0.0;
-            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[t + r * n], ss.Es[r + i * n], acc);
-            ss.FB[t + i * n] = acc;
-        }
-        wave_sync();
-        // G = -Luu^{-1} B^T F_next^T (:127-128): column t of G from row t of FB
-        if (lane < n) {
-            for (int i = 0; i < m; ++i) {
-                double v = -ss.FB[lane + i * n];
-                for (int j = 0; j < i; ++j) v -= L[i + j * LD] * ss.G[j + lane * m];
-                v /= L[i + i * LD];
-                ss.G[i + lane * m] = v;
-                Gb[(long long)k * m * n + i + lane * m] = v;
-            }
-        }
-        // Acl = A + B K (:129) ; ft = c + B d (:132)
-        for (int q = lane; q < n * n; q += 64) {
-            const int t = q % n, j = q / n;
-            double acc = ss.Es[t + (m + j) * n];
-            for (int i = 0; i < m; ++i) acc = __builtin_fma(ss.Es[t + i * n], ss.K[i + j * m], acc);
-            ss.Acl[q] = acc;
-        }
-        if (lane < n) {
-            double acc = ss.cv[lane];
-            for (int i = 0; i < m; ++i) acc = __builtin_fma(ss.Es[lane + i * n], ss.dv[i], acc);
-            ss.ft[lane] = acc;
-        }
-        wave_sync();
-        // F = F_next Acl (:130); f = F_next ft + f_next (:133); C = C_next + G^T G (:134)
-        for (int q = lane; q < n * n; q += 64) {
-            const int t = q % n, j = q / n;
-            double acc = 0.0;
-            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[t + r * n], ss.Acl[r + j * n], acc);
-            ss.Ft[q] = acc;
-            double cc = 0.0;
-            for (int i = 0; i < m; ++i) cc = __builtin_fma(ss.G[i + t * m], ss.G[i + j * m], cc);
-            ss.Ct[q] = ss.C[q] + cc;
-        }
-        double fnew = 0.0;
-        if (lane < n) {
-            double acc = 0.0;
-            for (int r = 0; r < n; ++r) acc = __builtin_fma(ss.F[lane + r * n], ss.ft[r], acc);
-            fnew = acc + ss.f[lane];
-        }
-        wave_sync();
-        for (int q = lane; q < n * n; q += 64) {
-            ss.F[q] = ss.Ft[q];
-            ss.C[q] = ss.Ct[q];
-        }
-        if (lane < n) ss.f[lane] = fnew;
-        wave_sync();
-    }
-    // ---- export the element (update_segment_data, lqr_solver_parallel.hpp:182-187) ----
-    double *eo = A.elem + (b * S + seg) * (long long)(3 * n * n + 2 * n);
-    Elem e = elem_view(eo, n);
-    for (int q = lane; q < n * n; q += 64) {
-        const int i = q % n, j = q / n;
-        double acc = 0.0;
-        for (int t = 0; t < n; ++t) acc = __builtin_fma(sm.L[(m + i) + (m + t) * LD], sm.L[(m + j) + (m + t) * LD], acc);
-        e.P[q] = acc;  // P = Lxx Lxx^T (condensed_system.hpp:69,188)
-        e.F[q] = last ? 0.0 : ss.F[q];
-        e.C[q] = last ? 0.0 : ss.C[q];
-    }
-    if (lane < n) {
-        e.f[lane] = last ? 0.0 : ss.f[lane];
-        e.p[lane] = sm.pv[lane];
-    }
-    if (lane == 0) A.seg_status[b * S + seg] = fail_stage < 0 ? 0 : fail_stage + 1;
-}
-
-// ---------------------------------------------------------------------------
 // Segment backward without factorization: reduction_without_factorization
 // (lqr_solver_parallel.hpp:190-211) with ParallelLQRKernel::
-// step_without_factorization (lqr_kernel_parallel.hpp:139-168).  The cached
-// factors L_k of the last factorising backward are reused; only the linear
-// terms change: lp_k, lu'_k (into the rollout record) and the element vectors
+// step_without_factorization (lqr_kernel_parallel.hpp:139-168).  The factor
+// cache of the last factorising backward is reused (P_k = Lxx Lxx^T per stage,
+// written by k_seg_bwd_aug, plus L(:, 0:m) in the rollout record); only the
+// linear terms change: lp_k, lu'_k (into the rollout record) and the element vectors
 // p, f.  f = F_{k+1}(c + B d) + f_{k+1} (:160-165) is evaluated as what it
 // is -- the end state of the segment's closed-loop rollout from x = 0 under
 // the new feed-forward d = -Luu^{-T} lu' -- so no per-stage F_k is stored.
@@ -290,8 +65,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd(SegArgs A) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
     constexpr int P = 32;
-    __shared__ double Lk[P * P];  // this stage's L (dense, ld s)
-    __shared__ double Ln[P * P];  // next stage's Lxx (ld n)
+    __shared__ double Pn[P * P];  // P_{k+1} (dense, ld n) from the factor cache
     __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P], xs[P], us[P];
     const int lane = threadIdx.x;
     const Shape &sh = A.sh;
@@ -307,51 +81,47 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
     double *FRb = A.FR + b * sh.perKD;
     const double *Lcb = A.Lc + b * sh.perHw;
     double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
-    // segment terminal: the real one (lqr_kernel.hpp:94-101) or the dummy L = 0, lp = 0
+    auto load_P = [&](int k) {  // packed lower n x n at stage offset k ps -> dense
+        for (int q = lane; q < n * n; q += 64) {
+            const int i = q % n, j = q / n;
+            Pn[q] = Lcb[(long long)k * sh.ps + (i >= j ? pidx(i, j, n) : pidx(j, i, n))];
+        }
+    };
+    // segment terminal: the real one (lqr_kernel.hpp:94-101) or the dummy P = 0, p = 0
     if (lane < n) pn[lane] = last ? hb[(long long)sh.N * s + lane] : 0.0;
     if (last && lpb && lane < n) lpb[(long long)sh.N * s + lane] = pn[lane];
-    for (int q = lane; q < n * n; q += 64) {
-        const int i = q % n, j = q / n;
-        Ln[q] = (last && i >= j) ? Lcb[(long long)sh.N * sh.ps + pidx(i, j, n)] : 0.0;
-    }
+    if (last) load_P(sh.N);
+    else
+        for (int q = lane; q < n * n; q += 64) Pn[q] = 0.0;
     wave_sync();
     for (int k = N1 - 1; k >= N0; --k) {
         const double *Ek = Eb + (long long)k * n * s;
-        for (int q = lane; q < s * s; q += 64) {
-            const int i = q % s, j = q / s;
-            Lk[q] = (i >= j) ? Lcb[(long long)k * sh.ps + pidx(i, j, s)] : 0.0;
-        }
+        const double *FRk = FRb + (long long)k * frs;  // L(i, j) = FRk[j s + i], j < m
         if (lane < n) cvec[lane] = cb[(long long)k * n + lane];
         wave_sync();
-        if (lane < n) {  // Pb_tmp = Lxx_next^T c
+        if (lane < n) {  // Pb = P_{k+1} c + p_{k+1}
             double a = 0.0;
-            for (int t = lane; t < n; ++t) a += Ln[t + lane * n] * cvec[t];
-            va[lane] = a;
-        }
-        wave_sync();
-        if (lane < n) {  // Pb = Lxx_next Pb_tmp + p_next
-            double a = 0.0;
-            for (int t = 0; t <= lane; ++t) a += Ln[lane + t * n] * va[t];
+            for (int t = 0; t < n; ++t) a = __builtin_fma(Pn[lane + t * n], cvec[t], a);
             vb[lane] = a + pn[lane];
         }
         wave_sync();
-        if (lane < s) {  // lp = h~ + E^T Pb
+        if (lane < s) {  // lp = h~ + E^T Pb (lqr_kernel.hpp:138-143)
             double a = 0.0;
-            for (int t = 0; t < n; ++t) a += Ek[t + lane * n] * vb[t];
+            for (int t = 0; t < n; ++t) a = __builtin_fma(Ek[t + lane * n], vb[t], a);
             lp[lane] = hb[(long long)k * s + lane] + a;
         }
         wave_sync();
         if (lane == 0) {  // lu <- Luu^{-1} lu
             for (int i = 0; i < m; ++i) {
                 double v = lp[i];
-                for (int j = 0; j < i; ++j) v -= Lk[i + j * s] * lp[j];
-                lp[i] = v / Lk[i + i * s];
+                for (int j = 0; j < i; ++j) v -= FRk[j * s + i] * lp[j];
+                lp[i] = v / FRk[i * s + i];
             }
         }
         wave_sync();
         if (lane < n) {  // p -= Lxu lu
             double a = 0.0;
-            for (int i = 0; i < m; ++i) a += Lk[(m + lane) + i * s] * lp[i];
+            for (int i = 0; i < m; ++i) a = __builtin_fma(FRk[i * s + m + lane], lp[i], a);
             const double pnew = lp[m + lane] - a;
             lp[m + lane] = pnew;
             pn[lane] = pnew;
@@ -359,10 +129,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
         wave_sync();
         if (lane < m) FRb[(long long)k * frs + (long long)s * m + lane] = lp[lane];
         if (lpb && lane < s) lpb[(long long)k * s + lane] = lp[lane];
-        for (int q = lane; q < n * n; q += 64) {
-            const int i = q % n, j = q / n;
-            Ln[q] = Lk[(m + i) + (m + j) * s];
-        }
+        load_P(k);
         wave_sync();
     }
     double *eo = A.elem + (b * S + seg) * (long long)(3 * n * n + 2 * n);
@@ -573,19 +340,6 @@ __global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
     }
 }
 
-// Resident segment waves the device can hold for this shape: CUs x the
-// segment backward's occupancy.  Refining the horizon beyond that adds scan
-// rounds without adding parallelism.
-int seg_backward_slots(const Shape &sh, int device) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    const size_t smem = seg_smem_doubles(sh.n, sh.m) * sizeof(double);
-    hipError_t e = sh.s <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<1>, 64, smem)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd<2>, 64, smem);
-    if (e != hipSuccess || per <= 0) per = 1;
-    return cus * per;
-}
-
 // Resident scan waves (one combine each) the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
@@ -595,19 +349,6 @@ int seg_scan_slots(const Shape &sh, int device) {
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2>, 64, smem);
     if (e != hipSuccess || per <= 0) per = 1;
     return cus * per;
-}
-
-int launch_seg_backward(const SegArgs &a, hipStream_t st) {
-    const dim3 grid((unsigned)(a.sh.batch * a.S)), blk(64);
-    const size_t smem = seg_smem_doubles(a.sh.n, a.sh.m) * sizeof(double);
-    if (a.sh.s <= 16) hipLaunchKernelGGL(k_seg_bwd<1>, grid, blk, smem, st, a);
-    else if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd<2>, grid, blk, smem, st, a);
-    else {
-        set_error("parallel solver: n + m > 32 is not supported by this build");
-        return PDPLQR_ERR_UNSUPPORTED;
-    }
-    PDPLQR_HIP_TRY(hipGetLastError());
-    return PDPLQR_OK;
 }
 
 static size_t elems_smem(int n, int elems) { return (size_t)elems * (3 * n * n + 2 * n) * sizeof(double); }

@@ -40,3 +40,9 @@ d = np.diff(t[:, :10], axis=1)
 print(f"blocks={len(t)}  wall_clock64 ticks (100 MHz): total median {np.median(t[:, 9] - t[:, 0]):.0f}")
 for k, nm in enumerate(names):
     print(f"  {nm:18s} {np.median(d[:, k]):8.0f}")
+seg = buf.reshape(1024, 16).astype(np.int64)
+seg = seg[seg[:, 12] > 0]
+if len(seg):
+    st = seg[:, 12]
+    print(f"segment backward ({len(seg)} waves, median {np.median(st):.0f} stages): ticks per stage "
+          f"riccati {np.median(seg[:, 10] / st):.0f}  element {np.median(seg[:, 11] / st):.0f}")
