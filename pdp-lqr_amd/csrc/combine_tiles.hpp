@@ -50,7 +50,6 @@ struct CombSmem {
     double B[P * PL];  // R -> U in place, then output staging (symmetrisation)
     alignas(16) double cb[P];  // pivot-row broadcast of chol_tiles
     double sinv[P], luq[P];
-    double v1[P], v2[P], v3[P], v4[P];
 };
 
 // M <- n x n block at p (column-major, leading dimension ld, or its transpose);
@@ -238,16 +237,6 @@ __device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, 
     }
 }
 
-// y = add + op(M) x  (n-vectors, M column-major ld), lanes over rows
-__device__ __forceinline__ void lds_mv(double *y, const double *M, int ld, bool trans, const double *x,
-                                       const double *add, double sgn, int n, int lane) {
-    if (lane < n) {
-        double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc = __builtin_fma(trans ? M[k + lane * ld] : M[lane + k * ld], x[k], acc);
-        y[lane] = (add ? add[lane] : 0.0) + sgn * acc;
-    }
-}
-
 // symmetric store: out = (M + M^T) / 2 (n x n, ld n) through the LDS staging buffer
 template <int T>
 __device__ __forceinline__ void wm_store_sym(const WM<T> &M, double *out, int n, CombSmem<T> &sm, int lane) {
@@ -261,16 +250,33 @@ __device__ __forceinline__ void wm_store_sym(const WM<T> &M, double *out, int n,
     wave_sync();
 }
 
-// out = a (x) b  (a earlier, b later).  Element memory (global or LDS):
-// [F | C | f | P | p], column-major n x n blocks.  out must not alias a or b.
-template <int T>
-__device__ __forceinline__ bool tcombine(double *out, const double *ea, const double *eb, int n, bool need_FCf,
-                                         bool need_Pp, CombSmem<T> &sm, int lane) {
-    const int g = lane >> 4, c = lane & 15;
+// Input element blocks, each column-major n x n (or n-vectors), anywhere in
+// global memory or LDS.
+struct ElemIn {
+    const double *F, *C, *f, *P, *p;
+};
+
+// [F | C | f | P | p] contiguous (the element layout of the scans)
+__device__ __forceinline__ ElemIn elem_in(const double *e, int n) {
     const int nn = n * n;
-    const double *aF = ea, *aC = ea + nn, *af = ea + 2 * nn, *aP = ea + 2 * nn + n, *ap = ea + 3 * nn + n;
-    const double *bF = eb, *bC = eb + nn, *bf = eb + 2 * nn, *bP = eb + 2 * nn + n, *bp = eb + 3 * nn + n;
-    double *oF = out, *oC = out + nn, *of = out + 2 * nn, *oP = out + 2 * nn + n, *op = out + 3 * nn + n;
+    return ElemIn{e, e + nn, e + 2 * nn, e + 2 * nn + n, e + 3 * nn + n};
+}
+
+// out = a (x) b  (a earlier, b later).  The output blocks are addressed
+// separately (oF, oC, of are not touched when need_FCf is false, oP, op not
+// when need_Pp is false) and must not alias the inputs.  P_a and C_b are read
+// once, as addends of the last products: they are loaded up front so a
+// global-memory source costs no exposed latency.
+template <int T>
+__device__ __forceinline__ bool tcombine_parts(double *oF, double *oC, double *of, double *oP, double *op,
+                                               const ElemIn &ea, const ElemIn &eb, int n, bool need_FCf,
+                                               bool need_Pp, CombSmem<T> &sm, int lane) {
+    const int g = lane >> 4, c = lane & 15;
+    const double *aF = ea.F, *aC = ea.C, *af = ea.f, *ap = ea.p;
+    const double *bF = eb.F, *bf = eb.f, *bP = eb.P, *bp = eb.p;
+    WM<T> Pa, Cb;
+    if (need_Pp) wm_load(Pa, ea.P, n, n, false, 0.0, g, c);
+    if (need_FCf) wm_load(Cb, eb.C, n, n, false, 0.0, g, c);
     WM<T> Ca, Y, Z, Zt;
     COMB_MARK(0);
     wm_load(Ca, aC, n, n, false, 0.0, g, c);
@@ -278,9 +284,8 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
     WM<T> Fa;
     wm_load(Fa, aF, n, n, false, 0.0, g, c);
     if (need_Pp) {  // P = P_a + F_a^T (Y F_a)
-        WM<T> W, Pn, Pa;
+        WM<T> W, Pn;
         wm_tn(W, Y, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);
-        wm_load(Pa, aP, n, n, false, 0.0, g, c);
         wm_tn(Pn, Fa, W, n, 1.0, 0.0, &Pa, g, c);
         wm_store_sym(Pn, oP, n, sm, lane);
     }
@@ -291,10 +296,9 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
         wm_tn(W, Zt, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);   // Z F_a
         wm_tn(Fn, Fbt, W, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // F_b Z F_a
         wm_store(Fn, oF, n, n, g, c);
-        WM<T> W2t, W3, Cn, Cb;
+        WM<T> W2t, W3, Cn;
         wm_tn(W2t, Ca, Zt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);   // C_a Z^T = (Z C_a)^T
         wm_tn(W3, W2t, Fbt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Z C_a F_b^T
-        wm_load(Cb, bC, n, n, false, 0.0, g, c);
         wm_tn(Cn, Fbt, W3, n, 1.0, 0.0, &Cb, g, c);                     // F_b Z C_a F_b^T + C_b
         wm_store_sym(Cn, oC, n, sm, lane);
     }
@@ -327,6 +331,14 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
     wave_sync();
     COMB_MARK(9);
     return ok;
+}
+
+template <int T>
+__device__ __forceinline__ bool tcombine(double *out, const double *ea, const double *eb, int n, bool need_FCf,
+                                         bool need_Pp, CombSmem<T> &sm, int lane) {
+    const int nn = n * n;
+    return tcombine_parts<T>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n, elem_in(ea, n),
+                             elem_in(eb, n), n, need_FCf, need_Pp, sm, lane);
 }
 
 }  // namespace pdplqr

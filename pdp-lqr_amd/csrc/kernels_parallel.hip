@@ -6,19 +6,24 @@
 //   * the segment backward (element e = (F, C, f, P, p) of every segment) is
 //     k_seg_bwd_aug in kernels_segment.hip; k_seg_bwd_nofact below is its
 //     linear-terms-only counterpart.
-//   * k_seg_scan: one Hillis-Steele round of the prefix and suffix scans of the
-//     elements under the associative operator
+//   * k_seg_scan: one Hillis-Steele round of the suffix scan of the elements
+//     under the associative operator
 //         Z = (I + C_a P_b)^{-1}, F = F_b Z F_a, C = F_b Z C_a F_b^T + C_b,
 //         f = F_b Z (f_a - C_a p_b) + f_b, P = P_a + F_a^T P_b Z F_a,
 //         p = p_a + F_a^T Z^T (p_b + P_b f_a).
 //     The reference folds the same operator serially on the master thread
 //     (condensed_system.hpp:82-137 LU form, :203-290 Cholesky form); here
 //     P_b Z = Y = R (I + R^T C_a R)^{-1} R^T with R = chol(P_b), an SPD solve,
-//     evaluated on MFMA tiles (combine_tiles.hpp).
-//   * k_seg_boundary: x_hat_i = (I + C_pre P_suf)^{-1}(F_pre x0 + f_pre - C_pre p_suf)
-//     and u_hat_i = p_suf(i+1) + P_suf(i+1) x_hat_{i+1} (condensed forward).
+//     evaluated on MFMA tiles (combine_tiles.hpp).  Suffix entry i is the value
+//     function (P, p) at the start of segment i.
+//   * k_seg_maps: the closed-loop boundary map of every segment under those
+//     value functions, x_{i+1} = Z_i (F_i x_i + f_i - C_i p_{i+1}),
+//     Z_i = (I + C_i P_{i+1})^{-1}; k_map_scan composes the maps (prefix scan
+//     of affine maps: one matrix product per combine, no factorisation) into
+//     the boundary states x_hat_i and costates lambda_i = P_i x_hat_i + p_i
+//     (the condensed forward).
 //   * the rollout reuses k_riccati_fwd with the G_k u_hat coupling
-//     (lqr_kernel_parallel.hpp:195-198).
+//     (lqr_kernel_parallel.hpp:195-198), u_hat from lambda_{i+1}.
 #define PDPLQR_COMB_PROFILE_TU 1  // the combine phase marks live in this translation unit
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
@@ -184,167 +189,221 @@ int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // One Hillis-Steele round: inclusive prefix (dir 0) or suffix (dir 1) scan.
 // ---------------------------------------------------------------------------
-// Both operand elements are prefetched into LDS with one LDS-DMA burst (a
-// single HBM/L2 latency) before the combine reads them.
-// (es = 3 n^2 + 2 n is odd for odd n: the last double goes by a plain copy;
-// the caller waits on vmcnt and then wave_sync()s.)
-template <int T>
-__device__ __forceinline__ void elem_prefetch(double *dst, const double *src, int es, int lane) {
-    const int chunks = es / 2;
-    for (int q = 0; q * 64 < chunks; ++q) {
-        const int ch = q * 64 + lane;
-        if (ch < chunks) dma16(src + 2 * ch, dst + 2 * q * 64);
+// LDS[dst, dst + len) <- src[0, len) (doubles) with one LDS-DMA burst (a single
+// HBM/L2 latency) when src and dst are 16-byte aligned, by a plain copy
+// otherwise.  The caller waits on vmcnt(0) and then wave_sync()s.
+__device__ __forceinline__ void stage_range(double *dst, const double *src, int len, int lane) {
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+        const int chunks = len >> 1;
+        for (int q = 0; q * 64 < chunks; ++q) {
+            const int ch = q * 64 + lane;
+            if (ch < chunks) dma16(src + 2 * ch, dst + 2 * q * 64);
+        }
+        if ((len & 1) && lane == 0) dst[len - 1] = src[len - 1];
+    } else {
+        for (int q = lane; q < len; q += 64) dst[q] = src[q];
     }
-    if ((es & 1) && lane == 0) dst[es - 1] = src[es - 1];
 }
+
+// LDS images of the two combine operands without the blocks read only once as
+// addends (P_a, C_b: loaded from global memory by tcombine_parts), 2 n^2 + 2 n
+// doubles each: a = [F | C | f | p], b = [F | f | P | p].  At 24/8 the scan
+// kernel then needs 19.2 KB of element LDS instead of 28.4 KB, and 4 blocks
+// fit a CU (the register file holds 4 waves of it anyway).
+__device__ __forceinline__ int op_stage_len(int n) { return (2 * n * n + 2 * n + 1) & ~1; }
+
+__device__ __forceinline__ ElemIn stage_left(double *dst, const double *e, int n, int lane) {
+    const int nn = n * n;
+    stage_range(dst, e, 2 * nn + n, lane);                  // F | C | f
+    stage_range(dst + 2 * nn + n, e + 3 * nn + n, n, lane);  // p
+    return ElemIn{dst, dst + nn, dst + 2 * nn, e + 2 * nn + n, dst + 2 * nn + n};
+}
+
+__device__ __forceinline__ ElemIn stage_right(double *dst, const double *e, int n, int lane) {
+    const int nn = n * n;
+    stage_range(dst, e, nn, lane);                        // F
+    stage_range(dst + nn, e + 2 * nn, nn + 2 * n, lane);  // f | P | p
+    return ElemIn{dst, e + nn, dst + nn, dst + nn + n, dst + 2 * nn + n};
+}
+
+static size_t op_stage_bytes(int n) { return 2 * (size_t)((2 * n * n + 2 * n + 1) & ~1) * sizeof(double); }
 
 template <int T>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
-    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 elements (launcher: elems_smem(n, 2))
+    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 operand images (op_stage_bytes)
     const int lane = threadIdx.x;
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
-    const long long b = blockIdx.x / (2 * S);
-    const int rem = blockIdx.x % (2 * S);
-    const int dir = rem / S, i = rem % S;
-    const double *in = (dir == 0 ? A.pre_in : A.suf_in) + b * (long long)S * es;
-    double *out = (dir == 0 ? A.pre_out : A.suf_out) + b * (long long)S * es;
-    int ia, ib;
-    if (dir == 0) {  // pre_i = pre_{i-d} (x) pre_i
-        if (i - d < 0) {
-            elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
-            return;
-        }
-        ia = i - d; ib = i;
-    } else {  // suf_i = suf_i (x) suf_{i+d}
-        if (i + d >= S) {
-            elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
-            return;
-        }
-        ia = i; ib = i + d;
+    const long long b = blockIdx.x / S;
+    const int i = blockIdx.x % S;
+    const double *in = A.in + b * (long long)S * es;
+    double *out = A.out + b * (long long)S * es;
+    if (i + d >= S) {  // suf_i already reaches the last segment
+        elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
+        return;
     }
-    // Both directions need full elements: the next round's combine reads the
-    // right operand's P, p (Z = (I + C_a P_b)^{-1}).  A suffix ending at the
-    // real terminal has F = C = f = 0.
-    const int esp = (es + 1) & ~1;  // 16-byte aligned second buffer
-    elem_prefetch<T>(ebuf, in + (long long)ia * es, es, lane);
-    elem_prefetch<T>(ebuf + esp, in + (long long)ib * es, es, lane);
+    // The right operand covers segments [i + d, min(i + 2d - 1, S - 1)].  When
+    // that range holds the real terminal its F = C = f = 0, and so are the
+    // result's: only the value function (P, p) is combined.
+    const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    const ElemIn ea = stage_left(ebuf, in + (long long)i * es, n, lane);
+    const ElemIn eb = stage_right(ebuf + op_stage_len(n), in + (long long)(i + d) * es, n, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
-    const bool ok = tcombine<T>(out + (long long)i * es, ebuf, ebuf + esp, n, true, true, sm, lane);
+    double *o = out + (long long)i * es;
+    const int nn = n * n;
+    const bool ok = tcombine_parts<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, eb, n, fcf, true,
+                                      sm, lane);
+    if (!fcf)
+        for (int q = lane; q < 2 * n * n + n; q += 64) o[q] = 0.0;  // [F | C | f]
     if (!ok && lane == 0) atomicOr(A.flag, 1);
 }
 
 // ---------------------------------------------------------------------------
-// Boundary states: x_hat_i from the exclusive prefix (optionally left-folded
-// with a global prefix) and the suffix (optionally right-folded with a global
-// suffix); u_hat_i in a second pass.
+// Boundary maps.  With the value function V_j = (P_j, p_j) at boundary j (the
+// suffix-scan entry j, right-folded with the global suffix of later shards),
+// the state at boundary j follows from the state at boundary j - 1 through
+// the element (F, C, f) of segment j - 1:
+//     x_j = Phi_j x_{j-1} + phi_j,  Z = (I + C P_j)^{-1},
+//     Phi_j = Z F,  phi_j = Z (f - C p_j)
+// -- the condensed forward of condensed_system.hpp:117-137 (LU form) and
+// :262-290 (Cholesky form), which walks this recursion serially.  Block j = 0
+// maps x0 through the global prefix of earlier shards (or the identity) and
+// writes x_0 directly.  maps: [b][S+1][Phi | phi], vfun: [b][S+1][P | p].
 // ---------------------------------------------------------------------------
 template <int T>
-__global__ __launch_bounds__(64) void k_seg_xhat(BoundaryArgs A) {
-    extern __shared__ __attribute__((aligned(16))) double dyn[];
+__global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double dyn[];  // 2 operand images when A.right
     __shared__ CombSmem<T> sm;
-    const int lane = threadIdx.x;
-    const int n = A.n, S = A.S;
-    const int es = 3 * n * n + 2 * n;
-    const long long b = blockIdx.x / (S + 1);
-    const int i = blockIdx.x % (S + 1);  // i == S: state after the last segment (shard mode)
-    double *pre = dyn, *suf = dyn + es, *tmp = dyn + 2 * es;  // tmp + es: combine output
-    const double *preb = A.pre + b * (long long)S * es;
-    const double *sufb = A.suf + b * (long long)S * es;
-    // prefix before segment i: global_left (x) pre_{i-1}
-    if (i == 0) {
-        if (A.left) elem_copy(pre, A.left + b * (long long)es, n, lane);
-        else {
-            Elem e = elem_view(pre, n);
-            for (int q = lane; q < n * n; q += 64) {
-                e.F[q] = (q % n == q / n) ? 1.0 : 0.0;
-                e.C[q] = 0.0;
-                e.P[q] = 0.0;
-            }
-            for (int q = lane; q < n; q += 64) { e.f[q] = 0.0; e.p[q] = 0.0; }
-        }
+    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int n = A.n, S = A.S, J = S + 1, nn = n * n;
+    const int es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    double *vo = A.vfun + (b * J + j) * (long long)mw;
+    double *mo = A.maps + (b * J + j) * (long long)mw;
+    bool ok = true;
+    // V_j: [P | p] at vP, vp (global), or absent (j == S on the last shard)
+    const double *vP = nullptr, *vp = nullptr;
+    if (j < S && A.right) {
+        const ElemIn ea = stage_left(dyn, A.suf + (b * S + j) * (long long)es, n, lane);
+        const ElemIn eb = stage_right(dyn + op_stage_len(n), A.right + b * (long long)es, n, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
+        ok = tcombine_parts<T>(nullptr, nullptr, nullptr, vo, vo + nn, ea, eb, n, false, true, sm, lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // vo is re-read by other lanes below
+        vP = vo;
+        vp = vo + nn;
     } else {
-        if (A.left) {
-            elem_copy(tmp, A.left + b * (long long)es, n, lane);
-            elem_copy(suf, preb + (long long)(i - 1) * es, n, lane);  // scratch
-            wave_sync();
-            tcombine<T>(pre, tmp, suf, n, true, false, sm, lane);
+        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : A.right ? A.right + b * (long long)es
+                                                                                  : nullptr;
+        if (src) {
+            vP = src + 2 * nn + n;
+            vp = src + 3 * nn + n;
+            for (int q = lane; q < mw; q += 64) vo[q] = q < nn ? vP[q] : vp[q - nn];
         } else {
-            elem_copy(pre, preb + (long long)(i - 1) * es, n, lane);
-            wave_sync();
+            for (int q = lane; q < mw; q += 64) vo[q] = 0.0;
         }
     }
-    // suffix from segment i: suf_i (x) global_right ; for i == S only global_right
-    bool have_suf = true;
-    if (i < S) {
-        if (A.right) {
-            elem_copy(tmp, sufb + (long long)i * es, n, lane);
-            elem_copy(suf, A.right + b * (long long)es, n, lane);
-            wave_sync();
-            double *o = tmp + es;  // scratch beyond tmp: pre | suf | tmp | tmp2 fit in 4 es (see launcher)
-            tcombine<T>(o, tmp, suf, n, false, true, sm, lane);
-            elem_copy(suf, o, n, lane);
-            wave_sync();
+    // source element: segment j - 1, the global prefix (j = 0, later shards), or the identity
+    const double *src = j > 0 ? A.elem + (b * S + j - 1) * (long long)es : A.left ? A.left + b * (long long)es
+                                                                                 : nullptr;
+    WM<T> Phi, PhiT;
+    WV<T> phi;
+    if (src) {
+        WM<T> Fs;
+        WV<T> fs;
+        wm_load(Fs, src, n, n, false, 0.0, g, c);
+        wv_load(fs, src + 2 * nn, n, g, c);
+        if (vP) {
+            WM<T> Cs, Y, Z, Zt;
+            WV<T> pv, v1;
+            wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
+            ok = comb_core(Y, Z, Zt, Cs, vP, n, sm, lane) && ok;
+            wv_load(pv, vp, n, g, c);
+            wv_tn(v1, Cs, pv, n, -1.0, &fs);  // f - C p_j  (C symmetric)
+            wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p_j)
+            if (j > 0) wm_tn(Phi, Zt, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Z F
+            else wm_tn(PhiT, Fs, Zt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // F^T Z^T
         } else {
-            elem_copy(suf, sufb + (long long)i * es, n, lane);
-            wave_sync();
-        }
-    } else {
-        if (A.right) {
-            elem_copy(suf, A.right + b * (long long)es, n, lane);
-            wave_sync();
-        } else {
-            have_suf = false;
+            phi = fs;
+            if (j > 0) Phi = Fs;
+            else wm_load(PhiT, src, n, n, true, 0.0, g, c);
         }
     }
-    Elem P = elem_view(pre, n), Sf = elem_view(suf, n);
-    double *x0 = tmp;  // reuse
-    if (lane < n) x0[lane] = A.x0[b * n + lane];
-    wave_sync();
-    // rhs = F_pre x0 + f_pre - C_pre p_suf
-    double *rhs = tmp + es;  // scratch (the fold output is consumed)
-    for (int r = lane; r < n; r += 64) {
-        double acc = P.f[r];
-        for (int k = 0; k < n; ++k) acc = __builtin_fma(P.F[r + k * n], x0[k], acc);
-        if (have_suf)
-            for (int k = 0; k < n; ++k) acc = __builtin_fma(-P.C[r + k * n], Sf.p[k], acc);
-        rhs[r] = acc;
+    if (!ok && lane == 0) atomicOr(A.flag, 2);
+    if (j > 0) {
+        wm_store(Phi, mo, n, n, g, c);
+        wv_store(phi, mo + nn, n, g, c);
+        return;
     }
-    wave_sync();
-    double *xh = A.xhat + (b * (long long)(S + 1) + i) * n;
-    if (have_suf) {
-        // x = (I + C_pre P_suf)^{-1} rhs = Z rhs with Z from comb_core(C_pre, P_suf)
-        constexpr int PL = 16 * T + 1;
-        WM<T> Ca, Y, Z, Zt;
-        wm_load(Ca, P.C, n, n, false, 0.0, lane >> 4, lane & 15);
-        const bool ok = comb_core(Y, Z, Zt, Ca, Sf.P, n, sm, lane);
-        if (!ok && lane == 0) atomicOr(A.flag, 2);
-        wm_store(Z, sm.A, PL, n, lane >> 4, lane & 15);
-        wave_sync();
-        lds_mv(sm.v2, sm.A, PL, false, rhs, nullptr, 1.0, n, lane);
-        wave_sync();
-        if (lane < n) xh[lane] = sm.v2[lane];
-        // costate at the start of segment i: lambda = P_suf x + p_suf (stored for u_hat_{i-1})
-        double *lam = A.lam + (b * (long long)(S + 1) + i) * n;
-        wave_sync();
-        for (int r = lane; r < n; r += 64) {
-            double acc = Sf.p[r];
-            for (int k = 0; k < n; ++k) acc = __builtin_fma(Sf.P[r + k * n], sm.v2[k], acc);
-            lam[r] = acc;
-        }
-    } else {
-        if (lane < n) xh[lane] = rhs[lane];
+    // j = 0: x_0 = Phi x0 + phi (x0 itself without a global prefix), lambda_0 = P_0 x_0 + p_0
+    WV<T> x0v, x;
+    wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
+    if (src) wv_tn(x, PhiT, x0v, n, 1.0, &phi);
+    else x = x0v;
+    wv_store(x, mo + nn, n, g, c);
+    wv_store(x, A.xhat + b * (long long)J * n, n, g, c);
+    if (vP) {
+        WM<T> Pv;
+        WV<T> pv, lam;
+        wm_load(Pv, vP, n, n, false, 0.0, g, c);
+        wv_load(pv, vp, n, g, c);
+        wv_tn(lam, Pv, x, n, 1.0, &pv);  // P symmetric
+        wv_store(lam, A.lam + b * (long long)J * n, n, g, c);
     }
+}
+
+// ---------------------------------------------------------------------------
+// One Hillis-Steele round of the prefix composition of the boundary maps:
+// m_j <- m_j o m_{j-d}.  Map 0 is the constant x_0, so after the round with
+// distance d the entries j < 2 d are anchored at x0: their phi is x_j (written
+// to xhat with lambda_j = P_j x_j + p_j) and their Phi is never read again.
+// ---------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
+    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int n = A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    const double *in = A.in + b * (long long)J * mw;
+    double *out = A.out + b * (long long)J * mw;
+    if (j < d) {  // anchored earlier: keep x_j for the next round's left operands
+        for (int q = lane; q < n; q += 64) out[(long long)j * mw + nn + q] = in[(long long)j * mw + nn + q];
+        return;
+    }
+    const int ia = j - d;
+    const double *ej = in + (long long)j * mw, *ea = in + (long long)ia * mw;
+    WM<T> PjT;
+    WV<T> pa, pj, po;
+    wm_load(PjT, ej, n, n, true, 0.0, g, c);
+    wv_load(pa, ea + nn, n, g, c);
+    wv_load(pj, ej + nn, n, g, c);
+    wv_tn(po, PjT, pa, n, 1.0, &pj);  // Phi_j phi_a + phi_j
+    wv_store(po, out + (long long)j * mw + nn, n, g, c);
+    if (ia >= d) {  // not anchored yet: compose the matrices
+        WM<T> Pa, Po;
+        wm_load(Pa, ea, n, n, false, 0.0, g, c);
+        wm_tn(Po, PjT, Pa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);
+        wm_store(Po, out + (long long)j * mw, n, n, g, c);
+        return;
+    }
+    wv_store(po, A.xhat + (b * J + j) * (long long)n, n, g, c);
+    const double *v = A.vfun + (b * J + j) * (long long)mw;
+    WM<T> Pv;
+    WV<T> pv, lam;
+    wm_load(Pv, v, n, n, false, 0.0, g, c);
+    wv_load(pv, v + nn, n, g, c);
+    wv_tn(lam, Pv, po, n, 1.0, &pv);
+    wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
 }
 
 // Resident scan waves (one combine each) the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    const size_t smem = 2 * (size_t)((3 * sh.n * sh.n + 2 * sh.n + 1) & ~1) * sizeof(double);
+    const size_t smem = op_stage_bytes(sh.n);
     hipError_t e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1>, 64, smem)
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2>, 64, smem);
     if (e != hipSuccess || per <= 0) per = 1;
@@ -356,9 +415,9 @@ static size_t elems_smem(int n, int elems) { return (size_t)elems * (3 * n * n +
 static int tile_order(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 0); }
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
-    const dim3 grid((unsigned)(batch * 2 * a.S)), blk(64);
+    const dim3 grid((unsigned)(batch * a.S)), blk(64);
     const int T = tile_order(a.n);
-    const size_t smem = 2 * (size_t)((3 * a.n * a.n + 2 * a.n + 1) & ~1) * sizeof(double);
+    const size_t smem = op_stage_bytes(a.n);
     if (T == 1) hipLaunchKernelGGL(k_seg_scan<1>, grid, blk, smem, st, a);
     else if (T == 2) hipLaunchKernelGGL(k_seg_scan<2>, grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
@@ -366,11 +425,22 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     return PDPLQR_OK;
 }
 
-int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st) {
+int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
-    if (T == 1) hipLaunchKernelGGL(k_seg_xhat<1>, grid, blk, elems_smem(a.n, 4), st, a);
-    else if (T == 2) hipLaunchKernelGGL(k_seg_xhat<2>, grid, blk, elems_smem(a.n, 4), st, a);
+    const size_t smem = a.right ? op_stage_bytes(a.n) : 0;
+    if (T == 1) hipLaunchKernelGGL(k_seg_maps<1>, grid, blk, smem, st, a);
+    else if (T == 2) hipLaunchKernelGGL(k_seg_maps<2>, grid, blk, smem, st, a);
+    else return PDPLQR_ERR_UNSUPPORTED;
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
+    const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
+    const int T = tile_order(a.n);
+    if (T == 1) hipLaunchKernelGGL(k_map_scan<1>, grid, blk, 0, st, a);
+    else if (T == 2) hipLaunchKernelGGL(k_map_scan<2>, grid, blk, 0, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;

@@ -19,20 +19,31 @@ struct SegArgs {
 
 struct ScanArgs {
     int n, S, dist;
-    const double *pre_in, *suf_in;
-    double *pre_out, *suf_out;
+    int terminal;              // the last element ends at the real terminal (F = C = f = 0)
+    const double *in;          // suffix scan ping-pong [b][S][es]
+    double *out;
     int *flag;
 };
 
-struct BoundaryArgs {
+struct MapArgs {
     int n, S;
-    const double *pre, *suf;   // inclusive prefix / suffix scans [b][S][es]
+    const double *elem;        // segment elements [b][S][es]
+    const double *suf;         // inclusive suffix scan [b][S][es]
     const double *left;        // optional global prefix element [b][es] (horizon shards)
     const double *right;       // optional global suffix element [b][es]
     const double *x0;          // [b][n]
-    double *xhat;              // [b][S+1][n]
-    double *lam;               // [b][S+1][n]  costate at segment starts
+    double *maps;              // [b][S+1][n^2 + n]  boundary maps (Phi | phi)
+    double *vfun;              // [b][S+1][n^2 + n]  value functions at the boundaries (P | p)
+    double *xhat, *lam;        // [b][S+1][n]
     int *flag;
+};
+
+struct MapScanArgs {
+    int n, S, dist;
+    const double *in;          // [b][S+1][n^2 + n]
+    double *out;
+    const double *vfun;
+    double *xhat, *lam;
 };
 
 struct SegFwd {
@@ -48,7 +59,8 @@ int seg_backward_slots(const Shape &sh, int device);
 int seg_scan_slots(const Shape &sh, int device);
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
-int launch_seg_xhat(const BoundaryArgs &a, int batch, hipStream_t st);
+int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
+int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,

@@ -21,7 +21,8 @@ struct ParallelState {
     int S = 0;
     int32_t *seg_start = nullptr, *seg_len = nullptr, *seg_status = nullptr;
     double *G = nullptr, *elem = nullptr, *bufA = nullptr, *bufB = nullptr, *xhat = nullptr, *lam = nullptr;
-    const double *pre_final = nullptr, *suf_final = nullptr;
+    double *mapA = nullptr, *mapB = nullptr, *vfun = nullptr;  // boundary maps (ping-pong), value functions
+    const double *suf_final = nullptr;
     int *flag = nullptr;
     // horizon shards
     double *left = nullptr, *right = nullptr, *gathered = nullptr;
@@ -92,20 +93,25 @@ static int parallel_init(pdplqr_handle h) {
     // device refinement: split every reference segment into pieces of <= Lsub
     // stages.  The number of device segments S per problem trades the serial
     // segment backward (N/S stages per wave, batch S waves over the resident
-    // slots) against the scans (log2 S rounds of 2 batch S combines):
-    //     t(S) = a ceil(N/S) ceil(batch S / slots_bwd) + b ceil(log2 S) ceil(2 batch S / slots_scan)
-    // with a, b the per-stage and per-combine latencies of one wave
-    // (profiles/r01: ~10 / 15 us for s <= 16, ~50 / 45 us for 24/8).
+    // slots) against the suffix scan (log2 S rounds of batch S combines), the
+    // boundary maps (one combine-sized round) and their composition (log2 S
+    // rounds of one matrix product each):
+    //     t(S) = a ceil(N/S) ceil(batch S / slots_bwd) + b (ceil(log2 S) + 1) ceil(batch S / slots_scan)
+    //            + c ceil(log2 (S + 1))
+    // with a, b, c the per-stage (backward + rollout), per-combine and
+    // per-composition latencies of one wave (profiles/r01 c4_v12: a ~10 us,
+    // b ~45 us, c ~5.5 us at 24/8; a ~10 us, b ~15 us for s <= 16).
     int Lsub = h->cfg.segment_len;
     if (Lsub <= 0) {
-        const double a = sh.s <= 16 ? 10.0 : 50.0, b = sh.s <= 16 ? 15.0 : 45.0;
+        const double a = 10.0, b = sh.s <= 16 ? 15.0 : 45.0, cm = sh.s <= 16 ? 4.0 : 5.5;
         const long long sb = seg_backward_slots(sh, h->cfg.device), ss = seg_scan_slots(sh, h->cfg.device);
         const long long B = sh.batch;
         auto cost = [&](long long S) {
-            const long long per = (sh.N + S - 1) / S, rb = (B * S + sb - 1) / sb, rs = (2 * B * S + ss - 1) / ss;
-            int lg = 0;
+            const long long per = (sh.N + S - 1) / S, rb = (B * S + sb - 1) / sb, rs = (B * S + ss - 1) / ss;
+            int lg = 0, lg1 = 0;
             while ((1LL << lg) < S) ++lg;
-            return a * per * rb + b * lg * rs;
+            while ((1LL << lg1) < S + 1) ++lg1;
+            return a * per * rb + b * (lg + 1) * rs + cm * lg1;
         };
         long long best = 1;
         double bc = cost(1);
@@ -141,6 +147,9 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->elem, B * S * es)) || (rc = palloc(h, &ps->bufA, B * S * es)) ||
         (rc = palloc(h, &ps->bufB, B * S * es)) || (rc = palloc(h, &ps->xhat, B * (S + 1) * sh.n)) ||
         (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, 1)) ||
+        (rc = palloc(h, &ps->mapA, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
+        (rc = palloc(h, &ps->mapB, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
+        (rc = palloc(h, &ps->vfun, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->left, B * es)) || (rc = palloc(h, &ps->right, B * es)) ||
         (rc = palloc(h, &ps->has_suf, 1)))
         return rc;
@@ -151,9 +160,9 @@ static int parallel_init(pdplqr_handle h) {
     return PDPLQR_OK;
 }
 
-// segment backward + prefix/suffix scans; `last_is_terminal` = 0 for a
-// non-final horizon shard.
-static int parallel_scans(pdplqr_handle h);
+// segment backward + suffix scan; `last_is_terminal` = 0 for a non-final
+// horizon shard.
+static int parallel_scans(pdplqr_handle h, int last_is_terminal);
 
 static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
     ParallelState *ps = h->par;
@@ -177,59 +186,69 @@ static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = 
     PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, sizeof(int), h->stream));
     int rc = fact ? launch_seg_backward(a, h->stream) : launch_seg_backward_nofact(a, h->stream);
     if (rc) return rc;
-    return parallel_scans(h);
+    return parallel_scans(h, last_is_terminal);
 }
 
-// inclusive prefix / suffix scans of the segment elements (log2 S rounds)
-static int parallel_scans(pdplqr_handle h) {
+// inclusive suffix scan of the segment elements (ceil(log2 S) rounds): entry i
+// is the value function at the start of segment i
+static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
     ParallelState *ps = h->par;
     const Shape &sh = h->sh;
-    int rc;
-    const double *pin = ps->elem, *sin = ps->elem;
-    double *preo[2] = {ps->bufA, ps->bufB};
-    if (!h->suf_bufs[0]) {  // suffix ping-pong buffers, allocated on first use
-        const long long es = 3LL * sh.n * sh.n + 2LL * sh.n;
-        if ((rc = palloc(h, &h->suf_bufs[0], (long long)sh.batch * ps->S * es)) ||
-            (rc = palloc(h, &h->suf_bufs[1], (long long)sh.batch * ps->S * es)))
-            return rc;
-    }
+    const double *sin = ps->elem;
+    double *bufs[2] = {ps->bufA, ps->bufB};
     int round = 0;
     for (int d = 1; d < ps->S; d <<= 1, ++round) {
         ScanArgs s;
         s.n = sh.n;
         s.S = ps->S;
         s.dist = d;
-        s.pre_in = pin;
-        s.suf_in = sin;
-        s.pre_out = preo[round & 1];
-        s.suf_out = h->suf_bufs[round & 1];
+        s.terminal = last_is_terminal;
+        s.in = sin;
+        s.out = bufs[round & 1];
         s.flag = ps->flag;
-        if ((rc = launch_seg_scan(s, sh.batch, h->stream))) return rc;
-        pin = s.pre_out;
-        sin = s.suf_out;
+        int rc = launch_seg_scan(s, sh.batch, h->stream);
+        if (rc) return rc;
+        sin = s.out;
     }
-    ps->pre_final = pin;
     ps->suf_final = sin;
     return PDPLQR_OK;
 }
 
+// condensed forward: boundary maps under the suffix value functions, their
+// prefix composition (ceil(log2 (S + 1)) rounds), then the segment rollouts
 static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const double *left, const double *right,
                             int last_is_terminal) {
     ParallelState *ps = h->par;
     const Shape &sh = h->sh;
-    BoundaryArgs ba;
-    ba.n = sh.n;
-    ba.S = ps->S;
-    ba.pre = ps->pre_final;
-    ba.suf = ps->suf_final;
-    ba.left = left;
-    ba.right = right;
-    ba.x0 = x0;
-    ba.xhat = ps->xhat;
-    ba.lam = ps->lam;
-    ba.flag = ps->flag;
-    int rc = launch_seg_xhat(ba, sh.batch, h->stream);
+    MapArgs ma;
+    ma.n = sh.n;
+    ma.S = ps->S;
+    ma.elem = ps->elem;
+    ma.suf = ps->suf_final;
+    ma.left = left;
+    ma.right = right;
+    ma.x0 = x0;
+    ma.maps = ps->mapA;
+    ma.vfun = ps->vfun;
+    ma.xhat = ps->xhat;
+    ma.lam = ps->lam;
+    ma.flag = ps->flag;
+    int rc = launch_seg_maps(ma, sh.batch, h->stream);
     if (rc) return rc;
+    double *mb[2] = {ps->mapA, ps->mapB};
+    int round = 0;
+    for (int d = 1; d < ps->S + 1; d <<= 1, ++round) {
+        MapScanArgs ms;
+        ms.n = sh.n;
+        ms.S = ps->S;
+        ms.dist = d;
+        ms.in = mb[round & 1];
+        ms.out = mb[(round + 1) & 1];
+        ms.vfun = ps->vfun;
+        ms.xhat = ps->xhat;
+        ms.lam = ps->lam;
+        if ((rc = launch_map_scan(ms, sh.batch, h->stream))) return rc;
+    }
     SegFwd sf;
     sf.S = ps->S;
     sf.seg_start = ps->seg_start;
@@ -441,7 +460,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
 }  // extern "C"
 
 // Internal diagnostics (not part of include/pdplqr.h): copy a PARALLEL
-// handle's segment buffers to host.  which: 0 elem, 1 prefix scan, 2 suffix
+// handle's segment buffers to host.  which: 0 elem, 1 boundary value functions [b][S+1][n^2+n], 2 suffix
 // scan, 3 xhat [b][S+1][n], 4 lam, 5 device segment starts/lengths (int32 pairs).
 extern "C" int pdplqr_debug_parallel(pdplqr_handle h, int which, void *out, long long bytes) {
     if (!h || !h->par) return PDPLQR_ERR_INVALID;
@@ -450,7 +469,7 @@ extern "C" int pdplqr_debug_parallel(pdplqr_handle h, int which, void *out, long
     const void *src = nullptr;
     switch (which) {
         case 0: src = ps->elem; break;
-        case 1: src = ps->pre_final; break;
+        case 1: src = ps->vfun; break;
         case 2: src = ps->suf_final; break;
         case 3: src = ps->xhat; break;
         case 4: src = ps->lam; break;
