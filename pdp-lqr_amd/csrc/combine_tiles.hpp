@@ -14,8 +14,8 @@
 //     Y = U^T U = P_b (I + C_a P_b)^{-1},  Z = I - C_a Y = (I + C_a P_b)^{-1}
 //     F = F_b Z F_a,  C = F_b Z C_a F_b^T + C_b,  f = F_b Z (f_a - C_a p_b) + f_b,
 //     P = P_a + F_a^T Y F_a,  p = p_a + F_a^T Z^T (p_b + P_b f_a).
-// Cholesky factors come from chol_tiles (device_common.hpp); the triangular
-// solve for U runs with the column in registers (Q staged in LDS); the
+// Both factorisations run on registers only (elim_regs: DPP / permlane
+// broadcasts); U is carried through the second one as extra columns; the
 // matrix-vector products are single-column MFMAs on the same operands.
 #pragma once
 
@@ -106,83 +106,181 @@ __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, 
         }
 }
 
-template <int T>
-__device__ __forceinline__ bool wm_chol(WM<T> &M, int n, CombSmem<T> &sm, int g, int c) {
-    double lpr[T][4];
+// ---------------------------------------------------------------------------
+// Register-only elimination (no LDS, no branches per pivot).  For pivot j the
+// lanes need the pivot column at their own rows and the pivot row at their own
+// columns.  In the C/D layout column j of tile (a, j/16) sits in lane
+// (g, j & 15) of every row group: DPP row_newbcast copies it to the 16 lanes of
+// the row (v_mov_b64_dpp, one instruction per double).  Row j sits in row group
+// j & 3: v_permlane16_swap / v_permlane32_swap on two copies of a register
+// leave the even- and odd-group (lower- and upper-half) values side by side,
+// and the compile-time group index picks the pivot's (4 VALU per double).
+// ---------------------------------------------------------------------------
+template <int S>
+__device__ __forceinline__ double dpp_newbcast(double v) {
+    long long b = __builtin_bit_cast(long long, v);
+    b = __builtin_amdgcn_update_dpp((long long)0, b, 0x150 + S, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, b);
+}
+
+// lane (g, c) <- lane (g, src) of v (src folds to a constant after unrolling)
+__device__ __forceinline__ double bcast_lane16(double v, int src) {
+    switch (src) {
+        case 0: return dpp_newbcast<0>(v);
+        case 1: return dpp_newbcast<1>(v);
+        case 2: return dpp_newbcast<2>(v);
+        case 3: return dpp_newbcast<3>(v);
+        case 4: return dpp_newbcast<4>(v);
+        case 5: return dpp_newbcast<5>(v);
+        case 6: return dpp_newbcast<6>(v);
+        case 7: return dpp_newbcast<7>(v);
+        case 8: return dpp_newbcast<8>(v);
+        case 9: return dpp_newbcast<9>(v);
+        case 10: return dpp_newbcast<10>(v);
+        case 11: return dpp_newbcast<11>(v);
+        case 12: return dpp_newbcast<12>(v);
+        case 13: return dpp_newbcast<13>(v);
+        case 14: return dpp_newbcast<14>(v);
+        default: return dpp_newbcast<15>(v);
+    }
+}
+
+// lane (g, c) <- lane (gj, c) of v.  v_permlane16_swap(x, y) with x = y = v
+// returns (x', y') = (value of the even group, value of the odd group) of each
+// 32-lane half; v_permlane32_swap likewise returns (lower half, upper half).
+__device__ __forceinline__ double bcast_group(double v, int gj) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    lo = (gj & 1) ? a[1] : a[0];
+    hi = (gj & 1) ? b[1] : b[0];
+    const auto a2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    lo = (gj & 2) ? a2[1] : a2[0];
+    hi = (gj & 2) ? b2[1] : b2[0];
+    return __hiloint2double(hi, lo);
+}
+
+// Right-looking elimination of the pivots 0..n-1 of the symmetric padded
+// matrix M (left unscaled: M's lower part ends as d_j L[:, j], L unit lower,
+// d_j the pivots), optionally carrying extra columns B through the same row
+// operations (B <- L^{-1} B).  colinv[b] = 1/sqrt(d) of column 16 b + c,
+// rowinv[a][r] = 1/sqrt(d) of row 16 a + 4 r + g (AUG only).  Upper-triangle
+// entries of M are left as garbage.  False if a pivot is not positive.
+template <int T, bool AUG, int NN>
+__device__ __forceinline__ bool elim_regs_n(WM<T> &M, WM<T> &B, int n_rt, double (&colinv)[T],
+                                            double (&rowinv)[T][4], int g, int c) {
+    constexpr int P = 16 * T;
+    const int n = NN > 0 ? NN : n_rt;
+    bool ok = true;
+#pragma unroll
+    for (int b = 0; b < T; ++b) colinv[b] = 1.0;
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) lpr[a][r] = 0.0;
-    const bool ok = chol_tiles<T>(M.t, lpr, sm.cb, sm.sinv, sm.luq, 0, n, 0, false, g, c);
-    finalize_L<T>(M.t, sm.sinv, 0, n, g, c);  // sinv[i] = 1 / L[i][i]
-    wave_sync();
+        for (int r = 0; r < 4; ++r) rowinv[a][r] = 1.0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        if (j < n) {
+            const int tj = j >> 4, cj = j & 15, gj = j & 3, rj = (j >> 2) & 3;
+            const double djj = readlane_f64(M.t[tj][tj][rj], (gj << 4) + cj);
+            ok = ok && (djj > 0.0);
+            const double inv = rsqrt_f64(djj), inv2 = inv * inv;
+            colinv[tj] = (c == cj) ? inv : colinv[tj];
+            if (AUG) rowinv[tj][rj] = (g == gj) ? inv : rowinv[tj][rj];
+            double lc[T], lb[T], li[T][4];
+#pragma unroll
+            for (int b = tj; b < T; ++b) {
+                const double v = bcast_group(M.t[tj][b][rj], gj);
+                lc[b] = (16 * b + c > j) ? v * inv2 : 0.0;
+            }
+            if (AUG)
+#pragma unroll
+                for (int b = 0; b < T; ++b) lb[b] = bcast_group(B.t[tj][b][rj], gj) * inv2;
+#pragma unroll
+            for (int a = tj; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = bcast_lane16(M.t[a][tj][r], cj);
+                    // rows <= j keep their values (finished rows of B)
+                    li[a][r] = (AUG && a == tj && 16 * a + 4 * r + g <= j) ? 0.0 : v;
+                }
+#pragma unroll
+            for (int a = tj; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                    for (int b = tj; b < T; ++b) M.t[a][b][r] = __builtin_fma(-li[a][r], lc[b], M.t[a][b][r]);
+                    if (AUG)
+#pragma unroll
+                        for (int b = 0; b < T; ++b) B.t[a][b][r] = __builtin_fma(-li[a][r], lb[b], B.t[a][b][r]);
+                }
+        }
+    }
     return ok;
 }
 
-// Y = P_b (I + C_a P_b)^{-1}, Z = I - C_a Y, Zt = Z^T.  False if P_b or the
-// SPD core is not positive definite.
+// The pivot count stays a runtime bound: a compile-time count (straight-line
+// code, 170 KB for the scan kernel) measured 5x slower -- instruction fetch
+// from L2 once the kernel outgrows the 64 KB instruction cache.
+template <int T, bool AUG>
+__device__ __forceinline__ bool elim_regs(WM<T> &M, WM<T> &B, int n, double (&colinv)[T], double (&rowinv)[T][4],
+                                          int g, int c) {
+    return elim_regs_n<T, AUG, 0>(M, B, n, colinv, rowinv, g, c);
+}
+
+// M <- chol(M) (lower, zeros above, identity padding kept) on registers only
 template <int T>
-__device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
-                                          CombSmem<T> &sm, int lane) {
-    constexpr int P = 16 * T, PL = P + 1;
-    const int g = lane >> 4, c = lane & 15;
-    WM<T> R, S;
-    COMB_MARK(1);
-    wm_load(R, Pb, n, n, false, 1.0, g, c);
-    bool ok = wm_chol(R, n, sm, g, c);
-    COMB_MARK(2);
-    {
-        WM<T> T1;
-        wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
-        wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
-    }
-    COMB_MARK(3);
-    ok = wm_chol(S, n, sm, g, c) && ok;  // Q
-    COMB_MARK(4);
-    // U = Q^{-1} R^T by forward substitution, column j on lane j with the
-    // column in registers (loops unrolled over the padded size P).  Q is
-    // staged transposed (row i of Q contiguous: 128-bit broadcast reads),
-    // R as is (lane j reads its row j = column j of R^T).
-    constexpr int PQ = P + 2;  // even row stride keeps the 16-byte alignment
-    double *Qt = sm.A, *Rs = sm.B;
+__device__ __forceinline__ bool wm_chol_regs(WM<T> &M, int n, int g, int c) {
+    double colinv[T], rowinv[T][4];
+    const bool ok = elim_regs<T, false>(M, M, n, colinv, rowinv, g, c);
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll
         for (int b = 0; b < T; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
-                Qt[j + i * PQ] = S.t[a][b][r];  // Qt[k + i PQ] = Q[i][k]
-                Rs[i + j * PL] = R.t[a][b][r];
+                const int i = 16 * a + 4 * r + g, jc = 16 * b + c;
+                if (jc < n) M.t[a][b][r] = (i >= jc) ? M.t[a][b][r] * colinv[b] : 0.0;
             }
-    wave_sync();
-    double u[P];
-    const int j = lane < P ? lane : P - 1;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        if (i < n) {
-            double v0 = (i <= j) ? Rs[j + i * PL] : 0.0, v1 = 0.0;
-            const double2 *qrow = reinterpret_cast<const double2 *>(Qt + i * PQ);
-#pragma unroll
-            for (int k2 = 0; k2 < (i + 1) / 2; ++k2) {
-                const double2 q = qrow[k2];
-                v0 = __builtin_fma(-q.x, u[2 * k2], v0);
-                if (2 * k2 + 1 < i) v1 = __builtin_fma(-q.y, u[2 * k2 + 1], v1);
-            }
-            u[i] = (v0 + v1) * sm.sinv[i];  // sinv[i] = 1 / Q[i][i]
-        } else {
-            u[i] = (i == j) ? 1.0 : 0.0;  // identity padding
-        }
+    return ok;
+}
+
+// Y = P_b (I + C_a P_b)^{-1}, Z = I - C_a Y, Zt = Z^T.  False if P_b or the
+// SPD core is not positive definite.
+//     R = chol(P_b), S = I + R^T C_a R = Q Q^T, U = Q^{-1} R^T, Y = U^T U
+// U comes out of the elimination of S carrying R^T as extra columns (row i
+// scaled by 1/sqrt(d_i) at the end), so no triangular solve is needed.
+template <int T>
+__device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
+                                          CombSmem<T> &sm, int lane) {
+    constexpr int PL = 16 * T + 1;
+    const int g = lane >> 4, c = lane & 15;
+    WM<T> R, S, U;
+    COMB_MARK(1);
+    wm_load(R, Pb, n, n, false, 1.0, g, c);
+    bool ok = wm_chol_regs(R, n, g, c);
+    COMB_MARK(2);
+    {
+        WM<T> T1;
+        wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
+        wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
     }
-    wave_sync();  // all reads of Qt / Rs done
-    // U (column j on lane j) -> C/D layout through LDS
-    if (lane < P)
-#pragma unroll
-        for (int i = 0; i < P; ++i) Rs[i + lane * PL] = u[i];
+    // R^T through LDS (identity padding)
+    wm_store(R, sm.B, PL, n, g, c);
     wave_sync();
+    wm_load(U, sm.B, PL, n, true, 1.0, g, c);
+    COMB_MARK(3);
+    double colinv[T], rowinv[T][4];
+    ok = elim_regs<T, true>(S, U, n, colinv, rowinv, g, c) && ok;
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) U.t[a][b][r] *= rowinv[a][r];
+    COMB_MARK(4);
     COMB_MARK(5);
-    WM<T> U;
-    wm_load(U, Rs, PL, P, false, 1.0, g, c);
     wm_tn(Y, U, U, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Y = U^T U
     wm_tn(Z, Ca, Y, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z = I - C_a Y
     wm_tn(Zt, Y, Ca, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z^T = I - Y C_a
