@@ -163,12 +163,12 @@ __device__ __forceinline__ double bcast_group(double v, int gj) {
 
 // Right-looking elimination of the pivots 0..n-1 of the symmetric padded
 // matrix M (left unscaled: M's lower part ends as d_j L[:, j], L unit lower,
-// d_j the pivots), optionally carrying extra columns B through the same row
+// d_j the pivots), optionally carrying TB column tiles B through the same row
 // operations (B <- L^{-1} B).  colinv[b] = 1/sqrt(d) of column 16 b + c,
 // rowinv[a][r] = 1/sqrt(d) of row 16 a + 4 r + g (AUG only).  Upper-triangle
 // entries of M are left as garbage.  False if a pivot is not positive.
-template <int T, bool AUG, int NN>
-__device__ __forceinline__ bool elim_regs_n(WM<T> &M, WM<T> &B, int n_rt, double (&colinv)[T],
+template <int T, bool AUG, int NN, int TB>
+__device__ __forceinline__ bool elim_regs_n(WM<T> &M, d4 (&B)[T][TB], int n_rt, double (&colinv)[T],
                                             double (&rowinv)[T][4], int g, int c) {
     constexpr int P = 16 * T;
     const int n = NN > 0 ? NN : n_rt;
@@ -179,16 +179,28 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, WM<T> &B, int n_rt, double
     for (int a = 0; a < T; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) rowinv[a][r] = 1.0;
+    // one uniform branch per BLK pivots: the BLK bodies are straight-line
+    // code, so a pivot's broadcasts and reciprocal overlap the previous
+    // updates.  Pivots past n inside the last block act on the identity
+    // padding (d = 1, zero row and column): exact no-ops.  Measured
+    // (scripts/ubench/elim_bench.hip): 16 x 16 with [B | I] 431 -> 317
+    // cycles per pivot, 24 of 32 with B 476 -> 392.
+    constexpr int BLK = T == 1 ? 16 : 8;
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-        if (j < n) {
+    for (int jb = 0; jb < P; jb += BLK) {
+        if (jb >= n) break;
+#pragma unroll
+        for (int jj = 0; jj < BLK; ++jj) {
+            const int j = jb + jj;
             const int tj = j >> 4, cj = j & 15, gj = j & 3, rj = (j >> 2) & 3;
             const double djj = readlane_f64(M.t[tj][tj][rj], (gj << 4) + cj);
             ok = ok && (djj > 0.0);
-            const double inv = rsqrt_f64(djj), inv2 = inv * inv;
+            // 1/d on the critical path (v_rcp_f64 + one third-order step);
+            // 1/sqrt(d) only feeds the final scaling
+            const double inv2 = rcp_f64(djj), inv = rsqrt_f64(djj);
             colinv[tj] = (c == cj) ? inv : colinv[tj];
             if (AUG) rowinv[tj][rj] = (g == gj) ? inv : rowinv[tj][rj];
-            double lc[T], lb[T], li[T][4];
+            double lc[T], lb[TB], li[T][4];
 #pragma unroll
             for (int b = tj; b < T; ++b) {
                 const double v = bcast_group(M.t[tj][b][rj], gj);
@@ -196,7 +208,7 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, WM<T> &B, int n_rt, double
             }
             if (AUG)
 #pragma unroll
-                for (int b = 0; b < T; ++b) lb[b] = bcast_group(B.t[tj][b][rj], gj) * inv2;
+                for (int b = 0; b < TB; ++b) lb[b] = bcast_group(B[tj][b][rj], gj) * inv2;
 #pragma unroll
             for (int a = tj; a < T; ++a)
 #pragma unroll
@@ -213,27 +225,27 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, WM<T> &B, int n_rt, double
                     for (int b = tj; b < T; ++b) M.t[a][b][r] = __builtin_fma(-li[a][r], lc[b], M.t[a][b][r]);
                     if (AUG)
 #pragma unroll
-                        for (int b = 0; b < T; ++b) B.t[a][b][r] = __builtin_fma(-li[a][r], lb[b], B.t[a][b][r]);
+                        for (int b = 0; b < TB; ++b) B[a][b][r] = __builtin_fma(-li[a][r], lb[b], B[a][b][r]);
                 }
         }
     }
     return ok;
 }
 
-// The pivot count stays a runtime bound: a compile-time count (straight-line
-// code, 170 KB for the scan kernel) measured 5x slower -- instruction fetch
-// from L2 once the kernel outgrows the 64 KB instruction cache.
-template <int T, bool AUG>
-__device__ __forceinline__ bool elim_regs(WM<T> &M, WM<T> &B, int n, double (&colinv)[T], double (&rowinv)[T][4],
-                                          int g, int c) {
-    return elim_regs_n<T, AUG, 0>(M, B, n, colinv, rowinv, g, c);
+// The pivot count stays a runtime bound: compile-time counts for several n
+// (straight-line copies, 170 KB for the scan kernel) measured 5x slower --
+// instruction fetch from L2 once the kernel outgrows the instruction cache.
+template <int T, bool AUG, int TB = T>
+__device__ __forceinline__ bool elim_regs(WM<T> &M, d4 (&B)[T][TB], int n, double (&colinv)[T],
+                                          double (&rowinv)[T][4], int g, int c) {
+    return elim_regs_n<T, AUG, 0, TB>(M, B, n, colinv, rowinv, g, c);
 }
 
 // M <- chol(M) (lower, zeros above, identity padding kept) on registers only
 template <int T>
 __device__ __forceinline__ bool wm_chol_regs(WM<T> &M, int n, int g, int c) {
     double colinv[T], rowinv[T][4];
-    const bool ok = elim_regs<T, false>(M, M, n, colinv, rowinv, g, c);
+    const bool ok = elim_regs<T, false>(M, M.t, n, colinv, rowinv, g, c);
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll
@@ -272,7 +284,7 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     wm_load(U, sm.B, PL, n, true, 1.0, g, c);
     COMB_MARK(3);
     double colinv[T], rowinv[T][4];
-    ok = elim_regs<T, true>(S, U, n, colinv, rowinv, g, c) && ok;
+    ok = elim_regs<T, true>(S, U.t, n, colinv, rowinv, g, c) && ok;
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll

@@ -22,6 +22,7 @@
 //                block forward/back substitution on -S, z = L^{-T}(w - V lam - U lam+).
 // Stage-0 state constraints are ignored by the KKT (kkt.hpp:218-221): C_00 has
 // only the u columns of D_0 and x0 enters only through S0 x0 and A0 x0.
+#include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "solvers.hpp"
 
@@ -40,7 +41,7 @@ struct KKTArgs {
     const int32_t *d_off, *y_off, *ncs;
     const int32_t *prim_off, *prim_dim, *dual_off, *gdim;
     double *blk;    // [b][N+1][6][P*P]: L, V, U, VtV, UtU, UtV
-    double *fac;    // [b][N+1][2][P*P]: Lkk, L_{k+1,k}
+    double *fac;    // [b][N+1][3][P*P]: Lkk, L_{k+1,k} (P = 16: its transpose), Lkk^{-1} (P = 16)
     double *rhs;    // [b][dim]
     double *wv;     // [b][N+1][4][P]: w, t, t1, lam
     int32_t *status;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64) void k_kkt_factor(KKTArgs A, const double *__re
         wave_sync();
         const bool ok = kchol(M, P, g, lane);
         if (!ok && !fail) fail = k + 1;
-        double *fk = A.fac + (b * (N + 1) + k) * 2LL * PP;
+        double *fk = A.fac + (b * (N + 1) + k) * 3LL * PP;
         kcopy_out(fk, M, PP, lane);
         if (k < N) {
             const int g1 = A.gdim[k + 1];
@@ -253,6 +254,147 @@ __global__ __launch_bounds__(64) void k_kkt_factor(KKTArgs A, const double *__re
     }
     // status: first failing dual group + 1, or N + 2 when a primal block failed
     if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
+}
+
+// ---------------------------------------------------------------------------
+// P = 16 (every primal and dual block fits one 16 x 16 MFMA tile, e.g. 12/4
+// with nc <= 4): the same block Cholesky on registers.  X_k = L_{k,k-1}^T
+// stays in C/D-layout registers from group to group:
+//     M = D_k - X_k^T X_k                        (one MFMA product)
+//     eliminate M's g pivots carrying [B^T | I]  (elim_regs, no LDS)
+//     Lkk = the scaled factor, X_{k+1} = Lkk^{-1} (U^T V)_k^T, Lkk^{-1}
+// Stored per group: Lkk, X_{k+1} (= L_{k+1,k}^T) and Lkk^{-1}, so the two
+// substitutions of the solve are matrix-vector products only.
+// ---------------------------------------------------------------------------
+struct KGroupIn {  // raw loads of group k (combined at use, so the loads stay a prefetch)
+    double vtv[4], utu[4], yr[4], bt[4];
+};
+
+// Branch-free loads with clamped addresses: a divergent or consumed load makes
+// the compiler wait on vmcnt(0), which would drain the prefetch.
+__device__ __forceinline__ void kgroup_load(KGroupIn &in, const KKTArgs &A, const double *ir, long long b, int k,
+                                            int g, int c) {
+    const int N = A.sh.N, n = A.sh.n, ny = A.sh.ny;
+    const double *bk = A.blk + (b * (N + 1) + k) * 6LL * 256;
+    const double *bp = bk - (k > 0 ? 6 * 256 : 0);
+    const int yo = k == 0 ? A.y_off[0] : A.y_off[k] - n;  // y index of dual row i: yo + i
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g, j = c;
+        in.vtv[r] = bk[3 * 256 + i + 16 * j];
+        in.utu[r] = bp[4 * 256 + i + 16 * j];
+        in.yr[r] = ny > 0 ? ir[min(max(yo + i, 0), ny - 1)] : 0.0;  // uniform branch
+        in.bt[r] = bk[5 * 256 + j + 16 * i];
+    }
+}
+
+// D_k (+ regularisation, identity padding) and (U^T V)_k^T from the raw loads
+__device__ __forceinline__ void kgroup_form(d4 &D, d4 &Bt, const KGroupIn &in, const KKTArgs &A, int k, int g, int c) {
+    const int N = A.sh.N, n = A.sh.n, ny = A.sh.ny;
+    const int gk = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
+    const int nl = k == 0 ? 0 : n;  // rows i < nl are lambda rows
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g, j = c;
+        const bool in_g = i < gk && j < gk;
+        const double reg = (i < nl) ? A.rho_dyn : (ny > 0 ? in.yr[r] : 0.0);
+        const double dv = in.vtv[r] + (k > 0 ? in.utu[r] : 0.0) + (i == j ? reg : 0.0);
+        D[r] = in_g ? dv : (i == j ? 1.0 : 0.0);
+        Bt[r] = (i < gk && j < g1) ? in.bt[r] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ inv_rho) {
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const double *ir = inv_rho + b * sh.ny;
+    int fail = 0;
+    WM<1> X;
+    X.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+    int gp = 0;
+    KGroupIn nxt;
+    kgroup_load(nxt, A, ir, b, 0, g, c);
+    for (int k = 0; k <= N; ++k) {
+        const KGroupIn in = nxt;
+        if (k < N) kgroup_load(nxt, A, ir, b, k + 1, g, c);
+        const int gk = A.gdim[k];
+        WM<1> M, D;
+        d4 Bt;
+        kgroup_form(D.t[0][0], Bt, in, A, k, g, c);
+        if (k > 0) wm_tn<1>(M, X, X, gp, -1.0, 0.0, &D, g, c);  // D_k - L_{k,k-1} L_{k,k-1}^T
+        else M = D;
+        d4 B[1][2];
+        B[0][0] = Bt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) B[0][1][r] = (4 * r + g == c) ? 1.0 : 0.0;
+        double colinv[1], rowinv[1][4];
+        const bool ok = elim_regs<1, true, 2>(M, B, gk, colinv, rowinv, g, c);
+        if (!ok && !fail) fail = k + 1;
+        double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            const double l = (c < gk) ? ((i >= c) ? M.t[0][0][r] * colinv[0] : 0.0) : M.t[0][0][r];
+            gstore(fk + i + 16 * c, l);
+            const double x = B[0][0][r] * rowinv[0][r];
+            gstore(fk + 256 + i + 16 * c, x);
+            gstore(fk + 512 + i + 16 * c, B[0][1][r] * rowinv[0][r]);
+            X.t[0][0][r] = x;
+        }
+        gp = gk;
+    }
+    if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
+}
+
+// forward phase 2, P = 16: L y = -(r_d - t - t1), then L^T lam = y, with the
+// stored Lkk^{-1} and X_{k+1} = L_{k+1,k}^T (single-column MFMA products)
+__global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A) {
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const double *rd = A.rhs + b * A.dim;
+    double *wvb = A.wv + b * (N + 1) * 4LL * 16;
+    const double *fb = A.fac + b * (N + 1) * 3LL * 256;
+    WV<1> y;
+    y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    int gp = 0;
+    for (int k = 0; k <= N; ++k) {
+        const int gk = A.gdim[k];
+        WM<1> Xk, LinvT;
+        if (k > 0) wm_load<1>(Xk, fb + (long long)(k - 1) * 3 * 256 + 256, 16, 16, false, 0.0, g, c);
+        wm_load<1>(LinvT, fb + (long long)k * 3 * 256 + 512, 16, 16, true, 0.0, g, c);
+        WV<1> v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            double bi = 0.0;
+            if (c == 0 && i < gk) {
+                const double t1 = k > 0 ? wvb[(long long)(k - 1) * 64 + 32 + i] : 0.0;
+                bi = -(rd[A.dual_off[k] + i] - wvb[(long long)k * 64 + 16 + i] - t1);
+            }
+            v.t[0][r] = bi;
+        }
+        if (k > 0) wv_tn<1>(v, Xk, y, gp, -1.0, &v);  // - L_{k,k-1} y_{k-1}
+        wv_tn<1>(y, LinvT, v, gk, 1.0, (const WV<1> *)nullptr);
+        wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+        gp = gk;
+    }
+    WV<1> lam;
+    lam.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    int g1 = 0;
+    for (int k = N; k >= 0; --k) {
+        const int gk = A.gdim[k];
+        WM<1> XnT, Linv;
+        if (k < N) wm_load<1>(XnT, fb + (long long)k * 3 * 256 + 256, 16, 16, true, 0.0, g, c);
+        wm_load<1>(Linv, fb + (long long)k * 3 * 256 + 512, 16, 16, false, 0.0, g, c);
+        WV<1> v;
+        wv_load<1>(v, wvb + (long long)k * 64 + 48, gk, g, c);
+        if (k < N) wv_tn<1>(v, XnT, lam, g1, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
+        wv_tn<1>(lam, Linv, v, gk, 1.0, (const WV<1> *)nullptr);
+        wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
+        g1 = gk;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -342,14 +484,14 @@ __global__ __launch_bounds__(64) void k_kkt_solve2(KKTArgs A) {
     const long long b = blockIdx.x;
     const double *rd = A.rhs + b * A.dim;
     double *wvb = A.wv + b * (N + 1) * 4LL * P;
-    const double *fb = A.fac + b * (N + 1) * 2LL * PP;
+    const double *fb = A.fac + b * (N + 1) * 3LL * PP;
     for (int q = lane; q < P; q += 64) yp[q] = 0.0;
     wave_sync();
     for (int k = 0; k <= N; ++k) {  // L y = b
         const int g = A.gdim[k];
         for (int q = lane; q < PP; q += 64) {
-            Lk[q] = fb[(long long)k * 2 * PP + q];
-            Lo[q] = k > 0 ? fb[(long long)(k - 1) * 2 * PP + PP + q] : 0.0;  // L_{k,k-1}
+            Lk[q] = fb[(long long)k * 3 * PP + q];
+            Lo[q] = k > 0 ? fb[(long long)(k - 1) * 3 * PP + PP + q] : 0.0;  // L_{k,k-1}
         }
         wave_sync();
         for (int i = lane; i < P; i += 64) {
@@ -375,8 +517,8 @@ __global__ __launch_bounds__(64) void k_kkt_solve2(KKTArgs A) {
     for (int k = N; k >= 0; --k) {  // L^T lam = y
         const int g = A.gdim[k];
         for (int q = lane; q < PP; q += 64) {
-            Lk[q] = fb[(long long)k * 2 * PP + q];
-            Lo[q] = k < N ? fb[(long long)k * 2 * PP + PP + q] : 0.0;  // L_{k+1,k}
+            Lk[q] = fb[(long long)k * 3 * PP + q];
+            Lo[q] = k < N ? fb[(long long)k * 3 * PP + PP + q] : 0.0;  // L_{k+1,k}
         }
         wave_sync();
         for (int i = lane; i < P; i += 64) {
@@ -537,7 +679,7 @@ int kkt_init(pdplqr_handle h) {
     if ((rc = kalloc(h, &ks->d_prim_off, N + 1)) || (rc = kalloc(h, &ks->d_prim_dim, N + 1)) ||
         (rc = kalloc(h, &ks->d_dual_off, N + 1)) || (rc = kalloc(h, &ks->d_gdim, N + 1)) ||
         (rc = kalloc(h, &ks->d_ncs, N + 1)) || (rc = kalloc(h, &ks->rows, ks->dim)) || (rc = kalloc(h, &ks->pstat, B)) ||
-        (rc = kalloc(h, &ks->blk, B * (N + 1) * 6 * PP)) || (rc = kalloc(h, &ks->fac, B * (N + 1) * 2 * PP)) ||
+        (rc = kalloc(h, &ks->blk, B * (N + 1) * 6 * PP)) || (rc = kalloc(h, &ks->fac, B * (N + 1) * 3 * PP)) ||
         (rc = kalloc(h, &ks->rhs, B * ks->dim)) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
         return rc;
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_off, ks->prim_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -587,7 +729,8 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
     const Shape &sh = h->sh;
     KKTArgs a = kkt_args(h);
     const size_t smem = 3 * (size_t)ks->P * ks->P * sizeof(double);
-    hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
+    if (ks->P == 16) hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, inv_rho);
+    else hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -600,7 +743,8 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
     hipLaunchKernelGGL(k_kkt_x0, probs, wave, 0, h->stream, a, x0);
     hipLaunchKernelGGL(k_kkt_solve1, stages, wave, (PP + P) * sizeof(double), h->stream, a);
-    hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
+    if (P == 16) hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a);
+    else hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
     hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
