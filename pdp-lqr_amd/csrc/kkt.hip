@@ -262,138 +262,222 @@ __global__ __launch_bounds__(64) void k_kkt_factor(KKTArgs A, const double *__re
 // stays in C/D-layout registers from group to group:
 //     M = D_k - X_k^T X_k                        (one MFMA product)
 //     eliminate M's g pivots carrying [B^T | I]  (elim_regs, no LDS)
-//     Lkk = the scaled factor, X_{k+1} = Lkk^{-1} (U^T V)_k^T, Lkk^{-1}
-// Stored per group: Lkk, X_{k+1} (= L_{k+1,k}^T) and Lkk^{-1}, so the two
-// substitutions of the solve are matrix-vector products only.
+//     X_{k+1} = Lkk^{-1} (U^T V)_k^T, Lkk^{-1}
+// Tiles in HBM use the tile-native order tn(i, j): lane (i & 3) 16 + j holds
+// rows i = 4 r + (i & 3), r = i >> 2, as 4 contiguous doubles -- one 32-byte
+// load per lane, 2 KB per tile, fully coalesced.
 // ---------------------------------------------------------------------------
-struct KGroupIn {  // raw loads of group k (combined at use, so the loads stay a prefetch)
-    double vtv[4], utu[4], yr[4], bt[4];
-};
-
-// Branch-free loads with clamped addresses: a divergent or consumed load makes
-// the compiler wait on vmcnt(0), which would drain the prefetch.
-__device__ __forceinline__ void kgroup_load(KGroupIn &in, const KKTArgs &A, const double *ir, long long b, int k,
-                                            int g, int c) {
-    const int N = A.sh.N, n = A.sh.n, ny = A.sh.ny;
-    const double *bk = A.blk + (b * (N + 1) + k) * 6LL * 256;
-    const double *bp = bk - (k > 0 ? 6 * 256 : 0);
-    const int yo = k == 0 ? A.y_off[0] : A.y_off[k] - n;  // y index of dual row i: yo + i
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = 4 * r + g, j = c;
-        in.vtv[r] = bk[3 * 256 + i + 16 * j];
-        in.utu[r] = bp[4 * 256 + i + 16 * j];
-        in.yr[r] = ny > 0 ? ir[min(max(yo + i, 0), ny - 1)] : 0.0;  // uniform branch
-        in.bt[r] = bk[5 * 256 + j + 16 * i];
-    }
+__device__ __forceinline__ d4 tn_load(const double *tile, int lane) {
+    return *reinterpret_cast<const d4 *>(tile + 4 * lane);
 }
 
-// D_k (+ regularisation, identity padding) and (U^T V)_k^T from the raw loads
-__device__ __forceinline__ void kgroup_form(d4 &D, d4 &Bt, const KGroupIn &in, const KKTArgs &A, int k, int g, int c) {
-    const int N = A.sh.N, n = A.sh.n, ny = A.sh.ny;
+__device__ __forceinline__ void tn_store(double *tile, int lane, const d4 &v) {
+    *(__attribute__((address_space(1))) d4 *)(tile + 4 * lane) = v;
+}
+
+// C/D-layout transpose of a 16 x 16 tile through LDS (t: 16 x 17 doubles)
+__device__ __forceinline__ d4 tile_transpose(const d4 &v, double *t, int g, int c) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t[(4 * r + g) + 17 * c] = v[r];
+    wave_sync();
+    d4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = t[c + 17 * (4 * r + g)];
+    wave_sync();
+    return o;
+}
+
+// once per model, after k_kkt_stage: D_k = (V^T V)_k + (U^T U)_{k-1} + rho_dyn
+// on the lambda diagonal (identity padding) and (U^T V)_k^T of every group in
+// tile-native order: dpk [b][N+1][2][256]
+__global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict__ dpk) {
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
     const int gk = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
-    const int nl = k == 0 ? 0 : n;  // rows i < nl are lambda rows
+    const double *bk = A.blk + (b * (N + 1) + k) * 6LL * 256;
+    const double *bp = bk - 6 * 256;
+    d4 D, Bt;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int i = 4 * r + g, j = c;
-        const bool in_g = i < gk && j < gk;
-        const double reg = (i < nl) ? A.rho_dyn : (ny > 0 ? in.yr[r] : 0.0);
-        const double dv = in.vtv[r] + (k > 0 ? in.utu[r] : 0.0) + (i == j ? reg : 0.0);
-        D[r] = in_g ? dv : (i == j ? 1.0 : 0.0);
-        Bt[r] = (i < gk && j < g1) ? in.bt[r] : 0.0;
+        const int i = 4 * r + g;
+        double v = (i == c) ? 1.0 : 0.0;
+        if (i < gk && c < gk) {
+            v = bk[3 * 256 + i + 16 * c] + (k > 0 ? bp[4 * 256 + i + 16 * c] : 0.0);
+            if (i == c && k > 0 && i < sh.n) v += A.rho_dyn;  // lambda rows: -rho_dyn I (frozen)
+        }
+        D[r] = v;
+        Bt[r] = (i < gk && c < g1) ? bk[5 * 256 + c + 16 * i] : 0.0;
+    }
+    double *o = dpk + (b * (N + 1) + k) * 512LL;
+    tn_store(o, lane, D);
+    tn_store(o + 256, lane, Bt);
+}
+
+// per backward: the y diagonal 1/rho of every group, dreg [b][N+1][16] (zero
+// on lambda rows and padding), so the serial factor reads no index arrays
+__global__ void k_kkt_dreg16(KKTArgs A, const double *__restrict__ inv_rho, double *__restrict__ dreg) {
+    const Shape &sh = A.sh;
+    const long long total = (long long)sh.batch * (sh.N + 1) * 16;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(t & 15);
+        const long long bk = t >> 4;
+        const int k = (int)(bk % (sh.N + 1));
+        const long long b = bk / (sh.N + 1);
+        const int nl = k == 0 ? 0 : sh.n, gk = A.gdim[k];
+        double v = 0.0;
+        if (i >= nl && i < gk) v = inv_rho[b * sh.ny + A.y_off[k] + i - nl];
+        dreg[t] = v;
     }
 }
 
-__global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ inv_rho) {
+// per forward, after solve1: the dual right-hand side of the forward
+// substitution, bvec [b][N+1][16] = -(r_d - t_k - t1_{k-1}) (zero padding)
+__global__ void k_kkt_bvec16(KKTArgs A, double *__restrict__ bvec) {
+    const Shape &sh = A.sh;
+    const long long total = (long long)sh.batch * (sh.N + 1) * 16;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(t & 15);
+        const long long bk = t >> 4;
+        const int k = (int)(bk % (sh.N + 1));
+        const long long b = bk / (sh.N + 1);
+        double v = 0.0;
+        if (i < A.gdim[k]) {
+            const double *w = A.wv + bk * 64;
+            const double t1 = k > 0 ? w[-64 + 32 + i] : 0.0;
+            v = -(A.rhs[b * A.dim + A.dual_off[k] + i] - w[16 + i] - t1);
+        }
+        bvec[t] = v;
+    }
+}
+
+// Every group is eliminated over all 16 pivots: the padding is the identity
+// (exact no-op pivots) and X's padding is zero, so the loop reads no group
+// dimensions -- only two tiles and the y diagonal, loaded two groups ahead.
+__global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ dpk,
+                                                     const double *__restrict__ dreg) {
     const Shape &sh = A.sh;
     const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
-    const double *ir = inv_rho + b * sh.ny;
+    const double *tiles = dpk + b * (N + 1) * 512LL;
+    const double *dg = dreg + b * (N + 1) * 16LL;
     int fail = 0;
     WM<1> X;
     X.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-    int gp = 0;
-    KGroupIn nxt;
-    kgroup_load(nxt, A, ir, b, 0, g, c);
+    d4 D1 = tn_load(tiles, lane), B1 = tn_load(tiles + 256, lane);
+    d4 D2 = tn_load(tiles + (N > 0 ? 512 : 0), lane), B2 = tn_load(tiles + (N > 0 ? 768 : 256), lane);
+    double r1[4], r2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        r1[r] = dg[4 * r + g];
+        r2[r] = dg[(N > 0 ? 16 : 0) + 4 * r + g];
+    }
     for (int k = 0; k <= N; ++k) {
-        const KGroupIn in = nxt;
-        if (k < N) kgroup_load(nxt, A, ir, b, k + 1, g, c);
-        const int gk = A.gdim[k];
         WM<1> M, D;
-        d4 Bt;
-        kgroup_form(D.t[0][0], Bt, in, A, k, g, c);
-        if (k > 0) wm_tn<1>(M, X, X, gp, -1.0, 0.0, &D, g, c);  // D_k - L_{k,k-1} L_{k,k-1}^T
-        else M = D;
         d4 B[1][2];
-        B[0][0] = Bt;
+        D.t[0][0] = D1;
+        B[0][0] = B1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D.t[0][0][r] += (4 * r + g == c) ? r1[r] : 0.0;
+        D1 = D2;
+        B1 = B2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r1[r] = r2[r];
+        const int kn = min(k + 2, N);  // (re)loads the last group past the end: harmless
+        D2 = tn_load(tiles + kn * 512LL, lane);
+        B2 = tn_load(tiles + kn * 512LL + 256, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r2[r] = dg[kn * 16 + 4 * r + g];
+        if (k > 0) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - L_{k,k-1} L_{k,k-1}^T
+        else M = D;
 #pragma unroll
         for (int r = 0; r < 4; ++r) B[0][1][r] = (4 * r + g == c) ? 1.0 : 0.0;
         double colinv[1], rowinv[1][4];
-        const bool ok = elim_regs<1, true, 2>(M, B, gk, colinv, rowinv, g, c);
+        const bool ok = elim_regs<1, true, 2>(M, B, 16, colinv, rowinv, g, c);
         if (!ok && !fail) fail = k + 1;
-        double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
+        d4 Linv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int i = 4 * r + g;
-            const double l = (c < gk) ? ((i >= c) ? M.t[0][0][r] * colinv[0] : 0.0) : M.t[0][0][r];
-            gstore(fk + i + 16 * c, l);
-            const double x = B[0][0][r] * rowinv[0][r];
-            gstore(fk + 256 + i + 16 * c, x);
-            gstore(fk + 512 + i + 16 * c, B[0][1][r] * rowinv[0][r]);
-            X.t[0][0][r] = x;
+            X.t[0][0][r] = B[0][0][r] * rowinv[0][r];
+            Linv[r] = B[0][1][r] * rowinv[0][r];
         }
-        gp = gk;
+        double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
+        tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1} = L_{k+1,k}^T
+        tn_store(fk + 512, lane, Linv);       // Lkk^{-1}
     }
     if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
 }
 
-// forward phase 2, P = 16: L y = -(r_d - t - t1), then L^T lam = y, with the
-// stored Lkk^{-1} and X_{k+1} = L_{k+1,k}^T (single-column MFMA products)
-__global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A) {
+// forward phase 2, P = 16: L y = bvec, then L^T lam = y, with the stored
+// Lkk^{-1} and X_{k+1} = L_{k+1,k}^T (single-column MFMA products over the
+// full padded tile; inputs loaded two steps ahead)
+__global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *__restrict__ bvec) {
+    __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
-    const double *rd = A.rhs + b * A.dim;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
     const double *fb = A.fac + b * (N + 1) * 3LL * 256;
+    const double *bv = bvec + b * (N + 1) * 16LL;
+    struct In {
+        d4 X, L;
+        double v[4];
+    };
+    // forward: X_k natural (stored by group k-1), Lkk^{-1} (transposed at use)
+    auto fload = [&](In &in, int k) {
+        in.X = tn_load(fb + (long long)max(k - 1, 0) * 768 + 256, lane);
+        in.L = tn_load(fb + (long long)k * 768 + 512, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) in.v[r] = bv[k * 16 + 4 * r + g];
+    };
     WV<1> y;
     y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
-    int gp = 0;
+    In nx1, nx2;
+    fload(nx1, 0);
+    fload(nx2, min(1, N));
     for (int k = 0; k <= N; ++k) {
-        const int gk = A.gdim[k];
+        const In in = nx1;
+        nx1 = nx2;
+        fload(nx2, min(k + 2, N));
         WM<1> Xk, LinvT;
-        if (k > 0) wm_load<1>(Xk, fb + (long long)(k - 1) * 3 * 256 + 256, 16, 16, false, 0.0, g, c);
-        wm_load<1>(LinvT, fb + (long long)k * 3 * 256 + 512, 16, 16, true, 0.0, g, c);
+        Xk.t[0][0] = in.X;
+        LinvT.t[0][0] = tile_transpose(in.L, tt, g, c);
         WV<1> v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 4 * r + g;
-            double bi = 0.0;
-            if (c == 0 && i < gk) {
-                const double t1 = k > 0 ? wvb[(long long)(k - 1) * 64 + 32 + i] : 0.0;
-                bi = -(rd[A.dual_off[k] + i] - wvb[(long long)k * 64 + 16 + i] - t1);
-            }
-            v.t[0][r] = bi;
-        }
-        if (k > 0) wv_tn<1>(v, Xk, y, gp, -1.0, &v);  // - L_{k,k-1} y_{k-1}
-        wv_tn<1>(y, LinvT, v, gk, 1.0, (const WV<1> *)nullptr);
+        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
+        if (k > 0) wv_tn<1>(v, Xk, y, 16, -1.0, &v);  // - L_{k,k-1} y_{k-1}
+        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
         wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
-        gp = gk;
     }
+    // backward: X_{k+1} transposed, Lkk^{-1} natural; y_k was written by this
+    // wave above (same lanes: wv_store / the loads below touch lanes c == 0 only)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    auto bload = [&](In &in, int k) {
+        in.X = tn_load(fb + (long long)min(k, N - 1) * 768 + 256, lane);
+        in.L = tn_load(fb + (long long)k * 768 + 512, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) in.v[r] = wvb[(long long)k * 64 + 48 + 4 * r + g];
+    };
     WV<1> lam;
     lam.t[0] = d4{0.0, 0.0, 0.0, 0.0};
-    int g1 = 0;
+    bload(nx1, N);
+    bload(nx2, max(N - 1, 0));
     for (int k = N; k >= 0; --k) {
-        const int gk = A.gdim[k];
+        const In in = nx1;
+        nx1 = nx2;
+        bload(nx2, max(k - 2, 0));
         WM<1> XnT, Linv;
-        if (k < N) wm_load<1>(XnT, fb + (long long)k * 3 * 256 + 256, 16, 16, true, 0.0, g, c);
-        wm_load<1>(Linv, fb + (long long)k * 3 * 256 + 512, 16, 16, false, 0.0, g, c);
+        XnT.t[0][0] = tile_transpose(in.X, tt, g, c);
+        Linv.t[0][0] = in.L;
         WV<1> v;
-        wv_load<1>(v, wvb + (long long)k * 64 + 48, gk, g, c);
-        if (k < N) wv_tn<1>(v, XnT, lam, g1, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
-        wv_tn<1>(lam, Linv, v, gk, 1.0, (const WV<1> *)nullptr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
+        if (k < N) wv_tn<1>(v, XnT, lam, 16, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
+        wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
         wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
-        g1 = gk;
     }
 }
 
@@ -587,6 +671,9 @@ struct KKTState {
     int4 *rows = nullptr;
     int32_t *pstat = nullptr;
     double *blk = nullptr, *fac = nullptr, *rhs = nullptr, *wv = nullptr;
+    double *dpk = nullptr;   // P = 16: D_k and (U^T V)_k^T tiles, tile-native [b][N+1][2][256]
+    double *dreg = nullptr;  // P = 16: y diagonal per group [b][N+1][16]
+    double *bvec = nullptr;  // P = 16: forward-substitution right-hand sides [b][N+1][16]
     bool formed = false;
 };
 
@@ -680,7 +767,9 @@ int kkt_init(pdplqr_handle h) {
         (rc = kalloc(h, &ks->d_dual_off, N + 1)) || (rc = kalloc(h, &ks->d_gdim, N + 1)) ||
         (rc = kalloc(h, &ks->d_ncs, N + 1)) || (rc = kalloc(h, &ks->rows, ks->dim)) || (rc = kalloc(h, &ks->pstat, B)) ||
         (rc = kalloc(h, &ks->blk, B * (N + 1) * 6 * PP)) || (rc = kalloc(h, &ks->fac, B * (N + 1) * 3 * PP)) ||
-        (rc = kalloc(h, &ks->rhs, B * ks->dim)) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
+        (rc = kalloc(h, &ks->rhs, B * ks->dim)) ||
+        (ks->P == 16 && ((rc = kalloc(h, &ks->dpk, B * (N + 1) * 512)) || (rc = kalloc(h, &ks->dreg, B * (N + 1) * 16)) ||
+                         (rc = kalloc(h, &ks->bvec, B * (N + 1) * 16)))) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
         return rc;
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_off, ks->prim_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_dim, ks->prim_dim.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -708,6 +797,10 @@ int kkt_on_model(pdplqr_handle h) {
     const size_t smem = 4 * (size_t)ks->P * ks->P * sizeof(double);
     hipLaunchKernelGGL(k_kkt_stage, dim3((unsigned)(sh.batch * (sh.N + 1))), dim3(64), smem, h->stream, a);
     PDPLQR_HIP_TRY(hipGetLastError());
+    if (ks->P == 16) {
+        hipLaunchKernelGGL(k_kkt_pack16, dim3((unsigned)(sh.batch * (sh.N + 1))), dim3(64), 0, h->stream, a, ks->dpk);
+        PDPLQR_HIP_TRY(hipGetLastError());
+    }
     ks->formed = true;
     return PDPLQR_OK;
 }
@@ -729,7 +822,12 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
     const Shape &sh = h->sh;
     KKTArgs a = kkt_args(h);
     const size_t smem = 3 * (size_t)ks->P * ks->P * sizeof(double);
-    if (ks->P == 16) hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, inv_rho);
+    if (ks->P == 16) {
+        const long long total = (long long)sh.batch * (sh.N + 1) * 16;
+        const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_kkt_dreg16, dim3(grid), dim3(256), 0, h->stream, a, inv_rho, ks->dreg);
+        hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, ks->dpk, ks->dreg);
+    }
     else hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -743,7 +841,12 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
     hipLaunchKernelGGL(k_kkt_x0, probs, wave, 0, h->stream, a, x0);
     hipLaunchKernelGGL(k_kkt_solve1, stages, wave, (PP + P) * sizeof(double), h->stream, a);
-    if (P == 16) hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a);
+    if (P == 16) {
+        const long long total = (long long)sh.batch * (sh.N + 1) * 16;
+        const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_kkt_bvec16, dim3(grid), dim3(256), 0, h->stream, a, ks->bvec);
+        hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a, (const double *)ks->bvec);
+    }
     else hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
     hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
     PDPLQR_HIP_TRY(hipGetLastError());
