@@ -44,6 +44,7 @@ struct KKTArgs {
     double *fac;    // [b][N+1][3][P*P]: Lkk, L_{k+1,k} (P = 16: its transpose), Lkk^{-1} (P = 16)
     double *rhs;    // [b][dim]
     double *wv;     // [b][N+1][4][P]: w, t, t1, lam
+    double *ppk;    // P = 16: primal tiles [b][N+1][6][256] (tile-native)
     int32_t *status;
     int32_t *pstat;  // per problem: a primal block H_k + sigma I was not positive definite
 };
@@ -313,6 +314,102 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     double *o = dpk + (b * (N + 1) + k) * 512LL;
     tn_store(o, lane, D);
     tn_store(o + 256, lane, Bt);
+    // primal tiles for the parallel solve phases, ppk [b][N+1][6][256]:
+    // L_k^{-T}, V_k, U_k (solve1) and V_k^T, U_k^T, L_k^{-1} (solve3).
+    // L^{-1} by re-eliminating L L^T carrying I (identity padding past p).
+    __shared__ double tt[16 * 17];
+    const int p = A.prim_dim[k];
+    WM<1> Lt, M;
+    wm_load<1>(Lt, bk, 16, p, true, 0.0, g, c);
+    wm_tn<1>(M, Lt, Lt, p, 1.0, 0.0, (const WM<1> *)nullptr, g, c);  // L L^T
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (4 * r + g == c && c >= p) M.t[0][0][r] = 1.0;
+    d4 Bi[1][1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Bi[0][0][r] = (4 * r + g == c) ? 1.0 : 0.0;
+    double colinv[1], rowinv[1][4];
+    elim_regs<1, true, 1>(M, Bi, 16, colinv, rowinv, g, c);
+    d4 Linv, V, U;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        Linv[r] = Bi[0][0][r] * rowinv[0][r];
+        V[r] = (i < p && c < gk) ? bk[256 + i + 16 * c] : 0.0;
+        U[r] = (i < p && c < g1) ? bk[512 + i + 16 * c] : 0.0;
+    }
+    double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
+    tn_store(q, lane, tile_transpose(Linv, tt, g, c));
+    tn_store(q + 256, lane, V);
+    tn_store(q + 512, lane, U);
+    tn_store(q + 768, lane, tile_transpose(V, tt, g, c));
+    tn_store(q + 1024, lane, tile_transpose(U, tt, g, c));
+    tn_store(q + 1280, lane, Linv);
+}
+
+// forward phase 1, P = 16 (parallel over stages): w = L^{-1} r_p, t = V^T w,
+// t1 = U^T w as single-column MFMA products on the packed primal tiles
+__global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int p = A.prim_dim[k];
+    const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
+    WM<1> LiT, V, U;
+    LiT.t[0][0] = tn_load(q, lane);
+    V.t[0][0] = tn_load(q + 256, lane);
+    U.t[0][0] = tn_load(q + 512, lane);
+    const double *rp = A.rhs + b * A.dim + A.prim_off[k];
+    WV<1> r, w, t, t1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = 4 * j + g;
+        r.t[0][j] = (c == 0 && i < p) ? rp[i] : 0.0;
+    }
+    wv_tn<1>(w, LiT, r, 16, 1.0, (const WV<1> *)nullptr);
+    wv_tn<1>(t, V, w, 16, 1.0, (const WV<1> *)nullptr);
+    wv_tn<1>(t1, U, w, 16, 1.0, (const WV<1> *)nullptr);
+    double *o = A.wv + (b * (N + 1) + k) * 64LL;
+    wv_store<1>(w, o, 16, g, c);
+    wv_store<1>(t, o + 16, 16, g, c);
+    wv_store<1>(t1, o + 32, 16, g, c);
+}
+
+// forward phase 3, P = 16 (parallel): z_k = L^{-T}(w - V lam_k - U lam_{k+1}), unpacked into ws
+__global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *__restrict__ x0,
+                                                      double *__restrict__ ws) {
+    __shared__ double zs[16];
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
+    WM<1> VT, UT, Li;
+    VT.t[0][0] = tn_load(q + 768, lane);
+    UT.t[0][0] = tn_load(q + 1024, lane);
+    Li.t[0][0] = tn_load(q + 1280, lane);
+    const double *wk = A.wv + (b * (N + 1) + k) * 64LL;
+    const double *wn = A.wv + (b * (N + 1) + min(k + 1, N)) * 64LL;  // U_N = 0
+    WV<1> w, lk, ln, v, z;
+    wv_load<1>(w, wk, 16, g, c);
+    wv_load<1>(lk, wk + 48, 16, g, c);
+    wv_load<1>(ln, wn + 48, 16, g, c);
+    wv_tn<1>(v, VT, lk, 16, -1.0, &w);
+    wv_tn<1>(v, UT, ln, 16, -1.0, &v);
+    wv_tn<1>(z, Li, v, 16, 1.0, (const WV<1> *)nullptr);
+    wv_store<1>(z, zs, 16, g, c);
+    wave_sync();
+    double *wb = ws + b * sh.perh;
+    if (k == 0) {  // ws[0] = [u0; x0] (qdldl_solver.hpp:133-134)
+        if (lane < m) wb[lane] = zs[lane];
+        else if (lane < s) wb[lane] = x0[b * n + lane - m];
+    } else if (k < N) {
+        if (lane < n) wb[(long long)k * s + m + lane] = zs[lane];
+        else if (lane < s) wb[(long long)k * s + lane - n] = zs[lane];
+    } else {
+        if (lane < n) wb[(long long)N * s + lane] = zs[lane];
+    }
 }
 
 // per backward: the y diagonal 1/rho of every group, dreg [b][N+1][16] (zero
@@ -674,6 +771,7 @@ struct KKTState {
     double *dpk = nullptr;   // P = 16: D_k and (U^T V)_k^T tiles, tile-native [b][N+1][2][256]
     double *dreg = nullptr;  // P = 16: y diagonal per group [b][N+1][16]
     double *bvec = nullptr;  // P = 16: forward-substitution right-hand sides [b][N+1][16]
+    double *ppk = nullptr;   // P = 16: primal tiles L^{-T}, V, U, V^T, U^T, L^{-1} [b][N+1][6][256]
     bool formed = false;
 };
 
@@ -715,6 +813,7 @@ static KKTArgs kkt_args(pdplqr_handle h) {
     a.fac = ks->fac;
     a.rhs = ks->rhs;
     a.wv = ks->wv;
+    a.ppk = ks->ppk;
     a.status = h->status;
     a.pstat = ks->pstat;
     return a;
@@ -769,7 +868,8 @@ int kkt_init(pdplqr_handle h) {
         (rc = kalloc(h, &ks->blk, B * (N + 1) * 6 * PP)) || (rc = kalloc(h, &ks->fac, B * (N + 1) * 3 * PP)) ||
         (rc = kalloc(h, &ks->rhs, B * ks->dim)) ||
         (ks->P == 16 && ((rc = kalloc(h, &ks->dpk, B * (N + 1) * 512)) || (rc = kalloc(h, &ks->dreg, B * (N + 1) * 16)) ||
-                         (rc = kalloc(h, &ks->bvec, B * (N + 1) * 16)))) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
+                         (rc = kalloc(h, &ks->bvec, B * (N + 1) * 16)) ||
+                         (rc = kalloc(h, &ks->ppk, B * (N + 1) * 1536)))) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
         return rc;
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_off, ks->prim_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_dim, ks->prim_dim.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -840,7 +940,8 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     const size_t P = ks->P, PP = P * P;
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
     hipLaunchKernelGGL(k_kkt_x0, probs, wave, 0, h->stream, a, x0);
-    hipLaunchKernelGGL(k_kkt_solve1, stages, wave, (PP + P) * sizeof(double), h->stream, a);
+    if (P == 16) hipLaunchKernelGGL(k_kkt_solve1_16, stages, wave, 0, h->stream, a);
+    else hipLaunchKernelGGL(k_kkt_solve1, stages, wave, (PP + P) * sizeof(double), h->stream, a);
     if (P == 16) {
         const long long total = (long long)sh.batch * (sh.N + 1) * 16;
         const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
@@ -848,7 +949,8 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
         hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a, (const double *)ks->bvec);
     }
     else hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
-    hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
+    if (P == 16) hipLaunchKernelGGL(k_kkt_solve3_16, stages, wave, 0, h->stream, a, x0, ws);
+    else hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
