@@ -194,8 +194,9 @@ template <int T>
 __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], double *cb, double *sinv, double *luq,
                                            int jbeg, int jend, int m, bool aug, int g, int c) {
     bool ok = true;
-    const bool lane0 = (g == 0) && (c == 0);
-    const double2 *rows = reinterpret_cast<const double2 *>(cb + g * 4 * T);
+    // cb holds one 16 T slot per row group: every group writes its own row
+    // (no exec-mask branch), readers take the pivot's group slot
+    double *myslot = cb + g * 16 * T;
     // pivot j = 16 tr + 4 rr + gj: (tr, rr) unrolled so register indices stay
     // compile-time, the row group gj is a runtime loop (keeps the scheduler
     // from hoisting work across all pivots, which would exhaust registers)
@@ -207,22 +208,22 @@ __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], d
             for (int gj = 0; gj < 4; ++gj) {
                 const int j = 16 * tr + 4 * rr + gj;
                 if (j < jbeg || j >= jend) continue;
-                if (g == gj) {
 #pragma unroll
-                    for (int b = 0; b < T; ++b) {
-                        const int jc = 16 * b + c;
-                        cb[colpos<T>(jc)] = (jc > j) ? M[tr][b][rr] : 0.0;
-                    }
+                for (int b = 0; b < T; ++b) {
+                    const int jc = 16 * b + c;
+                    myslot[colpos<T>(jc)] = (jc > j) ? M[tr][b][rr] : 0.0;
                 }
                 wave_sync();
+                const double *slot = cb + gj * 16 * T;
+                const double2 *rows = reinterpret_cast<const double2 *>(slot + g * 4 * T);
                 const double djj = readlane_f64(M[tr][tr][rr], (gj << 4) + (j & 15));
                 ok = ok && (djj > 0.0);
                 const double inv = rsqrt_f64(djj);
                 const double inv2 = inv * inv;
-                if (lane0) sinv[j] = inv;
+                sinv[j] = inv;  // all lanes, same value: no branch
                 double lc[T];
 #pragma unroll
-                for (int b = 0; b < T; ++b) lc[b] = cb[colpos<T>(16 * b + c)] * inv2;
+                for (int b = 0; b < T; ++b) lc[b] = slot[colpos<T>(16 * b + c)] * inv2;
                 const bool augj = aug && j < m;
                 const double lpj = augj ? readlane_f64(lpr[tr][rr], gj << 4) : 0.0;
                 const double qj = lpj * inv2;
@@ -242,7 +243,7 @@ __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], d
                         // q = lp_j / M[j][j]; lpr_i -= raw_i * q  (raw_i = 0 for i <= j)
                         if (augj) lpr[a][r] = __builtin_fma(-li[a][r], qj, lpr[a][r]);
                     }
-                if (augj && lane0) luq[j] = lpj * inv;
+                if (augj) luq[j] = lpj * inv;  // uniform condition, all lanes
                 wave_sync();
             }
         }
@@ -274,7 +275,7 @@ struct BwdSmem {
     static constexpr int P = 16 * T;
     static constexpr int LD = P + 1;  // odd leading dimension: conflict-free column reads
     double L[P * LD];                 // L_{k+1} then L_k (padded, column-major, lower, zero upper)
-    alignas(16) double col[P];        // Cholesky pivot-row broadcast (colpos order)
+    alignas(16) double col[4 * P];    // Cholesky pivot-row broadcast, one slot per row group (colpos order)
     double inv[P];                    // 1 / sqrt(pivot) per column
     double pbt[P];                    // Pb_tmp = Lxx_next^T c
     double pv[P];                     // p_{k+1}, then p_k

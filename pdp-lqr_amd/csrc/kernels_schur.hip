@@ -20,6 +20,7 @@
 //
 // The factor cache (keep_factors = 1, needed by backward_without_factorization
 // and get_value_function) still takes the full-factor kernels.
+#include "combine_tiles.hpp"
 #include "device_common.hpp"
 
 #include <stdint.h>
@@ -56,7 +57,7 @@ __device__ __forceinline__ void schur_load(SchurIn &in, const double *__restrict
 }
 
 struct SchurSmem {
-    alignas(16) double col[16];  // pivot-row broadcast (colpos order)
+    alignas(16) double col[64];  // pivot-row broadcast, one slot per row group (colpos order)
     alignas(16) double lpt[16];  // lp_k, column -> row redistribution (colpos order)
     double inv[16];              // 1 / sqrt(pivot), u columns
     double luq[16];              // lu' = Luu^{-1} lu
@@ -66,11 +67,88 @@ struct SchurSmem {
     };
 };
 
+// Compile-time m <= 4: the m u-pivots as ONE block step.  Every u row sits in
+// register 0 (row j = row group j), so
+//   * Muu (m x m) and lu come to every lane by v_readlane; Luu = chol(Muu),
+//     T = Luu^{-1} and lu' = T lu are computed wave-uniformly (no broadcast
+//     chain per pivot);
+//   * lane (g, c) forms W[c][g] = sum_l M[c][l] T[g][l] = L(c, g) -- the u
+//     columns of the factor (Lxu below, Luu on the u rows) -- from column c of
+//     the u rows (register 0 of groups l, gathered by permlane swaps);
+//   * that one value per lane is both MFMA operands of P_k = Mxx - W W^T and
+//     the A operand of lp_x -= W lu' (one 16x16x4 MFMA each).
+// The u block of the tile is left as Muu - Luu Luu^T (~0); only the x block
+// and the x rows of lp are read by the next stage.
+template <int MM>
+__device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], double &w, double (&luq)[4], int g,
+                                                   int c) {
+    static_assert(MM >= 1 && MM <= 4, "u block");
+    double a[4][4], lu[4], L[4][4], T[4][4], inv[4];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {
+        lu[i] = readlane_f64(lpr[0], 16 * i);
+#pragma unroll
+        for (int j = 0; j <= i; ++j) a[i][j] = readlane_f64(M[0], 16 * i + j);  // M[i][j]: group i, lane j
+    }
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {  // right-looking Cholesky of Muu (uniform values)
+        ok = ok && (a[j][j] > 0.0);
+        inv[j] = rsqrt_f64(a[j][j]);
+        L[j][j] = a[j][j] * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < MM; ++i) L[i][j] = a[i][j] * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < MM; ++i)
+#pragma unroll
+            for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-L[i][j], L[k][j], a[i][k]);
+    }
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {  // T = Luu^{-1} (lower), row by row
+        T[i][i] = inv[i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int k = j; k < i; ++k) v = __builtin_fma(L[i][k], T[k][j], v);
+            T[i][j] = -v * inv[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {  // lu' = T lu
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j <= i; ++j) v = __builtin_fma(T[i][j], lu[j], v);
+        luq[i] = v;
+    }
+    // column c of the u rows: m_l = M[l][c] (group l, register 0)
+    double ml[4];
+#pragma unroll
+    for (int l = 0; l < MM; ++l) ml[l] = bcast_group(M[0], l);
+    w = 0.0;
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        double v = 0.0;
+#pragma unroll
+        for (int l = 0; l <= j; ++l) v = __builtin_fma(T[j][l], ml[l], v);
+        w = (g == j) ? v : w;  // W[c][g]; groups g >= m keep 0
+    }
+    M = mfma_f64(-w, w, M);  // M - W W^T
+    // lp -= W lu': one MFMA with lu' as column 0 of the B operand, then the
+    // column-0 result to every lane of its row (DPP row_newbcast:0)
+    const double lb = (c == 0 && g < MM) ? luq[g < MM ? g : 0] : 0.0;
+    const d4 y = mfma_f64(w, lb, d4{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lpr[r] -= bcast_lane16(y[r], 0);
+    return ok;
+}
+
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
 // after the m u-pivots (trailing block P_k, u columns unscaled L).  prow:
 // p~ in row layout (prow[r] = p[4 r + g - m] on x rows).
+template <int MM>
 __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const SchurIn &in, SchurSmem &sm, int m,
-                                            int s, int g, int c) {
+                                            int s, int g, int c, double &w, double (&luq)[4]) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks that hold x rows
     d4 G = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -88,7 +166,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
             part = __builtin_fma(in.E[kk], prow[kk], part);
         }
     part = sum_groups(part);
-    if (g == 0) sm.lpt[colpos<1>(c)] = in.h + part;
+    sm.lpt[colpos<1>(c)] = in.h + part;  // every group holds the same sum: no branch
     wave_sync();
     double lpr[1][4];
     {
@@ -99,10 +177,16 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
         lpr[0][2] = b.x;
         lpr[0][3] = b.y;
     }
-    d4 Mt[1][1];
-    Mt[0][0] = Mn;
-    bool ok = chol_tiles<1>(Mt, lpr, sm.col, sm.inv, sm.luq, 0, m, m, true, g, c);
-    Pm = Mt[0][0];
+    bool ok;
+    if constexpr (MM > 0) {
+        ok = schur_block_pivots<MM>(Mn, lpr[0], w, luq, g, c);
+        Pm = Mn;
+    } else {
+        d4 Mt[1][1];
+        Mt[0][0] = Mn;
+        ok = chol_tiles<1>(Mt, lpr, sm.col, sm.inv, sm.luq, 0, m, m, true, g, c);
+        Pm = Mt[0][0];
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) prow[r] = lpr[0][r];
     // P_k <- (P_k + P_k^T) / 2.  The square-root recursion is symmetric by
@@ -142,19 +226,13 @@ __device__ __forceinline__ void schur_store_record(double *FRk, const d4 &Pm, co
 // Same record, staged in LDS and written with one dwordx4 store instruction
 // (lanes < FS/2): coalesced, and a fixed vm-op count for the DMA accounting.
 template <int M, int S>
-__device__ __forceinline__ void schur_store_record_staged(double *FRk, const d4 &Pm, SchurSmem &sm, int g, int c) {
+__device__ __forceinline__ void schur_store_record_staged(double *FRk, double w, const double (&luq)[4], SchurSmem &sm,
+                                                          int g, int c) {
     constexpr int FS = S * M + M;
     static_assert(FS % 2 == 0 && FS <= 128, "record staging");
     const int lane = 16 * g + c;
-    if (c < M) {
-        const double iv = sm.inv[c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 4 * r + g;
-            if (i < S) sm.rec[c * S + i] = (i >= c) ? Pm[r] * iv : 0.0;
-        }
-    }
-    if (lane < M) sm.rec[S * M + lane] = sm.luq[lane];
+    if (g < M) sm.rec[g * S + c] = (c >= g) ? w : 0.0;  // L(c, g), column g of the record
+    if (lane < M) sm.rec[S * M + lane] = luq[lane < M ? lane : 0];
     wave_sync();
     if (lane < FS / 2) gstore2(FRk + 2 * lane, reinterpret_cast<const d2v *>(sm.rec)[lane]);
 }
@@ -197,20 +275,6 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     const int frs = s * m + m;
     int fail_stage = -1;
 
-    auto dma = [&](int k, int slot) {
-#pragma unroll
-        for (int q = 0; q < NI; ++q) {
-            int ch = q * 64 + lane;
-            ch = ch < SH::CH ? ch : SH::CH - 1;  // surplus lanes re-load the last chunk
-            const int d = 2 * ch;
-            const double *src = d < SH::OC   ? Eb + (long long)k * SH::n * SH::s + d
-                                : d < SH::OH ? cb + (long long)k * SH::n + (d - SH::OC)
-                                : d < SH::OP ? hb + (long long)k * SH::s + (d - SH::OH)
-                                             : Hb + (long long)k * SH::ps + (d - SH::OP);
-            dma16(src, &stg[slot][q * 128]);
-        }
-    };
-
     // ---- terminal (lqr_kernel.hpp:80-91): P_N = H~_N, p_N = h~_N ----
     d4 Pm;
     double prow[4];
@@ -230,27 +294,81 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     }
 
     if constexpr (CT) {
-        // vm ops per iteration: NI DMA (stage k-1) + 1 record store, so after
-        // issuing DMA(k-1) "DMA(k) has landed" is vmcnt(NI + 1); the first
-        // iteration has no store behind DMA(N-1) yet.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // terminal loads
-        dma(N - 1, (N - 1) & 1);
-        for (int k = N - 1; k >= 0; --k) {
-            if (k > 0) {
-                dma(k - 1, (k - 1) & 1);
-                if (k == N - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 1) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // Stage records go HBM -> registers -> LDS: register sets RA / RB hold
+        // the records of the next two stages in flight (2 x NI x 16 B per lane),
+        // so each load has two stage steps to land; stage k - 1 is written to
+        // its LDS slot right after stage k is processed.  (The former one-ahead
+        // LDS-DMA ring had one step, ~3.5 us, which left the HBM latency
+        // exposed at 4 waves per SIMD.)
+        d2v RA[NI], RB[NI];
+        auto gload = [&](d2v(&R)[NI], int k) {
+#pragma unroll
+            for (int q = 0; q < NI; ++q) {
+                int ch = q * 64 + lane;
+                ch = ch < SH::CH ? ch : SH::CH - 1;
+                const int d = 2 * ch;
+                const double *src = d < SH::OC   ? Eb + (long long)k * SH::n * SH::s + d
+                                    : d < SH::OH ? cb + (long long)k * SH::n + (d - SH::OC)
+                                    : d < SH::OP ? hb + (long long)k * SH::s + (d - SH::OH)
+                                                 : Hb + (long long)k * SH::ps + (d - SH::OP);
+                // issued through asm: the compiler's waitcnt pass would otherwise
+                // wait for every outstanding load at the first use (its loop
+                // model merges the guarded loads); the waits are explicit below
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[q]) : "v"(src) : "memory");
             }
+        };
+        // R's loads have landed once at most `after` younger vm ops are
+        // outstanding.  One immediate per call site: a branchy wait made the
+        // compiler copy R (still in flight) into other registers.
+        auto vwait5 = [&](d2v(&R)[NI]) {
+            static_assert(NI == 3, "register staging");
+            asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+        };
+        auto vwait4 = [&](d2v(&R)[NI]) {
+            asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+        };
+        auto vwait0 = [&](d2v(&R)[NI]) {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+        };
+        auto lput = [&](const d2v(&R)[NI], int slot) {
+#pragma unroll
+            for (int q = 0; q < NI; ++q) *reinterpret_cast<d2v *>(&stg[slot][q * 128 + 2 * lane]) = R[q];
+        };
+        // Every step issues exactly 3 loads (stage k - 3, clamped to stage 0 at
+        // the end: re-loads that are never written to LDS) and 1 record store,
+        // so "X's loads have landed" is always vmcnt(5) -- the other set's 3
+        // loads and two stores are younger; the first step follows the
+        // prologue (3 loads + 1 store: vmcnt(4)).
+        auto step = [&](int k, d2v(&X)[NI], bool first) {  // X: stage k - 1 on entry, k - 3 on exit
             const double *R = stg[k & 1];
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
-            const bool ok = schur_stage(Pm, prow, in, sm, m, s, g, c);
+            double w, luq[4];
+            const bool ok = schur_stage<SH::m>(Pm, prow, in, sm, m, s, g, c, w, luq);
             if (!ok && fail_stage < 0) fail_stage = k;
-            schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
-            wave_sync();  // the record's LDS reads retire before the next DMA overwrites the slot
+            schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
+            wave_sync();  // stage k's LDS reads retire before slot reuse
+            if (first) vwait4(X);
+            else vwait5(X);
+            if (k >= 1) lput(X, (k - 1) & 1);
+            gload(X, k >= 3 ? k - 3 : 0);
+            wave_sync();
+        };
+        gload(RA, N - 1);
+        vwait0(RA);
+        lput(RA, (N - 1) & 1);
+        gload(RA, N >= 2 ? N - 2 : 0);
+        gload(RB, N >= 3 ? N - 3 : 0);
+        wave_sync();
+        step(N - 1, RA, true);
+        int k = N - 2;
+        for (; k >= 1; k -= 2) {
+            step(k, RB, false);
+            step(k - 1, RA, false);
         }
+        if (k == 0) step(0, RB, false);
+        vwait0(RA);  // nothing in flight may land in reused registers
+        vwait0(RB);
     } else {
         SchurIn nxt;
         schur_load(nxt, Eb + (long long)(N - 1) * n * s, cb + (long long)(N - 1) * n, Hb + (long long)(N - 1) * ps,
@@ -260,7 +378,8 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             if (k > 0)
                 schur_load(nxt, Eb + (long long)(k - 1) * n * s, cb + (long long)(k - 1) * n,
                            Hb + (long long)(k - 1) * ps, hb + (long long)(k - 1) * s, n, m, s, g, c);
-            const bool ok = schur_stage(Pm, prow, in, sm, m, s, g, c);
+            double w, luq[4];
+            const bool ok = schur_stage<0>(Pm, prow, in, sm, m, s, g, c, w, luq);
             if (!ok && fail_stage < 0) fail_stage = k;
             schur_store_record(FRb + (long long)k * frs, Pm, sm, m, s, g, c);
         }
