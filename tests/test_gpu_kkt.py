@@ -156,6 +156,42 @@ def test_batched_kkt_matches_oracle(n, m, N, batch, nc):
         assert rel_err(out[b], o.forward(x0[b])) < TOL, b
 
 
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 40, 3), (5, 3, 17, 2)])
+def test_batched_kkt_varying_constraints(n, m, N, batch):
+    """Per-stage constraint counts (kkt.hpp: ncs from time_step, lqr_model.hpp:87)
+    vary 0..4 and the terminal has its own: exercises the y offsets of the
+    16-wide tile path (dual groups of mixed size, group 0 possibly empty)."""
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 31 * n + N)
+    s = n + m
+    g = np.random.default_rng(5 + N)
+    ncs = g.integers(0, 5, size=N + 1).astype(np.int32)
+    ncs[0] = 3
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+    bs.set_model(E, c, H, h, D)
+    bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+    bs.backward(irho)
+    out = np.zeros((batch, N * s + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b])
+        o = OracleKKT(pm)
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        o.backward(irho[b])
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+
+
 def test_kkt_protocol():
     from pdplqr import BatchedLQRSolver, PdplqrError
 
