@@ -38,22 +38,30 @@ struct SchurIn {
 
 // Loads stage inputs from a stage record: E (n x s, column-major), c (n),
 // packed lower H~ (s), h~ (s).  Works on global memory and on the LDS copy.
+// Branch-free: addresses are clamped into the record and the values masked
+// (a guarded LDS read compiles to an exec-mask region per element).
 __device__ __forceinline__ void schur_load(SchurIn &in, const double *__restrict__ Ek, const double *__restrict__ ck,
                                            const double *__restrict__ Hk, const double *__restrict__ hk, int n,
                                            int m, int s, int g, int c) {
+    const int cc = c < s ? c : s - 1;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
         const int t = 4 * kk + g - m;
         const bool xr = t >= 0 && t < n;
-        in.E[kk] = (xr && c < s) ? Ek[t + c * n] : 0.0;
-        in.ct[kk] = xr ? ck[t] : 0.0;
+        const int tc = t < 0 ? 0 : (t < n ? t : n - 1);
+        const double e = Ek[tc + cc * n], cv = ck[tc];
+        in.E[kk] = (xr && c < s) ? e : 0.0;
+        in.ct[kk] = xr ? cv : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = 4 * r + g;
-        in.H[r] = (i < s && c < s) ? Hk[i >= c ? pidx(i, c, s) : pidx(c, i, s)] : (i == c ? 1.0 : 0.0);
+        const int ic = i < s ? i : s - 1;
+        const double v = Hk[ic >= cc ? pidx(ic, cc, s) : pidx(cc, ic, s)];
+        in.H[r] = (i < s && c < s) ? v : (i == c ? 1.0 : 0.0);
     }
-    in.h = (c < s) ? hk[c] : 0.0;
+    const double hv = hk[cc];
+    in.h = (c < s) ? hv : 0.0;
 }
 
 struct SchurSmem {
