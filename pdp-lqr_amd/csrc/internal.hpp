@@ -97,6 +97,12 @@ struct pdplqr_handle_s {
     std::vector<void *> allocs;
     pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)
     pdplqr::KKTState *kkt = nullptr;       // KKT solver state (kkt.hip)
-    double *suf_bufs[2] = {nullptr, nullptr};
     int shard_last = 1;  // last shard_backward's is_last_shard
+    // replayable launch sequences of backward / backward_without_factorization /
+    // forward (solvers.hip: hipGraph captured on first use per argument set)
+    struct Graph {
+        hipGraphExec_t exec = nullptr;
+        const void *k1 = nullptr, *k2 = nullptr;
+        hipStream_t stream = nullptr;
+    } graphs[3];
 };

@@ -1,5 +1,6 @@
 // solvers.hip -- dispatch of the protocol calls to the three solver kinds.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "parallel.hpp"
@@ -163,6 +164,7 @@ static int parallel_init(pdplqr_handle h) {
 // segment backward + suffix scan; `last_is_terminal` = 0 for a non-final
 // horizon shard.
 static int parallel_scans(pdplqr_handle h, int last_is_terminal);
+void graph_release(pdplqr_handle h);
 
 static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
     ParallelState *ps = h->par;
@@ -274,6 +276,7 @@ int solver_init(pdplqr_handle h) {
 }
 
 void solver_release(pdplqr_handle h) {
+    graph_release(h);
     delete h->par;
     h->par = nullptr;
     kkt_release(h);
@@ -290,31 +293,95 @@ int solver_update(pdplqr_handle h, const double *ws, const double *ys, const dou
                                       h->tab_n, h->stream);
 }
 
-int solver_backward(pdplqr_handle h, const double *rho) {
-    if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
-    int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
-                            h->max_nc, h->stream);
-    if (rc) return rc;
-    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) {
-        h->shard_last = 1;
-        return parallel_backward(h, 1);
+// ---------------------------------------------------------------------------
+// HIP graphs.  A protocol call issues a fixed sequence of launches whose
+// arguments depend only on the handle and on the call's device pointers (the
+// parallel solver: ~20 short kernels, launch-rate bound from the host).  The
+// sequence is captured once per (pointer set, stream) and replayed with one
+// hipGraphLaunch.  Host-side state the sequence sets is set outside the
+// captured part.  Opt-in (PDPLQR_GRAPH=1): measured on MI355X the replay is
+// not faster -- C2 (N = 1024 single problem, ~20 kernels) 0.169 ms issued
+// directly vs 0.176 ms replayed; the GPU-side dispatch gap, not the host
+// launch rate, separates the kernels.  A stream that cannot capture (the
+// legacy null stream) falls back to direct issue.
+// ---------------------------------------------------------------------------
+void graph_release(pdplqr_handle h) {
+    for (auto &g : h->graphs) {
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        g = pdplqr_handle_s::Graph{};
     }
-    return launch_riccati_backward(riccati_args(h), h->stream);
+}
+
+template <class Issue>
+static int run_graphed(pdplqr_handle h, int slot, const void *k1, const void *k2, Issue &&issue) {
+    static const bool off = getenv("PDPLQR_GRAPH") == nullptr;
+    if (off || !h->stream) return issue();
+    auto &g = h->graphs[slot];
+    if (g.exec && g.k1 == k1 && g.k2 == k2 && g.stream == h->stream) {
+        PDPLQR_HIP_TRY(hipGraphLaunch(g.exec, h->stream));
+        return PDPLQR_OK;
+    }
+    if (g.exec) {
+        (void)hipGraphExecDestroy(g.exec);
+        g = pdplqr_handle_s::Graph{};
+    }
+    if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return issue();
+    }
+    const int rc = issue();
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->stream, &graph);
+    if (rc || e != hipSuccess || !graph) {
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        return rc ? rc : issue();  // capture failed: run the sequence directly
+    }
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+        (void)hipGetLastError();
+        return issue();
+    }
+    g.exec = exec;
+    g.k1 = k1;
+    g.k2 = k2;
+    g.stream = h->stream;
+    PDPLQR_HIP_TRY(hipGraphLaunch(g.exec, h->stream));
+    return PDPLQR_OK;
+}
+
+int solver_backward(pdplqr_handle h, const double *rho) {
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) h->shard_last = 1;
+    return run_graphed(h, 0, rho, nullptr, [&]() -> int {
+        if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
+        int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
+                                h->max_nc, h->stream);
+        if (rc) return rc;
+        if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1);
+        return launch_riccati_backward(riccati_args(h), h->stream);
+    });
 }
 
 int solver_backward_nofact(pdplqr_handle h, const double *rho) {
-    int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 0,
-                            h->max_nc, h->stream);
-    if (rc) return rc;
-    // LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154)
-    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, h->shard_last, false);
-    return launch_riccati_backward_nofact(riccati_args(h), h->stream);
+    const int last = h->shard_last;
+    return run_graphed(h, 1, rho, reinterpret_cast<const void *>((intptr_t)(last + 1)), [&]() -> int {
+        int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 0,
+                                h->max_nc, h->stream);
+        if (rc) return rc;
+        // LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154)
+        if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, last, false);
+        return launch_riccati_backward_nofact(riccati_args(h), h->stream);
+    });
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {
-    if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_forward(h, x0, ws);
-    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
-    return launch_riccati_forward(h->sh, h->E, h->c, h->KD, x0, ws, h->stream);
+    return run_graphed(h, 2, x0, ws, [&]() -> int {
+        if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_forward(h, x0, ws);
+        if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
+        return launch_riccati_forward(h->sh, h->E, h->c, h->KD, x0, ws, h->stream);
+    });
 }
 
 int solver_clear(pdplqr_handle) { return PDPLQR_OK; }

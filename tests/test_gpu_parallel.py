@@ -159,3 +159,55 @@ def test_parallel_backward_without_factorization(name, ns, condensed, seglen):
         ref = o.forward(d["x0"])
         assert rel_err(np.concatenate(out), ref) < TOL, it
         ws2 = ws2 + 0.05 * g.standard_normal(ws2.shape)
+
+
+def test_graph_replay_matches_direct():
+    """Protocol calls replayed from a captured hipGraph (PDPLQR_GRAPH=1, read at
+    library load: run in a child process) give the same trajectory as direct
+    issue, across repeated calls and a changed x0."""
+    import subprocess
+    import sys
+    import textwrap
+
+    code = textwrap.dedent(r"""
+        import os, sys, numpy as np
+        sys.path[:0] = [os.environ["ROOT"], os.path.join(os.environ["ROOT"], "pdp-lqr_amd")]
+        import torch
+        from pdplqr import BatchedLQRSolver
+        from pdplqr.problems import random_batch_arrays
+        n, m, N, batch = 12, 4, 200, 3
+        E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 5)
+        dev = torch.device("cuda", 0)
+        t = lambda a: torch.as_tensor(a, device=dev)
+        outs = []
+        for solver in ("parallel", "serial"):
+            bs = BatchedLQRSolver(n, m, N, batch, solver=solver, num_segments=4)
+            bs.set_model(t(E), t(c), t(H), t(h))
+            bs.update_problem_data(torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev), sigma=1e-6)
+            out = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev)
+            X0 = t(x0)
+            for it in range(3):
+                bs.backward()
+                bs.forward(X0 * (1 + it), out)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+            bs.close()
+        np.save(os.environ["OUT"], np.stack(outs))
+    """)
+    import os
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for graph in ("0", "1"):
+        fd, path = tempfile.mkstemp(suffix=".npy")
+        os.close(fd)
+        env = dict(os.environ, ROOT=root, OUT=path)
+        if graph == "1":
+            env["PDPLQR_GRAPH"] = "1"
+        else:
+            env.pop("PDPLQR_GRAPH", None)
+        subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
+        res.append(np.load(path))
+        os.unlink(path)
+    assert np.all(np.isfinite(res[0]))
+    assert np.array_equal(res[0], res[1])
