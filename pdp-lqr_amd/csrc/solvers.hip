@@ -103,31 +103,57 @@ static int parallel_init(pdplqr_handle h) {
     // per-composition latencies of one wave (profiles/r01 c4_v12: a ~10 us,
     // b ~45 us, c ~5.5 us at 24/8; a ~10 us, b ~15 us for s <= 16).
     int Lsub = h->cfg.segment_len;
+    if (Lsub <= 0 && getenv("PDPLQR_SEGMENT_LEN")) Lsub = atoi(getenv("PDPLQR_SEGMENT_LEN"));  // diagnostics
     if (Lsub <= 0) {
         const double a = 10.0, b = sh.s <= 16 ? 15.0 : 45.0, cm = sh.s <= 16 ? 4.0 : 5.5;
         const long long sb = seg_backward_slots(sh, h->cfg.device), ss = seg_scan_slots(sh, h->cfg.device);
         const long long B = sh.batch;
-        auto cost = [&](long long S) {
-            const long long per = (sh.N + S - 1) / S, rb = (B * S + sb - 1) / sb, rs = (B * S + ss - 1) / ss;
+        // device segments and the longest one for a sub-segment length L (every
+        // reference segment is cut separately, so S can exceed N / L by up to ns)
+        auto pieces = [&](int L, int &longest) {
+            long long S = 0;
+            longest = 0;
+            for (int i = 0; i < ns; ++i) {
+                const int p = (ps->ref_len[i] + L - 1) / L;
+                S += p;
+                longest = std::max(longest, (ps->ref_len[i] + p - 1) / p);
+            }
+            return S;
+        };
+        auto cost = [&](long long S, long long per) {
+            const long long rb = (B * S + sb - 1) / sb, rs = (B * S + ss - 1) / ss;
             int lg = 0, lg1 = 0;
             while ((1LL << lg) < S) ++lg;
             while ((1LL << lg1) < S + 1) ++lg1;
             return a * per * rb + b * (lg + 1) * rs + cm * lg1;
         };
-        long long best = 1;
-        double bc = cost(1);
+        int maxlen = 1;
+        for (int i = 0; i < ns; ++i) maxlen = std::max(maxlen, (int)ps->ref_len[i]);
+        int lg0;
+        const long long S0 = pieces(maxlen, lg0);
+        double bc = cost(S0, lg0);
+        Lsub = maxlen;
         std::vector<long long> cand;
         for (long long S = 2; S <= sh.N; S <<= 1) cand.push_back(S);
         if (sb / B >= 1 && sb / B <= sh.N) cand.push_back(sb / B);
-        for (long long S : cand)
-            if (sh.N / S >= 4 || S == 1) {
-                const double cS = cost(S);
-                if (cS < bc) {
-                    bc = cS;
-                    best = S;
-                }
+        for (long long St : cand) {
+            // smallest L whose cut fits St segments: a target at the slot count
+            // must not spill a few segments into a second residency round
+            int lo = 1, hi = maxlen, dummy;
+            while (lo < hi) {
+                const int mid = (lo + hi) / 2;
+                if (pieces(mid, dummy) <= St) hi = mid;
+                else lo = mid + 1;
             }
-        Lsub = (int)((sh.N + best - 1) / best);
+            int longest;
+            const long long S = pieces(lo, longest);
+            if (longest < 4 && S > (long long)ns) continue;  // keep >= 4 stages per segment
+            const double cS = cost(S, longest);
+            if (cS < bc) {
+                bc = cS;
+                Lsub = lo;
+            }
+        }
     }
     for (int i = 0; i < ns; ++i) {
         const int pieces = (ps->ref_len[i] + Lsub - 1) / Lsub;
