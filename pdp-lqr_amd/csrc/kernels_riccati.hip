@@ -688,12 +688,16 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
             }
             ax[q] = a;
         }
-        // u = -Luu^{-T} v: back substitution, u_i broadcast from lane i
+        // u = -Luu^{-T} v: back substitution, u_i broadcast from lane i.  The
+        // reciprocals of the diagonal do not depend on the chain (rcp, hoisted).
+        double rdg[MM];
+#pragma unroll
+        for (int i = 0; i < MM; ++i) rdg[i] = rcp_f64(cur.luu[i]);  // used on lane cl == i only
         double acc = 0.0, myu = 0.0;
 #pragma unroll
         for (int i = MM - 1; i >= 0; --i) {
             if (i < m) {
-                const double cand = -(v + acc) / cur.luu[i];  // valid on lane cl == i (luu[i] = Luu[i][i])
+                const double cand = -(v + acc) * rdg[i];  // valid on lane cl == i (luu[i] = Luu[i][i])
                 const double ui = readlane_f64(cand, i);
                 if (cl == i) myu = ui;
                 acc = __builtin_fma(cur.luu[i], ui, acc);  // lanes cl < i: Luu[i][cl] u_i
