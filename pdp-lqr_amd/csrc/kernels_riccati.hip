@@ -740,6 +740,168 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
     }
 }
 
+// ---------------------------------------------------------------------------
+// Segment rollout with the stage records streamed through an LDS-DMA ring
+// (compile-time 16 < s <= 32 shapes, one wave per segment).  The generic
+// kernel above prefetches one stage ahead in registers, which at one wave per
+// SIMD leaves the HBM latency exposed (half of its wave cycles wait on
+// memory).  Here D - 1 stages are in flight: E_k, c_k, the rollout record and
+// G_k land in slot k % D by global_load_lds_dwordx4; the per-stage arithmetic
+// is the generic kernel's, reading the slot.  vm ops per iteration: NI DMA +
+// 1 u store + R x stores, so "stage k has landed" is a fixed vmcnt.
+// ---------------------------------------------------------------------------
+template <int NN, int MM>
+struct SegRec {
+    static constexpr int n = NN, m = MM, s = NN + MM, FRS = s * m + m;
+    static constexpr int OE = 0, OC = n * s, OF = OC + n, OG = OF + FRS, REC = OG + m * n;
+    static constexpr int CH = REC / 2, NI = (CH + 63) / 64, TAIL = CH - (NI - 1) * 64;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FRS % 2 == 0 && (m * n) % 2 == 0 && s > 16 &&
+                               s <= 32;
+};
+
+template <int NN, int MM, int D>
+__global__ __launch_bounds__(64) void k_seg_fwd_dma(Shape sh, const double *__restrict__ E,
+                                                    const double *__restrict__ c, const double *__restrict__ FR,
+                                                    double *__restrict__ ws, SegFwd sf) {
+    using SR = SegRec<NN, MM>;
+    static_assert(SR::ok, "segment rollout record layout");
+    constexpr int R = 2, NJ = 4 * R, n = NN, m = MM, s = NN + MM, NI = SR::NI;
+    constexpr int VM = (1 + R) + (D - 2) * (NI + 1 + R) + NI;  // vm ops younger than stage k's DMA
+    static_assert(VM <= 63, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) double ring[D][SR::REC];
+    __shared__ double sw[64];   // w_k = [u; x]
+    __shared__ double suh[64];  // u_hat of this segment
+    const int lane = threadIdx.x, g = lane >> 4, cl = lane & 15;
+    const long long b = blockIdx.x / sf.S;
+    const int seg = blockIdx.x % sf.S;
+    const int N0 = sf.seg_start[seg], N1 = N0 + sf.seg_len[seg];
+    const bool last = (seg == sf.S - 1) && sf.last_is_terminal;
+    const int N = sh.N;
+    const double *Eb = E + b * sh.perE;
+    const double *cb = c + b * sh.perc;
+    const double *Fb = FR + b * sh.perKD;
+    const double *Gb = sf.G + b * (long long)N * m * n;
+    double *wb = ws + b * sh.perh;
+    {
+        const double *xh = sf.xhat + (b * (sf.S + 1) + seg) * n;
+        if (lane < n) {
+            sw[m + lane] = xh[lane];
+            suh[lane] = last ? 0.0 : sf.lam[(b * (sf.S + 1) + seg + 1) * n + lane];
+        }
+        if (!last && seg == sf.S - 1 && lane < n)  // shard slice end: x after the slice
+            wb[(long long)N1 * s + lane] = sf.xhat[(b * (sf.S + 1) + sf.S) * n + lane];
+    }
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            if (q < NI - 1 || lane < SR::TAIL) {
+                const int d = 2 * (q * 64 + lane);
+                const double *src = d < SR::OC   ? Eb + (long long)k * (n * s) + d
+                                    : d < SR::OF ? cb + (long long)k * n + (d - SR::OC)
+                                    : d < SR::OG ? Fb + (long long)k * SR::FRS + (d - SR::OF)
+                                                 : Gb + (long long)k * (m * n) + (d - SR::OG);
+                dma16(src, &ring[slot][q * 128]);
+            }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) dma(N0 + j < N1 ? N0 + j : N1 - 1, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane < n) wb[(long long)N0 * s + m + lane] = sw[m + lane];  // ws[N0].tail(n) = x_hat
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    double uh[NJ];
+#pragma unroll
+    for (int qq = 0; qq < NJ; ++qq) {
+        const int t = 4 * qq + g;
+        uh[qq] = (!last && t < n) ? suh[t] : 0.0;
+    }
+    for (int k = N0; k < N1; ++k) {
+        const int kr = k - N0, kp = k + D - 1;
+        dma(kp < N1 ? kp : N1 - 1, (kr + D - 1) % D);  // past the end: re-load into a consumed slot
+        if (kr < D - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+        wave_sync();
+        const double *Rk = ring[kr % D];
+        FwdIn<R, MM> cur;
+        fwd_load<R, MM>(cur, Rk + SR::OE, Rk + SR::OC, Rk + SR::OF, n, m, s, g, cl);
+        double gq[NJ];
+#pragma unroll
+        for (int qq = 0; qq < NJ; ++qq) {
+            const int t = 4 * qq + g;
+            gq[qq] = (!last && cl < m && t < n) ? Rk[SR::OG + cl + t * m] : 0.0;
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < NJ; ++qq) {
+            const int t = 4 * qq + g;
+            const double xt = (t < n) ? sw[m + t] : 0.0;
+            v = __builtin_fma(cur.lxu[qq], xt, v);
+            v = __builtin_fma(-gq[qq], uh[qq], v);
+        }
+        v += shfl_xor_f64(v, 16);
+        v += shfl_xor_f64(v, 32);
+        v += cur.lu;
+        double ax[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            double a = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = 4 * jj + g;
+                if (j >= m && j < s) a = __builtin_fma(cur.E[q][jj], sw[j], a);
+            }
+            ax[q] = a;
+        }
+        double rdg[MM];
+#pragma unroll
+        for (int i = 0; i < MM; ++i) rdg[i] = rcp_f64(cur.luu[i]);
+        double acc = 0.0, myu = 0.0;
+#pragma unroll
+        for (int i = MM - 1; i >= 0; --i) {
+            const double cand = -(v + acc) * rdg[i];  // valid on lane cl == i
+            const double ui = readlane_f64(cand, i);
+            if (cl == i) myu = ui;
+            acc = __builtin_fma(cur.luu[i], ui, acc);
+            if (lane == 0) sw[i] = ui;
+        }
+        wave_sync();
+        const bool upd = last || (k < N1 - 1);  // update_x_next (lqr_solver_parallel.hpp:231)
+        double xn[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            double a = ax[q];
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = 4 * jj + g;
+                if (j < m) a = __builtin_fma(cur.E[q][jj], sw[j], a);
+            }
+            a += shfl_xor_f64(a, 16);
+            a += shfl_xor_f64(a, 32);
+            xn[q] = a + cur.c[q];
+        }
+        wave_sync();
+        if (g == 0 && cl < m) gstore(wb + (long long)k * s + cl, myu);
+        if (g == 0 && upd) {
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int t = cl + 16 * q;
+                if (t < n) {
+                    sw[m + t] = xn[q];
+                    gstore(wb + (long long)(k + 1) * s + ((k + 1 < N) ? m : 0) + t, xn[q]);
+                }
+            }
+        }
+        wave_sync();
+    }
+}
+
+static bool segfwd_aligned(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf) {
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return al(E) && al(c) && al(FR) && al(sf.G) && sh.perE % 2 == 0 && sh.perc % 2 == 0 && sh.perKD % 2 == 0 &&
+           ((long long)sh.N * sh.m * sh.n) % 2 == 0;
+}
+
 template <bool SEG>
 static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                       double *ws, const SegFwd &sf, hipStream_t st) {
@@ -772,6 +934,12 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st) {
+    if (sh.n == 24 && sh.m == 8 && segfwd_aligned(sh, E, c, FR, sf) && !getenv("PDPLQR_NO_DMA")) {
+        hipLaunchKernelGGL((k_seg_fwd_dma<24, 8, 3>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
+                           FR, ws, sf);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     return launch_fwd<true>(sh, E, c, FR, nullptr, ws, sf, st);
 }
 
