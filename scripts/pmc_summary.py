@@ -17,11 +17,20 @@ from collections import defaultdict
 def main():
     root, tag = sys.argv[1], sys.argv[2]
     per = defaultdict(lambda: defaultdict(list))
+    rows = []
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                k = row.get("Kernel_Name", "?")
-                per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            rows += list(csv.DictReader(fh))
+    # the bench also runs secondary configs through the same kernels (smaller
+    # grids): per kernel, only the dispatches of its largest grid (the bench
+    # workload) are averaged
+    gmax = defaultdict(int)
+    for row in rows:
+        gmax[row.get("Kernel_Name", "?")] = max(gmax[row.get("Kernel_Name", "?")], int(row.get("Grid_Size", 0)))
+    for row in rows:
+        k = row.get("Kernel_Name", "?")
+        if int(row.get("Grid_Size", 0)) == gmax[k]:
+            per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {"workload": tag, "kernels": {}}
     for k, d in per.items():
         short = k.split("(")[0].replace("void ", "")
