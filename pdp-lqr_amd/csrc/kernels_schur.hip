@@ -245,6 +245,28 @@ __device__ __forceinline__ void schur_store_record_staged(double *FRk, double w,
     if (lane < FS / 2) gstore2(FRk + 2 * lane, reinterpret_cast<const d2v *>(sm.rec)[lane]);
 }
 
+// Record from the tile (chol_tiles path): u columns of M scaled by 1/sqrt(d)
+// (sm.inv), lu' from sm.luq; staged in LDS, one coalesced store.
+template <int M, int S>
+__device__ __forceinline__ void schur_store_record_tile(double *FRk, const d4 &Pm, SchurSmem &sm, int g, int c) {
+    constexpr int FS = S * M + M;
+    const int lane = 16 * g + c;
+    const int cm = c < M ? c : M - 1;
+    const double iv = sm.inv[cm];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        if (c < M && i < S) sm.rec[c * S + i] = (i >= c) ? Pm[r] * iv : 0.0;
+    }
+    if (lane < M) sm.rec[S * M + lane] = sm.luq[lane];
+    wave_sync();
+    if (lane < FS / 2) gstore2(FRk + 2 * lane, reinterpret_cast<const d2v *>(sm.rec)[lane]);
+}
+
+#ifndef PDPLQR_SCHUR_BLOCK
+#define PDPLQR_SCHUR_BLOCK 1
+#endif
+
 // Stage-record layout of the LDS-DMA variant (compile-time shapes).
 template <int NN, int MM>
 struct SchurShape {
@@ -352,9 +374,10 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
             double w, luq[4];
-            const bool ok = schur_stage<SH::m>(Pm, prow, in, sm, m, s, g, c, w, luq);
+            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0>(Pm, prow, in, sm, m, s, g, c, w, luq);
             if (!ok && fail_stage < 0) fail_stage = k;
-            schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
+            if (PDPLQR_SCHUR_BLOCK) schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
+            else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
             wave_sync();  // stage k's LDS reads retire before slot reuse
             if (first) vwait4(X);
             else vwait5(X);
