@@ -257,7 +257,7 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
                                       sm, lane);
     if (!fcf)
         for (int q = lane; q < 2 * n * n + n; q += 64) o[q] = 0.0;  // [F | C | f]
-    if (!ok && lane == 0) atomicOr(A.flag, 1);
+    if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
 }
 
 // ---------------------------------------------------------------------------
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
             else wm_load(PhiT, src, n, n, true, 0.0, g, c);
         }
     }
-    if (!ok && lane == 0) atomicOr(A.flag, 2);
+    if (!ok && lane == 0) atomicOr(A.flag + b, 2);
     if (j > 0) {
         wm_store(Phi, mo, n, n, g, c);
         wv_store(phi, mo + nn, n, g, c);
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
             if (j == 0) {
                 elem_copy(acc, nx, n, lane);
             } else {
-                if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag, 4);
+                if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag + b, 4);
                 elem_copy(acc, o, n, lane);
             }
             wave_sync();
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     for (int j = R - 2; j > r; --j) {
         elem_copy(nx, elems + (long long)j * stride, n, lane);
         wave_sync();
-        if (!tcombine<T>(o, nx, acc, n, true, true, sm, lane) && lane == 0) atomicOr(flag, 8);
+        if (!tcombine<T>(o, nx, acc, n, true, true, sm, lane) && lane == 0) atomicOr(flag + b, 8);
         elem_copy(acc, o, n, lane);
         wave_sync();
     }

@@ -22,7 +22,7 @@ struct ScanArgs {
     int terminal;              // the last element ends at the real terminal (F = C = f = 0)
     const double *in;          // suffix scan ping-pong [b][S][es]
     double *out;
-    int *flag;
+    int *flag;                 // [b]: a combine was not positive definite
 };
 
 struct MapArgs {

@@ -173,7 +173,7 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->seg_status, B * S)) || (rc = palloc(h, &ps->G, B * sh.N * sh.m * sh.n)) ||
         (rc = palloc(h, &ps->elem, B * S * es)) || (rc = palloc(h, &ps->bufA, B * S * es)) ||
         (rc = palloc(h, &ps->bufB, B * S * es)) || (rc = palloc(h, &ps->xhat, B * (S + 1) * sh.n)) ||
-        (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, 1)) ||
+        (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, B)) ||
         (rc = palloc(h, &ps->mapA, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->mapB, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->vfun, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
@@ -182,7 +182,7 @@ static int parallel_init(pdplqr_handle h) {
         return rc;
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_start, ps->seg_start_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_len, ps->seg_len_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
-    PDPLQR_HIP_TRY(hipMemset(ps->flag, 0, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemset(ps->flag, 0, B * sizeof(int)));
     PDPLQR_HIP_TRY(hipMemset(ps->seg_status, 0, B * S * sizeof(int32_t)));
     return PDPLQR_OK;
 }
@@ -211,7 +211,7 @@ static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = 
     a.lpc = h->lpc;
     a.elem = ps->elem;
     a.seg_status = ps->seg_status;
-    PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, sizeof(int), h->stream));
+    PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, (size_t)sh.batch * sizeof(int), h->stream));
     int rc = fact ? launch_seg_backward(a, h->stream) : launch_seg_backward_nofact(a, h->stream);
     if (rc) return rc;
     return parallel_scans(h, last_is_terminal);
@@ -419,16 +419,15 @@ int solver_status(pdplqr_handle h, int32_t *flags) {
         return PDPLQR_OK;
     }
     ParallelState *ps = h->par;
-    std::vector<int32_t> st((size_t)sh.batch * ps->S);
-    int flag = 0;
+    std::vector<int32_t> st((size_t)sh.batch * ps->S), flag(sh.batch);
     PDPLQR_HIP_TRY(hipMemcpy(st.data(), ps->seg_status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-    PDPLQR_HIP_TRY(hipMemcpy(&flag, ps->flag, sizeof(int), hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(flag.data(), ps->flag, flag.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
     for (int b = 0; b < sh.batch; ++b) {
         int v = 0;
         for (int i = 0; i < ps->S; ++i) v = std::max(v, (int)st[(size_t)b * ps->S + i]);
         // a failed condensed (segment) combine is reported as N + 2, the
         // analogue of the condensed backward returning false (condensed_system.hpp:217-226)
-        flags[b] = v ? v : (flag ? sh.N + 2 : 0);
+        flags[b] = v ? v : (flag[b] ? sh.N + 2 : 0);
     }
     return PDPLQR_OK;
 }

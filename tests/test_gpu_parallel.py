@@ -211,3 +211,23 @@ def test_graph_replay_matches_direct():
         os.unlink(path)
     assert np.all(np.isfinite(res[0]))
     assert np.array_equal(res[0], res[1])
+
+
+def test_parallel_non_spd_status_is_per_problem():
+    """An indefinite stage in one problem of a batch is reported for that
+    problem only (stage + 1); the other problems' combines stay clean."""
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 4, 2, 40, 3
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 3)
+    s = n + m
+    H = H.copy()
+    H[1, 17 * s * s:18 * s * s] = -np.eye(s).reshape(-1)  # stage 17 of problem 1 indefinite
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(np.zeros((batch, N * s + n)), sigma=0.0)
+    bs.backward()
+    bs.forward(x0, np.zeros((batch, N * s + n)))
+    st = bs.status()
+    assert st[0] == 0 and st[2] == 0 and st[1] != 0, st
