@@ -47,6 +47,16 @@ __device__ __forceinline__ void load_M(d4 (&M)[T][T], const double *__restrict__
 // Wave-scope ordering of LDS traffic between lanes of ONE wavefront: LDS
 // instructions of a wave retire in issue order, so a compiler-level barrier is
 // all that is needed (no s_barrier; the workgroup is a single wave).
+// threadIdx.x of a one-wavefront block, with its range made known to the
+// compiler: index tests on g = lane >> 4 < 4 and c = lane & 15 then fold
+// (without it, per-element masks on provably valid tile rows compile to
+// exec-masked LDS loads and selects).
+__device__ __forceinline__ int wave_lane() {
+    const int l = threadIdx.x;
+    __builtin_assume(l >= 0 && l < 64);
+    return l;
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
     constexpr int P = 32;
     __shared__ double Pn[P * P];  // P_{k+1} (dense, ld n) from the factor cache
     __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P], xs[P], us[P];
-    const int lane = threadIdx.x;
+    const int lane = wave_lane();
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
     const long long b = blockIdx.x / S;
@@ -232,7 +232,7 @@ template <int T>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
     extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 operand images (op_stage_bytes)
-    const int lane = threadIdx.x;
+    const int lane = wave_lane();
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
     const long long b = blockIdx.x / S;
@@ -276,7 +276,7 @@ template <int T>
 __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];  // 2 operand images when A.right
     __shared__ CombSmem<T> sm;
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const int n = A.n, S = A.S, J = S + 1, nn = n * n;
     const int es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / J;
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
 // ---------------------------------------------------------------------------
 template <int T>
 __global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const int n = A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
                                                     double *out_pre_all, double *out_suf_all, int *has_suf, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     __shared__ CombSmem<T> sm;
-    const int lane = threadIdx.x;
+    const int lane = wave_lane();
     const int es = 3 * n * n + 2 * n;
     const long long b = blockIdx.x;
     // element j of problem b: elems_all[(j * batch + b) * es]; outputs [b][es]

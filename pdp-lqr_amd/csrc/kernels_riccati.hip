@@ -169,7 +169,7 @@ int launch_penalty(const Shape &sh, const double *D, const double *rho, const do
 template <int T>
 __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati_bwd(RiccatiArgs A) {
     __shared__ BwdSmem<T> sm;
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(64, (T == 1 ? PDPLQR_BWD_WAVES : 1)) void k_riccati
     static_assert(SH::ok, "fast path needs 16-byte stage sections");
     __shared__ BwdSmem<T> sm;
     __shared__ __attribute__((aligned(16))) double stg[2][NI * 128];
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
     const int N = sh.N;
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64) void k_riccati_bwd_nofact(RiccatiArgs A) {
     __shared__ double Lk[P * P];  // this stage's L (packed -> dense, column-major, ld = s)
     __shared__ double Ln[P * P];  // next stage's Lxx (ld = n)
     __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P];
-    const int lane = threadIdx.x;
+    const int lane = wave_lane();
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(64) void k_riccati_fwd(Shape sh, const double *__re
     constexpr int NJ = 4 * R;
     __shared__ double sw[64];  // w_k = [u; x]
     __shared__ double suh[64]; // u_hat of this segment
-    const int lane = threadIdx.x, g = lane >> 4, cl = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
     const int n = sh.n, m = sh.m, s = sh.s;
     long long b;
     int N0, N1;
@@ -771,7 +771,7 @@ __global__ __launch_bounds__(64) void k_seg_fwd_dma(Shape sh, const double *__re
     __shared__ __attribute__((aligned(16))) double ring[D][SR::REC];
     __shared__ double sw[64];   // w_k = [u; x]
     __shared__ double suh[64];  // u_hat of this segment
-    const int lane = threadIdx.x, g = lane >> 4, cl = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
     const long long b = blockIdx.x / sf.S;
     const int seg = blockIdx.x % sf.S;
     const int N0 = sf.seg_start[seg], N1 = N0 + sf.seg_len[seg];

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__re
     static_assert(SH::ok, "rollout DMA layout");
     __shared__ __attribute__((aligned(16))) double ring[D][SH::REC];
     __shared__ double sx[16];
-    const int lane = threadIdx.x, g = lane >> 4, cl = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
     const long long b = blockIdx.x;
     const int N = sh.N;
     const double *Eb = E + b * sh.perE;

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     constexpr int NI = CT ? SH::NI : 1;
     __shared__ SchurSmem sm;
     __shared__ __attribute__((aligned(16))) double stg[CT ? 2 : 1][CT ? NI * 128 : 2];
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
     const int n = CT ? NN : sh.n, m = CT ? MM : sh.m, s = n + m;

@@ -150,7 +150,7 @@ template <int T, int NN, int MM>
 __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
     constexpr bool CT = NN > 0;
     __shared__ AugSmem<T> sm;
-    const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const Shape &sh = A.sh;
     const int n = CT ? NN : sh.n, m = CT ? MM : sh.m, s = n + m, S = A.S;
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks holding x rows

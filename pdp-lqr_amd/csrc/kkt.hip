@@ -143,7 +143,7 @@ __global__ __launch_bounds__(64) void k_kkt_stage(KKTArgs A) {
     const int P = A.P, PP = P * P;
     double *L = lds, *V = lds + PP, *U = lds + 2 * PP, *T = lds + 3 * PP;
     const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane();
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void k_kkt_factor(KKTArgs A, const double *__re
     const int P = A.P, PP = P * P;
     double *M = lds, *Lp = lds + PP, *X = lds + 2 * PP;
     const Shape &sh = A.sh;
-    const int n = sh.n, N = sh.N, lane = threadIdx.x;
+    const int n = sh.n, N = sh.N, lane = wave_lane();
     const long long b = blockIdx.x;
     const double *ir = inv_rho + b * sh.ny;
     int fail = 0;
@@ -293,7 +293,7 @@ __device__ __forceinline__ d4 tile_transpose(const d4 &v, double *t, int g, int 
 // tile-native order: dpk [b][N+1][2][256]
 __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict__ dpk) {
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int gk = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
 // t1 = U^T w as single-column MFMA products on the packed primal tiles
 __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int p = A.prim_dim[k];
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *_
                                                       double *__restrict__ ws) {
     __shared__ double zs[16];
     const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
@@ -457,7 +457,7 @@ __global__ void k_kkt_bvec16(KKTArgs A, double *__restrict__ bvec) {
 __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ dpk,
                                                      const double *__restrict__ dreg) {
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const double *tiles = dpk + b * (N + 1) * 512LL;
     const double *dg = dreg + b * (N + 1) * 16LL;
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__
 __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *__restrict__ bvec) {
     __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
     const double *fb = A.fac + b * (N + 1) * 3LL * 256;
@@ -610,7 +610,7 @@ __global__ void k_kkt_rhs(KKTArgs A, const int4 *__restrict__ rows, const double
 // update_rhs_initial_stage (kkt.hpp:207-222): rhs_u0 += -S0 x0, rhs_lambda1 += -A0 x0
 __global__ __launch_bounds__(64) void k_kkt_x0(KKTArgs A, const double *__restrict__ x0) {
     const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, s = sh.s, lane = threadIdx.x;
+    const int n = sh.n, m = sh.m, s = sh.s, lane = wave_lane();
     const long long b = blockIdx.x;
     const double *H0 = A.H + b * sh.perH, *E0 = A.E + b * sh.perE, *x = x0 + b * n;
     double *r = A.rhs + b * A.dim;
@@ -632,7 +632,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve1(KKTArgs A) {
     const int P = A.P, PP = P * P;
     double *L = lds, *w = lds + PP;
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x;
+    const int N = sh.N, lane = wave_lane();
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve2(KKTArgs A) {
     const int P = A.P, PP = P * P;
     double *Lk = lds, *Lo = lds + PP, *v = lds + 2 * PP, *yp = v + P;
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = threadIdx.x;
+    const int N = sh.N, lane = wave_lane();
     const long long b = blockIdx.x;
     const double *rd = A.rhs + b * A.dim;
     double *wvb = A.wv + b * (N + 1) * 4LL * P;
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve3(KKTArgs A, const double *__re
     const int P = A.P, PP = P * P;
     double *L = lds, *z = lds + PP;
     const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = threadIdx.x;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane();
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int p = A.prim_dim[k], g = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
