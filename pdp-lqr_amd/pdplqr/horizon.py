@@ -128,12 +128,16 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     elem = torch.empty(shard.batch, shard.es, dtype=torch.float64, device=dev)
     if on_gpu:
+        # Run the slice on torch's current stream: ProcessGroupNCCL orders the
+        # all-gather after it and the stream after the all-gather, so the
+        # backward -> exchange -> forward chain needs no host round trip.
+        cur = torch.cuda.current_stream().cuda_stream
+        if shard.stream() != cur:
+            shard.synchronize()  # drain work queued on the previous stream
+            shard.handle.set_stream(cur)
         shard.backward(elem, rank == world - 1, rho)
-        # the element is produced on the handle's stream: order it before RCCL's
-        shard.synchronize()
         gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(gathered, elem, group=group)
-        torch.cuda.current_stream().synchronize()
     else:
         e_np = np.zeros((shard.batch, shard.es))
         shard.backward(e_np, rank == world - 1, None if rho is None else rho)

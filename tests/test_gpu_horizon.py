@@ -129,3 +129,56 @@ def test_two_process_gloo_exchange():
         if N1 == N:
             full[N * s:] = loc[0, (N1 - N0) * s:]
     assert rel_err(full, ref) < TOL
+
+
+def _nccl_worker(port, q):
+    """One rank on the RCCL backend: exercises solve_distributed's device path
+    (slice on torch's current stream, all-gather ordered by ProcessGroupNCCL,
+    no host synchronisation), twice, so the stream re-binding is also covered."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from pdplqr.horizon import HorizonShard
+
+        n, m, N = 12, 4, 96
+        E, c, H, h, x0 = _full(n, m, N, 2, 13)
+        dev = torch.device("cuda", 0)
+        sh = HorizonShard(n, m, N, 2, segment_len=8)
+        sh.set_model(*[torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (E, c, H, h)])
+        sh.update_problem_data(torch.zeros(2, N * (n + m) + n, dtype=torch.float64, device=dev), sigma=1e-6)
+        outs = []
+        from pdplqr.horizon import solve_distributed
+
+        for _ in range(2):
+            out = torch.full((2, N * (n + m) + n), float("nan"), dtype=torch.float64, device=dev)
+            solve_distributed(sh, torch.from_numpy(x0).to(dev), out)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+        q.put(outs)
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_single_rank_nccl_device_path():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(29300 + (os.getpid() % 400), q))
+    p.start()
+    outs = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    n, m, N = 12, 4, 96
+    E, c, H, h, x0 = _full(n, m, N, 2, 13)
+    ref = _oracle(n, m, N, E, c, H, h, x0)
+    for got in outs:
+        for b in range(2):
+            assert rel_err(got[b], ref[b]) < TOL, b
+    assert np.array_equal(outs[0], outs[1])
