@@ -446,46 +446,49 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
     return PDPLQR_OK;
 }
 
-// Combine a short list of elements on one wave (the per-rank fold of the
-// horizon-sharded solve): out_pre = e_0 (x) ... (x) e_{r-1} (identity if r = 0),
-// out_suf = e_{r+1} (x) ... (x) e_{R-1} (P = p = 0 marker when r = R-1).
+// Fold the all-gathered rank elements (horizon-sharded solve).  Block b
+// (< batch) folds the prefix out_pre = e_0 (x) ... (x) e_{r-1} of problem b
+// (identity if r = 0); block batch + b folds the suffix out_suf =
+// e_{r+1} (x) ... (x) e_{R-1}.  The two chains run concurrently, and each
+// combine forms only what its consumer reads: k_seg_maps maps x0 through the
+// prefix's (F, C, f) and right-folds the suffix's value function (P, p) into
+// the boundary value functions, and a right fold e_j (x) acc reads acc's
+// (P, p) only.  So the prefix chain skips the P path and the suffix chain the
+// F, C path; the unformed blocks are written as zeros.
 template <int T>
 __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int R, int r, int n, int batch,
                                                     double *out_pre_all, double *out_suf_all, int *has_suf, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     __shared__ CombSmem<T> sm;
     const int lane = wave_lane();
-    const int es = 3 * n * n + 2 * n;
-    const long long b = blockIdx.x;
+    const int es = 3 * n * n + 2 * n, nfcf = 2 * n * n + n;
+    const bool suffix = blockIdx.x >= (unsigned)batch;
+    const long long b = suffix ? blockIdx.x - batch : blockIdx.x;
     // element j of problem b: elems_all[(j * batch + b) * es]; outputs [b][es]
     const double *elems = elems_all + b * es;
     const long long stride = (long long)batch * es;
-    double *out_pre = out_pre_all + b * es, *out_suf = out_suf_all + b * es;
     double *acc = dyn, *nx = dyn + es, *o = dyn + 2 * es;
-    // prefix
-    {
-        Elem e = elem_view(acc, n);
-        for (int q = lane; q < n * n; q += 64) {
-            e.F[q] = (q % n == q / n) ? 1.0 : 0.0;
-            e.C[q] = 0.0;
-            e.P[q] = 0.0;
+    if (!suffix) {
+        double *out = out_pre_all + b * es;
+        if (r == 0) {
+            for (int q = lane; q < es; q += 64) out[q] = (q < n * n && q % n == q / n) ? 1.0 : 0.0;
+            return;
         }
-        for (int q = lane; q < n; q += 64) { e.f[q] = 0.0; e.p[q] = 0.0; }
+        elem_copy(acc, elems, n, lane);
         wave_sync();
-        for (int j = 0; j < r; ++j) {
+        for (int j = 1; j < r; ++j) {
             elem_copy(nx, elems + (long long)j * stride, n, lane);
             wave_sync();
-            if (j == 0) {
-                elem_copy(acc, nx, n, lane);
-            } else {
-                if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag + b, 4);
-                elem_copy(acc, o, n, lane);
-            }
+            if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag + b, 4);
             wave_sync();
+            double *t = acc;
+            acc = o;
+            o = t;
         }
-        elem_copy(out_pre, acc, n, lane);
+        for (int q = lane; q < es; q += 64) out[q] = q < nfcf ? acc[q] : 0.0;
+        return;
     }
-    // suffix (right fold from the end: e_{R-1}, then e_j (x) acc)
+    double *out = out_suf_all + b * es;
     if (r + 1 >= R) {
         if (lane == 0 && b == 0) *has_suf = 0;
         return;
@@ -495,11 +498,13 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     for (int j = R - 2; j > r; --j) {
         elem_copy(nx, elems + (long long)j * stride, n, lane);
         wave_sync();
-        if (!tcombine<T>(o, nx, acc, n, true, true, sm, lane) && lane == 0) atomicOr(flag + b, 8);
-        elem_copy(acc, o, n, lane);
+        if (!tcombine<T>(o, nx, acc, n, false, true, sm, lane) && lane == 0) atomicOr(flag + b, 8);
         wave_sync();
+        double *t = acc;
+        acc = o;
+        o = t;
     }
-    elem_copy(out_suf, acc, n, lane);
+    for (int q = lane; q < es; q += 64) out[q] = q < nfcf ? 0.0 : acc[q];
     if (lane == 0 && b == 0) *has_suf = 1;
 }
 
@@ -507,10 +512,10 @@ int launch_fold_shards(const double *elems, int R, int r, int n, int batch, doub
                        int *has_suf, int *flag, hipStream_t st) {
     const int T = tile_order(n);
     if (T == 1)
-        hipLaunchKernelGGL(k_fold_shards<1>, dim3(batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
+        hipLaunchKernelGGL(k_fold_shards<1>, dim3(2 * batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
                            out_pre, out_suf, has_suf, flag);
     else if (T == 2)
-        hipLaunchKernelGGL(k_fold_shards<2>, dim3(batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
+        hipLaunchKernelGGL(k_fold_shards<2>, dim3(2 * batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
                            out_pre, out_suf, has_suf, flag);
     else
         return PDPLQR_ERR_UNSUPPORTED;

@@ -128,16 +128,22 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     elem = torch.empty(shard.batch, shard.es, dtype=torch.float64, device=dev)
     if on_gpu:
-        # Run the slice on torch's current stream: ProcessGroupNCCL orders the
-        # all-gather after it and the stream after the all-gather, so the
-        # backward -> exchange -> forward chain needs no host round trip.
-        cur = torch.cuda.current_stream().cuda_stream
-        if shard.stream() != cur:
-            shard.synchronize()  # drain work queued on the previous stream
-            shard.handle.set_stream(cur)
+        # Device-side ordering between the handle's stream and torch's current
+        # stream (which ProcessGroupNCCL orders the all-gather against): events,
+        # no host round trip between backward, exchange and forward.
+        hs = torch.cuda.ExternalStream(shard.stream(), device=dev)
+        cur = torch.cuda.current_stream()
+        hs.wait_stream(cur)  # x0 / ws_out / rho produced on the current stream
+        elem.record_stream(hs)
         shard.backward(elem, rank == world - 1, rho)
+        cur.wait_stream(hs)
         gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(gathered, elem, group=group)
+        hs.wait_stream(cur)
+        gathered.record_stream(hs)
+        shard.forward(x0, gathered, world, rank, ws_out)
+        cur.wait_stream(hs)  # ws_out is read on the current stream
+        return ws_out
     else:
         e_np = np.zeros((shard.batch, shard.es))
         shard.backward(e_np, rank == world - 1, None if rho is None else rho)

@@ -133,8 +133,8 @@ def test_two_process_gloo_exchange():
 
 def _nccl_worker(port, q):
     """One rank on the RCCL backend: exercises solve_distributed's device path
-    (slice on torch's current stream, all-gather ordered by ProcessGroupNCCL,
-    no host synchronisation), twice, so the stream re-binding is also covered."""
+    (event ordering between the handle's stream and torch's current stream, no
+    host synchronisation), from the default stream and from a side stream."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -154,7 +154,9 @@ def _nccl_worker(port, q):
         outs = []
         from pdplqr.horizon import solve_distributed
 
-        for _ in range(2):
+        for it in range(2):  # torch's default stream, then a side stream
+            if it:
+                torch.cuda.set_stream(torch.cuda.Stream())
             out = torch.full((2, N * (n + m) + n), float("nan"), dtype=torch.float64, device=dev)
             solve_distributed(sh, torch.from_numpy(x0).to(dev), out)
             torch.cuda.synchronize()
