@@ -237,18 +237,19 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     const int es = 3 * n * n + 2 * n;
     const long long b = blockIdx.x / S;
     const int i = blockIdx.x % S;
-    const double *in = A.in + b * (long long)S * es;
+    const long long is = A.istride ? A.istride : es;
+    const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
     if (i + d >= S) {  // suf_i already reaches the last segment
-        elem_copy(out + (long long)i * es, in + (long long)i * es, n, lane);
+        elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
         return;
     }
     // The right operand covers segments [i + d, min(i + 2d - 1, S - 1)].  When
     // that range holds the real terminal its F = C = f = 0, and so are the
     // result's: only the value function (P, p) is combined.
     const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
-    const ElemIn ea = stage_left(ebuf, in + (long long)i * es, n, lane);
-    const ElemIn eb = stage_right(ebuf + op_stage_len(n), in + (long long)(i + d) * es, n, lane);
+    const ElemIn ea = stage_left(ebuf, in + (long long)i * is, n, lane);
+    const ElemIn eb = stage_right(ebuf + op_stage_len(n), in + (long long)(i + d) * is, n, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     double *o = out + (long long)i * es;
@@ -281,14 +282,15 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     const int es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
+    const double *right = A.right ? A.right + b * (A.rstride ? A.rstride : (long long)es) : nullptr;
     double *vo = A.vfun + (b * J + j) * (long long)mw;
     double *mo = A.maps + (b * J + j) * (long long)mw;
     bool ok = true;
     // V_j: [P | p] at vP, vp (global), or absent (j == S on the last shard)
     const double *vP = nullptr, *vp = nullptr;
-    if (j < S && A.right) {
+    if (j < S && right) {
         const ElemIn ea = stage_left(dyn, A.suf + (b * S + j) * (long long)es, n, lane);
-        const ElemIn eb = stage_right(dyn + op_stage_len(n), A.right + b * (long long)es, n, lane);
+        const ElemIn eb = stage_right(dyn + op_stage_len(n), right, n, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
         ok = tcombine_parts<T>(nullptr, nullptr, nullptr, vo, vo + nn, ea, eb, n, false, true, sm, lane);
@@ -296,8 +298,7 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
         vP = vo;
         vp = vo + nn;
     } else {
-        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : A.right ? A.right + b * (long long)es
-                                                                                  : nullptr;
+        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : right;
         if (src) {
             vP = src + 2 * nn + n;
             vp = src + 3 * nn + n;
@@ -506,6 +507,87 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     }
     for (int q = lane; q < es; q += 64) out[q] = q < nfcf ? 0.0 : acc[q];
     if (lane == 0 && b == 0) *has_suf = 1;
+}
+
+// Log-depth alternative of the prefix chain (pdplqr_shard_forward picks it
+// when it is shorter): with the rank suffix scan done (suf [b][R][es], entry
+// j = e_j (x) ... (x) e_{R-1}), the state at the start of rank j + 1's slice
+// follows from the state at the start of rank j's through the boundary map
+// of e_j under V_{j+1} = (P, p) of suffix entry j + 1 -- the same map as
+// k_seg_maps, Phi = Z F, phi = Z (f - C p), Z = (I + C P)^{-1}.  The r maps
+// of ranks j < r are formed in parallel (k_rank_maps); one wave applies them
+// to x0 in turn (k_rank_chain, matrix-vector products only) and writes the
+// prefix element (F = C = 0, f = x at the slice start), which k_seg_maps
+// maps to exactly that state.
+template <int T>
+__global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const double *suf, int R, int r, int n,
+                                                  int batch, double *maps, int *flag) {
+    __shared__ CombSmem<T> sm;
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / r;
+    const int j = blockIdx.x % r;
+    const double *src = elems_all + ((long long)j * batch + b) * es;  // e_j, rank-major all-gather
+    const double *v = suf + (b * R + j + 1) * (long long)es;           // V_{j+1}
+    WM<T> Fs, Cs, Y, Z, Zt, Phi;
+    WV<T> fs, pv, v1, phi;
+    wm_load(Fs, src, n, n, false, 0.0, g, c);
+    wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
+    wv_load(fs, src + 2 * nn, n, g, c);
+    const bool ok = comb_core(Y, Z, Zt, Cs, v + 2 * nn + n, n, sm, lane);
+    wv_load(pv, v + 3 * nn + n, n, g, c);
+    wv_tn(v1, Cs, pv, n, -1.0, &fs);                     // f - C p  (C symmetric)
+    wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p)
+    wm_tn(Phi, Zt, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Z F
+    double *mo = maps + (b * r + j) * (long long)mw;
+    wm_store(Phi, mo, n, n, g, c);
+    wv_store(phi, mo + nn, n, g, c);
+    if (!ok && lane == 0) atomicOr(flag + b, 4);
+}
+
+template <int T>
+__global__ __launch_bounds__(64) void k_rank_chain(const double *maps, const double *x0, int r, int n,
+                                                   double *out_pre_all) {
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x;
+    WV<T> x;
+    wv_load(x, x0 + b * n, n, g, c);
+    WM<T> PhiT;
+    WV<T> phi;
+    wm_load(PhiT, maps + b * r * (long long)mw, n, n, true, 0.0, g, c);
+    wv_load(phi, maps + b * r * (long long)mw + nn, n, g, c);
+    for (int j = 0; j < r; ++j) {
+        WV<T> y;
+        wv_tn(y, PhiT, x, n, 1.0, &phi);  // x <- Phi_j x + phi_j
+        x = y;
+        if (j + 1 < r) {  // the next map's loads do not depend on x
+            const double *mo = maps + (b * r + j + 1) * (long long)mw;
+            wm_load(PhiT, mo, n, n, true, 0.0, g, c);
+            wv_load(phi, mo + nn, n, g, c);
+        }
+    }
+    double *out = out_pre_all + b * es;
+    for (int q = lane; q < es; q += 64)
+        if (q < 2 * nn || q >= 2 * nn + n) out[q] = 0.0;
+    wv_store(x, out + 2 * nn, n, g, c);
+}
+
+int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
+                          double *maps, double *out_pre, int *flag, hipStream_t st) {
+    if (r <= 0) return PDPLQR_OK;
+    const int T = tile_order(n);
+    if (T == 1) {
+        hipLaunchKernelGGL(k_rank_maps<1>, dim3(batch * r), dim3(64), 0, st, elems, suf, R, r, n, batch, maps, flag);
+        hipLaunchKernelGGL(k_rank_chain<1>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
+    } else if (T == 2) {
+        hipLaunchKernelGGL(k_rank_maps<2>, dim3(batch * r), dim3(64), 0, st, elems, suf, R, r, n, batch, maps, flag);
+        hipLaunchKernelGGL(k_rank_chain<2>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
+    } else {
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
 }
 
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,

@@ -21,6 +21,7 @@ struct ScanArgs {
     int n, S, dist;
     int terminal;              // the last element ends at the real terminal (F = C = f = 0)
     const double *in;          // suffix scan ping-pong [b][S][es]
+    long long istride = 0, bstride = 0;  // element / problem strides of `in` (0: [b][S][es])
     double *out;
     int *flag;                 // [b]: a combine was not positive definite
 };
@@ -31,6 +32,7 @@ struct MapArgs {
     const double *suf;         // inclusive suffix scan [b][S][es]
     const double *left;        // optional global prefix element [b][es] (horizon shards)
     const double *right;       // optional global suffix element [b][es]
+    long long rstride = 0;     // problem stride of `right` (0: es)
     const double *x0;          // [b][n]
     double *maps;              // [b][S+1][n^2 + n]  boundary maps (Phi | phi)
     double *vfun;              // [b][S+1][n^2 + n]  value functions at the boundaries (P | p)
@@ -63,6 +65,8 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, hipStream_t st);
+int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
+                          double *maps, double *out_pre, int *flag, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st);
 

@@ -28,6 +28,8 @@ struct ParallelState {
     // horizon shards
     double *left = nullptr, *right = nullptr, *gathered = nullptr;
     int gathered_cap = 0;
+    double *rscan[2] = {nullptr, nullptr}, *rmaps = nullptr;  // rank suffix scan, rank maps
+    int rcap = 0;
     int *has_suf = nullptr;
 };
 
@@ -245,7 +247,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
 // condensed forward: boundary maps under the suffix value functions, their
 // prefix composition (ceil(log2 (S + 1)) rounds), then the segment rollouts
 static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const double *left, const double *right,
-                            int last_is_terminal) {
+                            int last_is_terminal, long long rstride = 0) {
     ParallelState *ps = h->par;
     const Shape &sh = h->sh;
     MapArgs ma;
@@ -255,6 +257,7 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     ma.suf = ps->suf_final;
     ma.left = left;
     ma.right = right;
+    ma.rstride = rstride;
     ma.x0 = x0;
     ma.maps = ps->mapA;
     ma.vfun = ps->vfun;
@@ -534,13 +537,65 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
         delems = ps->gathered;
         dx0 = h->st_x0;
     }
-    int rc = launch_fold_shards(delems, num_shards, shard_id, sh.n, sh.batch, ps->left, ps->right, ps->has_suf,
+    // Fold of the gathered rank elements.  Chain (k_fold_shards): the longer of
+    // the prefix / suffix chains, max(r - 1, R - r - 2) sequential combines.
+    // Scan: the rank suffix scan (ceil(log2 R) rounds of k_seg_scan, every
+    // suffix entry) plus, for r > 0, the rank boundary maps (one combine-sized
+    // round) and their matrix-vector chain.  The shorter one runs;
+    // PDPLQR_SHARD_FOLD=chain|scan forces one (diagnostics and tests).
+    const int R = num_shards, r = shard_id;
+    int lgR = 0;
+    while ((1 << lgR) < R) ++lgR;
+    bool use_scan = lgR + (r > 0 ? 1 : 0) < std::max(r - 1, R - r - 2);
+    if (const char *f = getenv("PDPLQR_SHARD_FOLD")) use_scan = R > 1 && f[0] == 's';
+    int rc;
+    const double *left = nullptr, *right = nullptr;
+    long long rstride = 0;
+    if (use_scan) {
+        if (ps->rcap < R) {
+            if ((rc = palloc(h, &ps->rscan[0], (long long)sh.batch * R * es)) ||
+                (rc = palloc(h, &ps->rscan[1], (long long)sh.batch * R * es)) ||
+                (rc = palloc(h, &ps->rmaps, (long long)sh.batch * R * (sh.n * sh.n + sh.n))))
+                return rc;
+            ps->rcap = R;
+        }
+        const double *sin = delems;
+        int round = 0;
+        for (int d = 1; d < R; d <<= 1, ++round) {
+            ScanArgs sa;
+            sa.n = sh.n;
+            sa.S = R;
+            sa.dist = d;
+            sa.terminal = 1;  // the last rank's element ends at the real terminal
+            sa.in = sin;
+            if (round == 0) {  // rank-major all-gather layout [R][batch][es]
+                sa.istride = (long long)sh.batch * es;
+                sa.bstride = es;
+            }
+            sa.out = ps->rscan[round & 1];
+            sa.flag = ps->flag;
+            if ((rc = launch_seg_scan(sa, sh.batch, h->stream))) return rc;
+            sin = sa.out;
+        }
+        if (r + 1 < R) {
+            right = sin + (long long)(r + 1) * es;
+            rstride = (long long)R * es;
+        }
+        if (r > 0) {
+            if ((rc = launch_rank_fold_maps(delems, sin, dx0, R, r, sh.n, sh.batch, ps->rmaps, ps->left, ps->flag,
+                                            h->stream)))
+                return rc;
+            left = ps->left;
+        }
+    } else {
+        rc = launch_fold_shards(delems, num_shards, shard_id, sh.n, sh.batch, ps->left, ps->right, ps->has_suf,
                                 ps->flag, h->stream);
-    if (rc) return rc;
-    const double *left = shard_id > 0 ? ps->left : nullptr;
-    const double *right = shard_id + 1 < num_shards ? ps->right : nullptr;
+        if (rc) return rc;
+        left = shard_id > 0 ? ps->left : nullptr;
+        right = shard_id + 1 < num_shards ? ps->right : nullptr;
+    }
     double *dws = mem == PDPLQR_MEM_DEVICE ? ws : h->st_ws;
-    if ((rc = parallel_forward(h, dx0, dws, left, right, h->shard_last))) return rc;
+    if ((rc = parallel_forward(h, dx0, dws, left, right, h->shard_last, rstride))) return rc;
     if (mem != PDPLQR_MEM_DEVICE) {
         PDPLQR_HIP_TRY(hipMemcpyAsync(ws, dws, (size_t)sh.batch * sh.perh * sizeof(double), hipMemcpyDeviceToHost,
                                       h->stream));

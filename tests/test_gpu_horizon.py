@@ -83,6 +83,20 @@ def test_virtual_ranks_match_oracle(n, m, N, batch, R, seglen):
         assert rel_err(got[b], ref[b]) < TOL, b
 
 
+@pytest.mark.parametrize("fold", ["scan", "chain"])
+@pytest.mark.parametrize("n,m,N,batch,R,seglen", [(12, 4, 200, 2, 3, 7), (12, 4, 320, 3, 8, 8),
+                                                  (24, 8, 128, 1, 8, 4), (24, 8, 150, 2, 5, 6),
+                                                  (4, 2, 60, 2, 6, 3)])
+def test_virtual_ranks_fold_variants(n, m, N, batch, R, seglen, fold, monkeypatch):
+    """Both folds of the gathered rank elements (PDPLQR_SHARD_FOLD): the
+    sequential prefix / suffix chains and the log-depth rank suffix scan with
+    rank boundary maps (rank-major strides exercised by batch > 1)."""
+    monkeypatch.setenv("PDPLQR_SHARD_FOLD", fold)
+    got, ref = _run_virtual(n, m, N, batch, R, seglen, seed=5)
+    for b in range(batch):
+        assert rel_err(got[b], ref[b]) < TOL, b
+
+
 def _dist_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
