@@ -249,6 +249,44 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
             "scaling": "strong", "finite": ok, "exchange": "all-gather of 3n^2+2n doubles per rank"}
 
 
+def bench_end_to_end(bs, E, c, H, h, x0, ws0, out, dev, dist, local, steps=3, warmup=1, host_batch=256):
+    """the solve with what the timed step leaves out.
+    device_resident: update_problem_data + backward + forward on the bench
+    workload (model resident in HBM).  host_pcie: a host-memory caller on a
+    sub-batch of the same problems -- set_model from pageable host arrays (H2D of
+    E, c, H, h), update_problem_data from host ws, backward, forward into host
+    ws (D2H): the PCIe-inclusive rate (never the headline value)."""
+    from pdplqr import BatchedLQRSolver
+
+    B, N = ws0.shape[0], bs.N
+    n, m = bs.n, bs.m
+
+    def dev_step():
+        bs.update_problem_data(ws0, sigma=1e-6)
+        bs.backward()
+        bs.forward(x0, out)
+
+    t_dev = _timed(dev_step, steps, warmup, dev, dist)
+    Bh = min(host_batch, B)
+    Eh, ch, Hh, hh, x0h = (t[:Bh].cpu().numpy() for t in (E, c, H, h, x0))
+    wsh = np.zeros((Bh, ws0.shape[1]))
+    outh = np.empty_like(wsh)
+    hs = BatchedLQRSolver(n, m, N, Bh, keep_factors=False, device=local)
+
+    def host_step():
+        hs.set_model(Eh, ch, Hh, hh)
+        hs.update_problem_data(wsh, sigma=1e-6)
+        hs.backward()
+        hs.forward(x0h, outh)
+
+    t_host = _timed(host_step, steps, warmup, dev, dist)
+    hs.close()
+    return {"device_resident": {"ms_per_solve": t_dev * 1e3, "stages_per_s": N * B / t_dev,
+                                "includes": "update_problem_data + backward + forward"},
+            "host_pcie": {"batch": Bh, "ms_per_solve": t_host * 1e3, "stages_per_s": N * Bh / t_host,
+                          "includes": "set_model H2D + update_problem_data + backward + forward + ws D2H"}}
+
+
 def bwd_kernel_name(n, m, keep):
     """The backward kernel the C ABI dispatches for this shape (kernels_schur.hip /
     kernels_riccati.hip launch_riccati_backward)."""
@@ -306,7 +344,9 @@ def main():
     out = torch.empty_like(ws0)
     bs = BatchedLQRSolver(n, m, N, B, keep_factors=args.keep_factors, device=local)
     bs.set_model(E, c, H, h)
-    del H  # the handle holds its own copy
+    # the handle holds its own copy; a sub-batch is kept for the host-memory (PCIe) line
+    Hk = H[:256].clone() if not args.no_secondary else None
+    del H
     bs.update_problem_data(ws0, sigma=1e-6)
     bs.synchronize()
     stream = torch.cuda.ExternalStream(bs.handle.stream(), device=dev)
@@ -373,8 +413,10 @@ def main():
         "solve_hbm_frac": bytes_stage * stages / ((ms_bwd + ms_fwd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "status_ok": bool(np.all(st == 0)),
     }
+    if not args.no_secondary:
+        res["end_to_end"] = bench_end_to_end(bs, E, c, Hk, h, x0, ws0, out, dev, dist, local)
     bs.close()
-    del E, c, h, x0, ws0, out
+    del E, c, h, x0, ws0, out, Hk
     torch.cuda.empty_cache()
     if not args.no_secondary:
         res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),

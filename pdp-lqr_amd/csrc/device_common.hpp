@@ -94,12 +94,23 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // prefetch.  Callers own the vmcnt accounting (loads retire in issue order).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; it is only live inside this asm
+// PDPLQR_NT_STREAM=1: once-read stage records carry the non-temporal hint
+// (MI355X_MICROARCH.md nt-weights: issued -> landed about 18 % shorter).
+#ifndef PDPLQR_NT_STREAM
+#define PDPLQR_NT_STREAM 0
+#endif
+#if PDPLQR_NT_STREAM
+#define PDPLQR_NT_SUFFIX " nt"
+#else
+#define PDPLQR_NT_SUFFIX ""
+#endif
+
 __device__ __forceinline__ void dma16(const void *src, const void *lds_dst) {
     const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)lds_dst;
     asm volatile(
         "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, off" ::"v"(src),
+        "global_load_lds_dwordx4 %0, off" PDPLQR_NT_SUFFIX ::"v"(src),
         "s"(__builtin_amdgcn_readfirstlane(base))
         : "memory", "m0");
 }

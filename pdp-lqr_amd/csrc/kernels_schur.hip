@@ -344,7 +344,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
                 // issued through asm: the compiler's waitcnt pass would otherwise
                 // wait for every outstanding load at the first use (its loop
                 // model merges the guarded loads); the waits are explicit below
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[q]) : "v"(src) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off" PDPLQR_NT_SUFFIX : "=v"(R[q]) : "v"(src) : "memory");
             }
         };
         // R's loads have landed once at most `after` younger vm ops are
