@@ -21,6 +21,8 @@
 // The factor cache (keep_factors = 1, needed by backward_without_factorization
 // and get_value_function) still takes the full-factor kernels.
 #include "combine_tiles.hpp"
+#include <type_traits>
+
 #include "device_common.hpp"
 
 #include <stdint.h>
@@ -154,9 +156,9 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
 // after the m u-pivots (trailing block P_k, u columns unscaled L).  prow:
 // p~ in row layout (prow[r] = p[4 r + g - m] on x rows).
-template <int MM>
+template <int MM, bool SYM = true>
 __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const SchurIn &in, SchurSmem &sm, int m,
-                                            int s, int g, int c, double &w, double (&luq)[4]) {
+                                            int s, int g, int c, double &w, double (&luq)[4], bool sym_rt = true) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks that hold x rows
     d4 G = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -200,12 +202,17 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
     // P_k <- (P_k + P_k^T) / 2.  The square-root recursion is symmetric by
     // construction; here the rounding-level antisymmetric part of M_k would
     // otherwise be carried as A^T e A from stage to stage and grow with the
-    // open-loop dynamics (the next stage reads P's registers as P^T).
+    // open-loop dynamics (the next stage reads P's registers as P^T).  It
+    // grows by ~||A||^2 per stage, so resetting it every few stages (SYM on a
+    // subset of the stages, PDPLQR_SYM_EVERY) keeps it at rounding level while
+    // the LDS round trip leaves the other stages' chains.
+    if (SYM && sym_rt) {  // wave-uniform
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sm.tp[(4 * r + g) * 17 + c] = Pm[r];
-    wave_sync();
+        for (int r = 0; r < 4; ++r) sm.tp[(4 * r + g) * 17 + c] = Pm[r];
+        wave_sync();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * 17 + 4 * r + g]);
+        for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * 17 + 4 * r + g]);
+    }
     // P_k = Lxx Lxx^T has a positive diagonal whenever M_k is positive definite
     bool bad = false;
 #pragma unroll
@@ -276,6 +283,14 @@ struct SchurShape {
     static constexpr int CH = Q / 2, NI = (CH + 63) / 64;
     static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && s % 2 == 0 && ps % 2 == 0 && s <= 16;
 };
+
+// Symmetrise P every PDPLQR_SYM_EVERY stages (1, 2 or 4) on the compile-time
+// shape path; the runtime-shape path symmetrises every stage.
+#ifndef PDPLQR_SYM_EVERY
+#define PDPLQR_SYM_EVERY 4
+#endif
+using SymOn = std::integral_constant<bool, true>;
+using SymOff = std::integral_constant<bool, false>;
 
 #ifndef PDPLQR_SCHUR_WAVES
 #define PDPLQR_SCHUR_WAVES 4
@@ -369,12 +384,13 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // so "X's loads have landed" is always vmcnt(5) -- the other set's 3
         // loads and two stores are younger; the first step follows the
         // prologue (3 loads + 1 store: vmcnt(4)).
-        auto step = [&](int k, d2v(&X)[NI], bool first) {  // X: stage k - 1 on entry, k - 3 on exit
+        auto step = [&](int k, d2v(&X)[NI], bool first, auto sym, bool sym_rt) {  // X: stage k - 1 on entry, k - 3 on exit
             const double *R = stg[k & 1];
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
             double w, luq[4];
-            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0>(Pm, prow, in, sm, m, s, g, c, w, luq);
+            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value>(Pm, prow, in, sm, m, s,
+                                                                                              g, c, w, luq, sym_rt);
             if (!ok && fail_stage < 0) fail_stage = k;
             if (PDPLQR_SCHUR_BLOCK) schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
             else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
@@ -391,13 +407,16 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         gload(RA, N >= 2 ? N - 2 : 0);
         gload(RB, N >= 3 ? N - 3 : 0);
         wave_sync();
-        step(N - 1, RA, true);
+        // pairs (k, k - 1): the pair head symmetrises (every pair head for
+        // PDPLQR_SYM_EVERY = 2, every other one for 4), the second stage only
+        // when PDPLQR_SYM_EVERY = 1
+        step(N - 1, RA, true, SymOn{}, true);
         int k = N - 2;
         for (; k >= 1; k -= 2) {
-            step(k, RB, false);
-            step(k - 1, RA, false);
+            step(k, RB, false, SymOn{}, PDPLQR_SYM_EVERY < 4 || ((N - 2 - k) & 2) == 0);
+            step(k - 1, RA, false, std::integral_constant<bool, (PDPLQR_SYM_EVERY <= 1)>{}, true);
         }
-        if (k == 0) step(0, RB, false);
+        if (k == 0) step(0, RB, false, SymOn{}, true);
         vwait0(RA);  // nothing in flight may land in reused registers
         vwait0(RB);
     } else {

@@ -94,8 +94,9 @@ def test_value_form_backward_matches_golden(name):
     assert rel_err(u_parts(w, n, m, N), u_parts(d["w_riccati"], n, m, N)) < 1e-6
 
 
-@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 200, 5), (12, 4, 7, 3), (12, 4, 1, 2), (12, 4, 2, 3), (12, 4, 3, 2), (5, 3, 40, 4), (1, 1, 30, 2), (13, 3, 25, 3),
-                                         (8, 8, 20, 2), (3, 5, 17, 3)])
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 200, 5), (12, 4, 7, 3), (12, 4, 1, 2), (12, 4, 2, 3), (12, 4, 3, 2),
+                                         (12, 4, 4, 2), (12, 4, 5, 2), (12, 4, 6, 2), (12, 4, 9, 2), (12, 4, 10, 2),
+                                         (5, 3, 40, 4), (1, 1, 30, 2), (13, 3, 25, 3), (8, 8, 20, 2), (3, 5, 17, 3)])
 def test_value_form_batched_shapes(n, m, N, batch):
     """Both value-form variants (LDS-DMA 12/4 and runtime shape) against the oracle."""
     from oracle.oracle import OracleSerial
@@ -148,6 +149,42 @@ def test_backward_without_factorization(name):
     o.update_problem_data(ws2, d["ys"], zs2, d["inv_rho"], float(d["sigma"]))
     o.backward_without_factorization(d["rho"])
     assert rel_err(np.concatenate(out), o.forward(d["x0"])) < TOL
+
+
+@pytest.mark.parametrize("spread", [0.1, 0.3])
+def test_value_form_symmetrisation_long_horizon(spread):
+    """The value-form backward resets the rounding-level antisymmetric part of
+    P every few stages (kernels_schur.hip, PDPLQR_SYM_EVERY); without any reset
+    it grows with the open-loop dynamics (1e-8 at N = 200, NaN at N = 1024).
+    Stronger dynamics (A = I + spread * N(0, 1)) at N = 1024 against the oracle."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 1024, 3
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 2024)
+    if spread != 0.1:  # rescale the A blocks' off-identity part (E = [B A], column-major n x s)
+        Eb = E.reshape(batch, N, s, n)
+        Eb[:, :, m:, :] = np.eye(n) + (Eb[:, :, m:, :] - np.eye(n)) * (spread / 0.1)
+        E = np.ascontiguousarray(Eb.reshape(batch, N * n * s))
+    ws0 = np.zeros((batch, N * s + n))
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws0)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        ref = o.forward(x0[b])
+        assert np.all(np.isfinite(out[b]))
+        assert rel_err(out[b], ref) < TOL, b
 
 
 def _batched_case(n, m, N, batch, seed, device_buffers=False, keep=False):
