@@ -220,7 +220,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
         const int i = 4 * r + g;
         if (i == c && i >= m && i < s && !(Pm[r] > 0.0)) bad = true;
     }
-    return ok && !__any(bad);
+    return (int)ok & (int)!__any(bad);  // no short-circuit: no branch
 }
 
 // Rollout record FR_k = [L(:, 0:m) | lu'] (same format as the full-factor path).
@@ -346,16 +346,26 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // LDS-DMA ring had one step, ~3.5 us, which left the HBM latency
         // exposed at 4 waves per SIMD.)
         d2v RA[NI], RB[NI];
+        // per-lane stage-0 address and stage stride of each 16-byte chunk,
+        // fixed for the whole horizon: the loop only forms base + k stride
+        // (selecting the source array per stage made divergent branches)
+        const double *gbase[NI];
+        int gstride[NI];
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            int ch = q * 64 + lane;
+            ch = ch < SH::CH ? ch : SH::CH - 1;
+            const int d = 2 * ch;
+            gbase[q] = d < SH::OC   ? Eb + d
+                       : d < SH::OH ? cb + (d - SH::OC)
+                       : d < SH::OP ? hb + (d - SH::OH)
+                                    : Hb + (d - SH::OP);
+            gstride[q] = d < SH::OC ? SH::n * SH::s : d < SH::OH ? SH::n : d < SH::OP ? SH::s : SH::ps;
+        }
         auto gload = [&](d2v(&R)[NI], int k) {
 #pragma unroll
             for (int q = 0; q < NI; ++q) {
-                int ch = q * 64 + lane;
-                ch = ch < SH::CH ? ch : SH::CH - 1;
-                const int d = 2 * ch;
-                const double *src = d < SH::OC   ? Eb + (long long)k * SH::n * SH::s + d
-                                    : d < SH::OH ? cb + (long long)k * SH::n + (d - SH::OC)
-                                    : d < SH::OP ? hb + (long long)k * SH::s + (d - SH::OH)
-                                                 : Hb + (long long)k * SH::ps + (d - SH::OP);
+                const double *src = gbase[q] + (long long)k * gstride[q];
                 // issued through asm: the compiler's waitcnt pass would otherwise
                 // wait for every outstanding load at the first use (its loop
                 // model merges the guarded loads); the waits are explicit below
@@ -391,7 +401,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             double w, luq[4];
             const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value>(Pm, prow, in, sm, m, s,
                                                                                               g, c, w, luq, sym_rt);
-            if (!ok && fail_stage < 0) fail_stage = k;
+            fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
             if (PDPLQR_SCHUR_BLOCK) schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
             else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
             wave_sync();  // stage k's LDS reads retire before slot reuse
