@@ -232,6 +232,88 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, d4 (&B)[T][TB], int n_rt, 
     return ok;
 }
 
+// Blocked Cholesky of a full symmetric 16 x 16 tile M = C C^T (both
+// triangles held, as MFMA products leave them), carrying TB column tiles:
+// B <- C^{-1} B (final, no row scaling left).  Four pivots per block:
+//   - the 4 x 4 diagonal block reaches every lane by readlane; its Cholesky
+//     factor and inverse T4 are formed wave-uniformly;
+//   - the panel V (lane (g, c) = C[c][j0 + g]) comes from the block's own ROW
+//     (register blk of the row groups, the symmetric image of the column) by
+//     four row-group broadcasts, masked to the trailing rows c >= j0 + 4;
+//   - the trailing updates are ONE MFMA per tile: M -= V V^T and
+//     B -= V (T4 B_block), whose B operand is the block's register itself.
+// Against one pivot at a time (elim_regs) the dependent chain per pivot shrinks
+// to a quarter of the broadcasts and rank-1 updates.  False if a pivot is not
+// positive.  M is left stale (only B is an output).
+template <int TB>
+__device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) {
+    bool ok = true;
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+        const int j0 = 4 * blk;
+        double a[4][4], L[4][4], T[4][4], inv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k) a[i][k] = readlane_f64(M[blk], 16 * i + j0 + k);  // M[j0+i][j0+k]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // right-looking Cholesky (uniform values)
+            ok = ok && (a[j][j] > 0.0);
+            inv[j] = rsqrt_f64(a[j][j]);
+            L[j][j] = a[j][j] * inv[j];
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i) L[i][j] = a[i][j] * inv[j];
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i)
+#pragma unroll
+                for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-L[i][j], L[k][j], a[i][k]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // T = L^{-1} (lower)
+            T[i][i] = inv[i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int k = j; k < i; ++k) v = __builtin_fma(L[i][k], T[k][j], v);
+                T[i][j] = -v * inv[i];
+            }
+        }
+        // row-block values M[j0 + k][c] (register blk, row group k) -> V
+        double ml[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ml[k] = bcast_group(M[blk], k);
+        double v = 0.0;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k <= jj; ++k) s = __builtin_fma(T[jj][k], ml[k], s);
+            v = (g == jj) ? s : v;
+        }
+        const double vt = (c >= j0 + 4) ? v : 0.0;  // trailing rows only
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) {  // block rows of B: T4 B_block (in place, register blk)
+            double bl[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bl[k] = bcast_group(B[tb][blk], k);
+            double s4 = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k <= jj; ++k) s = __builtin_fma(T[jj][k], bl[k], s);
+                s4 = (g == jj) ? s : s4;
+            }
+            B[tb][blk] = s4;
+        }
+        if (blk < 3) M = mfma_f64(-vt, vt, M);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) B[tb] = mfma_f64(-vt, B[tb][blk], B[tb]);
+    }
+    return ok;
+}
+
 // The pivot count stays a runtime bound: compile-time counts for several n
 // (straight-line copies, 170 KB for the scan kernel) measured 5x slower --
 // instruction fetch from L2 once the kernel outgrows the instruction cache.

@@ -454,6 +454,12 @@ __global__ void k_kkt_bvec16(KKTArgs A, double *__restrict__ bvec) {
 // Every group is eliminated over all 16 pivots: the padding is the identity
 // (exact no-op pivots) and X's padding is zero, so the loop reads no group
 // dimensions -- only two tiles and the y diagonal, loaded two groups ahead.
+// PDPLQR_KKT_BLK4: the per-group factorisation as 4-pivot blocks with MFMA
+// trailing updates (chol_blk4_aug) instead of 16 single pivots (elim_regs).
+#ifndef PDPLQR_KKT_BLK4
+#define PDPLQR_KKT_BLK4 1
+#endif
+
 __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ dpk,
                                                      const double *__restrict__ dreg) {
     const Shape &sh = A.sh;
@@ -492,15 +498,22 @@ __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__
         else M = D;
 #pragma unroll
         for (int r = 0; r < 4; ++r) B[0][1][r] = (4 * r + g == c) ? 1.0 : 0.0;
+        d4 Linv;
+#if PDPLQR_KKT_BLK4
+        const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);  // B <- C^{-1} B, final
+        if (!ok && !fail) fail = k + 1;
+        X.t[0][0] = B[0][0];
+        Linv = B[0][1];
+#else
         double colinv[1], rowinv[1][4];
         const bool ok = elim_regs<1, true, 2>(M, B, 16, colinv, rowinv, g, c);
         if (!ok && !fail) fail = k + 1;
-        d4 Linv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             X.t[0][0][r] = B[0][0][r] * rowinv[0][r];
             Linv[r] = B[0][1][r] * rowinv[0][r];
         }
+#endif
         double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
         tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1} = L_{k+1,k}^T
         tn_store(fk + 512, lane, Linv);       // Lkk^{-1}
