@@ -314,6 +314,107 @@ __device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) 
     return ok;
 }
 
+// chol_blk4_aug generalised to T x T tiles and a runtime order n (identity
+// padding past n; blocks past ceil(n / 4) are skipped as exact no-ops).
+// AUG: carries TB column tiles, B <- C^{-1} B (final); M is left stale.
+// !AUG: M <- C^T, the transposed factor (upper triangle, zeros below,
+// identity padding kept): each block's ROW of C^T is exactly its panel V.
+template <int T, bool AUG, int TB>
+__device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g, int c) {
+    bool ok = true;
+    const int nb = (n + 3) >> 2;
+#pragma unroll
+    for (int blk = 0; blk < 4 * T; ++blk) {
+        if (blk >= nb) break;  // wave-uniform
+        const int tj = blk >> 2, rj = blk & 3, cj = 4 * rj, j0 = 4 * blk;
+        double a[4][4], L[4][4], Ti[4][4], inv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k) a[i][k] = readlane_f64(M.t[tj][tj][rj], 16 * i + cj + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ok = ok && (a[j][j] > 0.0);
+            inv[j] = rsqrt_f64(a[j][j]);
+            L[j][j] = a[j][j] * inv[j];
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i) L[i][j] = a[i][j] * inv[j];
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i)
+#pragma unroll
+                for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-L[i][j], L[k][j], a[i][k]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            Ti[i][i] = inv[i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int k = j; k < i; ++k) v = __builtin_fma(L[i][k], Ti[k][j], v);
+                Ti[i][j] = -v * inv[i];
+            }
+        }
+        double vt[T];
+#pragma unroll
+        for (int ta = 0; ta < T; ++ta) {
+            vt[ta] = 0.0;
+            if (ta < tj) continue;
+            double ml[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ml[k] = bcast_group(M.t[tj][ta][rj], k);  // M[j0 + k][16 ta + c]
+            double v = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k <= jj; ++k) s = __builtin_fma(Ti[jj][k], ml[k], s);
+                v = (g == jj) ? s : v;
+            }
+            const int col = 16 * ta + c;
+            vt[ta] = (col >= j0 + 4) ? v : 0.0;  // trailing rows of the panel
+            if (!AUG) M.t[tj][ta][rj] = (col >= j0) ? v : 0.0;  // row block of C^T, final
+        }
+        if (AUG) {
+#pragma unroll
+            for (int tb = 0; tb < TB; ++tb) {  // block rows of B: T4 B_block (register rj of tile row tj)
+                double bl[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) bl[k] = bcast_group(B[tj][tb][rj], k);
+                double s4 = 0.0;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int k = 0; k <= jj; ++k) s = __builtin_fma(Ti[jj][k], bl[k], s);
+                    s4 = (g == jj) ? s : s4;
+                }
+                B[tj][tb][rj] = s4;
+            }
+        }
+#pragma unroll
+        for (int ta = 0; ta < T; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < T; ++tb)
+                if (ta >= tj && tb >= tj) M.t[ta][tb] = mfma_f64(-vt[ta], vt[tb], M.t[ta][tb]);
+        if (AUG)
+#pragma unroll
+            for (int ta = 0; ta < T; ++ta)
+#pragma unroll
+                for (int tb = 0; tb < TB; ++tb)
+                    if (ta >= tj) B[ta][tb] = mfma_f64(-vt[ta], B[tj][tb][rj], B[ta][tb]);
+    }
+    if (!AUG)
+#pragma unroll
+        for (int ta = 0; ta < T; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < T; ++tb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (16 * ta + 4 * r + g > 16 * tb + c) M.t[ta][tb][r] = 0.0;
+    return ok;
+}
+
 // The pivot count stays a runtime bound: compile-time counts for several n
 // (straight-line copies, 170 KB for the scan kernel) measured 5x slower --
 // instruction fetch from L2 once the kernel outgrows the instruction cache.
@@ -345,6 +446,10 @@ __device__ __forceinline__ bool wm_chol_regs(WM<T> &M, int n, int g, int c) {
 //     R = chol(P_b), S = I + R^T C_a R = Q Q^T, U = Q^{-1} R^T, Y = U^T U
 // U comes out of the elimination of S carrying R^T as extra columns (row i
 // scaled by 1/sqrt(d_i) at the end), so no triangular solve is needed.
+#ifndef PDPLQR_COMB_BLK4
+#define PDPLQR_COMB_BLK4 1
+#endif
+
 template <int T>
 __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
                                           CombSmem<T> &sm, int lane) {
@@ -352,6 +457,23 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     const int g = lane >> 4, c = lane & 15;
     WM<T> R, S, U;
     COMB_MARK(1);
+#if PDPLQR_COMB_BLK4
+    // blocked factors (chol_blk4): R^T comes out directly, R through LDS
+    wm_load(U, Pb, n, n, false, 1.0, g, c);
+    bool ok = chol_blk4<T, false, T>(U, U.t, n, g, c);  // U = R^T
+    wm_store(U, sm.B, PL, n, g, c);
+    wave_sync();
+    wm_load(R, sm.B, PL, n, true, 1.0, g, c);
+    COMB_MARK(2);
+    {
+        WM<T> T1;
+        wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
+        wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
+    }
+    COMB_MARK(3);
+    ok = chol_blk4<T, true, T>(S, U.t, n, g, c) && ok;  // U = Q^{-1} R^T
+    COMB_MARK(4);
+#else
     wm_load(R, Pb, n, n, false, 1.0, g, c);
     bool ok = wm_chol_regs(R, n, g, c);
     COMB_MARK(2);
@@ -374,6 +496,7 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
 #pragma unroll
             for (int r = 0; r < 4; ++r) U.t[a][b][r] *= rowinv[a][r];
     COMB_MARK(4);
+#endif
     COMB_MARK(5);
     wm_tn(Y, U, U, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Y = U^T U
     wm_tn(Z, Ca, Y, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z = I - C_a Y
