@@ -83,6 +83,20 @@ __device__ __forceinline__ void wm_store(const WM<T> &M, double *p, int ld, int 
             }
 }
 
+// p <- M^T (n x n block, column-major, leading dimension n)
+template <int T>
+__device__ __forceinline__ void wm_store_t(const WM<T> &M, double *p, int n, int g, int c) {
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g, j = 16 * b + c;
+                if (i < n && j < n) p[j + i * n] = M.t[a][b][r];
+            }
+}
+
 // C = sgn X^T Y + diag I (+ add); only the K chunks that hold rows < n
 template <int T>
 __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, int n, double sgn, double diag,

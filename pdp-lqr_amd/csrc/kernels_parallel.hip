@@ -400,6 +400,57 @@ __global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
     wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
 }
 
+// Radix-4 form of the same composition (PDPLQR_MAP_RADIX = 4): one round of
+// distance d composes m_j with m_{j-d}, m_{j-2d}, m_{j-3d} in turn, stopping at
+// the first anchored partner (index < d), so after the round the entries
+// j < 4 d are anchored: ceil(log4 (S + 1)) launches instead of
+// ceil(log2 (S + 1)), each at most three products in sequence.  The running
+// map is kept transposed (Phi^T), the form the matrix-vector product reads.
+template <int T>
+__global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const int n = A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    const double *in = A.in + b * (long long)J * mw;
+    double *out = A.out + b * (long long)J * mw;
+    if (j < d) {  // anchored earlier: keep x_j for this round's partners
+        for (int q = lane; q < n; q += 64) out[(long long)j * mw + nn + q] = in[(long long)j * mw + nn + q];
+        return;
+    }
+    WM<T> PaccT;
+    WV<T> pacc;
+    wm_load(PaccT, in + (long long)j * mw, n, n, true, 0.0, g, c);
+    wv_load(pacc, in + (long long)j * mw + nn, n, g, c);
+#pragma unroll 1
+    for (int k = 1; k <= 3; ++k) {
+        const int ia = j - k * d;  // >= 0: the previous partner was not anchored (>= d)
+        const double *ea = in + (long long)ia * mw;
+        WV<T> pa, po;
+        wv_load(pa, ea + nn, n, g, c);
+        wv_tn(po, PaccT, pa, n, 1.0, &pacc);  // Phi_acc phi_a + phi_acc
+        if (ia < d) {  // anchored partner: po = x_j
+            wv_store(po, out + (long long)j * mw + nn, n, g, c);
+            wv_store(po, A.xhat + (b * J + j) * (long long)n, n, g, c);
+            const double *v = A.vfun + (b * J + j) * (long long)mw;
+            WM<T> Pv;
+            WV<T> pv, lam;
+            wm_load(Pv, v, n, n, false, 0.0, g, c);
+            wv_load(pv, v + nn, n, g, c);
+            wv_tn(lam, Pv, po, n, 1.0, &pv);
+            wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
+            return;
+        }
+        WM<T> Pa, Pn;
+        wm_load(Pa, ea, n, n, false, 0.0, g, c);
+        wm_tn(Pn, Pa, PaccT, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi_a^T Phi_acc^T = (Phi_acc Phi_a)^T
+        PaccT = Pn;
+        pacc = po;
+    }
+    wm_store_t(PaccT, out + (long long)j * mw, n, g, c);  // Phi_acc (natural) from its transpose
+    wv_store(pacc, out + (long long)j * mw + nn, n, g, c);
+}
+
 // Resident scan waves (one combine each) the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
@@ -440,7 +491,11 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
-    if (T == 1) hipLaunchKernelGGL(k_map_scan<1>, grid, blk, 0, st, a);
+    if (PDPLQR_MAP_RADIX == 4) {
+        if (T == 1) hipLaunchKernelGGL(k_map_scan4<1>, grid, blk, 0, st, a);
+        else if (T == 2) hipLaunchKernelGGL(k_map_scan4<2>, grid, blk, 0, st, a);
+        else return PDPLQR_ERR_UNSUPPORTED;
+    } else if (T == 1) hipLaunchKernelGGL(k_map_scan<1>, grid, blk, 0, st, a);
     else if (T == 2) hipLaunchKernelGGL(k_map_scan<2>, grid, blk, 0, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());

@@ -62,6 +62,10 @@ int seg_scan_slots(const Shape &sh, int device);
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
+// Composition radix of the boundary-map prefix scan (2 or 4).
+#ifndef PDPLQR_MAP_RADIX
+#define PDPLQR_MAP_RADIX 4
+#endif
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, hipStream_t st);

@@ -268,7 +268,7 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     if (rc) return rc;
     double *mb[2] = {ps->mapA, ps->mapB};
     int round = 0;
-    for (int d = 1; d < ps->S + 1; d <<= 1, ++round) {
+    for (int d = 1; d < ps->S + 1; d *= PDPLQR_MAP_RADIX, ++round) {
         MapScanArgs ms;
         ms.n = sh.n;
         ms.S = ps->S;
