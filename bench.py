@@ -110,7 +110,34 @@ def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
     stages = reps * sample_batch * N
     return {"value": stages / el, "unit": "stages/s", "cores": threads, "kind": "port",
             "sample": f"{reps} x {sample_batch} problems of N={N} nx={n} nu={m} (batched serial Riccati, "
-                      f"OpenMP over problems, {el:.1f} s)"}
+                      f"OpenMP over problems, {el:.1f} s)",
+            "variants": {"C2_serial_1core": cpu_single_problem(n, m, N)}}
+
+
+def cpu_single_problem(n, m, N, seconds=2.0):
+    """SURVEY.md 8(d) baseline (i): one problem, the serial LQRSolver
+    restatement on one core (backward + forward), the CPU counterpart of the
+    C2 line; bounded to ~2 s."""
+    from oracle.oracle import OracleSerial
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, 1, 77)
+    pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[0], c[0], H[0], h[0], np.zeros(0))
+    o = OracleSerial(pm)
+    o.update_problem_data(np.zeros(N * (n + m) + n), None, None, None, 1e-6)
+    o.backward(None)
+    o.forward(x0[0])  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        o.backward(None)
+        o.forward(x0[0])
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"ms_per_solve": el / reps * 1e3, "stages_per_s": N * reps / el, "cores": 1,
+            "sample": f"{reps} solves of one N={N} nx={n} nu={m} problem"}
 
 
 BACKEND = os.environ.get("PDPLQR_BENCH_BACKEND", "nccl")
