@@ -252,6 +252,19 @@ __device__ __forceinline__ void schur_store_record_staged(double *FRk, double w,
     if (lane < FS / 2) gstore2(FRk + 2 * lane, reinterpret_cast<const d2v *>(sm.rec)[lane]);
 }
 
+// The same record stored straight from the registers (PDPLQR_REC_DIRECT): for
+// m = 4, s = 16 column g of L is lane (g, c)'s own slot FR[16 g + c], so the
+// 64 lanes write the L part with ONE contiguous store and lanes 0..3 the lu'
+// part with a second; no LDS round trip.  Two stores per stage.
+template <int M, int S>
+__device__ __forceinline__ void schur_store_record_direct(double *FRk, double w, const double (&luq)[4], int g,
+                                                          int c) {
+    static_assert(M == 4 && S == 16, "one record column per row group");
+    const int lane = 16 * g + c;
+    gstore(FRk + lane, (c >= g) ? w : 0.0);
+    if (lane < M) gstore(FRk + S * M + lane, luq[lane < M ? lane : 0]);
+}
+
 // Record from the tile (chol_tiles path): u columns of M scaled by 1/sqrt(d)
 // (sm.inv), lu' from sm.luq; staged in LDS, one coalesced store.
 template <int M, int S>
@@ -291,6 +304,10 @@ struct SchurShape {
 #endif
 using SymOn = std::integral_constant<bool, true>;
 using SymOff = std::integral_constant<bool, false>;
+
+#ifndef PDPLQR_REC_DIRECT
+#define PDPLQR_REC_DIRECT 1
+#endif
 
 #ifndef PDPLQR_SCHUR_WAVES
 #define PDPLQR_SCHUR_WAVES 4
@@ -375,12 +392,14 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // R's loads have landed once at most `after` younger vm ops are
         // outstanding.  One immediate per call site: a branchy wait made the
         // compiler copy R (still in flight) into other registers.
-        auto vwait5 = [&](d2v(&R)[NI]) {
+        auto vwait5 = [&](d2v(&R)[NI]) {  // steady state
             static_assert(NI == 3, "register staging");
-            asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if (PDPLQR_REC_DIRECT) asm volatile("s_waitcnt vmcnt(7)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            else asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
         };
-        auto vwait4 = [&](d2v(&R)[NI]) {
-            asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+        auto vwait4 = [&](d2v(&R)[NI]) {  // first step
+            if (PDPLQR_REC_DIRECT) asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            else asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
         };
         auto vwait0 = [&](d2v(&R)[NI]) {
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
@@ -390,10 +409,11 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             for (int q = 0; q < NI; ++q) *reinterpret_cast<d2v *>(&stg[slot][q * 128 + 2 * lane]) = R[q];
         };
         // Every step issues exactly 3 loads (stage k - 3, clamped to stage 0 at
-        // the end: re-loads that are never written to LDS) and 1 record store,
-        // so "X's loads have landed" is always vmcnt(5) -- the other set's 3
-        // loads and two stores are younger; the first step follows the
-        // prologue (3 loads + 1 store: vmcnt(4)).
+        // the end: re-loads that are never written to LDS) and 1 record store
+        // (2 with PDPLQR_REC_DIRECT), so "X's loads have landed" is always
+        // vmcnt(5) (7) -- the other set's 3 loads and two steps' stores are
+        // younger; the first step follows the prologue (3 loads + one step's
+        // stores: vmcnt(4) (5)).
         auto step = [&](int k, d2v(&X)[NI], bool first, auto sym, bool sym_rt) {  // X: stage k - 1 on entry, k - 3 on exit
             const double *R = stg[k & 1];
             SchurIn in;
@@ -402,7 +422,10 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value>(Pm, prow, in, sm, m, s,
                                                                                               g, c, w, luq, sym_rt);
             fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
-            if (PDPLQR_SCHUR_BLOCK) schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
+            if (PDPLQR_SCHUR_BLOCK && PDPLQR_REC_DIRECT)
+                schur_store_record_direct<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, g, c);
+            else if (PDPLQR_SCHUR_BLOCK)
+                schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
             else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
             wave_sync();  // stage k's LDS reads retire before slot reuse
             if (first) vwait4(X);
