@@ -265,6 +265,7 @@ int pdplqr_set_model(pdplqr_handle h, const double *E, const double *c, const do
     if (sh.ndD > 0) PDPLQR_HIP_TRY(hipMemcpyAsync(h->D, D, B * sh.ndD * sizeof(double), kind, h->stream));
     if (mem != PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
     h->model_set = true;
+    h->hw_cached = false;  // H~ is re-formed from the new model
     h->updated = false;
     // The factor cache survives a model upload: the reference re-reads model_
     // lazily and never invalidates its workspace factors (lqr_solver.hpp:25,65-70).
@@ -365,6 +366,7 @@ int pdplqr_clear_workspace(pdplqr_handle h) {
     const Shape &sh = h->sh;
     const long long B = sh.batch;
     PDPLQR_HIP_TRY(hipMemsetAsync(h->Hw, 0, B * sh.perHw * sizeof(double), h->stream));
+    h->hw_cached = false;
     PDPLQR_HIP_TRY(hipMemsetAsync(h->hw, 0, B * sh.perh * sizeof(double), h->stream));
     if (sh.ny) PDPLQR_HIP_TRY(hipMemsetAsync(h->gw, 0, B * sh.ny * sizeof(double), h->stream));
     PDPLQR_HIP_TRY(hipMemsetAsync(h->KD, 0, B * sh.perKD * sizeof(double), h->stream));

@@ -56,7 +56,7 @@ struct RiccatiArgs {
 int launch_update_problem_data(const Shape &sh, const double *H, const double *hv, const double *ws,
                                const double *ys, const double *zs, const double *irho, double sigma, double *Hw,
                                double *hw, double *gw, const short2 *tab_s, const short2 *tab_n,
-                               hipStream_t st);
+                               hipStream_t st, bool skipH = false);
 int launch_penalty(const Shape &sh, const double *D, const double *rho, const double *gw, double *Hw,
                    double *hw, const int32_t *d_off, const int32_t *y_off, const short2 *tab_s,
                    const short2 *tab_n, int with_H, int max_nc, hipStream_t st);
@@ -86,6 +86,12 @@ struct pdplqr_handle_s {
     // workspace
     double *Hw = nullptr, *hw = nullptr, *gw = nullptr;
     double *KD = nullptr, *Lc = nullptr, *lpc = nullptr;
+    // H~ = H + sigma I (Hw) depends only on the model and sigma when no stage
+    // has constraints (no rho penalty is folded into Hw): kept across
+    // update_problem_data calls with the same sigma, re-formed after set_model
+    // or clear_workspace
+    bool hw_cached = false;
+    double hw_sigma = 0.0;
     int32_t *status = nullptr;
     int32_t *d_off = nullptr, *y_off = nullptr;
     short2 *tab_s = nullptr, *tab_n = nullptr;

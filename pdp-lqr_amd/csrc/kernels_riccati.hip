@@ -36,8 +36,10 @@ __global__ void k_update_problem_data(Shape sh, const double *__restrict__ H, co
                                       const double *__restrict__ zs, const double *__restrict__ irho,
                                       double sigma, double *__restrict__ Hw, double *__restrict__ hw,
                                       double *__restrict__ gw, const short2 *__restrict__ tab_s,
-                                      const short2 *__restrict__ tab_n) {
-    const long long totH = sh.perHw * sh.batch, toth = sh.perh * sh.batch, totg = (long long)sh.ny * sh.batch;
+                                      const short2 *__restrict__ tab_n, int skipH) {
+    // skipH: H~ is already in Hw for this sigma (pdplqr_handle::hw_cached)
+    const long long totH = skipH ? 0 : sh.perHw * sh.batch, toth = sh.perh * sh.batch,
+                    totg = (long long)sh.ny * sh.batch;
     const long long total = totH + toth + totg;
     const long long stepg = (long long)gridDim.x * blockDim.x;
     const int s = sh.s;
@@ -77,14 +79,14 @@ __global__ void k_update_problem_data(Shape sh, const double *__restrict__ H, co
 int launch_update_problem_data(const Shape &sh, const double *H, const double *hv, const double *ws,
                                const double *ys, const double *zs, const double *irho, double sigma, double *Hw,
                                double *hw, double *gw, const short2 *tab_s, const short2 *tab_n,
-                               hipStream_t st) {
-    const long long total = (sh.perHw + sh.perh + sh.ny) * (long long)sh.batch;
+                               hipStream_t st, bool skipH) {
+    const long long total = ((skipH ? 0 : sh.perHw) + sh.perh + sh.ny) * (long long)sh.batch;
     const int threads = 256;
     long long blocks = (total + threads - 1) / threads;
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_update_problem_data, dim3((unsigned)blocks), dim3(threads), 0, st, sh, H, hv, ws, ys, zs,
-                       irho, sigma, Hw, hw, gw, tab_s, tab_n);
+                       irho, sigma, Hw, hw, gw, tab_s, tab_n, (int)skipH);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

@@ -318,8 +318,13 @@ int solver_on_model(pdplqr_handle h) {
 int solver_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
                   double sigma) {
     if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_update(h, ws, ys, zs, irho, sigma);
-    return launch_update_problem_data(h->sh, h->H, h->h, ws, ys, zs, irho, sigma, h->Hw, h->hw, h->gw, h->tab_s,
-                                      h->tab_n, h->stream);
+    const bool cacheable = h->max_nc <= 0 && !getenv("PDPLQR_NO_HCACHE");
+    const bool skipH = cacheable && h->hw_cached && h->hw_sigma == sigma;
+    const int rc = launch_update_problem_data(h->sh, h->H, h->h, ws, ys, zs, irho, sigma, h->Hw, h->hw, h->gw,
+                                              h->tab_s, h->tab_n, h->stream, skipH);
+    h->hw_cached = rc == PDPLQR_OK && cacheable;
+    h->hw_sigma = sigma;
+    return rc;
 }
 
 // ---------------------------------------------------------------------------

@@ -187,6 +187,45 @@ def test_value_form_symmetrisation_long_horizon(spread):
         assert rel_err(out[b], ref) < TOL, b
 
 
+@pytest.mark.parametrize("keep", [False, True])
+def test_update_reuses_htilde_only_when_valid(keep):
+    """H~ = H + sigma I is kept across update_problem_data calls with the same
+    sigma (no constraints): a new ws alone, a new sigma, and a new model must
+    each give the oracle's answer for the current data."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 48, 3
+    s = n + m
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+    rng = np.random.default_rng(5)
+
+    def check(E, c, H, h, x0, ws, sigma):
+        bs.update_problem_data(ws, sigma=sigma)
+        bs.backward()
+        out = np.zeros_like(ws)
+        bs.forward(x0, out)
+        for b in range(batch):
+            pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+            o = OracleSerial(pm)
+            o.update_problem_data(ws[b], None, None, None, sigma)
+            o.backward(None)
+            assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 31)
+    bs.set_model(E, c, H, h)
+    check(E, c, H, h, x0, np.zeros((batch, N * s + n)), 1e-3)
+    check(E, c, H, h, x0, rng.standard_normal((batch, N * s + n)), 1e-3)  # same sigma, new ws
+    check(E, c, H, h, x0, rng.standard_normal((batch, N * s + n)), 0.5)   # new sigma
+    E2, c2, H2, h2, _ = random_batch_arrays(n, m, N, batch, 32)
+    bs.set_model(E2, c2, H2, h2)                                          # new model, same sigma
+    check(E2, c2, H2, h2, x0, rng.standard_normal((batch, N * s + n)), 0.5)
+    bs.handle.clear_workspace()
+    check(E2, c2, H2, h2, x0, rng.standard_normal((batch, N * s + n)), 0.5)  # after clear_workspace
+
+
 def _batched_case(n, m, N, batch, seed, device_buffers=False, keep=False):
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
