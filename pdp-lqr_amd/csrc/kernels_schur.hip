@@ -77,6 +77,10 @@ struct SchurSmem {
     };
 };
 
+#ifndef PDPLQR_LP_IN_P
+#define PDPLQR_LP_IN_P 1
+#endif
+
 // Compile-time m <= 4: the m u-pivots as ONE block step.  Every u row sits in
 // register 0 (row j = row group j), so
 //   * Muu (m x m) and lu come to every lane by v_readlane; Luu = chol(Muu),
@@ -143,6 +147,19 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         for (int l = 0; l <= j; ++l) v = __builtin_fma(T[j][l], ml[l], v);
         w = (g == j) ? v : w;  // W[c][g]; groups g >= m keep 0
     }
+#if PDPLQR_LP_IN_P
+    // lp -= W lu' rides in the same MFMA: column 0 of M (u column 0: dead
+    // after this stage -- the next stage reads P's x rows through the x
+    // K-chunks only, and G's u rows are never used) carries lp in, the B
+    // operand's column 0 carries lu', so D[:, 0] = lp - W lu'; then the
+    // column-0 result to every lane of its row (DPP row_newbcast:0)
+    const double lq = (g < MM) ? luq[g < MM ? g : 0] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) M[r] = (c == 0) ? lpr[r] : M[r];
+    M = mfma_f64(-w, (c == 0) ? lq : w, M);  // M - W W^T; column 0: lp - W lu'
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lpr[r] = bcast_lane16(M[r], 0);
+#else
     M = mfma_f64(-w, w, M);  // M - W W^T
     // lp -= W lu': one MFMA with lu' as column 0 of the B operand, then the
     // column-0 result to every lane of its row (DPP row_newbcast:0)
@@ -150,6 +167,7 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
     const d4 y = mfma_f64(w, lb, d4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
     for (int r = 0; r < 4; ++r) lpr[r] -= bcast_lane16(y[r], 0);
+#endif
     return ok;
 }
 
