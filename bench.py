@@ -457,6 +457,11 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
+    if not res["status_ok"]:
+        # a solve that flagged a failed factorisation on the timed batch does
+        # not back its number: report it, then fail the run
+        print("bench: status_ok is false (non-SPD pivot or non-finite value on the timed batch)", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

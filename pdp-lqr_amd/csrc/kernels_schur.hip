@@ -432,7 +432,9 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // vmcnt(5) (7) -- the other set's 3 loads and two steps' stores are
         // younger; the first step follows the prologue (3 loads + one step's
         // stores: vmcnt(4) (5)).
-        auto step = [&](int k, d2v(&X)[NI], bool first, auto sym, bool sym_rt) {  // X: stage k - 1 on entry, k - 3 on exit
+        // Stage k: its record is read from LDS slot k & 1, its rollout record
+        // stored (1 or 2 vm ops).
+        auto process = [&](int k, auto sym, bool sym_rt) {
             const double *R = stg[k & 1];
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
@@ -446,12 +448,26 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
                 schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
             else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
             wave_sync();  // stage k's LDS reads retire before slot reuse
+        };
+        auto step = [&](int k, d2v(&X)[NI], bool first, auto sym, bool sym_rt) {  // X: stage k - 1 on entry, k - 3 on exit
+            process(k, sym, sym_rt);
             if (first) vwait4(X);
             else vwait5(X);
             if (k >= 1) lput(X, (k - 1) & 1);
             gload(X, k >= 3 ? k - 3 : 0);
             wave_sync();
         };
+        // No load may still be in flight where control flow joins: the
+        // compiler is free to copy an asm output there (it cannot know the
+        // value is still arriving) and to reuse the source registers, which
+        // the landing load then overwrites.  (It did exactly that at the loop
+        // exit: the set loaded by the last pair's head was moved into other
+        // registers and its old registers became the final stage's MFMA
+        // accumulators -- stage 0 of a random ~2 % of the problems came out
+        // wrong or NaN, depending on when the load landed.)  So the last pair
+        // drains the counter with an operand-less wait, and the final stage
+        // reads only LDS.
+        auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
         gload(RA, N - 1);
         vwait0(RA);
         lput(RA, (N - 1) & 1);
@@ -462,14 +478,14 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // PDPLQR_SYM_EVERY = 2, every other one for 4), the second stage only
         // when PDPLQR_SYM_EVERY = 1
         step(N - 1, RA, true, SymOn{}, true);
+        if (N < 3) drain();
         int k = N - 2;
         for (; k >= 1; k -= 2) {
             step(k, RB, false, SymOn{}, PDPLQR_SYM_EVERY < 4 || ((N - 2 - k) & 2) == 0);
             step(k - 1, RA, false, std::integral_constant<bool, (PDPLQR_SYM_EVERY <= 1)>{}, true);
+            if (k < 3) drain();  // wave-uniform: the last pair
         }
-        if (k == 0) step(0, RB, false, SymOn{}, true);
-        vwait0(RA);  // nothing in flight may land in reused registers
-        vwait0(RB);
+        if (k == 0) process(0, SymOn{}, true);  // its record went to LDS slot 0 in step 1
     } else {
         SchurIn nxt;
         schur_load(nxt, Eb + (long long)(N - 1) * n * s, cb + (long long)(N - 1) * n, Hb + (long long)(N - 1) * ps,

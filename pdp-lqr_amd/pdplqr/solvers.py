@@ -107,28 +107,69 @@ class _Handle:
         except Exception:
             pass
 
+    # stream ordering with torch ---------------------------------------------
+    # The handle launches on its own (non-blocking) stream.  When a call is
+    # handed torch CUDA tensors, that stream first waits for torch's current
+    # stream (the tensors may have been written there), and torch's current
+    # stream waits for the handle's work after the call (outputs are read
+    # there, inputs may be freed or overwritten there): events only, no host
+    # synchronisation.  Host (numpy) calls are synchronous in the C ABI.
+    def _torch_stream(self):
+        import torch
+
+        hs = getattr(self, "_ts", None)
+        if hs is None:
+            hs = self._ts = torch.cuda.ExternalStream(self.stream(), device=torch.device("cuda", self.cfg.device))
+        return hs
+
+    def _enter(self, *objs):
+        if not any(o is not None and _is_torch(o) and o.is_cuda for o in objs):
+            return None
+        import torch
+
+        hs = self._torch_stream()
+        cur = torch.cuda.current_stream(hs.device)
+        if cur.cuda_stream == hs.cuda_stream:
+            return None
+        hs.wait_stream(cur)
+        return cur
+
+    def _leave(self, cur):
+        if cur is not None:
+            cur.wait_stream(self._torch_stream())
+
     # raw protocol (pointers already validated) -----------------------------
     def set_model(self, E, c, H, h, D=None):
         ps = [_ptr(E, "E"), _ptr(c, "c"), _ptr(H, "H"), _ptr(h, "h"), _ptr(D, "D")]
         mem = _mem_of(*ps)
+        cur = self._enter(E, c, H, h, D)
         check(lib().pdplqr_set_model(self.h, ps[0][0], ps[1][0], ps[2][0], ps[3][0], ps[4][0], mem))
+        self._leave(cur)
 
     def update_problem_data(self, ws, ys, zs, inv_rho, sigma):
         ps = [_ptr(ws, "ws"), _ptr(ys, "ys"), _ptr(zs, "zs"), _ptr(inv_rho, "inv_rho")]
         mem = _mem_of(*ps)
+        cur = self._enter(ws, ys, zs, inv_rho)
         check(lib().pdplqr_update_problem_data(self.h, ps[0][0], ps[1][0], ps[2][0], ps[3][0], float(sigma), mem))
+        self._leave(cur)
 
     def backward(self, rho):
         p = _ptr(rho, "rho")
+        cur = self._enter(rho)
         check(lib().pdplqr_backward(self.h, p[0], _mem_of(p)))
+        self._leave(cur)
 
     def backward_without_factorization(self, rho):
         p = _ptr(rho, "rho")
+        cur = self._enter(rho)
         check(lib().pdplqr_backward_without_factorization(self.h, p[0], _mem_of(p)))
+        self._leave(cur)
 
     def forward(self, x0, ws_out):
         ps = [_ptr(x0, "x0"), _ptr(ws_out, "ws")]
+        cur = self._enter(x0, ws_out)
         check(lib().pdplqr_forward(self.h, ps[0][0], ps[1][0], _mem_of(*ps)))
+        self._leave(cur)
 
     def clear_workspace(self):
         check(lib().pdplqr_clear_workspace(self.h))
@@ -141,6 +182,7 @@ class _Handle:
 
     def set_stream(self, stream_ptr: int):
         check(lib().pdplqr_set_stream(self.h, C.c_void_p(stream_ptr)))
+        self._ts = None
 
     def status(self) -> np.ndarray:
         out = np.zeros(self.batch, dtype=np.int32)

@@ -328,6 +328,8 @@ def test_full_size_properties():
     bs.backward()
     out = np.zeros_like(ws0)
     bs.forward(x0, out)
+    st = bs.status()
+    assert np.count_nonzero(st) == 0, [(int(b), int(st[b]) - 1) for b in np.nonzero(st)[0][:16]]
     assert np.all(np.isfinite(out))
     Eb = E.reshape(batch, N, s, n).transpose(0, 1, 3, 2)  # (b, k, n, s)
     w = out[:, :N * s].reshape(batch, N, s)
