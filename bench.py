@@ -111,7 +111,51 @@ def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
     return {"value": stages / el, "unit": "stages/s", "cores": threads, "kind": "port",
             "sample": f"{reps} x {sample_batch} problems of N={N} nx={n} nu={m} (batched serial Riccati, "
                       f"OpenMP over problems, {el:.1f} s)",
-            "variants": {"C2_serial_1core": cpu_single_problem(n, m, N)}}
+            "cpu_model": cpu_model(),
+            "variants": {"C2_serial_1core": cpu_single_problem(n, m, N),
+                         "C2_parallel_all_cores": cpu_parallel_problem(n, m, N, threads)}}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_parallel_problem(n, m, N, threads, seconds=2.0):
+    """SURVEY.md 8(d) baseline (ii): one problem, the LQRParallelSolver
+    restatement with num_segments = the host cores granted (an OpenMP team of
+    that many threads, pinned one per CPU as lqr_solver_parallel.hpp:102-112
+    does), load balancing (alpha = 1.55), CHOLESKY condensed system; bounded
+    to ~2 s.  Run last: the pinning stays on the OpenMP pool's threads."""
+    from oracle.oracle import OracleParallel
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, 1, 77)
+    pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[0], c[0], H[0], h[0], np.zeros(0))
+    saved = os.sched_getaffinity(0)
+    o = OracleParallel(pm, threads, load_balancing=True, condensed="CHOLESKY")
+    pinned = o.set_threads(True, True)
+    o.update_problem_data(np.zeros(N * (n + m) + n), None, None, None, 1e-6)
+    o.backward(None)
+    o.forward(x0[0])  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        o.backward(None)
+        o.forward(x0[0])
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    os.sched_setaffinity(0, saved)  # the calling thread was team thread 0
+    return {"ms_per_solve": el / reps * 1e3, "stages_per_s": N * reps / el, "cores": threads,
+            "threads_pinned": pinned, "num_segments": threads,
+            "sample": f"{reps} solves of one N={N} nx={n} nu={m} problem"}
 
 
 def cpu_single_problem(n, m, N, seconds=2.0):
@@ -165,6 +209,26 @@ def _timed(fn, steps, warmup, dev, dist):
     if dist:
         el = _max_over_ranks(dist, el, dev)
     return el / steps
+
+
+def measured_copy_gbs(dev, nbytes=1 << 32, reps=5):
+    """Device-to-device copy rate of a large buffer (read + write bytes / time):
+    the achievable HBM ceiling the roofline is also quoted against."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def bench_single(local, dev, dist, steps=10, warmup=3):
@@ -440,6 +504,9 @@ def main():
         "solve_hbm_frac": bytes_stage * stages / ((ms_bwd + ms_fwd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "status_ok": bool(np.all(st == 0)),
     }
+    copy_gbs = measured_copy_gbs(dev)
+    res["roofline"]["peak_measured_copy"] = copy_gbs
+    res["roofline"]["frac_of_measured_copy"] = achieved / copy_gbs
     if not args.no_secondary:
         res["end_to_end"] = bench_end_to_end(bs, E, c, Hk, h, x0, ws0, out, dev, dist, local)
     bs.close()

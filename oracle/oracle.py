@@ -54,6 +54,8 @@ def lib():
         L.orc_parallel_backward_ok.argtypes = [vp]
         L.orc_parallel_backward_ok.restype = C.c_int
         L.orc_parallel_segments.argtypes = [vp, _ip, _ip]
+        L.orc_parallel_set_threads.argtypes = [vp, C.c_int, C.c_int]
+        L.orc_parallel_set_threads.restype = C.c_int
         L.orc_parallel_get_segment.argtypes = [vp, C.c_int, _dp, _dp, _dp, _dp]
         L.orc_segmentation.argtypes = [C.c_int, C.c_int, C.c_int, _ip, _ip]
         L.orc_segmentation.restype = C.c_int
@@ -187,6 +189,12 @@ class OracleParallel(_Base):
         if getattr(self, "h", None):
             lib().orc_parallel_destroy(self.h)
             self.h = None
+
+    def set_threads(self, on=True, pin=True) -> int:
+        """Run the segments on an OpenMP team of num_segments threads, pinned
+        like the reference (lqr_solver_parallel.hpp:102-112); returns the
+        number of threads pinned."""
+        return int(lib().orc_parallel_set_threads(self.h, int(bool(on)), int(bool(pin))))
 
     def segments(self):
         a = np.zeros(self.ns, dtype=np.int32)

@@ -26,7 +26,9 @@
  *   ws : ragged like h (k < N: s entries, k = N: n entries)
  *   ys, zs, rho, inv_rho : ragged, stage k has nc_k entries
  */
+#define _GNU_SOURCE /* sched_setaffinity: the reference's thread pinning (lqr_solver_parallel.hpp:102-112) */
 #include <math.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 #include <stdint.h>
@@ -760,6 +762,7 @@ typedef struct {
     orc_stage **data; /* per segment Nseg+1 stages */
     orc_condensed *cs;
     int last_backward_ok;
+    int threads; /* 0: one thread (segments in turn); > 0: OpenMP team of ns threads (CPU baseline (ii)) */
 } orc_parallel;
 
 /* Segmentation (lqr_solver_parallel.hpp:64-88): Nseg_i = int(N/(scale+ns-1))
@@ -845,9 +848,48 @@ static void par_reduction(orc_parallel *o, int tid, const double *rho, int fact)
         cond_update_vec(o->cs, d[0].lp + (d[0].dim - n), d[0].f, tid);
 }
 
+#ifdef _OPENMP
+#include <omp.h>
+#define PAR_FOR _Pragma("omp parallel for num_threads(o->ns) schedule(static, 1) if (o->threads > 0)")
+#else
+#define PAR_FOR
+#endif
+
+/* The reference's OpenMP team: num_segments threads, thread tid pinned to core
+ * tid (lqr_solver_parallel.hpp:102-112).  Here "core tid" is the tid-th CPU of
+ * the process's allowed set (the GPU box grants a CPU share, not cores 0..).
+ * Results do not depend on it: segments own disjoint workspaces. */
+int orc_parallel_set_threads(void *p, int on, int pin) {
+    orc_parallel *o = (orc_parallel *)p;
+    int pinned = 0;
+    o->threads = on ? o->ns : 0;
+#ifdef _OPENMP
+    if (on && pin) {
+        cpu_set_t allowed;
+        if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return 0;
+#pragma omp parallel num_threads(o->ns) reduction(+ : pinned)
+        {
+            int tid = omp_get_thread_num(), cpu, seen = -1;
+            for (cpu = 0; cpu < CPU_SETSIZE; ++cpu)
+                if (CPU_ISSET(cpu, &allowed) && ++seen == tid) {
+                    cpu_set_t one;
+                    CPU_ZERO(&one);
+                    CPU_SET(cpu, &one);
+                    pinned += sched_setaffinity(0, sizeof(one), &one) == 0;
+                    break;
+                }
+        }
+    }
+#else
+    (void)pin;
+#endif
+    return pinned;
+}
+
 void orc_parallel_backward(void *p, const double *rho) { /* :142-146 */
     orc_parallel *o = (orc_parallel *)p;
     int i;
+    PAR_FOR
     for (i = 0; i < o->ns; ++i) par_reduction(o, i, rho, 1);
     o->last_backward_ok = (o->cs->type == 0) ? cond_lu_backward(o->cs) : cond_chol_backward(o->cs);
 }
@@ -855,6 +897,7 @@ void orc_parallel_backward(void *p, const double *rho) { /* :142-146 */
 void orc_parallel_backward_without_factorization(void *p, const double *rho) { /* :148-154 */
     orc_parallel *o = (orc_parallel *)p;
     int i;
+    PAR_FOR
     for (i = 0; i < o->ns; ++i) par_reduction(o, i, rho, 0);
 }
 
@@ -862,11 +905,12 @@ int orc_parallel_backward_ok(void *p) { return ((orc_parallel *)p)->last_backwar
 
 void orc_parallel_forward(void *p, const double *x0, double *ws) { /* :213-238 */
     orc_parallel *o = (orc_parallel *)p;
-    int n = o->md->n, m = o->md->m, s = n + m, i, k, a, t;
+    int n = o->md->n, m = o->md->m, s = n + m, i;
     if (o->cs->type == 0) cond_lu_forward(o->cs, x0);
     else cond_chol_forward(o->cs, x0);
+    PAR_FOR
     for (i = 0; i < o->ns; ++i) {
-        int N0 = o->idx_start[i], N1 = N0 + o->Nseg[i], last = (i == o->ns - 1);
+        int N0 = o->idx_start[i], N1 = N0 + o->Nseg[i], last = (i == o->ns - 1), k, a, t;
         const double *uhat = o->cs->seg[i].uhat;
         memcpy(ws + (size_t)N0 * s + m, o->cs->seg[i].xhat, sizeof(double) * n);
         for (k = N0; k < N1; ++k) {
@@ -1259,9 +1303,6 @@ void orc_kkt_get_csc(void *p, int *Ap, int *Ai, double *Ax) {
 /* (the reference has no batch API; BASELINE.md section 4 variant iii).       */
 /* Data is batch-major: problem b's arrays follow each other.  nc = 0.        */
 /* ------------------------------------------------------------------------ */
-#ifdef _OPENMP
-#include <omp.h>
-#endif
 int orc_batched_serial_solve(int n, int m, int N, int batch, const double *E, const double *c, const double *H,
                              const double *h, const double *x0, double sigma, double *ws_out, int threads) {
     int s = n + m;

@@ -46,9 +46,14 @@ extern __device__ unsigned long long g_comb_t[1024 * 16];
 template <int T>
 struct CombSmem {
     static constexpr int P = 16 * T, PL = P + 1;
-    alignas(16) double A[P * (P + 2)];  // Q^T (row stride P + 2), then Z (vector products)
-    double B[P * PL];  // R -> U in place, then output staging (symmetrisation)
-    alignas(16) double cb[P];  // pivot-row broadcast of chol_tiles
+    union {
+        struct {
+            alignas(16) double A[P * (P + 2)];  // Q^T (row stride P + 2), then Z (vector products)
+            double B[P * PL];  // R -> U in place, then output staging (symmetrisation)
+        };
+        alignas(16) double W[2 * P * P];  // [I + P_b C_a | P_b] of the LU form (comb_core_lu)
+    };
+    alignas(16) double cb[P];  // pivot-row broadcast of chol_tiles; pivot rows of the LU form
     double sinv[P], luq[P];
 };
 
@@ -520,6 +525,94 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     return ok;
 }
 
+// LU form of the same core (CondensedSystemLUSolver, condensed_system.hpp:
+// 32-147, which factors I + C P with PartialPivLU): no definiteness needed --
+// for PSD C_a, P_b every eigenvalue of I + P_b C_a is >= 1, so a semidefinite
+// value function (zero state cost) combines where the Cholesky form fails.
+//     Y = (I + P_b C_a)^{-1} P_b  (= P_b (I + C_a P_b)^{-1}, symmetric)
+// by Gauss-Jordan elimination with partial (row) pivoting on [I + P_b C_a | P_b]
+// in LDS: the same pivot rows as PartialPivLU (largest |a| among the rows not
+// yet used, lowest row on ties), kept in place instead of swapped.  Lanes own
+// rows (lane % 16 T) and interleaved column sets (lane / 16 T); the pivot row
+// reaches every lane as a broadcast LDS read.  Y is symmetrised on the way
+// back to registers; Z, Z^T follow as in the Cholesky form.  False if a pivot
+// is zero or not finite.
+template <int T>
+__device__ __forceinline__ bool comb_core_lu(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
+                                             CombSmem<T> &sm, int lane) {
+    constexpr int P = 16 * T, LP = 64 / P;
+    const int g = lane >> 4, c = lane & 15;
+    double *W = sm.W;  // [A | P_b] column-major, leading dimension n
+    int *piv_row = reinterpret_cast<int *>(sm.cb);  // piv_row[k]: the row that pivoted column k
+    {
+        WM<T> Pm, Am;
+        wm_load(Pm, Pb, n, n, false, 0.0, g, c);
+        wm_tn(Am, Pm, Ca, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);  // I + P_b C_a (P_b symmetric)
+        wave_sync();
+        wm_store(Am, W, n, n, g, c);
+        wm_store(Pm, W + n * n, n, n, g, c);
+        wave_sync();
+    }
+    const bool row = lane % P < n;
+    const int i = row ? lane % P : 0, q = lane / P;  // rows >= n read row 0 and write nothing
+    bool used = false, ok = true;
+    for (int k = 0; k < n; ++k) {
+        // pivot: max |a_ik| over the unused rows (lowest row on ties)
+        double v = (row && q == 0 && !used) ? fabs(W[i + k * n]) : -1.0;
+        int arg = lane % P;
+#pragma unroll
+        for (int mk = 1; mk < 64; mk <<= 1) {
+            const double ov = shfl_xor_f64(v, mk);
+            const int oa = __shfl_xor(arg, mk, 64);
+            if (ov > v || (ov == v && oa < arg)) {
+                v = ov;
+                arg = oa;
+            }
+        }
+        const int p = __builtin_amdgcn_readfirstlane(arg);
+        const double piv = W[p + k * n];
+        ok = ok && piv != 0.0 && fabs(piv) <= 1.7976931348623157e308;
+        const double inv = 1.0 / piv;
+        const bool me = row && i == p;
+        used = used || me;
+        if (lane == 0) piv_row[k] = p;
+        const double mi = W[i + k * n] * inv;  // this row's multiplier
+        wave_sync();
+        for (int j = q; j < 2 * n; j += LP) {
+            const double rp = W[p + j * n];  // pivot row: broadcast read
+            const double own = W[i + j * n];
+            const double nv = me ? rp * inv : __builtin_fma(-mi, rp, own);
+            if (row) W[i + j * n] = nv;
+        }
+        wave_sync();
+    }
+    // row piv_row[k] now holds row k of Y = [A | P_b]'s solved right-hand side
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ii = 16 * a + 4 * r + g, jj = 16 * b + c;
+                double y = 0.0;
+                if (ii < n && jj < n)
+                    y = 0.5 * (W[piv_row[ii] + (n + jj) * n] + W[piv_row[jj] + (n + ii) * n]);
+                Y.t[a][b][r] = y;
+            }
+    wave_sync();
+    wm_tn(Z, Ca, Y, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);   // Z = I - C_a Y
+    wm_tn(Zt, Y, Ca, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z^T = I - Y C_a
+    return ok;
+}
+
+// the core of either condensed form (CondensedSystemSolverType)
+template <int T, bool LU>
+__device__ __forceinline__ bool comb_core_t(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
+                                            CombSmem<T> &sm, int lane) {
+    if constexpr (LU) return comb_core_lu<T>(Y, Z, Zt, Ca, Pb, n, sm, lane);
+    else return comb_core<T>(Y, Z, Zt, Ca, Pb, n, sm, lane);
+}
+
 // n-vectors in the B-operand / C-layout column 0 of the tiles: lane (g, 0)
 // holds x[16 kt + 4 r + g] in t[kt][r]; other lanes hold 0.
 template <int T>
@@ -596,7 +689,7 @@ __device__ __forceinline__ ElemIn elem_in(const double *e, int n) {
 // when need_Pp is false) and must not alias the inputs.  P_a and C_b are read
 // once, as addends of the last products: they are loaded up front so a
 // global-memory source costs no exposed latency.
-template <int T>
+template <int T, bool LU = false>
 __device__ __forceinline__ bool tcombine_parts(double *oF, double *oC, double *of, double *oP, double *op,
                                                const ElemIn &ea, const ElemIn &eb, int n, bool need_FCf,
                                                bool need_Pp, CombSmem<T> &sm, int lane) {
@@ -609,7 +702,7 @@ __device__ __forceinline__ bool tcombine_parts(double *oF, double *oC, double *o
     WM<T> Ca, Y, Z, Zt;
     COMB_MARK(0);
     wm_load(Ca, aC, n, n, false, 0.0, g, c);
-    const bool ok = comb_core(Y, Z, Zt, Ca, bP, n, sm, lane);
+    const bool ok = comb_core_t<T, LU>(Y, Z, Zt, Ca, bP, n, sm, lane);
     WM<T> Fa;
     wm_load(Fa, aF, n, n, false, 0.0, g, c);
     if (need_Pp) {  // P = P_a + F_a^T (Y F_a)
@@ -662,11 +755,11 @@ __device__ __forceinline__ bool tcombine_parts(double *oF, double *oC, double *o
     return ok;
 }
 
-template <int T>
+template <int T, bool LU = false>
 __device__ __forceinline__ bool tcombine(double *out, const double *ea, const double *eb, int n, bool need_FCf,
                                          bool need_Pp, CombSmem<T> &sm, int lane) {
     const int nn = n * n;
-    return tcombine_parts<T>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n, elem_in(ea, n),
+    return tcombine_parts<T, LU>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n, elem_in(ea, n),
                              elem_in(eb, n), n, need_FCf, need_Pp, sm, lane);
 }
 

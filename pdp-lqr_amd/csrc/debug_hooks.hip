@@ -3,15 +3,16 @@
 // (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
 #include "combine_tiles.hpp"
 
-// out = a (x) b on the device (one wave), elements in host memory.
-template <int T>
+// out = a (x) b on the device (one wave), elements in host memory; LU: the
+// LU form of the combine (CondensedSystemSolverType::LU).
+template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_debug_combine(const double *a, const double *b, double *out, int n, int *ok) {
     __shared__ pdplqr::CombSmem<T> sm;
-    const bool good = pdplqr::tcombine<T>(out, a, b, n, true, true, sm, threadIdx.x);
+    const bool good = pdplqr::tcombine<T, LU>(out, a, b, n, true, true, sm, threadIdx.x);
     if (threadIdx.x == 0) *ok = good ? 1 : 0;
 }
 
-extern "C" int pdplqr_debug_combine(int n, const double *a, const double *b, double *out) {
+extern "C" int pdplqr_debug_combine_form(int n, const double *a, const double *b, double *out, int lu) {
     using namespace pdplqr;
     const int T = n <= 16 ? 1 : (n <= 32 ? 2 : 0);
     if (!T) return PDPLQR_ERR_UNSUPPORTED;
@@ -24,14 +25,20 @@ extern "C" int pdplqr_debug_combine(int n, const double *a, const double *b, dou
     PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
     const double *da = d, *db = (const double *)((char *)d + es);
     double *dout = (double *)((char *)d + 2 * es);
-    if (T == 1) hipLaunchKernelGGL(k_debug_combine<1>, dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
-    else hipLaunchKernelGGL(k_debug_combine<2>, dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    if (T == 1 && lu) hipLaunchKernelGGL((k_debug_combine<1, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    else if (T == 1) hipLaunchKernelGGL((k_debug_combine<1, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    else if (lu) hipLaunchKernelGGL((k_debug_combine<2, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    else hipLaunchKernelGGL((k_debug_combine<2, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     PDPLQR_HIP_TRY(hipDeviceSynchronize());
     PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
     PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));
     (void)hipFree(d);
     (void)hipFree(dok);
     return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
+}
+
+extern "C" int pdplqr_debug_combine(int n, const double *a, const double *b, double *out) {
+    return pdplqr_debug_combine_form(n, a, b, out, 0);
 }
 
 

@@ -80,6 +80,18 @@ __device__ __forceinline__ double sum_groups(double v) {
     return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
 }
 
+// Status semantics of a value-function diagonal (P_k = Lxx Lxx^T): the
+// reference's Eigen LLT stops at the first non-positive pivot and the
+// remaining columns flow through unfactored (lqr_kernel.hpp:89,126 ignore
+// info()), so a positive SEMIdefinite value function -- zero state cost,
+// Q_N = 0 with sigma = 0 -- is a valid solve there and is not flagged here.
+// Flagged: non-finite values, and diagonals below -PDPLQR_PSD_TOL (an
+// indefinite stage matrix).  Control pivots (Muu) must stay positive.
+#ifndef PDPLQR_PSD_TOL
+#define PDPLQR_PSD_TOL 1e-8
+#endif
+__device__ __forceinline__ bool psd_bad(double v) { return !(v >= -PDPLQR_PSD_TOL && v < 1.0e300); }
+
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -214,7 +226,7 @@ __device__ __forceinline__ constexpr int colpos(int i) {
 template <int T>
 __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], double *cb, double *sinv, double *luq,
                                            int jbeg, int jend, int m, bool aug, int g, int c) {
-    bool ok = true;
+    bool ok = true, live = true;
     // cb holds one 16 T slot per row group: every group writes its own row
     // (no exec-mask branch), readers take the pivot's group slot
     double *myslot = cb + g * 16 * T;
@@ -238,10 +250,15 @@ __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], d
                 const double *slot = cb + gj * 16 * T;
                 const double2 *rows = reinterpret_cast<const double2 *>(slot + g * 4 * T);
                 const double djj = readlane_f64(M[tr][tr][rr], (gj << 4) + (j & 15));
-                ok = ok && (djj > 0.0);
-                const double inv = rsqrt_f64(djj);
+                // control pivots (j < m) must be positive; a state pivot <= 0
+                // stops the factorisation as Eigen's LLT does (the remaining
+                // columns stay unfactored, unscaled), flagged only if clearly
+                // negative or not finite (psd_bad)
+                ok = ok && (j < m ? djj > 0.0 : !psd_bad(djj));
+                live = live && (j < m || djj > 0.0);
+                const double inv = live ? rsqrt_f64(djj) : 0.0;
                 const double inv2 = inv * inv;
-                sinv[j] = inv;  // all lanes, same value: no branch
+                sinv[j] = live ? inv : 1.0;  // all lanes, same value: no branch
                 double lc[T];
 #pragma unroll
                 for (int b = 0; b < T; ++b) lc[b] = slot[colpos<T>(16 * b + c)] * inv2;

@@ -228,7 +228,7 @@ __device__ __forceinline__ ElemIn stage_right(double *dst, const double *e, int 
 
 static size_t op_stage_bytes(int n) { return 2 * (size_t)((2 * n * n + 2 * n + 1) & ~1) * sizeof(double); }
 
-template <int T>
+template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
     extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 operand images (op_stage_bytes)
@@ -254,8 +254,8 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     wave_sync();
     double *o = out + (long long)i * es;
     const int nn = n * n;
-    const bool ok = tcombine_parts<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, eb, n, fcf, true,
-                                      sm, lane);
+    const bool ok = tcombine_parts<T, LU>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, eb, n, fcf,
+                                          true, sm, lane);
     if (!fcf)
         for (int q = lane; q < 2 * n * n + n; q += 64) o[q] = 0.0;  // [F | C | f]
     if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
 // maps x0 through the global prefix of earlier shards (or the identity) and
 // writes x_0 directly.  maps: [b][S+1][Phi | phi], vfun: [b][S+1][P | p].
 // ---------------------------------------------------------------------------
-template <int T>
+template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];  // 2 operand images when A.right
     __shared__ CombSmem<T> sm;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
         const ElemIn eb = stage_right(dyn + op_stage_len(n), right, n, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
-        ok = tcombine_parts<T>(nullptr, nullptr, nullptr, vo, vo + nn, ea, eb, n, false, true, sm, lane);
+        ok = tcombine_parts<T, LU>(nullptr, nullptr, nullptr, vo, vo + nn, ea, eb, n, false, true, sm, lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // vo is re-read by other lanes below
         vP = vo;
         vp = vo + nn;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
             WM<T> Cs, Y, Z, Zt;
             WV<T> pv, v1;
             wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
-            ok = comb_core(Y, Z, Zt, Cs, vP, n, sm, lane) && ok;
+            ok = comb_core_t<T, LU>(Y, Z, Zt, Cs, vP, n, sm, lane) && ok;
             wv_load(pv, vp, n, g, c);
             wv_tn(v1, Cs, pv, n, -1.0, &fs);  // f - C p_j  (C symmetric)
             wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p_j)
@@ -456,8 +456,8 @@ int seg_scan_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const size_t smem = op_stage_bytes(sh.n);
-    hipError_t e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1>, 64, smem)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2>, 64, smem);
+    hipError_t e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1, false>, 64, smem)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2, false>, 64, smem);
     if (e != hipSuccess || per <= 0) per = 1;
     return cus * per;
 }
@@ -470,8 +470,10 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
-    if (T == 1) hipLaunchKernelGGL(k_seg_scan<1>, grid, blk, smem, st, a);
-    else if (T == 2) hipLaunchKernelGGL(k_seg_scan<2>, grid, blk, smem, st, a);
+    if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_scan<1, true>), grid, blk, smem, st, a);
+    else if (T == 1) hipLaunchKernelGGL((k_seg_scan<1, false>), grid, blk, smem, st, a);
+    else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_scan<2, true>), grid, blk, smem, st, a);
+    else if (T == 2) hipLaunchKernelGGL((k_seg_scan<2, false>), grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -481,8 +483,10 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = a.right ? op_stage_bytes(a.n) : 0;
-    if (T == 1) hipLaunchKernelGGL(k_seg_maps<1>, grid, blk, smem, st, a);
-    else if (T == 2) hipLaunchKernelGGL(k_seg_maps<2>, grid, blk, smem, st, a);
+    if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_maps<1, true>), grid, blk, smem, st, a);
+    else if (T == 1) hipLaunchKernelGGL((k_seg_maps<1, false>), grid, blk, smem, st, a);
+    else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_maps<2, true>), grid, blk, smem, st, a);
+    else if (T == 2) hipLaunchKernelGGL((k_seg_maps<2, false>), grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -511,7 +515,7 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
 // the boundary value functions, and a right fold e_j (x) acc reads acc's
 // (P, p) only.  So the prefix chain skips the P path and the suffix chain the
 // F, C path; the unformed blocks are written as zeros.
-template <int T>
+template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int R, int r, int n, int batch,
                                                     double *out_pre_all, double *out_suf_all, int *has_suf, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
         for (int j = 1; j < r; ++j) {
             elem_copy(nx, elems + (long long)j * stride, n, lane);
             wave_sync();
-            if (!tcombine<T>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag + b, 4);
+            if (!tcombine<T, LU>(o, acc, nx, n, true, false, sm, lane) && lane == 0) atomicOr(flag + b, 4);
             wave_sync();
             double *t = acc;
             acc = o;
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
     for (int j = R - 2; j > r; --j) {
         elem_copy(nx, elems + (long long)j * stride, n, lane);
         wave_sync();
-        if (!tcombine<T>(o, nx, acc, n, false, true, sm, lane) && lane == 0) atomicOr(flag + b, 8);
+        if (!tcombine<T, LU>(o, nx, acc, n, false, true, sm, lane) && lane == 0) atomicOr(flag + b, 8);
         wave_sync();
         double *t = acc;
         acc = o;
@@ -574,7 +578,7 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
 // to x0 in turn (k_rank_chain, matrix-vector products only) and writes the
 // prefix element (F = C = 0, f = x at the slice start), which k_seg_maps
 // maps to exactly that state.
-template <int T>
+template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const double *suf, int R, int r, int n,
                                                   int batch, double *maps, int *flag) {
     __shared__ CombSmem<T> sm;
@@ -589,7 +593,7 @@ __global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const
     wm_load(Fs, src, n, n, false, 0.0, g, c);
     wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
     wv_load(fs, src + 2 * nn, n, g, c);
-    const bool ok = comb_core(Y, Z, Zt, Cs, v + 2 * nn + n, n, sm, lane);
+    const bool ok = comb_core_t<T, LU>(Y, Z, Zt, Cs, v + 2 * nn + n, n, sm, lane);
     wv_load(pv, v + 3 * nn + n, n, g, c);
     wv_tn(v1, Cs, pv, n, -1.0, &fs);                     // f - C p  (C symmetric)
     wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p)
@@ -629,14 +633,17 @@ __global__ __launch_bounds__(64) void k_rank_chain(const double *maps, const dou
 }
 
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
-                          double *maps, double *out_pre, int *flag, hipStream_t st) {
+                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st) {
     if (r <= 0) return PDPLQR_OK;
     const int T = tile_order(n);
+    const dim3 gm(batch * r), blk(64);
     if (T == 1) {
-        hipLaunchKernelGGL(k_rank_maps<1>, dim3(batch * r), dim3(64), 0, st, elems, suf, R, r, n, batch, maps, flag);
+        if (lu) hipLaunchKernelGGL((k_rank_maps<1, true>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
+        else hipLaunchKernelGGL((k_rank_maps<1, false>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
         hipLaunchKernelGGL(k_rank_chain<1>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else if (T == 2) {
-        hipLaunchKernelGGL(k_rank_maps<2>, dim3(batch * r), dim3(64), 0, st, elems, suf, R, r, n, batch, maps, flag);
+        if (lu) hipLaunchKernelGGL((k_rank_maps<2, true>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
+        else hipLaunchKernelGGL((k_rank_maps<2, false>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
         hipLaunchKernelGGL(k_rank_chain<2>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else {
         return PDPLQR_ERR_UNSUPPORTED;
@@ -646,14 +653,22 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
 }
 
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
-                       int *has_suf, int *flag, hipStream_t st) {
+                       int *has_suf, int *flag, bool lu, hipStream_t st) {
     const int T = tile_order(n);
-    if (T == 1)
-        hipLaunchKernelGGL(k_fold_shards<1>, dim3(2 * batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
-                           out_pre, out_suf, has_suf, flag);
+    const dim3 gr(2 * batch), blk(64);
+    const size_t sm = elems_smem(n, 3);
+    if (T == 1 && lu)
+        hipLaunchKernelGGL((k_fold_shards<1, true>), gr, blk, sm, st, elems, R, r, n, batch, out_pre, out_suf, has_suf,
+                           flag);
+    else if (T == 1)
+        hipLaunchKernelGGL((k_fold_shards<1, false>), gr, blk, sm, st, elems, R, r, n, batch, out_pre, out_suf,
+                           has_suf, flag);
+    else if (T == 2 && lu)
+        hipLaunchKernelGGL((k_fold_shards<2, true>), gr, blk, sm, st, elems, R, r, n, batch, out_pre, out_suf, has_suf,
+                           flag);
     else if (T == 2)
-        hipLaunchKernelGGL(k_fold_shards<2>, dim3(2 * batch), dim3(64), elems_smem(n, 3), st, elems, R, r, n, batch,
-                           out_pre, out_suf, has_suf, flag);
+        hipLaunchKernelGGL((k_fold_shards<2, false>), gr, blk, sm, st, elems, R, r, n, batch, out_pre, out_suf,
+                           has_suf, flag);
     else
         return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());

@@ -231,12 +231,12 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * 17 + 4 * r + g]);
     }
-    // P_k = Lxx Lxx^T has a positive diagonal whenever M_k is positive definite
+    // P_k = Lxx Lxx^T: semidefinite (psd_bad: non-finite or clearly negative diagonal)
     bool bad = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = 4 * r + g;
-        if (i == c && i >= m && i < s && !(Pm[r] > 0.0)) bad = true;
+        if (i == c && i >= m && i < s && psd_bad(Pm[r])) bad = true;
     }
     return (int)ok & (int)!__any(bad);  // no short-circuit: no branch
 }
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             const int i = 4 * r + g;
             const bool xr = i >= m && i < s;
             prow[r] = xr ? hb[(long long)N * s + (i - m)] : 0.0;
-            if (i == c && xr && !(Pm[r] > 0.0)) bad = true;
+            if (i == c && xr && psd_bad(Pm[r])) bad = true;  // P_N = H~_N semidefinite is valid
         }
         if (__any(bad)) fail_stage = N;
     }

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
                     double v = 0.0;
                     if (last) {
                         if (xi && xj) v = HN[i >= j ? pidx(i - m, j - m, n) : pidx(j - m, i - m, n)];
-                        if (xi && i == j && !(v > 0.0)) bad = true;
+                        if (xi && i == j && psd_bad(v)) bad = true;
                     } else if ((xi && j == i - m + s) || (xj && i == j - m + s)) {
                         v = 1.0;
                     }
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
                         if (i >= m && j >= m && i < s && j < s) {
                             const double v = 0.5 * (Q[a < T ? a : 0][bt < T ? bt : 0][r] + sm.tp[j * 33 + i]);
                             Q[a < T ? a : 0][bt < T ? bt : 0][r] = v;
-                            if (i == j && !(v > 0.0)) bad = true;
+                            if (i == j && psd_bad(v)) bad = true;
                         }
                     }
         ok = ok && !__any(bad);

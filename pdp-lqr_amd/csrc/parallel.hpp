@@ -24,6 +24,7 @@ struct ScanArgs {
     long long istride = 0, bstride = 0;  // element / problem strides of `in` (0: [b][S][es])
     double *out;
     int *flag;                 // [b]: a combine was not positive definite
+    int lu = 0;                // LU form of the combine (CondensedSystemSolverType::LU)
 };
 
 struct MapArgs {
@@ -38,6 +39,7 @@ struct MapArgs {
     double *vfun;              // [b][S+1][n^2 + n]  value functions at the boundaries (P | p)
     double *xhat, *lam;        // [b][S+1][n]
     int *flag;
+    int lu = 0;                // LU form of the combine
 };
 
 struct MapScanArgs {
@@ -68,9 +70,9 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 #endif
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
-                       int *has_suf, int *flag, hipStream_t st);
+                       int *has_suf, int *flag, bool lu, hipStream_t st);
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
-                          double *maps, double *out_pre, int *flag, hipStream_t st);
+                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st);
 

@@ -236,6 +236,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
         s.in = sin;
         s.out = bufs[round & 1];
         s.flag = ps->flag;
+        s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
         int rc = launch_seg_scan(s, sh.batch, h->stream);
         if (rc) return rc;
         sin = s.out;
@@ -264,6 +265,7 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     ma.xhat = ps->xhat;
     ma.lam = ps->lam;
     ma.flag = ps->flag;
+    ma.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
     int rc = launch_seg_maps(ma, sh.batch, h->stream);
     if (rc) return rc;
     double *mb[2] = {ps->mapA, ps->mapB};
@@ -579,6 +581,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
             }
             sa.out = ps->rscan[round & 1];
             sa.flag = ps->flag;
+            sa.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
             if ((rc = launch_seg_scan(sa, sh.batch, h->stream))) return rc;
             sin = sa.out;
         }
@@ -588,13 +591,13 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
         }
         if (r > 0) {
             if ((rc = launch_rank_fold_maps(delems, sin, dx0, R, r, sh.n, sh.batch, ps->rmaps, ps->left, ps->flag,
-                                            h->stream)))
+                                            h->cfg.condensed_type == PDPLQR_CONDENSED_LU, h->stream)))
                 return rc;
             left = ps->left;
         }
     } else {
         rc = launch_fold_shards(delems, num_shards, shard_id, sh.n, sh.batch, ps->left, ps->right, ps->has_suf,
-                                ps->flag, h->stream);
+                                ps->flag, h->cfg.condensed_type == PDPLQR_CONDENSED_LU, h->stream);
         if (rc) return rc;
         left = shard_id > 0 ? ps->left : nullptr;
         right = shard_id + 1 < num_shards ? ps->right : nullptr;

@@ -74,11 +74,22 @@ class HorizonShard:
     """One rank's slice of a horizon-sharded solve (batch problems share the split)."""
 
     def __init__(self, n: int, m: int, N_local: int, batch: int = 1, device: int = 0, segment_len: int = 0,
-                 ncs=None):
+                 ncs=None, condensed: str = "CHOLESKY"):
+        """``condensed`` picks the form of every segment / rank combine, as
+        ``CondensedSystemSolverType`` does for ``LQRParallelSolver``
+        (lqr_solver_parallel.hpp:14-17): CHOLESKY (default; needs positive
+        definite value functions at the boundaries) or LU (semidefinite ones
+        too).  The device segmentation is internal (segment_len); the handle's
+        reference segment count only has to satisfy CHOLESKY's ns >= 2."""
         self.n, self.m, self.N, self.batch = n, m, N_local, batch
         self.es = 3 * n * n + 2 * n
-        self._hd = _Handle(n, m, N_local, batch, _lib.PDPLQR_SOLVER_PARALLEL, num_segments=1,
-                           condensed_type=_lib.PDPLQR_CONDENSED_LU, device=device, keep_factors=True, ncs=ncs,
+        ctype = {"LU": _lib.PDPLQR_CONDENSED_LU, "CHOLESKY": _lib.PDPLQR_CONDENSED_CHOLESKY}[condensed]
+        ns = 2 if ctype == _lib.PDPLQR_CONDENSED_CHOLESKY and N_local >= 3 else 1
+        if ns == 1:
+            ctype = _lib.PDPLQR_CONDENSED_LU  # a slice of < 3 stages: one reference segment
+        self.condensed = "CHOLESKY" if ctype == _lib.PDPLQR_CONDENSED_CHOLESKY else "LU"
+        self._hd = _Handle(n, m, N_local, batch, _lib.PDPLQR_SOLVER_PARALLEL, num_segments=ns,
+                           condensed_type=ctype, device=device, keep_factors=True, ncs=ncs,
                            segment_len=segment_len)
 
     @property

@@ -69,3 +69,18 @@ def boundary_state(pre, suf, x0):
     _, _, _, Ps, ps = suf
     n = Fp.shape[0]
     return np.linalg.solve(np.eye(n) + Cp @ Ps, Fp @ x0 + fp - Cp @ ps)
+
+
+def combine_lu(a, b):
+    """a (x) b in the LU form (condensed_system.hpp:82-137): Z = (I + C_a P_b)^{-1}
+    by a general solve -- no definiteness needed (P_b, C_a semidefinite)."""
+    Fa, Ca, fa, Pa, pa = a
+    Fb, Cb, fb, Pb, pb = b
+    n = Fa.shape[0]
+    Z = np.linalg.solve(np.eye(n) + Ca @ Pb, np.eye(n))
+    F = Fb @ Z @ Fa
+    C = Fb @ Z @ Ca @ Fb.T + Cb
+    f = Fb @ Z @ (fa - Ca @ pb) + fb
+    P = Pa + Fa.T @ Pb @ Z @ Fa
+    p = pa + Fa.T @ Z.T @ (pb + Pb @ fa)
+    return (F, 0.5 * (C + C.T), f, 0.5 * (P + P.T), p)

@@ -1,0 +1,187 @@
+"""GPU: the LU condensed form and the semidefinite edge cases (VERDICT r1
+item 6).  CondensedSystemSolverType.LU runs the LU form of every segment
+combine (combine_tiles.hpp comb_core_lu: Gauss-Jordan with partial pivoting on
+I + P_b C_a, condensed_system.hpp:32-147); CHOLESKY keeps the SPD form
+(R = chol(P_b), :151-299) and reports a singular boundary value function.
+Semidefinite value functions (zero state cost, Q_N = 0, sigma = 0) are valid
+solves of the serial paths, as in the reference (Eigen's LLT stops at the
+first non-positive pivot): status 0 and oracle parity.  Tolerance 1e-9 rel."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from psd_models import psd_model
+from seg_ref import combine, combine_lu
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0
+
+
+def _elem(n, rng, P_rank=None, C_rank=None):
+    F = np.eye(n) + 0.2 * rng.standard_normal((n, n))
+    G = rng.standard_normal((n, n if C_rank is None else C_rank))
+    Cm = G @ G.T / n
+    f = rng.standard_normal(n)
+    Hh = rng.standard_normal((n, n if P_rank is None else P_rank))
+    P = Hh @ Hh.T / n + (np.eye(n) if P_rank is None else 0.0)
+    p = rng.standard_normal(n)
+    return F, Cm, f, P, p
+
+
+def _pack(e):
+    F, Cm, f, P, p = e
+    return np.concatenate([F.ravel(order="F"), Cm.ravel(order="F"), f, P.ravel(order="F"), p])
+
+
+def _unpack(v, n):
+    nn = n * n
+    return (v[:nn].reshape(n, n, order="F"), v[nn:2 * nn].reshape(n, n, order="F"), v[2 * nn:2 * nn + n],
+            v[2 * nn + n:3 * nn + n].reshape(n, n, order="F"), v[3 * nn + n:])
+
+
+def _debug_combine(n, a, b, lu):
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_form.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    va, vb = _pack(a), _pack(b)
+    out = np.zeros_like(va)
+    rc = L.pdplqr_debug_combine_form(n, va.ctypes.data, vb.ctypes.data, out.ctypes.data, int(lu))
+    return rc, _unpack(out, n)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 12, 16, 17, 24, 32])
+@pytest.mark.parametrize("case", ["spd", "P_b_zero", "P_b_rank1", "C_a_rank1"])
+def test_lu_combine_matches_numpy(n, case):
+    rng = np.random.default_rng(300 + n)
+    a = _elem(n, rng, C_rank=1 if case == "C_a_rank1" else None)
+    b = _elem(n, rng, P_rank={"P_b_zero": 0, "P_b_rank1": 1}.get(case))
+    rc, got = _debug_combine(n, a, b, lu=True)
+    assert rc == 0
+    ref = combine_lu(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        assert np.linalg.norm(x - y) <= 1e-11 * max(1.0, np.linalg.norm(y)), name
+    if case == "spd":  # both forms agree where both apply
+        rc2, got2 = _debug_combine(n, a, b, lu=False)
+        assert rc2 == 0
+        for x, y in zip(got2, combine(a, b)):
+            assert np.linalg.norm(x - y) <= 1e-11 * max(1.0, np.linalg.norm(y))
+    else:
+        if case == "P_b_zero" or (case == "P_b_rank1" and n > 1):
+            rc2, _ = _debug_combine(n, a, b, lu=False)
+            assert rc2 != 0  # chol(P_b) of a singular P_b fails: the CHOLESKY form reports it
+
+
+def _oracle(pm, x0):
+    from oracle.oracle import OracleSerial
+
+    o = OracleSerial(pm)
+    o.update_problem_data(np.zeros(pm.N * (pm.n + pm.m) + pm.n), None, None, None, 0.0)
+    o.backward(None)
+    return o.forward(x0)
+
+
+def _run(sol, model, x0):
+    n, m, N = model.n, model.m, model.N
+    ws = [np.zeros(n + m) for _ in range(N)] + [np.zeros(n)]
+    e = [np.zeros(0) for _ in range(N + 1)]
+    sol.update_problem_data(ws, e, e, e, 0.0)
+    sol.backward(e)
+    out = [w.copy() for w in ws]
+    sol.forward(x0, out)
+    return np.concatenate(out), sol.status()
+
+
+@pytest.mark.parametrize("kind", ["zero_state_cost", "zero_terminal"])
+@pytest.mark.parametrize("solver", ["serial_fullfactor", "batched_value_form", "parallel_LU"])
+def test_semidefinite_solves(kind, solver):
+    from pdplqr import BatchedLQRSolver, CondensedSystemSolverType, LQRParallelSolver, LQRSolver
+
+    pm, model, x0 = psd_model(kind)
+    ref = _oracle(pm, x0)
+    if solver == "serial_fullfactor":
+        w, st = _run(LQRSolver(model), model, x0)
+    elif solver == "parallel_LU":
+        w, st = _run(LQRParallelSolver(model, 4, True, CondensedSystemSolverType.LU), model, x0)
+    else:
+        n, m, N = pm.n, pm.m, pm.N
+        bs = BatchedLQRSolver(n, m, N, 2)
+        rep = lambda a: np.ascontiguousarray(np.stack([a, a]))
+        bs.set_model(rep(pm.E), rep(pm.c), rep(pm.H), rep(pm.h))
+        bs.update_problem_data(np.zeros((2, N * (n + m) + n)), sigma=0.0)
+        bs.backward()
+        out = np.zeros((2, N * (n + m) + n))
+        bs.forward(rep(x0), out)
+        w, st = out[1], int(np.max(bs.status()))
+    assert st == 0
+    assert np.all(np.isfinite(w))
+    assert rel_err(w, ref) < TOL
+
+
+def test_parallel_cholesky_reports_singular_boundary():
+    """Zero state cost: P = 0 at every segment boundary; the CHOLESKY form
+    cannot factor it (the reference's condensed backward returns false,
+    ignored at lqr_solver_parallel.hpp:145) -- reported as status N + 2."""
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+
+    pm, model, x0 = psd_model("zero_state_cost")
+    _, st = _run(LQRParallelSolver(model, 4, True, CondensedSystemSolverType.CHOLESKY), model, x0)
+    assert st == pm.N + 2
+
+
+def test_parallel_cholesky_zero_terminal_only():
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+
+    pm, model, x0 = psd_model("zero_terminal")
+    w, st = _run(LQRParallelSolver(model, 4, True, CondensedSystemSolverType.CHOLESKY), model, x0)
+    assert st == 0
+    assert rel_err(w, _oracle(pm, x0)) < TOL
+
+
+@pytest.mark.parametrize("condensed", ["LU", "CHOLESKY"])
+def test_horizon_shards_both_forms(condensed):
+    """Virtual ranks (R = 4) with either combine form on standard data."""
+    from pdplqr.horizon import HorizonShard, slice_arrays, split_horizon
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch, R = 12, 4, 200, 2, 4
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 21)
+    sl = split_horizon(N, R)
+    shards, elems = [], []
+    for r, (N0, N1) in enumerate(sl):
+        last = r == R - 1
+        sh = HorizonShard(n, m, N1 - N0, batch, segment_len=7, condensed=condensed)
+        assert sh.condensed == condensed
+        sh.set_model(*slice_arrays(E, c, H, h, n, m, N, N0, N1, last))
+        sh.update_problem_data(np.zeros((batch, (N1 - N0) * s + n)), sigma=1e-6)
+        e = np.zeros((batch, 3 * n * n + 2 * n))
+        sh.backward(e, last)
+        shards.append(sh)
+        elems.append(e)
+    gathered = np.ascontiguousarray(np.stack(elems))
+    full = np.zeros((batch, N * s + n))
+    for r, (N0, N1) in enumerate(sl):
+        loc = np.zeros((batch, (N1 - N0) * s + n))
+        shards[r].forward(x0, gathered, R, r, loc)
+        full[:, N0 * s:N1 * s] = loc[:, :(N1 - N0) * s]
+        if r == R - 1:
+            full[:, N * s:] = loc[:, (N1 - N0) * s:]
+    from oracle.oracle import OracleSerial
+
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(np.zeros(N * s + n), None, None, None, 1e-6)
+        o.backward(None)
+        assert rel_err(full[b], o.forward(x0[b])) < TOL
