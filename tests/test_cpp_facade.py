@@ -100,3 +100,29 @@ def test_cpp_facade_example_kat(facade_bin, tmp_path):
     """lqr_example.cpp's quadrotor through the C++ facade: u0 = -2.8980566697 (x4)."""
     pm, d, w = _run(facade_bin, str(tmp_path), "quadrotor_N100", ["serial"])
     assert np.allclose(w[:4], [-2.8980566697, 2.8980566697, -2.8980566697, 2.8980566697], rtol=0, atol=5e-10)
+
+
+@pytest.mark.gpu
+def test_reference_example_program(facade_bin):
+    """examples/lqr_example.cpp -- the reference example's quadrotor MPC
+    written against the facade headers -- runs all three solvers on the GPU:
+    the Riccati solvers give the known answer u0 = (-, +, -, +) 2.8980566697,
+    the QDLDL path the rho_dyn-regularised -2.8980026778."""
+    exe = os.path.join(os.path.dirname(facade_bin), "lqr_example")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    blocks = {}
+    cur = None
+    for line in r.stdout.splitlines():
+        if not line.startswith(" "):
+            cur = line.split()[0]
+            blocks[cur] = {}
+        elif line.strip().startswith("u0 ="):
+            blocks[cur]["u0"] = [float(v) for v in line.split("=")[1].split()]
+        elif line.strip().startswith("x_N ="):
+            blocks[cur]["xN"] = [float(v) for v in line.split("=")[1].split()]
+    kat = np.array([-2.8980566697, 2.8980566697, -2.8980566697, 2.8980566697])
+    for name in ("LQRSolver", "LQRParallelSolver(4)"):
+        assert np.allclose(blocks[name]["u0"], kat, rtol=0, atol=5e-10), name
+        assert abs(blocks[name]["xN"][2] - 0.9999999) < 1e-6
+    assert np.allclose(blocks["QDLDLSolver"]["u0"], kat * (2.8980026778 / 2.8980566697), rtol=0, atol=5e-9)
