@@ -169,6 +169,41 @@ int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard,
 int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_all, int32_t num_shards,
                          int32_t shard_id, double *ws, int mem);
 
+/* ---------------------------------------------------------------------- */
+/* ADMM outer loop for conic LQ (new).  The         */
+/* reference stores e_lb <= D_con w <= e_ub (lqr_model.hpp:21-24) and       */
+/* solves the ADMM x-update (update_problem_data / backward / forward,      */
+/* lqr_solver.hpp:41-77), but the outer loop is absent (README.md:8).       */
+/* This runs it on the device for the whole batch: OSQP's iteration        */
+/* (Stellato et al. 2020, Algorithm 1) with the dynamics solved exactly by  */
+/* the handle's solver, projection onto [lb, ub], fixed rho and sigma, and   */
+/* the ADMM residuals of admm.hip's header.  Works with all three solver    */
+/* kinds; iterations >= 2 reuse the first iteration's factorization         */
+/* (backward_without_factorization with keep_factors = 1).                  */
+/* ---------------------------------------------------------------------- */
+typedef struct {
+    double sigma;        /* proximal weight (lqr_example.cpp:170: 1e-6)            */
+    double alpha;        /* over-relaxation, 0 < alpha < 2 (OSQP default 1.6)      */
+    int32_t max_iter;    /* iteration cap                                          */
+    int32_t check_every; /* termination test period (one 4-byte D2H read each)     */
+    double eps_abs, eps_rel; /* tolerances (OSQP defaults 1e-3); 0 = run max_iter  */
+} pdplqr_admm_settings;
+
+void pdplqr_admm_settings_init(pdplqr_admm_settings *s);
+
+/* x0 [batch][n]; lb, ub, rho [batch][ny] (e_lb, e_ub, rho_vecs of          */
+/* lqr_example.cpp:12-50,169); ws [batch][N*s+n], ys, zs [batch][ny]: warm   */
+/* start in, solution out (w^k, y^k, z^k of the last iteration).  After the */
+/* call the handle is "updated and factored" (forward may follow).          */
+int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *s, const double *x0, const double *lb,
+                      const double *ub, const double *rho, double *ws, double *ys, double *zs, int mem);
+
+/* Per-problem outcome of the last admm_solve (host arrays of `batch`        */
+/* entries, each may be NULL): iterations run, 1 if the termination test     */
+/* passed, primal / dual residual at the last test.  Returns the number of   */
+/* iterations of the batch (>= 1) or an error code.                           */
+int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double *prim_res, double *dual_res);
+
 /* Device info helpers (for hosts that do not link HIP). */
 int pdplqr_device_count(int32_t *count);
 

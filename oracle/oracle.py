@@ -291,3 +291,82 @@ def segmentation(N, ns, load_balancing=True):
     b = np.zeros(ns, dtype=np.int32)
     ok = lib().orc_segmentation(N, ns, int(bool(load_balancing)), _i(a), _i(b))
     return bool(ok), a, b
+
+
+def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", sigma=1e-6, alpha=1.6,
+               max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3, **solver_kw):
+    """CPU restatement of the ADMM outer loop (TEST INFRASTRUCTURE).
+
+    Not in the reference (README.md:8).  Restates OSQP's
+    published iteration (Stellato et al. 2020, Algorithm 1) around the
+    reference's x-update protocol, exactly as pdp-lqr_amd/csrc/admm.hip
+    documents it: the LQ solve is this module's restatement of
+    update_problem_data / backward / forward (lqr_solver.hpp:41-77), with
+    backward_without_factorization from iteration 2 on (lqr_solver.hpp:65-70;
+    the QDLDL path re-solves with its first factor), the bounds are
+    e_lb / e_ub of lqr_model.hpp:21-24, and the termination test is the primal
+    residual |Dw - z|_inf and the ADMM dual residual |D^T rho (z+ - z)|_inf
+    with OSQP's absolute/relative tolerances, every check_every iterations and
+    at max_iter.  One problem (PackedModel arrays of one batch entry).
+    Returns (ws, ys, zs, info)."""
+    n, m, N = pm.n, pm.m, pm.N
+    s = n + m
+    ncs = [int(x) for x in pm.ncs]
+    ny = sum(ncs)
+    w = np.zeros(N * s + n) if ws is None else np.array(ws, dtype=np.float64)
+    y = np.zeros(ny) if ys is None else np.array(ys, dtype=np.float64)
+    z = np.zeros(ny) if zs is None else np.array(zs, dtype=np.float64)
+    lb = np.asarray(lb, dtype=np.float64)
+    ub = np.asarray(ub, dtype=np.float64)
+    rho = np.asarray(rho, dtype=np.float64)
+    irho = 1.0 / rho
+    cls = {"serial": OracleSerial, "parallel": OracleParallel, "kkt": OracleKKT}[solver]
+    solv = cls(pm, **solver_kw)
+    # stage blocks: D_k (nc x dim, column-major), w_k, y_k offsets
+    blocks = []
+    doff = yoff = 0
+    for k in range(N + 1):
+        nc, dim = ncs[k], (s if k < N else n)
+        Dk = pm.D[doff:doff + nc * dim].reshape(nc, dim, order="F") if nc else np.zeros((0, dim))
+        blocks.append((k * s, dim, yoff, nc, Dk))
+        doff += nc * dim
+        yoff += nc
+    it = 0
+    conv = False
+    rp = rd = 0.0
+    for it in range(1, max_iter + 1):
+        solv.update_problem_data(w, y if ny else None, z if ny else None, irho if ny else None, sigma)
+        if it == 1:
+            solv.backward(irho if solver == "kkt" else rho)
+        elif solver != "kkt":
+            solv.backward_without_factorization(rho)
+        wt = solv.forward(x0)
+        if ny == 0:
+            w = wt
+            conv = True
+            break
+        check = it == max_iter or it % check_every == 0
+        wn = alpha * wt + (1.0 - alpha) * w
+        zn = np.empty(ny)
+        yn = np.empty(ny)
+        rp = dwm = zm = rd = dty = 0.0
+        for (wo, dim, yo, nc, Dk) in blocks:
+            if nc == 0:
+                continue
+            sl = slice(yo, yo + nc)
+            v = Dk @ wt[wo:wo + dim]
+            vrel = alpha * v + (1.0 - alpha) * z[sl]
+            zn[sl] = np.minimum(np.maximum(vrel + irho[sl] * y[sl], lb[sl]), ub[sl])
+            yn[sl] = y[sl] + rho[sl] * (vrel - zn[sl])
+            if check:
+                dwn = alpha * v + (1.0 - alpha) * (Dk @ w[wo:wo + dim])
+                rp = max(rp, float(np.max(np.abs(dwn - zn[sl]))))
+                dwm = max(dwm, float(np.max(np.abs(dwn))))
+                zm = max(zm, float(np.max(np.abs(zn[sl]))))
+                rd = max(rd, float(np.max(np.abs(Dk.T @ (rho[sl] * (zn[sl] - z[sl]))))))
+                dty = max(dty, float(np.max(np.abs(Dk.T @ yn[sl]))))
+        w, y, z = wn, yn, zn
+        if check and rp <= eps_abs + eps_rel * max(dwm, zm) and rd <= eps_abs + eps_rel * dty:
+            conv = True
+            break
+    return w, y, z, {"iters": it, "converged": conv, "prim_res": rp, "dual_res": rd}

@@ -71,7 +71,8 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 }  // namespace pdplqr
 
 namespace pdplqr { struct ParallelState;
-struct KKTState; }
+struct KKTState;
+struct AdmmState; }
 
 struct pdplqr_handle_s {
     pdplqr_config cfg;
@@ -103,6 +104,8 @@ struct pdplqr_handle_s {
     std::vector<void *> allocs;
     pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)
     pdplqr::KKTState *kkt = nullptr;       // KKT solver state (kkt.hip)
+    pdplqr::AdmmState *admm = nullptr;     // ADMM outer loop state (admm.hip), allocated on first use
+    int admm_iters = 0;                    // iterations of the last admm_solve
     int shard_last = 1;  // last shard_backward's is_last_shard
     // replayable launch sequences of backward / backward_without_factorization /
     // forward (solvers.hip: hipGraph captured on first use per argument set)

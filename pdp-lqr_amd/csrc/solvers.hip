@@ -308,6 +308,7 @@ int solver_init(pdplqr_handle h) {
 
 void solver_release(pdplqr_handle h) {
     graph_release(h);
+    admm_release(h);
     delete h->par;
     h->par = nullptr;
     kkt_release(h);
@@ -410,6 +411,13 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho) {
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, last, false);
         return launch_riccati_backward_nofact(riccati_args(h), h->stream);
     });
+}
+
+int solver_backward_prepared(pdplqr_handle h) {
+    const bool fact = h->Lc == nullptr || h->lpc == nullptr;
+    if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1, fact);
+    return fact ? launch_riccati_backward(riccati_args(h), h->stream)
+                : launch_riccati_backward_nofact(riccati_args(h), h->stream);
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {

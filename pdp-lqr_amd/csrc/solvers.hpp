@@ -10,6 +10,12 @@ int solver_update(pdplqr_handle h, const double *ws, const double *ys, const dou
                   double sigma);
 int solver_backward(pdplqr_handle h, const double *rho);
 int solver_backward_nofact(pdplqr_handle h, const double *rho);
+// Riccati solvers: backward on a workspace whose rho penalty is already folded
+// in (H~ from the last factorizing backward, h~ formed by k_admm_update):
+// backward_without_factorization when the factors are kept, else the
+// factorizing kernels on the unchanged H~
+int solver_backward_prepared(pdplqr_handle h);
+void admm_release(pdplqr_handle h);  // admm.hip
 int solver_forward(pdplqr_handle h, const double *x0, double *ws);
 int solver_clear(pdplqr_handle h);
 int solver_status(pdplqr_handle h, int32_t *flags);  // per-problem status (host)

@@ -30,6 +30,7 @@ EXPORTS = [
     "pdplqr_backward", "pdplqr_backward_without_factorization", "pdplqr_forward", "pdplqr_clear_workspace",
     "pdplqr_get_value_function", "pdplqr_get_status", "pdplqr_get_segments", "pdplqr_shard_element_size",
     "pdplqr_shard_backward", "pdplqr_shard_forward", "pdplqr_device_count",
+    "pdplqr_admm_settings_init", "pdplqr_admm_solve", "pdplqr_admm_info",
 ]
 
 
@@ -46,6 +47,13 @@ class Config(C.Structure):
         ("condensed_type", C.c_int32), ("device", C.c_int32), ("keep_factors", C.c_int32),
         ("ncs", C.POINTER(C.c_int32)), ("rho_dyn", C.c_double), ("kkt_sigma", C.c_double),
         ("segment_len", C.c_int32),
+    ]
+
+
+class AdmmSettings(C.Structure):
+    _fields_ = [
+        ("sigma", C.c_double), ("alpha", C.c_double), ("max_iter", C.c_int32), ("check_every", C.c_int32),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
     ]
 
 
@@ -92,9 +100,13 @@ def lib() -> C.CDLL:
     L.pdplqr_shard_backward.argtypes = [vp, dp, C.c_int, dp, C.c_int]
     L.pdplqr_shard_forward.argtypes = [vp, dp, dp, i32, i32, dp, C.c_int]
     L.pdplqr_device_count.argtypes = [ip]
+    L.pdplqr_admm_settings_init.argtypes = [C.POINTER(AdmmSettings)]
+    L.pdplqr_admm_settings_init.restype = None
+    L.pdplqr_admm_solve.argtypes = [vp, C.POINTER(AdmmSettings), dp, dp, dp, dp, dp, dp, dp, C.c_int]
+    L.pdplqr_admm_info.argtypes = [vp, ip, ip, dp, dp]
     for nm in EXPORTS:
         f = getattr(L, nm)
-        if nm not in ("pdplqr_config_init", "pdplqr_last_error", "pdplqr_get_stream"):
+        if nm not in ("pdplqr_config_init", "pdplqr_last_error", "pdplqr_get_stream", "pdplqr_admm_settings_init"):
             f.restype = C.c_int
     _lib = L
     return L

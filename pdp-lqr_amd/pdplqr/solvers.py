@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import Config, check, lib
+from ._lib import AdmmSettings, Config, check, lib
 from .model import LQRModel, pack_model, pack_stage_vectors, w_sizes
 
 
@@ -197,12 +197,39 @@ class _Handle:
                                               C.c_void_p(p.ctypes.data)))
         return P.reshape(n, n, order="F"), p
 
+    def admm_solve(self, x0, lb, ub, rho, ws, ys, zs, settings: "AdmmSettings"):
+        ps = [_ptr(x0, "x0"), _ptr(lb, "lb"), _ptr(ub, "ub"), _ptr(rho, "rho"), _ptr(ws, "ws"), _ptr(ys, "ys"),
+              _ptr(zs, "zs")]
+        mem = _mem_of(*ps)
+        cur = self._enter(x0, lb, ub, rho, ws, ys, zs)
+        check(lib().pdplqr_admm_solve(self.h, C.byref(settings), *[p[0] for p in ps], mem))
+        self._leave(cur)
+
+    def admm_info(self):
+        it = np.zeros(self.batch, dtype=np.int32)
+        cv = np.zeros(self.batch, dtype=np.int32)
+        rp = np.zeros(self.batch)
+        rd = np.zeros(self.batch)
+        i32 = C.POINTER(C.c_int32)
+        n = check(lib().pdplqr_admm_info(self.h, it.ctypes.data_as(i32), cv.ctypes.data_as(i32),
+                                         C.c_void_p(rp.ctypes.data), C.c_void_p(rd.ctypes.data)))
+        return {"iterations": int(n), "iters": it, "converged": cv.astype(bool), "prim_res": rp, "dual_res": rd}
+
     def segments(self, ns: int):
         a = np.zeros(ns, dtype=np.int32)
         b = np.zeros(ns, dtype=np.int32)
         check(lib().pdplqr_get_segments(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)),
                                         b.ctypes.data_as(C.POINTER(C.c_int32))))
         return a, b
+
+
+def admm_settings(sigma=1e-6, alpha=1.6, max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3) -> AdmmSettings:
+    st = AdmmSettings()
+    lib().pdplqr_admm_settings_init(C.byref(st))
+    st.sigma, st.alpha = float(sigma), float(alpha)
+    st.max_iter, st.check_every = int(max_iter), int(check_every)
+    st.eps_abs, st.eps_rel = float(eps_abs), float(eps_rel)
+    return st
 
 
 def _stage_vecs(model: LQRModel, vecs, what):
@@ -256,6 +283,38 @@ class _ModelSolver:
 
     def status(self) -> int:
         return int(self._hd.status()[0])
+
+    def admm_solve(self, x0, ws: List[np.ndarray], ys, zs, rho_vecs, sigma: float = 1e-6, alpha: float = 1.6,
+                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3):
+        """ADMM outer loop over this solver (new: absent in the reference,
+        README.md:8) for the bounds ``e_lb <= D_con w <= e_ub`` stored in the
+        model's nodes (lqr_model.hpp:21-24).  ``ws, ys, zs`` are the warm start
+        (``initialize_vectors``) and are overwritten in place with the solution;
+        ``rho_vecs`` as the reference's.  Returns admm_info() of problem 0."""
+        m = self.model_
+        if self._reupload_model:
+            self._upload_model()
+        ncs = [int(x) for x in m.ncs]
+        w = np.ascontiguousarray(pack_stage_vectors(ws, w_sizes(m.n, m.m, m.N)))
+        lb = np.ascontiguousarray(pack_stage_vectors([nd.e_lb for nd in m.nodes], ncs)) if self._hd.ny else None
+        ub = np.ascontiguousarray(pack_stage_vectors([nd.e_ub for nd in m.nodes], ncs)) if self._hd.ny else None
+        y, z, r = self._y(ys), self._y(zs), self._y(rho_vecs)
+        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel)
+        self._hd.admm_solve(np.ascontiguousarray(x0, dtype=np.float64), lb, ub, r, w, y, z, st)
+        s = m.n + m.m
+        for k in range(m.N):
+            ws[k][:] = w[k * s:(k + 1) * s]
+        ws[m.N][:] = w[m.N * s:]
+        off = 0
+        for k, nc in enumerate(ncs):
+            if nc:
+                ys[k][:] = y[off:off + nc]
+                zs[k][:] = z[off:off + nc]
+            off += nc
+        info = self._hd.admm_info()
+        return {"iterations": info["iterations"], "iters": int(info["iters"][0]),
+                "converged": bool(info["converged"][0]), "prim_res": float(info["prim_res"][0]),
+                "dual_res": float(info["dual_res"][0])}
 
 
 class LQRSolver(_ModelSolver):
@@ -350,6 +409,18 @@ class BatchedLQRSolver:
 
     def status(self):
         return self._hd.status()
+
+    def admm_solve(self, x0, lb, ub, rho, ws, ys=None, zs=None, sigma: float = 1e-6, alpha: float = 1.6,
+                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3):
+        """ADMM outer loop for the box constraints lb <= D w <= ub on the device
+        (include/pdplqr.h: pdplqr_admm_solve).  ws/ys/zs hold the warm start and
+        are overwritten with the solution; returns admm_info()."""
+        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel)
+        self._hd.admm_solve(x0, lb, ub, rho, ws, ys, zs, st)
+        return self._hd.admm_info()
+
+    def admm_info(self):
+        return self._hd.admm_info()
 
     def value_function(self, b, k):
         return self._hd.value_function(b, k)
