@@ -298,6 +298,43 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
         res["kkt" if solver == "kkt" else "riccati"] = {"ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
                                                         "status_ok": ok}
         bs.close()
+    # the ADMM outer loop on the same data (pdplqr_admm_solve): |u| <= 0.5,
+    # rho = 1, from a cold start.  (a) 100 fixed iterations (eps = 0, one
+    # termination test at the end): iterations/s of the batch; (b) a run to
+    # OSQP's default tolerances (1e-3, test every 25 iterations, at most 500).
+    lb = torch.full((batch, ny), -0.5, dtype=torch.float64, device=dev)
+    ub = torch.full((batch, ny), 0.5, dtype=torch.float64, device=dev)
+    rho1 = torch.full((batch, ny), 1.0, dtype=torch.float64, device=dev)
+    w0 = torch.zeros(batch, N * s + n, dtype=torch.float64, device=dev)
+    y0 = torch.zeros(batch, ny, dtype=torch.float64, device=dev)
+    wa, ya, za = w0.clone(), y0.clone(), y0.clone()
+    for solver in ("serial", "kkt"):
+        bs = BatchedLQRSolver(n, m, N, batch, solver=solver, ncs=ncs, keep_factors=(solver == "serial"),
+                              device=local)
+        bs.set_model(E, c, H, h, D)
+        iters = 100 if solver == "serial" else 30
+
+        def step():
+            wa.copy_(w0)
+            ya.zero_()
+            za.zero_()
+            bs.admm_solve(x0, lb, ub, rho1, wa, ya, za, max_iter=iters, check_every=iters, eps_abs=0.0, eps_rel=0.0)
+
+        t = _timed(step, max(1, steps // 2), 1, dev, dist)
+        ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(wa).all().item())
+        wa.copy_(w0)
+        ya.zero_()
+        za.zero_()
+        t0 = time.perf_counter()
+        info = bs.admm_solve(x0, lb, ub, rho1, wa, ya, za, max_iter=500)
+        torch.cuda.synchronize(dev)
+        t_conv = time.perf_counter() - t0
+        res[f"admm_{'riccati' if solver == 'serial' else 'kkt'}"] = {
+            "iterations": iters, "ms_per_iteration": t * 1e3 / iters, "iterations_per_s": iters / t,
+            "stages_per_s": N * batch * iters / t, "status_ok": ok,
+            "to_tolerance": {"eps": 1e-3, "iterations": info["iterations"],
+                             "converged_frac": float(np.mean(info["converged"])), "ms": t_conv * 1e3}}
+        bs.close()
     del E, H, D
     torch.cuda.empty_cache()
     return res

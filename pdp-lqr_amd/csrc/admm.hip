@@ -26,8 +26,8 @@
 //
 // With rho fixed the stage matrices never change after the first backward, so
 // iterations >= 2 need only vectors:
-//   * k_admm_update (one thread per stage, one 64-stage wave per problem slice)
-//     does the z/y/w step AND the next update_problem_data + penalty linear
+//   * k_admm_update (one block per problem, LPS lanes per stage) does the
+//     z/y/w step, the termination test AND the next update_problem_data + penalty linear
 //     term in the same pass: h~ = h - sigma w^{k+1} - D^T (rho o g^{k+1}),
 //     g^{k+1} = z^{k+1} - inv_rho o y^{k+1} -- in the same operation order as
 //     k_update_problem_data followed by k_penalty, so the fused and the
@@ -47,10 +47,8 @@ struct AdmmState {
     double *wt = nullptr;  // LQ solution of the current iteration (forward output)
     double *w = nullptr, *y = nullptr, *z = nullptr;
     double *lb = nullptr, *ub = nullptr, *rho = nullptr, *irho = nullptr;
-    double *dzr = nullptr;  // rho o (z^{k+1} - z^k), scratch of the residual pass
     double *x0 = nullptr;
     double *prim = nullptr, *dual = nullptr;  // [b] residuals at the last check
-    unsigned long long *acc = nullptr;         // [b][5] running maxima (bit patterns of non-negative doubles)
     int32_t *done = nullptr, *iters = nullptr, *conv = nullptr, *active = nullptr;
     int32_t *active_h = nullptr;  // pinned
 };
@@ -58,13 +56,22 @@ struct AdmmState {
 struct AdmmArgs {
     Shape sh;
     const double *D, *hv, *wt, *lb, *ub, *rho, *irho;
-    double *w, *y, *z, *dzr, *hw, *gw;
-    const int32_t *d_off, *y_off, *done;
-    unsigned long long *acc;
-    double alpha, sigma;
+    double *w, *y, *z, *hw, *gw;
+    const int32_t *d_off, *y_off;
+    int32_t *done, *iters, *conv, *active;
+    double *prim, *dual;
+    double alpha, sigma, eps_abs, eps_rel;
+    int max_nc, it;
 };
 
-enum { ACC_PRIM = 0, ACC_DW = 1, ACC_Z = 2, ACC_DUAL = 3, ACC_DTY = 4, ACC_N = 5 };
+// sum over the LPS lanes of one stage (xor butterflies: every lane ends with
+// the same bits)
+template <int LPS>
+__device__ __forceinline__ double stage_sum(double v) {
+#pragma unroll
+    for (int m = 1; m < LPS; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
 
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -72,119 +79,138 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
-// grid (ceil((N + 1) / 256), batch), 256 threads: thread = stage k of problem b
-template <bool FUSE, bool CHECK>
+// One 256-thread block per problem.  A stage takes LPS lanes (one per entry
+// of w_k: LPS = 16 for s <= 16, 32 for s <= 32), so a wave covers 64 / LPS
+// consecutive stages with coalesced w / w~ / h loads; the block strides over
+// the horizon.  Row r of D_k w~ is a butterfly sum over the stage's lanes;
+// every lane then holds the row's new z, y, g and adds its column's share of
+// D^T (rho o g), D^T rho (z+ - z), D^T y+ on the spot (no second pass).
+// CHECK: the five maxima of the termination test reduce over the block and
+// thread 0 decides (OSQP's test, admm.hip header), so there is no separate
+// check launch and no atomics on the residuals.
+template <int LPS, bool FUSE, bool CHECK>
 __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
     const Shape &sh = a.sh;
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool act = k <= sh.N && a.done[b] == 0;
+    const int b = blockIdx.x;
+    if (a.done[b]) return;  // block-uniform
+    constexpr int SPW = 64 / LPS;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane / LPS, j = lane % LPS;
+    const double al = a.alpha, bl = 1.0 - a.alpha;
     double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
-    if (act) {
-        const int dim = k < sh.N ? sh.s : sh.n;
-        const long long wo = (long long)b * sh.perh + (long long)k * sh.s;
-        const int yo0 = a.y_off[k], nc = a.y_off[k + 1] - yo0;
+    for (int kb = wv * SPW; kb <= sh.N; kb += 4 * SPW) {
+        // wave-uniform trip count: lanes past the horizon idle in the loop
+        const int k = kb + sub;
+        const bool stg = k <= sh.N;
+        const int kk = stg ? k : sh.N;
+        const int dim = kk < sh.N ? sh.s : sh.n;
+        const bool col = stg && j < dim;
+        const long long wo = (long long)b * sh.perh + (long long)kk * sh.s + (j < dim ? j : 0);
+        const int yo0 = a.y_off[kk], nc = stg ? a.y_off[kk + 1] - yo0 : 0;
         const long long yo = (long long)b * sh.ny + yo0;
-        const double *Dk = a.D + (long long)b * sh.ndD + a.d_off[k];
-        const double *wt = a.wt + wo;
-        double *w = a.w + wo;
-        const double al = a.alpha, bl = 1.0 - a.alpha;
-        for (int r = 0; r < nc; ++r) {
-            double v = 0.0, vw = 0.0;
-            for (int j = 0; j < dim; ++j) {
-                const double d = Dk[r + j * nc];
-                v += d * wt[j];
-                vw += d * w[j];
-            }
-            const double zr = a.z[yo + r], yr = a.y[yo + r], rr = a.rho[yo + r], ir = a.irho[yo + r];
-            const double vrel = al * v + bl * zr;
-            const double zn = fmin(fmax(vrel + ir * yr, a.lb[yo + r]), a.ub[yo + r]);
-            const double yn = yr + rr * (vrel - zn);
-            a.z[yo + r] = zn;
-            a.y[yo + r] = yn;
-            if (FUSE) a.gw[yo + r] = zn - ir * yn;
-            if (CHECK) {
-                a.dzr[yo + r] = rr * (zn - zr);
-                const double dwn = al * v + bl * vw;  // D w^{k+1}
-                rp = fmax(rp, fabs(dwn - zn));
-                dwm = fmax(dwm, fabs(dwn));
-                zm = fmax(zm, fabs(zn));
+        const double *Dk = a.D + (long long)b * sh.ndD + a.d_off[kk];
+        const double wtj = col ? a.wt[wo] : 0.0, wj = col ? a.w[wo] : 0.0;
+        const double wn = al * wtj + bl * wj;
+        double ag = 0.0, ad = 0.0, ay = 0.0;
+        for (int r = 0; r < a.max_nc; ++r) {
+            const bool row = r < nc;
+            const double d = (row && col) ? Dk[r + j * nc] : 0.0;
+            const double v = stage_sum<LPS>(d * wtj);
+            const double vw = stage_sum<LPS>(d * wj);
+            if (row) {
+                const double zr = a.z[yo + r], yr = a.y[yo + r], rr = a.rho[yo + r], ir = a.irho[yo + r];
+                const double vrel = al * v + bl * zr;
+                const double zn = fmin(fmax(vrel + ir * yr, a.lb[yo + r]), a.ub[yo + r]);
+                const double yn = yr + rr * (vrel - zn);
+                const double gn = zn - ir * yn;
+                if (j == 0) {
+                    a.z[yo + r] = zn;
+                    a.y[yo + r] = yn;
+                    if (FUSE) a.gw[yo + r] = gn;
+                }
+                if (FUSE) ag += d * (rr * gn);  // k_penalty's order: D[q][i] * (rho_q * g_q)
+                if (CHECK) {
+                    const double dwn = al * v + bl * vw;  // D w^{k+1}
+                    rp = fmax(rp, fabs(dwn - zn));
+                    dwm = fmax(dwm, fabs(dwn));
+                    zm = fmax(zm, fabs(zn));
+                    ad += d * (rr * (zn - zr));
+                    ay += d * yn;
+                }
             }
         }
-        const double *hk = a.hv + wo;
-        double *hwk = a.hw + wo;
-        const double *gk = a.gw + yo;
-        for (int j = 0; j < dim; ++j) {
-            const double wn = al * wt[j] + bl * w[j];
-            w[j] = wn;
-            if (FUSE || CHECK) {
-                double ag = 0.0, ad = 0.0, ay = 0.0;
-                for (int r = 0; r < nc; ++r) {
-                    const double d = Dk[r + j * nc];
-                    if (FUSE) ag += d * (a.rho[yo + r] * gk[r]);
-                    if (CHECK) {
-                        ad += d * a.dzr[yo + r];
-                        ay += d * a.y[yo + r];
-                    }
-                }
-                if (FUSE) {
-                    // k_update_problem_data then k_penalty: (h - sigma w) - sum
-                    double hj = hk[j] - a.sigma * wn;
-                    if (nc > 0) hj -= ag;
-                    hwk[j] = hj;
-                }
-                if (CHECK) {
-                    rd = fmax(rd, fabs(ad));
-                    dty = fmax(dty, fabs(ay));
-                }
+        if (col) {
+            a.w[wo] = wn;
+            if (FUSE) {
+                // k_update_problem_data then k_penalty: (h - sigma w) - sum
+                double hj = a.hv[wo] - a.sigma * wn;
+                if (nc > 0) hj -= ag;
+                a.hw[wo] = hj;
             }
+        }
+        if (CHECK) {
+            rd = fmax(rd, fabs(ad));
+            dty = fmax(dty, fabs(ay));
         }
     }
     if (CHECK) {
-        // one problem per block: wave maxima, then one atomic per wave
+        __shared__ double red[4][5];
         rp = wave_max(rp);
         dwm = wave_max(dwm);
         zm = wave_max(zm);
         rd = wave_max(rd);
         dty = wave_max(dty);
-        if ((threadIdx.x & 63) == 0 && a.done[b] == 0) {
-            unsigned long long *ac = a.acc + (long long)b * ACC_N;
-            atomicMax(ac + ACC_PRIM, (unsigned long long)__double_as_longlong(rp));
-            atomicMax(ac + ACC_DW, (unsigned long long)__double_as_longlong(dwm));
-            atomicMax(ac + ACC_Z, (unsigned long long)__double_as_longlong(zm));
-            atomicMax(ac + ACC_DUAL, (unsigned long long)__double_as_longlong(rd));
-            atomicMax(ac + ACC_DTY, (unsigned long long)__double_as_longlong(dty));
+        if (lane == 0) {
+            red[wv][0] = rp;
+            red[wv][1] = dwm;
+            red[wv][2] = zm;
+            red[wv][3] = rd;
+            red[wv][4] = dty;
         }
-    }
-}
-
-// per problem: termination test of iteration `it`, then reset the maxima
-__global__ void k_admm_check(int batch, int it, double eps_abs, double eps_rel, unsigned long long *acc,
-                             int32_t *done, int32_t *iters, int32_t *conv, double *prim, double *dual,
-                             int32_t *active) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= batch || done[b]) return;
-    unsigned long long *ac = acc + (long long)b * ACC_N;
-    const double rp = __longlong_as_double((long long)ac[ACC_PRIM]), dw = __longlong_as_double((long long)ac[ACC_DW]),
-                 zm = __longlong_as_double((long long)ac[ACC_Z]), rd = __longlong_as_double((long long)ac[ACC_DUAL]),
-                 dty = __longlong_as_double((long long)ac[ACC_DTY]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
 #pragma unroll
-    for (int q = 0; q < ACC_N; ++q) ac[q] = 0ull;
-    iters[b] = it;
-    prim[b] = rp;
-    dual[b] = rd;
-    const bool ok = rp <= eps_abs + eps_rel * fmax(dw, zm) && rd <= eps_abs + eps_rel * dty;
-    if (ok) {
-        done[b] = 1;
-        conv[b] = 1;
-    } else {
-        atomicAdd(active, 1);
+            for (int q = 1; q < 4; ++q) {
+                rp = fmax(rp, red[q][0]);
+                dwm = fmax(dwm, red[q][1]);
+                zm = fmax(zm, red[q][2]);
+                rd = fmax(rd, red[q][3]);
+                dty = fmax(dty, red[q][4]);
+            }
+            a.iters[b] = a.it;
+            a.prim[b] = rp;
+            a.dual[b] = rd;
+            if (rp <= a.eps_abs + a.eps_rel * fmax(dwm, zm) && rd <= a.eps_abs + a.eps_rel * dty) {
+                a.done[b] = 1;
+                a.conv[b] = 1;
+            } else {
+                atomicAdd(a.active, 1);
+            }
+        }
     }
 }
 
 __global__ void k_admm_init(long long ny_total, const double *__restrict__ rho, double *__restrict__ irho) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < ny_total) irho[t] = 1.0 / rho[t];
+}
+
+static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check, dim3 grid, dim3 blk,
+                              hipStream_t S) {
+#define PDPLQR_ADMM_LAUNCH(L, F, C) hipLaunchKernelGGL((k_admm_update<L, F, C>), grid, blk, 0, S, a)
+    if (l16) {
+        if (fuse && check) PDPLQR_ADMM_LAUNCH(16, true, true);
+        else if (fuse) PDPLQR_ADMM_LAUNCH(16, true, false);
+        else if (check) PDPLQR_ADMM_LAUNCH(16, false, true);
+        else PDPLQR_ADMM_LAUNCH(16, false, false);
+    } else {
+        if (fuse && check) PDPLQR_ADMM_LAUNCH(32, true, true);
+        else if (fuse) PDPLQR_ADMM_LAUNCH(32, true, false);
+        else if (check) PDPLQR_ADMM_LAUNCH(32, false, true);
+        else PDPLQR_ADMM_LAUNCH(32, false, false);
+    }
+#undef PDPLQR_ADMM_LAUNCH
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
 }
 
 template <typename X>
@@ -210,9 +236,9 @@ static int admm_alloc(pdplqr_handle h) {
     int rc;
     if ((rc = aalloc(h, &s->wt, W)) || (rc = aalloc(h, &s->w, W)) || (rc = aalloc(h, &s->y, Y)) ||
         (rc = aalloc(h, &s->z, Y)) || (rc = aalloc(h, &s->lb, Y)) || (rc = aalloc(h, &s->ub, Y)) ||
-        (rc = aalloc(h, &s->rho, Y)) || (rc = aalloc(h, &s->irho, Y)) || (rc = aalloc(h, &s->dzr, Y)) ||
+        (rc = aalloc(h, &s->rho, Y)) || (rc = aalloc(h, &s->irho, Y)) ||
         (rc = aalloc(h, &s->x0, B * sh.n)) || (rc = aalloc(h, &s->prim, B)) || (rc = aalloc(h, &s->dual, B)) ||
-        (rc = aalloc(h, &s->acc, B * ACC_N)) || (rc = aalloc(h, &s->done, B)) || (rc = aalloc(h, &s->iters, B)) ||
+        (rc = aalloc(h, &s->done, B)) || (rc = aalloc(h, &s->iters, B)) ||
         (rc = aalloc(h, &s->conv, B)) || (rc = aalloc(h, &s->active, 1)))
         return rc;
     PDPLQR_HIP_TRY(hipHostMalloc((void **)&s->active_h, sizeof(int32_t), hipHostMallocDefault));
@@ -281,7 +307,6 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         hipLaunchKernelGGL(k_admm_init, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, s->rho, s->irho);
         PDPLQR_HIP_TRY(hipGetLastError());
     }
-    PDPLQR_HIP_TRY(hipMemsetAsync(s->acc, 0, B * ACC_N * sizeof(unsigned long long), S));
     PDPLQR_HIP_TRY(hipMemsetAsync(s->done, 0, B * sizeof(int32_t), S));
     PDPLQR_HIP_TRY(hipMemsetAsync(s->conv, 0, B * sizeof(int32_t), S));
     PDPLQR_HIP_TRY(hipMemsetAsync(s->iters, 0, B * sizeof(int32_t), S));
@@ -301,16 +326,23 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     a.w = s->w;
     a.y = s->y;
     a.z = s->z;
-    a.dzr = s->dzr;
     a.hw = h->hw;
     a.gw = h->gw;
     a.d_off = h->d_off;
     a.y_off = h->y_off;
     a.done = s->done;
-    a.acc = s->acc;
+    a.iters = s->iters;
+    a.conv = s->conv;
+    a.active = s->active;
+    a.prim = s->prim;
+    a.dual = s->dual;
     a.alpha = st->alpha;
     a.sigma = st->sigma;
-    const dim3 ugrid((unsigned)((sh.N + 1 + 255) / 256), (unsigned)B), ublk(256);
+    a.eps_abs = st->eps_abs;
+    a.eps_rel = st->eps_rel;
+    a.max_nc = h->max_nc;
+    a.it = 0;
+    const dim3 ugrid((unsigned)B), ublk(256);
     const double *irho_or_null = Y > 0 ? s->irho : nullptr;
     int it = 1;
     for (;; ++it) {
@@ -337,17 +369,10 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         const bool last = it >= st->max_iter;
         const bool check = last || it % st->check_every == 0;
         const bool fuse = !kkt && !last;
-        if (fuse && check) hipLaunchKernelGGL((k_admm_update<true, true>), ugrid, ublk, 0, S, a);
-        else if (fuse) hipLaunchKernelGGL((k_admm_update<true, false>), ugrid, ublk, 0, S, a);
-        else if (check) hipLaunchKernelGGL((k_admm_update<false, true>), ugrid, ublk, 0, S, a);
-        else hipLaunchKernelGGL((k_admm_update<false, false>), ugrid, ublk, 0, S, a);
-        PDPLQR_HIP_TRY(hipGetLastError());
+        a.it = it;
+        if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, sizeof(int32_t), S));
+        if ((rc = launch_admm_update(a, sh.s <= 16, fuse, check, ugrid, ublk, S))) return rc;
         if (check) {
-            PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, sizeof(int32_t), S));
-            hipLaunchKernelGGL(k_admm_check, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, S, (int)B, it,
-                               st->eps_abs, st->eps_rel, s->acc, s->done, s->iters, s->conv, s->prim, s->dual,
-                               s->active);
-            PDPLQR_HIP_TRY(hipGetLastError());
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, sizeof(int32_t), hipMemcpyDeviceToHost, S));
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));
             if (*s->active_h == 0) break;

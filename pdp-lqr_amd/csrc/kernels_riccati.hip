@@ -548,6 +548,11 @@ __global__ __launch_bounds__(64) void k_riccati_bwd_nofact(RiccatiArgs A) {
 }
 
 int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st) {
+    // compile-time shapes: the streamed vector recursion (kernels_nofact.hip)
+    if (!getenv("PDPLQR_NO_NOFACT_DMA")) {
+        const int rc = launch_nofact_dma(a, st);
+        if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
+    }
     if (a.sh.s > 32) {
         set_error("backward_without_factorization: n + m > 32 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;

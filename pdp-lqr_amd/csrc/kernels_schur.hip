@@ -42,16 +42,17 @@ struct SchurIn {
 // packed lower H~ (s), h~ (s).  Works on global memory and on the LDS copy.
 // Branch-free: addresses are clamped into the record and the values masked
 // (a guarded LDS read compiles to an exec-mask region per element).
+// `lde` is E's column stride (n in HBM; padded in the LDS copy, see SchurShape).
 __device__ __forceinline__ void schur_load(SchurIn &in, const double *__restrict__ Ek, const double *__restrict__ ck,
                                            const double *__restrict__ Hk, const double *__restrict__ hk, int n,
-                                           int m, int s, int g, int c) {
+                                           int m, int s, int g, int c, int lde) {
     const int cc = c < s ? c : s - 1;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
         const int t = 4 * kk + g - m;
         const bool xr = t >= 0 && t < n;
         const int tc = t < 0 ? 0 : (t < n ? t : n - 1);
-        const double e = Ek[tc + cc * n], cv = ck[tc];
+        const double e = Ek[tc + cc * lde], cv = ck[tc];
         in.E[kk] = (xr && c < s) ? e : 0.0;
         in.ct[kk] = xr ? cv : 0.0;
     }
@@ -66,13 +67,28 @@ __device__ __forceinline__ void schur_load(SchurIn &in, const double *__restrict
     in.h = (c < s) ? hv : 0.0;
 }
 
+// LDS layouts chosen by the bank rule of ds_read_b64 (32-lane halves, bank =
+// double index mod 32; MI355X_MICROARCH.md section LDS): PDPLQR_LDS_PAD = 1
+//   * P's transpose with leading dimension 18 (2 x odd): the read c * 18 + 4 r + g
+//     of a half (g in {0,1} or {2,3}, c = 0..15) hits 32 distinct banks
+//     (stride 17 puts (c = 15, g = 1) on (c = 0, g = 0): 2-way);
+//   * E's columns in the staged record at stride 14 instead of 12 (below);
+//   * lp_k written by row group 0 only.
+// Measured (profiles/r02, same box, interleaved): SQ_LDS_BANK_CONFLICT
+// 149 -> 130 M cycles per launch, backward 3.13 -> 3.14 ms (no gain: the
+// conflicts sit on the LDS pipe beside the VALU / MFMA chain), so it is off.
+#ifndef PDPLQR_LDS_PAD
+#define PDPLQR_LDS_PAD 0
+#endif
+#define PDPLQR_TP_LD (PDPLQR_LDS_PAD ? 18 : 17)
+
 struct SchurSmem {
     alignas(16) double col[64];  // pivot-row broadcast, one slot per row group (colpos order)
     alignas(16) double lpt[16];  // lp_k, column -> row redistribution (colpos order)
     double inv[16];              // 1 / sqrt(pivot), u columns
     double luq[16];              // lu' = Luu^{-1} lu
     union {
-        double tp[16 * 17];           // transpose of P_k (odd leading dimension: conflict-free)
+        double tp[16 * PDPLQR_TP_LD];  // transpose of P_k (leading dimension: see PDPLQR_TP_LD)
         alignas(16) double rec[128];  // rollout record staging (one coalesced store per stage)
     };
 };
@@ -194,7 +210,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
             part = __builtin_fma(in.E[kk], prow[kk], part);
         }
     part = sum_groups(part);
-    sm.lpt[colpos<1>(c)] = in.h + part;  // every group holds the same sum: no branch
+    if (!PDPLQR_LDS_PAD || g == 0) sm.lpt[colpos<1>(c)] = in.h + part;  // every group holds the same sum
     wave_sync();
     double lpr[1][4];
     {
@@ -226,10 +242,10 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
     // the LDS round trip leaves the other stages' chains.
     if (SYM && sym_rt) {  // wave-uniform
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sm.tp[(4 * r + g) * 17 + c] = Pm[r];
+        for (int r = 0; r < 4; ++r) sm.tp[(4 * r + g) * PDPLQR_TP_LD + c] = Pm[r];
         wave_sync();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * 17 + 4 * r + g]);
+        for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * PDPLQR_TP_LD + 4 * r + g]);
     }
     // P_k = Lxx Lxx^T: semidefinite (psd_bad: non-finite or clearly negative diagonal)
     bool bad = false;
@@ -306,12 +322,23 @@ __device__ __forceinline__ void schur_store_record_tile(double *FRk, const d4 &P
 #endif
 
 // Stage-record layout of the LDS-DMA variant (compile-time shapes).
+// HBM record = E (n x s, column-major), c, h~, packed H~ (offsets OE..OP).
+// The LDS copy stores E's columns at stride LDE: the read of E~ row
+// 4 kk + g - m, column c by a 32-lane half is LDE c + g (+ const); LDE = n = 12
+// puts c and c + 8 on one bank (2-way on all four reads), LDE = 2 x odd = 14
+// hits 32 distinct banks.  A 16-byte chunk (2 rows of one column, n even)
+// moves as a unit, so the copy stays one ds_write_b128 per chunk with a fixed
+// per-lane destination (LO* = LDS offsets).
 template <int NN, int MM>
 struct SchurShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
     static constexpr int ps = s * (s + 1) / 2;
     static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, Q = OP + ps;
     static constexpr int CH = Q / 2, NI = (CH + 63) / 64;
+    static constexpr int LDE = PDPLQR_LDS_PAD ? ((n / 2) % 2 == 1 ? n : n + 2) : n;
+    static constexpr int LSH = (LDE - n) * s;  // shift of everything after E in the LDS copy
+    static constexpr int LOC = OC + LSH, LOH = OH + LSH, LOP = OP + LSH;
+    static constexpr int SLOT = NI * 128 + LSH;  // every lane's chunk of the last load lands inside
     static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && s % 2 == 0 && ps % 2 == 0 && s <= 16;
 };
 
@@ -340,7 +367,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     using SH = SchurShape<(CT ? NN : 2), (CT ? MM : 2)>;
     constexpr int NI = CT ? SH::NI : 1;
     __shared__ SchurSmem sm;
-    __shared__ __attribute__((aligned(16))) double stg[CT ? 2 : 1][CT ? NI * 128 : 2];
+    __shared__ __attribute__((aligned(16))) double stg[CT ? 2 : 1][CT ? SH::SLOT : 2];
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
@@ -424,7 +451,21 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         };
         auto lput = [&](const d2v(&R)[NI], int slot) {
 #pragma unroll
-            for (int q = 0; q < NI; ++q) *reinterpret_cast<d2v *>(&stg[slot][q * 128 + 2 * lane]) = R[q];
+            for (int q = 0; q < NI; ++q) {
+                // chunk ch (doubles 2 ch, 2 ch + 1) of the HBM record to its LDS
+                // place: E's column ch / (n/2) moves by (LDE - n) per column,
+                // everything after E by LSH (recomputed per stage from the lane
+                // id: held across the loop it spilled)
+                // (lanes past the record's last chunk write copies of it
+                // past the record's end, inside the slot)
+                const int ch = q * 64 + lane;
+                constexpr int EC = SH::OC / 2;  // chunks of E
+                const int dst = (q * 64 >= EC)       ? 2 * ch + SH::LSH
+                                : (q * 64 + 63 < EC) ? 2 * ch + (SH::LDE - SH::n) * (ch / (SH::n / 2))
+                                                     : 2 * ch + (SH::LDE - SH::n) * min(ch / (SH::n / 2), SH::s);
+                __builtin_assume((dst & 1) == 0);  // 16-byte chunks: keeps one ds_write_b128
+                *reinterpret_cast<d2v *>(&stg[slot][dst]) = R[q];
+            }
         };
         // Every step issues exactly 3 loads (stage k - 3, clamped to stage 0 at
         // the end: re-loads that are never written to LDS) and 1 record store
@@ -437,7 +478,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         auto process = [&](int k, auto sym, bool sym_rt) {
             const double *R = stg[k & 1];
             SchurIn in;
-            schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c);
+            schur_load(in, R + SH::OE, R + SH::LOC, R + SH::LOP, R + SH::LOH, n, m, s, g, c, SH::LDE);
             double w, luq[4];
             const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value>(Pm, prow, in, sm, m, s,
                                                                                               g, c, w, luq, sym_rt);
@@ -489,12 +530,12 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     } else {
         SchurIn nxt;
         schur_load(nxt, Eb + (long long)(N - 1) * n * s, cb + (long long)(N - 1) * n, Hb + (long long)(N - 1) * ps,
-                   hb + (long long)(N - 1) * s, n, m, s, g, c);
+                   hb + (long long)(N - 1) * s, n, m, s, g, c, n);
         for (int k = N - 1; k >= 0; --k) {
             const SchurIn in = nxt;
             if (k > 0)
                 schur_load(nxt, Eb + (long long)(k - 1) * n * s, cb + (long long)(k - 1) * n,
-                           Hb + (long long)(k - 1) * ps, hb + (long long)(k - 1) * s, n, m, s, g, c);
+                           Hb + (long long)(k - 1) * ps, hb + (long long)(k - 1) * s, n, m, s, g, c, n);
             double w, luq[4];
             const bool ok = schur_stage<0>(Pm, prow, in, sm, m, s, g, c, w, luq);
             if (!ok && fail_stage < 0) fail_stage = k;

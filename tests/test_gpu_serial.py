@@ -342,3 +342,51 @@ def test_full_size_properties():
         o.update_problem_data(ws0[b], None, None, None, 1e-6)
         o.backward(None)
         assert rel_err(out[b], o.forward(x0[b])) < TOL
+
+
+@pytest.mark.parametrize("N,batch", [(1, 3), (2, 5), (300, 37)])
+def test_nofact_streamed_kernel_batched(N, batch):
+    """backward_without_factorization at 12/4 takes the streamed vector kernel
+    (kernels_nofact.hip, k_nofact_dma): equal to the generic LDS kernel
+    (PDPLQR_NO_NOFACT_DMA) to 1e-12 and to the oracle to 1e-9 on a batch with
+    new w-bar between the two backwards; short horizons cover the ring prologue."""
+    import os
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m = 12, 4
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 77 + N)
+    g = np.random.default_rng(N)
+    ws1 = g.standard_normal((batch, N * (n + m) + n))
+    ws2 = g.standard_normal((batch, N * (n + m) + n))
+    outs = {}
+    for mode in ("dma", "generic"):
+        if mode == "generic":
+            os.environ["PDPLQR_NO_NOFACT_DMA"] = "1"
+        try:
+            bs = BatchedLQRSolver(n, m, N, batch, keep_factors=True)
+            bs.set_model(E, c, H, h)
+            bs.update_problem_data(ws1, sigma=0.5)
+            bs.backward()
+            bs.update_problem_data(ws2, sigma=0.5)
+            bs.backward_without_factorization()
+            out = np.zeros_like(ws1)
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            outs[mode] = out
+            bs.close()
+        finally:
+            os.environ.pop("PDPLQR_NO_NOFACT_DMA", None)
+    d = np.linalg.norm(outs["dma"] - outs["generic"], axis=1) / np.linalg.norm(outs["generic"], axis=1)
+    assert float(d.max()) < 1e-12, float(d.max())
+    for b in sorted({0, batch - 1, batch // 2}):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws1[b], None, None, None, 0.5)
+        o.backward(None)
+        o.update_problem_data(ws2[b], None, None, None, 0.5)
+        o.backward_without_factorization(None)
+        assert rel_err(outs["dma"][b], o.forward(x0[b])) < TOL, b
