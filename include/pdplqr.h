@@ -176,7 +176,8 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
 /* lqr_solver.hpp:41-77), but the outer loop is absent (README.md:8).       */
 /* This runs it on the device for the whole batch: OSQP's iteration        */
 /* (Stellato et al. 2020, Algorithm 1) with the dynamics solved exactly by  */
-/* the handle's solver, projection onto [lb, ub], fixed rho and sigma, and   */
+/* the handle's solver, projection onto [lb, ub], sigma fixed, rho fixed or */
+/* adapted by OSQP's rule (settings.adaptive_rho), and                     */
 /* the ADMM residuals of admm.hip's header.  Works with all three solver    */
 /* kinds; iterations >= 2 reuse the first iteration's factorization         */
 /* (backward_without_factorization with keep_factors = 1).                  */
@@ -187,6 +188,9 @@ typedef struct {
     int32_t max_iter;    /* iteration cap                                          */
     int32_t check_every; /* termination test period (one 4-byte D2H read each)     */
     double eps_abs, eps_rel; /* tolerances (OSQP defaults 1e-3); 0 = run max_iter  */
+    int32_t adaptive_rho;    /* 1: OSQP's rho update at each termination test (a  */
+                             /* per-problem scale of rho, then one refactorization) */
+    double adaptive_rho_tolerance; /* rescale when the estimate leaves [1/tol, tol] (5) */
 } pdplqr_admm_settings;
 
 void pdplqr_admm_settings_init(pdplqr_admm_settings *s);
@@ -200,9 +204,11 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *s, const doub
 
 /* Per-problem outcome of the last admm_solve (host arrays of `batch`        */
 /* entries, each may be NULL): iterations run, 1 if the termination test     */
-/* passed, primal / dual residual at the last test.  Returns the number of   */
-/* iterations of the batch (>= 1) or an error code.                           */
-int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double *prim_res, double *dual_res);
+/* passed, primal / dual residual at the last test; `rho` (batch * ny, may be */
+/* NULL) the final rho vectors.  Returns the number of iterations of the     */
+/* batch (>= 1) or an error code.                                             */
+int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double *prim_res, double *dual_res,
+                     double *rho);
 
 /* Device info helpers (for hosts that do not link HIP). */
 int pdplqr_device_count(int32_t *count);

@@ -294,7 +294,8 @@ def segmentation(N, ns, load_balancing=True):
 
 
 def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", sigma=1e-6, alpha=1.6,
-               max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3, **solver_kw):
+               max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3, adaptive_rho=True,
+               adaptive_rho_tolerance=5.0, **solver_kw):
     """CPU restatement of the ADMM outer loop (TEST INFRASTRUCTURE).
 
     Not in the reference (README.md:8).  Restates OSQP's
@@ -307,8 +308,12 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
     e_lb / e_ub of lqr_model.hpp:21-24, and the termination test is the primal
     residual |Dw - z|_inf and the ADMM dual residual |D^T rho (z+ - z)|_inf
     with OSQP's absolute/relative tolerances, every check_every iterations and
-    at max_iter.  One problem (PackedModel arrays of one batch entry).
-    Returns (ws, ys, zs, info)."""
+    at max_iter.  Adaptive rho (OSQP's compute_rho_estimate / update_rho rule):
+    at a test that does not terminate, rho scales by
+    e = sqrt((r_prim / max(|Dw|, |z|)) / (r_dual / |D^T y|)) (guards 1e-30, rows
+    clamped to [1e-6, 1e6]) when e leaves [1/tol, tol], and the next x-update
+    re-forms and refactors.  One problem (PackedModel arrays of one batch
+    entry).  Returns (ws, ys, zs, info)."""
     n, m, N = pm.n, pm.m, pm.N
     s = n + m
     ncs = [int(x) for x in pm.ncs]
@@ -334,10 +339,13 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
     it = 0
     conv = False
     rp = rd = 0.0
+    refactor = True
+    rho_updates = 0
     for it in range(1, max_iter + 1):
         solv.update_problem_data(w, y if ny else None, z if ny else None, irho if ny else None, sigma)
-        if it == 1:
+        if refactor:
             solv.backward(irho if solver == "kkt" else rho)
+            refactor = False
         elif solver != "kkt":
             solv.backward_without_factorization(rho)
         wt = solv.forward(x0)
@@ -369,4 +377,12 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
         if check and rp <= eps_abs + eps_rel * max(dwm, zm) and rd <= eps_abs + eps_rel * dty:
             conv = True
             break
-    return w, y, z, {"iters": it, "converged": conv, "prim_res": rp, "dual_res": rd}
+        if check and adaptive_rho and it < max_iter:
+            e = np.sqrt((rp / (max(dwm, zm) + 1e-30)) / (rd / (dty + 1e-30) + 1e-30))
+            if e > adaptive_rho_tolerance or e < 1.0 / adaptive_rho_tolerance:
+                rho = np.minimum(np.maximum(rho * e, 1e-6), 1e6)
+                irho = 1.0 / rho
+                refactor = True
+                rho_updates += 1
+    return w, y, z, {"iters": it, "converged": conv, "prim_res": rp, "dual_res": rd, "rho": rho,
+                     "rho_updates": rho_updates}

@@ -34,6 +34,11 @@
 //     protocol-level iterations agree bit for bit;
 //   * the backward is backward_without_factorization (keep_factors = 1) or
 //     the factorizing kernel on the unchanged H~ (keep_factors = 0);
+//   * adaptive rho (OSQP's rule, on by default): at a termination test a
+//     problem whose normalised residual ratio e = sqrt((r_prim / max(|Dw|,|z|))
+//     / (r_dual / |D^T y|)) leaves [1/tol, tol] scales its rho by e (clamped to
+//     [1e-6, 1e6]); the next x-update then re-forms H~ and refactors the batch
+//     (a problem whose rho did not move gets the same factor back);
 //   * the KKT solver re-forms its right-hand side (form_rhs) and re-solves
 //     with the factor of the first iteration (the KKT matrix depends on rho
 //     only, qdldl_solver.hpp:88-109).
@@ -49,8 +54,10 @@ struct AdmmState {
     double *lb = nullptr, *ub = nullptr, *rho = nullptr, *irho = nullptr;
     double *x0 = nullptr;
     double *prim = nullptr, *dual = nullptr;  // [b] residuals at the last check
-    int32_t *done = nullptr, *iters = nullptr, *conv = nullptr, *active = nullptr;
-    int32_t *active_h = nullptr;  // pinned
+    double *rscale = nullptr;                 // [b] adaptive-rho factor decided at the last test (1 = keep)
+    int32_t *done = nullptr, *iters = nullptr, *conv = nullptr;
+    int32_t *active = nullptr;    // [0] problems still iterating, [1] some rho changed
+    int32_t *active_h = nullptr;  // pinned copy of active[0..1]
 };
 
 struct AdmmArgs {
@@ -59,9 +66,9 @@ struct AdmmArgs {
     double *w, *y, *z, *hw, *gw;
     const int32_t *d_off, *y_off;
     int32_t *done, *iters, *conv, *active;
-    double *prim, *dual;
-    double alpha, sigma, eps_abs, eps_rel;
-    int max_nc, it;
+    double *prim, *dual, *rscale;
+    double alpha, sigma, eps_abs, eps_rel, rho_tol;
+    int max_nc, it, adaptive;
 };
 
 // sum over the LPS lanes of one stage (xor butterflies: every lane ends with
@@ -179,12 +186,24 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
             a.iters[b] = a.it;
             a.prim[b] = rp;
             a.dual[b] = rd;
+            double f = 1.0;
             if (rp <= a.eps_abs + a.eps_rel * fmax(dwm, zm) && rd <= a.eps_abs + a.eps_rel * dty) {
                 a.done[b] = 1;
                 a.conv[b] = 1;
             } else {
                 atomicAdd(a.active, 1);
+                if (a.adaptive) {
+                    // OSQP's rho estimate (compute_rho_estimate): the ratio of the
+                    // normalised residuals, with its division guard 1e-30
+                    const double pn = rp / (fmax(dwm, zm) + 1e-30), dn = rd / (dty + 1e-30);
+                    const double e = sqrt(pn / (dn + 1e-30));
+                    if (e > a.rho_tol || e < 1.0 / a.rho_tol) {
+                        f = e;
+                        atomicOr(a.active + 1, 1);
+                    }
+                }
             }
+            a.rscale[b] = f;
         }
     }
 }
@@ -192,6 +211,19 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
 __global__ void k_admm_init(long long ny_total, const double *__restrict__ rho, double *__restrict__ irho) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < ny_total) irho[t] = 1.0 / rho[t];
+}
+
+// adaptive rho: every row of problem b scales by rscale[b], clamped to OSQP's
+// [RHO_MIN, RHO_MAX] = [1e-6, 1e6]
+__global__ void k_admm_rescale(long long ny_total, int ny, const double *__restrict__ rscale, double *__restrict__ rho,
+                               double *__restrict__ irho) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ny_total) return;
+    const double f = rscale[t / ny];
+    if (f == 1.0) return;
+    const double r = fmin(fmax(rho[t] * f, 1e-6), 1e6);
+    rho[t] = r;
+    irho[t] = 1.0 / r;
 }
 
 static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check, dim3 grid, dim3 blk,
@@ -239,9 +271,9 @@ static int admm_alloc(pdplqr_handle h) {
         (rc = aalloc(h, &s->rho, Y)) || (rc = aalloc(h, &s->irho, Y)) ||
         (rc = aalloc(h, &s->x0, B * sh.n)) || (rc = aalloc(h, &s->prim, B)) || (rc = aalloc(h, &s->dual, B)) ||
         (rc = aalloc(h, &s->done, B)) || (rc = aalloc(h, &s->iters, B)) ||
-        (rc = aalloc(h, &s->conv, B)) || (rc = aalloc(h, &s->active, 1)))
+        (rc = aalloc(h, &s->conv, B)) || (rc = aalloc(h, &s->active, 2)) || (rc = aalloc(h, &s->rscale, B)))
         return rc;
-    PDPLQR_HIP_TRY(hipHostMalloc((void **)&s->active_h, sizeof(int32_t), hipHostMallocDefault));
+    PDPLQR_HIP_TRY(hipHostMalloc((void **)&s->active_h, 2 * sizeof(int32_t), hipHostMallocDefault));
     return PDPLQR_OK;
 }
 
@@ -266,6 +298,8 @@ void pdplqr_admm_settings_init(pdplqr_admm_settings *s) {
     s->check_every = 25;
     s->eps_abs = 1e-3;
     s->eps_rel = 1e-3;
+    s->adaptive_rho = 1;
+    s->adaptive_rho_tolerance = 5.0;  // OSQP defaults
 }
 
 int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const double *x0, const double *lb,
@@ -285,8 +319,9 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         return PDPLQR_ERR_INVALID;
     }
     if (st->max_iter < 1 || st->check_every < 1 || !(st->alpha > 0.0 && st->alpha < 2.0) || !(st->sigma >= 0.0) ||
-        !(st->eps_abs >= 0.0) || !(st->eps_rel >= 0.0)) {
-        set_error("admm_solve: bad settings (max_iter >= 1, check_every >= 1, 0 < alpha < 2, sigma, eps >= 0)");
+        !(st->eps_abs >= 0.0) || !(st->eps_rel >= 0.0) || (st->adaptive_rho && !(st->adaptive_rho_tolerance >= 1.0))) {
+        set_error("admm_solve: bad settings (max_iter >= 1, check_every >= 1, 0 < alpha < 2, sigma, eps >= 0, "
+                  "adaptive_rho_tolerance >= 1)");
         return PDPLQR_ERR_INVALID;
     }
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
@@ -336,6 +371,9 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     a.active = s->active;
     a.prim = s->prim;
     a.dual = s->dual;
+    a.rscale = s->rscale;
+    a.adaptive = st->adaptive_rho ? 1 : 0;
+    a.rho_tol = st->adaptive_rho_tolerance;
     a.alpha = st->alpha;
     a.sigma = st->sigma;
     a.eps_abs = st->eps_abs;
@@ -345,15 +383,19 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     const dim3 ugrid((unsigned)B), ublk(256);
     const double *irho_or_null = Y > 0 ? s->irho : nullptr;
     int it = 1;
+    bool refactor = true;  // iteration 1, and after an adaptive rho change
+    int rho_updates = 0;
     for (;; ++it) {
-        // x-update: the reference protocol (iteration 1), then vectors only
-        if (it == 1 || kkt) {
+        // x-update: the reference protocol (iteration 1 and after a rho
+        // change: H~ depends on rho), then vectors only
+        if (refactor || kkt) {
             if ((rc = solver_update(h, s->w, s->y, s->z, irho_or_null, st->sigma))) return rc;
             h->updated = true;
         }
-        if (it == 1) {
+        if (refactor) {
             if ((rc = solver_backward(h, kkt ? s->irho : s->rho))) return rc;
             h->factored = true;
+            refactor = false;
         } else if (!kkt) {
             if ((rc = solver_backward_prepared(h))) return rc;
         }
@@ -370,12 +412,19 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         const bool check = last || it % st->check_every == 0;
         const bool fuse = !kkt && !last;
         a.it = it;
-        if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, sizeof(int32_t), S));
+        if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
         if ((rc = launch_admm_update(a, sh.s <= 16, fuse, check, ugrid, ublk, S))) return rc;
         if (check) {
-            PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, sizeof(int32_t), hipMemcpyDeviceToHost, S));
+            PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));
-            if (*s->active_h == 0) break;
+            if (s->active_h[0] == 0) break;
+            if (s->active_h[1] && !last) {  // some problem's rho moved: rescale, refactor the batch
+                hipLaunchKernelGGL(k_admm_rescale, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, sh.ny,
+                                   s->rscale, s->rho, s->irho);
+                PDPLQR_HIP_TRY(hipGetLastError());
+                refactor = true;
+                ++rho_updates;
+            }
         }
         if (last) break;
     }
@@ -390,10 +439,12 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     if (mem != PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipStreamSynchronize(S));
     h->hw_cached = false;
     h->admm_iters = it;
+    h->admm_rho_updates = rho_updates;
     return PDPLQR_OK;
 }
 
-int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double *prim_res, double *dual_res) {
+int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double *prim_res, double *dual_res,
+                     double *rho) {
     if (!h) return PDPLQR_ERR_INVALID;
     if (!h->admm) {
         set_error("admm_info before admm_solve");
@@ -407,6 +458,8 @@ int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double
     if (converged) PDPLQR_HIP_TRY(hipMemcpy(converged, s->conv, B * sizeof(int32_t), hipMemcpyDeviceToHost));
     if (prim_res) PDPLQR_HIP_TRY(hipMemcpy(prim_res, s->prim, B * sizeof(double), hipMemcpyDeviceToHost));
     if (dual_res) PDPLQR_HIP_TRY(hipMemcpy(dual_res, s->dual, B * sizeof(double), hipMemcpyDeviceToHost));
+    if (rho && h->sh.ny > 0)
+        PDPLQR_HIP_TRY(hipMemcpy(rho, s->rho, B * h->sh.ny * sizeof(double), hipMemcpyDeviceToHost));
     return h->admm_iters;
 }
 

@@ -107,6 +107,7 @@ struct pdplqr_handle_s {
     pdplqr::KKTState *kkt = nullptr;       // KKT solver state (kkt.hip)
     pdplqr::AdmmState *admm = nullptr;     // ADMM outer loop state (admm.hip), allocated on first use
     int admm_iters = 0;                    // iterations of the last admm_solve
+    int admm_rho_updates = 0;              // adaptive-rho refactorizations of the last admm_solve
     int shard_last = 1;  // last shard_backward's is_last_shard
     // replayable launch sequences of backward / backward_without_factorization /
     // forward (solvers.hip: hipGraph captured on first use per argument set)

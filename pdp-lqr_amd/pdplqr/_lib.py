@@ -53,7 +53,8 @@ class Config(C.Structure):
 class AdmmSettings(C.Structure):
     _fields_ = [
         ("sigma", C.c_double), ("alpha", C.c_double), ("max_iter", C.c_int32), ("check_every", C.c_int32),
-        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double), ("adaptive_rho", C.c_int32),
+        ("adaptive_rho_tolerance", C.c_double),
     ]
 
 
@@ -103,7 +104,7 @@ def lib() -> C.CDLL:
     L.pdplqr_admm_settings_init.argtypes = [C.POINTER(AdmmSettings)]
     L.pdplqr_admm_settings_init.restype = None
     L.pdplqr_admm_solve.argtypes = [vp, C.POINTER(AdmmSettings), dp, dp, dp, dp, dp, dp, dp, C.c_int]
-    L.pdplqr_admm_info.argtypes = [vp, ip, ip, dp, dp]
+    L.pdplqr_admm_info.argtypes = [vp, ip, ip, dp, dp, dp]
     for nm in EXPORTS:
         f = getattr(L, nm)
         if nm not in ("pdplqr_config_init", "pdplqr_last_error", "pdplqr_get_stream", "pdplqr_admm_settings_init"):

@@ -210,10 +210,13 @@ class _Handle:
         cv = np.zeros(self.batch, dtype=np.int32)
         rp = np.zeros(self.batch)
         rd = np.zeros(self.batch)
+        rho = np.zeros((self.batch, max(self.ny, 1)))
         i32 = C.POINTER(C.c_int32)
         n = check(lib().pdplqr_admm_info(self.h, it.ctypes.data_as(i32), cv.ctypes.data_as(i32),
-                                         C.c_void_p(rp.ctypes.data), C.c_void_p(rd.ctypes.data)))
-        return {"iterations": int(n), "iters": it, "converged": cv.astype(bool), "prim_res": rp, "dual_res": rd}
+                                         C.c_void_p(rp.ctypes.data), C.c_void_p(rd.ctypes.data),
+                                         C.c_void_p(rho.ctypes.data)))
+        return {"iterations": int(n), "iters": it, "converged": cv.astype(bool), "prim_res": rp, "dual_res": rd,
+                "rho": rho[:, :self.ny]}
 
     def segments(self, ns: int):
         a = np.zeros(ns, dtype=np.int32)
@@ -223,12 +226,14 @@ class _Handle:
         return a, b
 
 
-def admm_settings(sigma=1e-6, alpha=1.6, max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3) -> AdmmSettings:
+def admm_settings(sigma=1e-6, alpha=1.6, max_iter=4000, check_every=25, eps_abs=1e-3, eps_rel=1e-3,
+                  adaptive_rho=True, adaptive_rho_tolerance=5.0) -> AdmmSettings:
     st = AdmmSettings()
     lib().pdplqr_admm_settings_init(C.byref(st))
     st.sigma, st.alpha = float(sigma), float(alpha)
     st.max_iter, st.check_every = int(max_iter), int(check_every)
     st.eps_abs, st.eps_rel = float(eps_abs), float(eps_rel)
+    st.adaptive_rho, st.adaptive_rho_tolerance = int(bool(adaptive_rho)), float(adaptive_rho_tolerance)
     return st
 
 
@@ -285,7 +290,8 @@ class _ModelSolver:
         return int(self._hd.status()[0])
 
     def admm_solve(self, x0, ws: List[np.ndarray], ys, zs, rho_vecs, sigma: float = 1e-6, alpha: float = 1.6,
-                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3):
+                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3,
+                   adaptive_rho: bool = True, adaptive_rho_tolerance: float = 5.0):
         """ADMM outer loop over this solver (new: absent in the reference,
         README.md:8) for the bounds ``e_lb <= D_con w <= e_ub`` stored in the
         model's nodes (lqr_model.hpp:21-24).  ``ws, ys, zs`` are the warm start
@@ -299,7 +305,8 @@ class _ModelSolver:
         lb = np.ascontiguousarray(pack_stage_vectors([nd.e_lb for nd in m.nodes], ncs)) if self._hd.ny else None
         ub = np.ascontiguousarray(pack_stage_vectors([nd.e_ub for nd in m.nodes], ncs)) if self._hd.ny else None
         y, z, r = self._y(ys), self._y(zs), self._y(rho_vecs)
-        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel)
+        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel, adaptive_rho,
+                           adaptive_rho_tolerance)
         self._hd.admm_solve(np.ascontiguousarray(x0, dtype=np.float64), lb, ub, r, w, y, z, st)
         s = m.n + m.m
         for k in range(m.N):
@@ -411,11 +418,13 @@ class BatchedLQRSolver:
         return self._hd.status()
 
     def admm_solve(self, x0, lb, ub, rho, ws, ys=None, zs=None, sigma: float = 1e-6, alpha: float = 1.6,
-                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3):
+                   max_iter: int = 4000, check_every: int = 25, eps_abs: float = 1e-3, eps_rel: float = 1e-3,
+                   adaptive_rho: bool = True, adaptive_rho_tolerance: float = 5.0):
         """ADMM outer loop for the box constraints lb <= D w <= ub on the device
         (include/pdplqr.h: pdplqr_admm_solve).  ws/ys/zs hold the warm start and
         are overwritten with the solution; returns admm_info()."""
-        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel)
+        st = admm_settings(sigma, alpha, max_iter, check_every, eps_abs, eps_rel, adaptive_rho,
+                           adaptive_rho_tolerance)
         self._hd.admm_solve(x0, lb, ub, rho, ws, ys, zs, st)
         return self._hd.admm_info()
 

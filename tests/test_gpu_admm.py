@@ -225,3 +225,28 @@ def test_model_level_api_quadrotor():
     ow, oy, oz, oi = oracle_admm(pm, x0, lb, ub, np.full(lb.size, 0.1), solver="kkt", **st)
     assert info["converged"] == oi["converged"]
     assert rel_err(np.concatenate(ws), ow) < 1e-7
+
+
+@pytest.mark.parametrize("solver", ["serial", "parallel-LU", "kkt"])
+def test_adaptive_rho_matches_oracle(solver):
+    """OSQP's adaptive rho on the device: from rho = 0.1 (which stalls on these
+    problems) every problem rescales on its own schedule and converges; the
+    per-problem iteration counts, final rho and iterate equal the oracle's."""
+    if solver == "kkt":
+        models, x0s = _ubox_models(3, n=12, m=4, N=48, nc=4, bound=0.5, seed0=400)
+    else:
+        models, x0s = _ubox_models(4)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s, warm=False)
+    rho = np.full(lb.shape, 0.1)
+    st = dict(max_iter=3000, check_every=25, eps_abs=1e-7, eps_rel=1e-7)
+    w, y, z, info = _run_gpu(solver, pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, **st)
+    okw = {"num_segments": 4, "condensed": "LU"} if solver.startswith("parallel") else {}
+    tol = TOL_KKT if solver == "kkt" else 1e-9
+    for b in range(len(pms)):
+        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], solver=solver.split("-")[0], **st, **okw)
+        assert oi["converged"] and oi["rho_updates"] >= 1, oi
+        assert bool(info["converged"][b]) and info["iters"][b] == oi["iters"], (b, info["iters"][b], oi["iters"])
+        # rho is a product of residual ratios: residuals are differences of
+        # iterates, so they carry the path's tolerance amplified (KKT: 1e-8)
+        assert rel_err(info["rho"][b], oi["rho"]) < (1e-6 if solver == "kkt" else 1e-9), b
+        assert rel_err(w[b], ow) < tol and rel_err(y[b], oy) < tol, b

@@ -111,3 +111,16 @@ def test_admm_without_constraints_is_one_solve():
     o.update_problem_data(np.zeros(pm.N * (pm.n + pm.m) + pm.n), None, None, None, 1e-6)
     o.backward(None)
     assert rel_err(w, o.forward(x0)) < 1e-15
+
+
+def test_adaptive_rho_recovers_a_poor_rho():
+    """rho = 0.1 stalls on the unstable ubox case (see RHO); OSQP's adaptive
+    rho rule moves it and the run converges to the KKT point."""
+    model, pm, x0, lb, ub = _case("ubox")
+    rho = np.full(int(np.sum(pm.ncs)), 0.1)
+    st = dict(max_iter=3000, check_every=25, eps_abs=1e-8, eps_rel=1e-8)
+    _, _, _, fixed = admm_solve(pm, x0, lb, ub, rho, adaptive_rho=False, **st)
+    w, y, z, info = admm_solve(pm, x0, lb, ub, rho, adaptive_rho=True, **st)
+    assert not fixed["converged"]
+    assert info["converged"] and info["rho_updates"] >= 1 and info["rho"][0] > 0.5, info
+    assert _certificate(pm, x0, w, y, lb, ub, 1e-6) < 1e-6
