@@ -90,7 +90,10 @@ typedef struct {
 } pdplqr_config;
 
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,
- * CHOLESKY, rho_dyn = kkt_sigma = 1e-6). */
+ * CHOLESKY, rho_dyn = kkt_sigma = 1e-6).
+ * Hard limit of this build: nx + nu <= 32 (a stage matrix is at most 2 x 2 MFMA
+ * tiles of 16 in one wavefront); pdplqr_create returns PDPLQR_ERR_UNSUPPORTED
+ * for larger shapes (the reference is size-generic, lqr_kernel.hpp:104-147). */
 void pdplqr_config_init(pdplqr_config *cfg);
 
 int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out);
