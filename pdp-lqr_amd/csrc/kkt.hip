@@ -592,6 +592,275 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
 }
 
 // ---------------------------------------------------------------------------
+// P = 16, two waves per problem: the TWISTED block factorisation of -S.
+// The serial chain above walks all N + 1 dual groups with one wave per problem
+// (one wave per SIMD at C5's batch 1024: latency-bound).  Here wave 0
+// eliminates groups 0 .. p-1 top-down exactly as k_kkt_factor16 and wave 1
+// eliminates groups N .. p+1 bottom-up (the same recursion on the reversed
+// system, whose coupling block is Bt_{k-1}^T):
+//     M'_k = D_k - Z_k^T Z_k,  L'_kk = chol(M'_k),  Z_{k-1} = L'_kk^{-1} Bt_{k-1}^T
+// and the middle group p = N / 2 takes both sides' Schur complements:
+//     M_p = D_p - X_p^T X_p - Z_p^T Z_p.
+// The factor is a different (twisted) elimination order of the same SPD
+// matrix, so the solution agrees with QDLDL's natural order to rounding.  Each
+// wave's chain is half as long and two waves share a SIMD.  Storage: group
+// k < p as before (X_{k+1}, Lkk^{-1}); group k > p: Z_{k-1} at +256,
+// L'_kk^{-1} at +512; group p: L_pp^{-1} at +512.
+// ---------------------------------------------------------------------------
+#ifndef PDPLQR_KKT_TWIST
+#define PDPLQR_KKT_TWIST 1
+#endif
+
+__device__ __forceinline__ d4 tile_identity(int g, int c) {
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (4 * r + g == c) ? 1.0 : 0.0;
+    return v;
+}
+
+__global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double *__restrict__ dpk,
+                                                        const double *__restrict__ dreg) {
+    __shared__ double tt[16 * 17];            // wave 1's transposes
+    __shared__ __attribute__((aligned(32))) double zmid[256];  // Z_p, C/D layout per lane
+    __shared__ int wfail[2];
+    const Shape &sh = A.sh;
+    const int N = sh.N, p = N / 2;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    __builtin_assume(lane >= 0 && lane < 64);
+    const long long b = blockIdx.x;
+    const double *tiles = dpk + b * (N + 1) * 512LL;
+    const double *dg = dreg + b * (N + 1) * 16LL;
+    double *fb = A.fac + b * (N + 1) * 3LL * 256;
+    int fail = 0;  // 1 + the lowest failing group
+    WM<1> X;       // wave 0: X_k = L_{k,k-1}^T; wave 1: Z_k
+    X.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+    auto load_D = [&](int k) {
+        d4 D = tn_load(tiles + k * 512LL, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D[r] += (4 * r + g == c) ? dg[k * 16 + 4 * r + g] : 0.0;
+        return D;
+    };
+    if (wv == 0) {
+        d4 D1 = load_D(0), B1 = tn_load(tiles + 256, lane);
+        d4 D2 = load_D(min(1, p)), B2 = tn_load(tiles + min(1, p) * 512LL + 256, lane);
+        for (int k = 0; k < p; ++k) {
+            WM<1> M, D;
+            d4 B[1][2];
+            D.t[0][0] = D1;
+            B[0][0] = B1;
+            D1 = D2;
+            B1 = B2;
+            const int kn = min(k + 2, p);  // two groups ahead (re-loads past the end: harmless)
+            D2 = load_D(kn);
+            B2 = tn_load(tiles + kn * 512LL + 256, lane);
+            if (k > 0) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - X_k^T X_k
+            else M = D;
+            B[0][1] = tile_identity(g, c);
+            const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);
+            if (!ok && !fail) fail = k + 1;
+            X.t[0][0] = B[0][0];
+            double *fk = fb + k * 768LL;
+            tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1}
+            tn_store(fk + 512, lane, B[0][1]);    // Lkk^{-1}
+        }
+    } else {
+        d4 D1 = load_D(N), B1 = tn_load(tiles + (N - 1) * 512LL + 256, lane);
+        const int k2 = max(N - 1, p + 1);
+        d4 D2 = load_D(k2), B2 = tn_load(tiles + (k2 - 1) * 512LL + 256, lane);
+        for (int k = N; k > p; --k) {
+            WM<1> M, D;
+            d4 B[1][2];
+            D.t[0][0] = D1;
+            const d4 Bt = tile_transpose(B1, tt, g, c);  // Bt_{k-1}^T
+            D1 = D2;
+            B1 = B2;
+            const int kn = max(k - 2, p + 1);
+            D2 = load_D(kn);
+            B2 = tn_load(tiles + (kn - 1) * 512LL + 256, lane);
+            if (k < N) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - Z_k^T Z_k
+            else M = D;
+            B[0][0] = Bt;
+            B[0][1] = tile_identity(g, c);
+            const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);
+            if (!ok) fail = k + 1;  // descending: the last one is the lowest
+            X.t[0][0] = B[0][0];  // Z_{k-1}
+            double *fk = fb + k * 768LL;
+            tn_store(fk + 256, lane, X.t[0][0]);
+            tn_store(fk + 512, lane, B[0][1]);  // L'_kk^{-1}
+        }
+        *reinterpret_cast<d4 *>(zmid + 4 * lane) = X.t[0][0];  // Z_p
+    }
+    if (lane == 0) wfail[wv] = fail;
+    __syncthreads();
+    if (wv == 0) {
+        WM<1> Z, M, M1, D;
+        Z.t[0][0] = *reinterpret_cast<const d4 *>(zmid + 4 * lane);
+        D.t[0][0] = load_D(p);
+        if (p > 0) {
+            wm_tn<1>(M1, X, X, 16, -1.0, 0.0, &D, g, c);
+            wm_tn<1>(M, Z, Z, 16, -1.0, 0.0, &M1, g, c);  // D_p - X_p^T X_p - Z_p^T Z_p
+        } else {
+            wm_tn<1>(M, Z, Z, 16, -1.0, 0.0, &D, g, c);
+        }
+        d4 B[2];
+        B[0] = d4{0.0, 0.0, 0.0, 0.0};
+        B[1] = tile_identity(g, c);
+        const bool ok = chol_blk4_aug<2>(M.t[0][0], B, g, c);
+        tn_store(fb + p * 768LL + 512, lane, B[1]);  // L_pp^{-1}
+        int f = fail;
+        if (!ok && (!f || p + 1 < f)) f = p + 1;
+        if (wfail[1] && (!f || wfail[1] < f)) f = wfail[1];
+        if (lane == 0) A.status[b] = f ? f : (A.pstat[b] ? N + 2 : 0);
+    }
+}
+
+// forward phase 2 on the twisted factor: L y = bvec from both ends toward the
+// middle group, its 16 x 16 solve, then L^T lam = y outward (two waves)
+__global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const double *__restrict__ bvec) {
+    __shared__ double tt[2][16 * 17];
+    __shared__ double vmid[16], lmid[16];
+    const Shape &sh = A.sh;
+    const int N = sh.N, p = N / 2;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    __builtin_assume(lane >= 0 && lane < 64);
+    const long long b = blockIdx.x;
+    double *wvb = A.wv + b * (N + 1) * 4LL * 16;
+    const double *fb = A.fac + b * (N + 1) * 3LL * 256;
+    const double *bv = bvec + b * (N + 1) * 16LL;
+    double *T = tt[wv];
+    auto vin = [&](const double *src) {  // a 16-vector into column 0 (lanes c == 0)
+        WV<1> v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? src[4 * r + g] : 0.0;
+        return v;
+    };
+    // one step's inputs: the coupling tile, Lkk^{-1} and a 16-vector, loaded
+    // two steps ahead (the steps are HBM-latency bound otherwise)
+    struct In {
+        d4 X, L;
+        WV<1> v;
+    };
+    auto load = [&](In &in, long long xoff, int k, const double *vsrc) {
+        in.X = tn_load(fb + xoff, lane);
+        in.L = tn_load(fb + k * 768LL + 512, lane);
+        in.v = vin(vsrc);
+    };
+    WV<1> y;
+    y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    // ---- forward substitution from both ends ----
+    if (wv == 0) {
+        // step k: X_k (stored by group k - 1), Lkk^{-1}, bvec_k
+        auto ld = [&](In &in, int k) { load(in, max(k - 1, 0) * 768LL + 256, k, bv + k * 16); };
+        In n1, n2;
+        if (p > 0) {
+            ld(n1, 0);
+            ld(n2, min(1, p - 1));
+        }
+        for (int k = 0; k < p; ++k) {
+            const In in = n1;
+            n1 = n2;
+            ld(n2, min(k + 2, p - 1));
+            WV<1> v = in.v;
+            if (k > 0) {
+                WM<1> Xk;
+                Xk.t[0][0] = in.X;
+                wv_tn<1>(v, Xk, y, 16, -1.0, &v);  // - L_{k,k-1} y_{k-1}
+            }
+            WM<1> LinvT;
+            LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
+            wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
+            wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+        }
+    } else {
+        // step k: Z_k (stored by group k + 1), L'_kk^{-1}, bvec_k
+        auto ld = [&](In &in, int k) { load(in, min(k + 1, N) * 768LL + 256, k, bv + k * 16); };
+        In n1, n2;
+        ld(n1, N);
+        ld(n2, max(N - 1, p + 1));
+        for (int k = N; k > p; --k) {
+            const In in = n1;
+            n1 = n2;
+            ld(n2, max(k - 2, p + 1));
+            WV<1> v = in.v;
+            if (k < N) {
+                WM<1> Zk;
+                Zk.t[0][0] = in.X;
+                wv_tn<1>(v, Zk, y, 16, -1.0, &v);
+            }
+            WM<1> LinvT;
+            LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
+            wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
+            wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+        }
+        wv_store<1>(y, vmid, 16, g, c);  // y'_{p+1}
+    }
+    __syncthreads();
+    // ---- the middle group ----
+    if (wv == 0) {
+        WV<1> v = vin(bv + p * 16);
+        if (p > 0) {
+            WM<1> Xp;
+            Xp.t[0][0] = tn_load(fb + (p - 1) * 768LL + 256, lane);
+            wv_tn<1>(v, Xp, y, 16, -1.0, &v);
+        }
+        WM<1> Zp;
+        Zp.t[0][0] = tn_load(fb + (p + 1) * 768LL + 256, lane);
+        const WV<1> yb = vin(vmid);
+        wv_tn<1>(v, Zp, yb, 16, -1.0, &v);
+        WM<1> Linv, LinvT;
+        Linv.t[0][0] = tn_load(fb + p * 768LL + 512, lane);
+        LinvT.t[0][0] = tile_transpose(Linv.t[0][0], T, g, c);
+        WV<1> yp, lam;
+        wv_tn<1>(yp, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
+        wv_tn<1>(lam, Linv, yp, 16, 1.0, (const WV<1> *)nullptr);
+        wv_store<1>(lam, wvb + (long long)p * 64 + 48, 16, g, c);
+        wv_store<1>(lam, lmid, 16, g, c);
+    }
+    __syncthreads();
+    // ---- back substitution outward; y_k was written by this wave (same lanes) ----
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    WV<1> lam = vin(lmid);
+    // step k: the coupling tile stored by group k (X_{k+1} above p, Z_{k-1}
+    // below), Lkk^{-1}, y_k
+    auto ld = [&](In &in, int k) { load(in, k * 768LL + 256, k, wvb + (long long)k * 64 + 48); };
+    if (wv == 0) {
+        In n1, n2;
+        if (p > 0) {
+            ld(n1, p - 1);
+            ld(n2, max(p - 2, 0));
+        }
+        for (int k = p - 1; k >= 0; --k) {
+            const In in = n1;
+            n1 = n2;
+            ld(n2, max(k - 2, 0));
+            WV<1> v = in.v;
+            WM<1> XnT, Linv;
+            XnT.t[0][0] = tile_transpose(in.X, T, g, c);  // X_{k+1}^T
+            wv_tn<1>(v, XnT, lam, 16, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
+            Linv.t[0][0] = in.L;
+            wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
+            wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
+        }
+    } else {
+        In n1, n2;
+        ld(n1, p + 1);
+        ld(n2, min(p + 2, N));
+        for (int k = p + 1; k <= N; ++k) {
+            const In in = n1;
+            n1 = n2;
+            ld(n2, min(k + 2, N));
+            WV<1> v = in.v;
+            WM<1> ZT, Linv;
+            ZT.t[0][0] = tile_transpose(in.X, T, g, c);  // Z_{k-1}^T
+            wv_tn<1>(v, ZT, lam, 16, -1.0, &v);
+            Linv.t[0][0] = in.L;
+            wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
+            wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_kkt_rhs: form_rhs (kkt.hpp:224-300) -- one thread per (problem, KKT row)
 // row descriptors: kind 0 = primal (stage, KKT index), 1 = y (stage, q),
 // 2 = lambda_{k+1} (k, i)
@@ -939,7 +1208,11 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
         const long long total = (long long)sh.batch * (sh.N + 1) * 16;
         const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
         hipLaunchKernelGGL(k_kkt_dreg16, dim3(grid), dim3(256), 0, h->stream, a, inv_rho, ks->dreg);
-        hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, ks->dpk, ks->dreg);
+        if (PDPLQR_KKT_TWIST && !getenv("PDPLQR_KKT_NO_TWIST"))
+            hipLaunchKernelGGL(k_kkt_factor16_tw, dim3((unsigned)sh.batch), dim3(128), 0, h->stream, a, ks->dpk,
+                               ks->dreg);
+        else
+            hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, ks->dpk, ks->dreg);
     }
     else hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -959,7 +1232,10 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
         const long long total = (long long)sh.batch * (sh.N + 1) * 16;
         const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
         hipLaunchKernelGGL(k_kkt_bvec16, dim3(grid), dim3(256), 0, h->stream, a, ks->bvec);
-        hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a, (const double *)ks->bvec);
+        if (PDPLQR_KKT_TWIST && !getenv("PDPLQR_KKT_NO_TWIST"))
+            hipLaunchKernelGGL(k_kkt_solve2_16_tw, probs, dim3(128), 0, h->stream, a, (const double *)ks->bvec);
+        else
+            hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a, (const double *)ks->bvec);
     }
     else hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
     if (P == 16) hipLaunchKernelGGL(k_kkt_solve3_16, stages, wave, 0, h->stream, a, x0, ws);

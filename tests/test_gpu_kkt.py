@@ -200,3 +200,53 @@ def test_kkt_protocol():
         bs.backward_without_factorization()  # QDLDLSolver has none
     with pytest.raises(PdplqrError):
         bs.forward(np.zeros((1, 4)), np.zeros((1, 5 * 6 + 4)))  # before backward
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 65, 200])
+def test_twisted_factor_equals_natural_order(N):
+    """P = 16 (12/4, nc = 4): the two-wave twisted factorisation and solve
+    (k_kkt_factor16_tw / k_kkt_solve2_16_tw, the default) agree with the
+    natural-order one-wave kernels (PDPLQR_KKT_NO_TWIST) to 1e-11 and with the
+    oracle to 1e-8; short horizons put the middle group at 0 and 1."""
+    import os
+
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, nc, batch = 12, 4, 4, 6
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 900 + N)
+    g = np.random.default_rng(N)
+    ncs = np.full(N + 1, nc, dtype=np.int32)
+    ncs[N] = 0
+    D = np.concatenate([g.standard_normal((batch, nc * s)) for _ in range(N)], axis=1)
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    outs = {}
+    for mode in ("twist", "natural"):
+        if mode == "natural":
+            os.environ["PDPLQR_KKT_NO_TWIST"] = "1"
+        try:
+            bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+            bs.set_model(E, c, H, h, D)
+            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+            bs.backward(irho)
+            out = np.zeros((batch, N * s + n))
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            outs[mode] = out
+            bs.close()
+        finally:
+            os.environ.pop("PDPLQR_KKT_NO_TWIST", None)
+    d = np.linalg.norm(outs["twist"] - outs["natural"], axis=1) / np.linalg.norm(outs["natural"], axis=1)
+    assert float(d.max()) < 1e-11, float(d.max())
+    for b in (0, batch - 1):
+        pm = PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b])
+        o = OracleKKT(pm)
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        o.backward(irho[b])
+        assert rel_err(outs["twist"][b], o.forward(x0[b])) < TOL, b
