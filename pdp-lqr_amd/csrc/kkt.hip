@@ -716,6 +716,30 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
 
 // forward phase 2 on the twisted factor: L y = bvec from both ends toward the
 // middle group, its 16 x 16 solve, then L^T lam = y outward (two waves)
+// In of step i of a sweep: loaded two steps ahead into one of two buffers
+// used alternately (a 2x-unrolled loop: no register rotation, which made the
+// compiler wait for the freshly issued loads at every back edge)
+struct SolveIn {
+    d4 X, L;
+    WV<1> v;
+};
+
+template <class LD, class ST>
+__device__ __forceinline__ void sweep2(int cnt, LD &&ld, ST &&step) {
+    if (cnt <= 0) return;
+    SolveIn a, b;
+    ld(a, 0);
+    ld(b, min(1, cnt - 1));
+    int i = 0;
+    for (; i + 1 < cnt; i += 2) {
+        step(a, i);
+        ld(a, min(i + 2, cnt - 1));  // past the end: re-loads the last step (harmless)
+        step(b, i + 1);
+        ld(b, min(i + 3, cnt - 1));
+    }
+    if (i < cnt) step(a, i);
+}
+
 __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const double *__restrict__ bvec) {
     __shared__ double tt[2][16 * 17];
     __shared__ double vmid[16], lmid[16];
@@ -731,67 +755,43 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     auto vin = [&](const double *src) {  // a 16-vector into column 0 (lanes c == 0)
         WV<1> v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? src[4 * r + g] : 0.0;
+        for (int r = 0; r < 4; ++r) {
+            const double x = src[4 * r + g];  // every lane loads (branch-free), column 0 keeps it
+            v.t[0][r] = (c == 0) ? x : 0.0;
+        }
         return v;
     };
-    // one step's inputs: the coupling tile, Lkk^{-1} and a 16-vector, loaded
-    // two steps ahead (the steps are HBM-latency bound otherwise)
-    struct In {
-        d4 X, L;
-        WV<1> v;
-    };
-    auto load = [&](In &in, long long xoff, int k, const double *vsrc) {
+    auto load = [&](SolveIn &in, long long xoff, int k, const double *vsrc) {
         in.X = tn_load(fb + xoff, lane);
         in.L = tn_load(fb + k * 768LL + 512, lane);
         in.v = vin(vsrc);
     };
     WV<1> y;
     y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    // forward step: y_k = Lkk^{-1} (bvec_k - C^T y_prev), C = X_k (top) or Z_k (bottom)
+    auto fstep = [&](const SolveIn &in, int k, bool first) {
+        WV<1> v = in.v;
+        if (!first) {
+            WM<1> Ck;
+            Ck.t[0][0] = in.X;
+            wv_tn<1>(v, Ck, y, 16, -1.0, &v);
+        }
+        WM<1> LinvT;
+        LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
+        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
+        wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+    };
     // ---- forward substitution from both ends ----
-    if (wv == 0) {
-        // step k: X_k (stored by group k - 1), Lkk^{-1}, bvec_k
-        auto ld = [&](In &in, int k) { load(in, max(k - 1, 0) * 768LL + 256, k, bv + k * 16); };
-        In n1, n2;
-        if (p > 0) {
-            ld(n1, 0);
-            ld(n2, min(1, p - 1));
-        }
-        for (int k = 0; k < p; ++k) {
-            const In in = n1;
-            n1 = n2;
-            ld(n2, min(k + 2, p - 1));
-            WV<1> v = in.v;
-            if (k > 0) {
-                WM<1> Xk;
-                Xk.t[0][0] = in.X;
-                wv_tn<1>(v, Xk, y, 16, -1.0, &v);  // - L_{k,k-1} y_{k-1}
-            }
-            WM<1> LinvT;
-            LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
-            wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-            wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
-        }
-    } else {
-        // step k: Z_k (stored by group k + 1), L'_kk^{-1}, bvec_k
-        auto ld = [&](In &in, int k) { load(in, min(k + 1, N) * 768LL + 256, k, bv + k * 16); };
-        In n1, n2;
-        ld(n1, N);
-        ld(n2, max(N - 1, p + 1));
-        for (int k = N; k > p; --k) {
-            const In in = n1;
-            n1 = n2;
-            ld(n2, max(k - 2, p + 1));
-            WV<1> v = in.v;
-            if (k < N) {
-                WM<1> Zk;
-                Zk.t[0][0] = in.X;
-                wv_tn<1>(v, Zk, y, 16, -1.0, &v);
-            }
-            WM<1> LinvT;
-            LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
-            wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-            wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
-        }
+    if (wv == 0) {  // steps k = 0 .. p-1: X_k stored by group k - 1
+        sweep2(p, [&](SolveIn &in, int i) { load(in, max(i - 1, 0) * 768LL + 256, i, bv + i * 16); },
+               [&](const SolveIn &in, int i) { fstep(in, i, i == 0); });
+    } else {  // steps k = N .. p+1: Z_k stored by group k + 1
+        sweep2(N - p,
+               [&](SolveIn &in, int i) {
+                   const int k = N - i;
+                   load(in, min(k + 1, N) * 768LL + 256, k, bv + k * 16);
+               },
+               [&](const SolveIn &in, int i) { fstep(in, N - i, i == 0); });
         wv_store<1>(y, vmid, 16, g, c);  // y'_{p+1}
     }
     __syncthreads();
@@ -820,44 +820,24 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     // ---- back substitution outward; y_k was written by this wave (same lanes) ----
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     WV<1> lam = vin(lmid);
-    // step k: the coupling tile stored by group k (X_{k+1} above p, Z_{k-1}
-    // below), Lkk^{-1}, y_k
-    auto ld = [&](In &in, int k) { load(in, k * 768LL + 256, k, wvb + (long long)k * 64 + 48); };
-    if (wv == 0) {
-        In n1, n2;
-        if (p > 0) {
-            ld(n1, p - 1);
-            ld(n2, max(p - 2, 0));
-        }
-        for (int k = p - 1; k >= 0; --k) {
-            const In in = n1;
-            n1 = n2;
-            ld(n2, max(k - 2, 0));
-            WV<1> v = in.v;
-            WM<1> XnT, Linv;
-            XnT.t[0][0] = tile_transpose(in.X, T, g, c);  // X_{k+1}^T
-            wv_tn<1>(v, XnT, lam, 16, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
-            Linv.t[0][0] = in.L;
-            wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
-            wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
-        }
-    } else {
-        In n1, n2;
-        ld(n1, p + 1);
-        ld(n2, min(p + 2, N));
-        for (int k = p + 1; k <= N; ++k) {
-            const In in = n1;
-            n1 = n2;
-            ld(n2, min(k + 2, N));
-            WV<1> v = in.v;
-            WM<1> ZT, Linv;
-            ZT.t[0][0] = tile_transpose(in.X, T, g, c);  // Z_{k-1}^T
-            wv_tn<1>(v, ZT, lam, 16, -1.0, &v);
-            Linv.t[0][0] = in.L;
-            wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
-            wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
-        }
-    }
+    // step k: lam_k = Lkk^{-T} (y_k - C lam_prev), C = X_{k+1} (top) or Z_{k-1}
+    // (bottom), both stored by group k
+    auto bload = [&](SolveIn &in, int k) { load(in, k * 768LL + 256, k, wvb + (long long)k * 64 + 48); };
+    auto bstep = [&](const SolveIn &in, int k) {
+        WV<1> v = in.v;
+        WM<1> CT, Linv;
+        CT.t[0][0] = tile_transpose(in.X, T, g, c);
+        wv_tn<1>(v, CT, lam, 16, -1.0, &v);
+        Linv.t[0][0] = in.L;
+        wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
+        wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
+    };
+    if (wv == 0)
+        sweep2(p, [&](SolveIn &in, int i) { bload(in, p - 1 - i); },
+               [&](const SolveIn &in, int i) { bstep(in, p - 1 - i); });
+    else
+        sweep2(N - p, [&](SolveIn &in, int i) { bload(in, p + 1 + i); },
+               [&](const SolveIn &in, int i) { bstep(in, p + 1 + i); });
 }
 
 // ---------------------------------------------------------------------------
