@@ -618,6 +618,35 @@ __device__ __forceinline__ d4 tile_identity(int g, int c) {
     return v;
 }
 
+// Inputs of step i of a sweep are loaded two steps ahead into one of two
+// buffers used alternately (a 2x-unrolled loop: no register rotation, which
+// made the compiler wait for the freshly issued loads at every back edge).
+struct SolveIn {
+    d4 X, L;
+    WV<1> v;
+};
+
+struct FacIn {
+    d4 D, B;
+    double dr[4];
+};
+
+template <class In, class LD, class ST>
+__device__ __forceinline__ void sweep2(int cnt, LD &&ld, ST &&step) {
+    if (cnt <= 0) return;
+    In a, b;
+    ld(a, 0);
+    ld(b, min(1, cnt - 1));
+    int i = 0;
+    for (; i + 1 < cnt; i += 2) {
+        step(a, i);
+        ld(a, min(i + 2, cnt - 1));  // past the end: re-loads the last step (harmless)
+        step(b, i + 1);
+        ld(b, min(i + 3, cnt - 1));
+    }
+    if (i < cnt) step(a, i);
+}
+
 __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double *__restrict__ dpk,
                                                         const double *__restrict__ dreg) {
     __shared__ double tt[16 * 17];            // wave 1's transposes
@@ -640,54 +669,37 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
         for (int r = 0; r < 4; ++r) D[r] += (4 * r + g == c) ? dg[k * 16 + 4 * r + g] : 0.0;
         return D;
     };
+    // group k's inputs: D_k (tile-native) with the y diagonal dreg_k, and the
+    // coupling tile Bt_{kb} (kb = k top-down, k - 1 bottom-up)
+    auto fload = [&](FacIn &in, int k, int kb) {
+        in.D = tn_load(tiles + k * 512LL, lane);
+        in.B = tn_load(tiles + kb * 512LL + 256, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) in.dr[r] = dg[k * 16 + 4 * r + g];
+    };
+    auto fstep = [&](const FacIn &in, int k, bool first, bool bottom) {
+        WM<1> M, D;
+        d4 B[2];
+        D.t[0][0] = in.D;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D.t[0][0][r] += (4 * r + g == c) ? in.dr[r] : 0.0;
+        B[0] = bottom ? tile_transpose(in.B, tt, g, c) : in.B;  // Bt_{k-1}^T bottom-up
+        if (!first) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - X_k^T X_k (Z_k^T Z_k)
+        else M = D;
+        B[1] = tile_identity(g, c);
+        const bool ok = chol_blk4_aug<2>(M.t[0][0], B, g, c);
+        if (!ok && (bottom || !fail)) fail = k + 1;  // bottom-up: the last one is the lowest
+        X.t[0][0] = B[0];
+        double *fk = fb + k * 768LL;
+        tn_store(fk + 256, lane, B[0]);  // X_{k+1} (top) / Z_{k-1} (bottom)
+        tn_store(fk + 512, lane, B[1]);  // Lkk^{-1} / L'_kk^{-1}
+    };
     if (wv == 0) {
-        d4 D1 = load_D(0), B1 = tn_load(tiles + 256, lane);
-        d4 D2 = load_D(min(1, p)), B2 = tn_load(tiles + min(1, p) * 512LL + 256, lane);
-        for (int k = 0; k < p; ++k) {
-            WM<1> M, D;
-            d4 B[1][2];
-            D.t[0][0] = D1;
-            B[0][0] = B1;
-            D1 = D2;
-            B1 = B2;
-            const int kn = min(k + 2, p);  // two groups ahead (re-loads past the end: harmless)
-            D2 = load_D(kn);
-            B2 = tn_load(tiles + kn * 512LL + 256, lane);
-            if (k > 0) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - X_k^T X_k
-            else M = D;
-            B[0][1] = tile_identity(g, c);
-            const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);
-            if (!ok && !fail) fail = k + 1;
-            X.t[0][0] = B[0][0];
-            double *fk = fb + k * 768LL;
-            tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1}
-            tn_store(fk + 512, lane, B[0][1]);    // Lkk^{-1}
-        }
+        sweep2<FacIn>(p, [&](FacIn &in, int i) { fload(in, i, i); },
+                      [&](const FacIn &in, int i) { fstep(in, i, i == 0, false); });
     } else {
-        d4 D1 = load_D(N), B1 = tn_load(tiles + (N - 1) * 512LL + 256, lane);
-        const int k2 = max(N - 1, p + 1);
-        d4 D2 = load_D(k2), B2 = tn_load(tiles + (k2 - 1) * 512LL + 256, lane);
-        for (int k = N; k > p; --k) {
-            WM<1> M, D;
-            d4 B[1][2];
-            D.t[0][0] = D1;
-            const d4 Bt = tile_transpose(B1, tt, g, c);  // Bt_{k-1}^T
-            D1 = D2;
-            B1 = B2;
-            const int kn = max(k - 2, p + 1);
-            D2 = load_D(kn);
-            B2 = tn_load(tiles + (kn - 1) * 512LL + 256, lane);
-            if (k < N) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - Z_k^T Z_k
-            else M = D;
-            B[0][0] = Bt;
-            B[0][1] = tile_identity(g, c);
-            const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);
-            if (!ok) fail = k + 1;  // descending: the last one is the lowest
-            X.t[0][0] = B[0][0];  // Z_{k-1}
-            double *fk = fb + k * 768LL;
-            tn_store(fk + 256, lane, X.t[0][0]);
-            tn_store(fk + 512, lane, B[0][1]);  // L'_kk^{-1}
-        }
+        sweep2<FacIn>(N - p, [&](FacIn &in, int i) { fload(in, N - i, N - i - 1); },
+                      [&](const FacIn &in, int i) { fstep(in, N - i, i == 0, true); });
         *reinterpret_cast<d4 *>(zmid + 4 * lane) = X.t[0][0];  // Z_p
     }
     if (lane == 0) wfail[wv] = fail;
@@ -716,30 +728,6 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
 
 // forward phase 2 on the twisted factor: L y = bvec from both ends toward the
 // middle group, its 16 x 16 solve, then L^T lam = y outward (two waves)
-// In of step i of a sweep: loaded two steps ahead into one of two buffers
-// used alternately (a 2x-unrolled loop: no register rotation, which made the
-// compiler wait for the freshly issued loads at every back edge)
-struct SolveIn {
-    d4 X, L;
-    WV<1> v;
-};
-
-template <class LD, class ST>
-__device__ __forceinline__ void sweep2(int cnt, LD &&ld, ST &&step) {
-    if (cnt <= 0) return;
-    SolveIn a, b;
-    ld(a, 0);
-    ld(b, min(1, cnt - 1));
-    int i = 0;
-    for (; i + 1 < cnt; i += 2) {
-        step(a, i);
-        ld(a, min(i + 2, cnt - 1));  // past the end: re-loads the last step (harmless)
-        step(b, i + 1);
-        ld(b, min(i + 3, cnt - 1));
-    }
-    if (i < cnt) step(a, i);
-}
-
 __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const double *__restrict__ bvec) {
     __shared__ double tt[2][16 * 17];
     __shared__ double vmid[16], lmid[16];
@@ -783,10 +771,10 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     };
     // ---- forward substitution from both ends ----
     if (wv == 0) {  // steps k = 0 .. p-1: X_k stored by group k - 1
-        sweep2(p, [&](SolveIn &in, int i) { load(in, max(i - 1, 0) * 768LL + 256, i, bv + i * 16); },
+        sweep2<SolveIn>(p, [&](SolveIn &in, int i) { load(in, max(i - 1, 0) * 768LL + 256, i, bv + i * 16); },
                [&](const SolveIn &in, int i) { fstep(in, i, i == 0); });
     } else {  // steps k = N .. p+1: Z_k stored by group k + 1
-        sweep2(N - p,
+        sweep2<SolveIn>(N - p,
                [&](SolveIn &in, int i) {
                    const int k = N - i;
                    load(in, min(k + 1, N) * 768LL + 256, k, bv + k * 16);
@@ -833,10 +821,10 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
     };
     if (wv == 0)
-        sweep2(p, [&](SolveIn &in, int i) { bload(in, p - 1 - i); },
+        sweep2<SolveIn>(p, [&](SolveIn &in, int i) { bload(in, p - 1 - i); },
                [&](const SolveIn &in, int i) { bstep(in, p - 1 - i); });
     else
-        sweep2(N - p, [&](SolveIn &in, int i) { bload(in, p + 1 + i); },
+        sweep2<SolveIn>(N - p, [&](SolveIn &in, int i) { bload(in, p + 1 + i); },
                [&](const SolveIn &in, int i) { bstep(in, p + 1 + i); });
 }
 
