@@ -294,9 +294,17 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
             bs.forward(x0, out)
 
         t = _timed(step, steps, warmup, dev, dist)
+        # one fresh protocol round for the check: the KKT forward accumulates the
+        # x0 terms of its rhs on every call (kkt.hpp:207-222, as the reference)
+        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+        step()
+        torch.cuda.synchronize(dev)
         ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
         res["kkt" if solver == "kkt" else "riccati"] = {"ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
-                                                        "status_ok": ok}
+                                                        "status_ok": ok,
+                                                        "oracle_rel_err": _conic_oracle_err(solver, n, m, N, ncs, E, c,
+                                                                                            H, h, D, x0, ws, ys, zs,
+                                                                                            irho, rho, out)}
         bs.close()
     # the ADMM outer loop on the same data (pdplqr_admm_solve): |u| <= 0.5,
     # rho = 1, from a cold start.  (a) 100 fixed iterations (eps = 0, one
@@ -340,6 +348,24 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
     return res
 
 
+def _conic_oracle_err(solver, n, m, N, ncs, E, c, H, h, D, x0, ws, ys, zs, irho, rho, out, probs=(0, -1)):
+    """Max relative error of the timed output against the CPU oracle on two
+    sampled problems (test infrastructure, outside the timed region)."""
+    from oracle.oracle import OracleKKT, OracleSerial
+    from pdplqr.model import PackedModel
+
+    err = 0.0
+    for b in probs:
+        a = [t[b].cpu().numpy() for t in (E, c, H, h, D, x0, ws, ys, zs, irho, rho, out)]
+        pm = PackedModel(n, m, N, ncs, *a[:5])
+        o = OracleKKT(pm) if solver == "kkt" else OracleSerial(pm)
+        o.update_problem_data(a[6], a[7], a[8], a[9], 1e-6)
+        o.backward(a[9] if solver == "kkt" else a[10])
+        ref = o.forward(a[5])
+        err = max(err, float(np.linalg.norm(a[11] - ref) / np.linalg.norm(ref)))
+    return err
+
+
 def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     """C4: one N = Ntot, 24/8 problem, horizon-sharded over the ranks (strong
     scaling): shard backward -> all-gather of slice elements (RCCL when nccl)
@@ -361,6 +387,7 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     ws0 = torch.zeros(1, Nl * s + n, dtype=torch.float64, device=dev)
     out = torch.empty_like(ws0)
     sh.update_problem_data(ws0, sigma=1e-6)
+    E0, H0 = E, H  # kept for the oracle check of the 1-GPU line
     del E, H
     if dist:
         step = lambda: solve_distributed(sh, x0, out)
@@ -373,8 +400,23 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     t = _timed(step, steps, warmup, dev, dist)
     ok = bool(torch.isfinite(out).all().item())
     sh.close()
+    oerr = None
+    if world == 1:  # the whole horizon is this rank's: check it against the serial oracle
+        from oracle.oracle import OracleSerial
+        from pdplqr.model import PackedModel
+
+        pm = PackedModel(n, m, Ntot, np.zeros(Ntot + 1, dtype=np.int32), E0[0].cpu().numpy(), c[0].cpu().numpy(),
+                         H0[0].cpu().numpy(), h[0].cpu().numpy(), np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(np.zeros(Ntot * s + n), None, None, None, 1e-6)
+        o.backward(None)
+        ref = o.forward(x0[0].cpu().numpy())
+        oerr = float(np.linalg.norm(out[0].cpu().numpy() - ref) / np.linalg.norm(ref))
+        del pm, o, ref
+    del E0, H0
     return {"N": Ntot, "nx": n, "nu": m, "n_gpus": world, "ms_per_solve": t * 1e3, "stages_per_s": Ntot / t,
-            "scaling": "strong", "finite": ok, "exchange": "all-gather of 3n^2+2n doubles per rank"}
+            "scaling": "strong", "finite": ok, "oracle_rel_err": oerr,
+            "exchange": "all-gather of 3n^2+2n doubles per rank"}
 
 
 def bench_end_to_end(bs, E, c, H, h, x0, ws0, out, dev, dist, local, steps=3, warmup=1, host_batch=256):
