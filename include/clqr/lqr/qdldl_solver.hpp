@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "clqr/detail/bridge.hpp"
+#include "clqr/lqr/kkt.hpp"
 
 namespace lqr {
 
@@ -37,6 +38,11 @@ public:
     }
 
     void forward(const VectorXs &x0, std::vector<VectorXs> &ws) { hd_.forward(x0, ws); }
+
+    // qdldl_solver.hpp:19,47-78: the QDLDL workspace (elimination tree, column
+    // counts, factor buffers) of a KKT matrix, e.g. KKTSystem::get_KKT_csc_matrix's.
+    // Host-side; the GPU factorisation does not use it.
+    std::unique_ptr<QDLDLData> create_workspace(const CscMatrix &Kkt) { return detail::create_qdldl_workspace(Kkt); }
 
 private:
     const LQRModel &model_;

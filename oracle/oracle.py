@@ -72,6 +72,7 @@ def lib():
         L.orc_kkt_forward.argtypes = [vp, _dp, _dp]
         L.orc_kkt_get_solution.argtypes = [vp, _dp]
         L.orc_kkt_get_csc.argtypes = [vp, _ip, _ip, _dp]
+        L.orc_kkt_get_rhs.argtypes = [vp, _dp]
         L.orc_batched_serial_solve.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp,
                                                C.c_double, _dp, C.c_int]
         L.orc_batched_serial_solve.restype = C.c_int
@@ -266,6 +267,11 @@ class OracleKKT(_Base):
         x = np.zeros(self.dim)
         lib().orc_kkt_get_solution(self.h, _d(x))
         return x
+
+    def rhs(self):
+        r = np.zeros(self.dim)
+        lib().orc_kkt_get_rhs(self.h, _d(r))
+        return r
 
     def csc(self):
         Ap = np.zeros(self.dim + 1, dtype=np.int32)

@@ -1284,6 +1284,13 @@ void orc_kkt_forward(void *p, const double *x0, double *ws) {
     memcpy(ws + (size_t)N * s, o->x + off, sizeof(double) * n);
 }
 
+/* The KKT right-hand side as the last forward left it (form_rhs plus the
+ * accumulated update_rhs_initial_stage terms, kkt.hpp:207-300). */
+void orc_kkt_get_rhs(void *p, double *r) {
+    orc_kkt *o = (orc_kkt *)p;
+    memcpy(r, o->rhs, sizeof(double) * o->dim);
+}
+
 /* Full KKT solution vector [primal | dual] after forward. */
 void orc_kkt_get_solution(void *p, double *x) {
     orc_kkt *o = (orc_kkt *)p;
