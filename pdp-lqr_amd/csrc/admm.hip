@@ -33,7 +33,10 @@
 //     k_update_problem_data followed by k_penalty, so the fused and the
 //     protocol-level iterations agree bit for bit;
 //   * the backward is backward_without_factorization (keep_factors = 1) or
-//     the factorizing kernel on the unchanged H~ (keep_factors = 0);
+//     the factorizing kernel on the unchanged H~ (keep_factors = 0); at 12/4
+//     with 4 constraint rows per stage (the C5 layout) the serial solver runs
+//     the update of iteration it INSIDE the streamed backward of it + 1
+//     (k_nofact_admm_dma), so no separate update pass touches HBM;
 //   * adaptive rho (OSQP's rule, on by default): at a termination test a
 //     problem whose normalised residual ratio e = sqrt((r_prim / max(|Dw|,|z|))
 //     / (r_dual / |D^T y|)) leaves [1/tol, tol] scales its rho by e (clamped to
@@ -44,6 +47,7 @@
 //     only, qdldl_solver.hpp:88-109).
 #include <algorithm>
 
+#include "admm.hpp"
 #include "solvers.hpp"
 
 namespace pdplqr {
@@ -58,17 +62,6 @@ struct AdmmState {
     int32_t *done = nullptr, *iters = nullptr, *conv = nullptr;
     int32_t *active = nullptr;    // [0] problems still iterating, [1] some rho changed
     int32_t *active_h = nullptr;  // pinned copy of active[0..1]
-};
-
-struct AdmmArgs {
-    Shape sh;
-    const double *D, *hv, *wt, *lb, *ub, *rho, *irho;
-    double *w, *y, *z, *hw, *gw;
-    const int32_t *d_off, *y_off;
-    int32_t *done, *iters, *conv, *active;
-    double *prim, *dual, *rscale;
-    double alpha, sigma, eps_abs, eps_rel, rho_tol;
-    int max_nc, it, adaptive;
 };
 
 // sum over the LPS lanes of one stage (xor butterflies: every lane ends with
@@ -183,27 +176,7 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
                 rd = fmax(rd, red[q][3]);
                 dty = fmax(dty, red[q][4]);
             }
-            a.iters[b] = a.it;
-            a.prim[b] = rp;
-            a.dual[b] = rd;
-            double f = 1.0;
-            if (rp <= a.eps_abs + a.eps_rel * fmax(dwm, zm) && rd <= a.eps_abs + a.eps_rel * dty) {
-                a.done[b] = 1;
-                a.conv[b] = 1;
-            } else {
-                atomicAdd(a.active, 1);
-                if (a.adaptive) {
-                    // OSQP's rho estimate (compute_rho_estimate): the ratio of the
-                    // normalised residuals, with its division guard 1e-30
-                    const double pn = rp / (fmax(dwm, zm) + 1e-30), dn = rd / (dty + 1e-30);
-                    const double e = sqrt(pn / (dn + 1e-30));
-                    if (e > a.rho_tol || e < 1.0 / a.rho_tol) {
-                        f = e;
-                        atomicOr(a.active + 1, 1);
-                    }
-                }
-            }
-            a.rscale[b] = f;
+            admm_decide(a, b, rp, dwm, zm, rd, dty);
         }
     }
 }
@@ -384,6 +357,8 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     const double *irho_or_null = Y > 0 ? s->irho : nullptr;
     int it = 1;
     bool refactor = true;  // iteration 1, and after an adaptive rho change
+    bool fused = false;    // this iteration's backward already ran inside the fused update
+    bool can_fuse = !kkt && Y > 0 && h->Lc != nullptr;  // cleared when the fused kernel does not apply
     int rho_updates = 0;
     for (;; ++it) {
         // x-update: the reference protocol (iteration 1 and after a rho
@@ -396,9 +371,10 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             if ((rc = solver_backward(h, kkt ? s->irho : s->rho))) return rc;
             h->factored = true;
             refactor = false;
-        } else if (!kkt) {
+        } else if (!kkt && !fused) {
             if ((rc = solver_backward_prepared(h))) return rc;
         }
+        fused = false;
         if ((rc = solver_forward(h, s->x0, s->wt))) return rc;
         if (Y == 0) {  // nothing to split: one LQ solve is the answer
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->w, s->wt, W * sizeof(double), hipMemcpyDeviceToDevice, S));
@@ -413,7 +389,15 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         const bool fuse = !kkt && !last;
         a.it = it;
         if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
-        if ((rc = launch_admm_update(a, sh.s <= 16, fuse, check, ugrid, ublk, S))) return rc;
+        if (fuse && can_fuse) {
+            // the update of this iteration and the backward_without_factorization
+            // of the next in one streamed pass (kernels_nofact.hip)
+            rc = solver_nofact_admm(h, a, check);
+            if (rc == PDPLQR_OK) fused = true;
+            else if (rc == PDPLQR_ERR_UNSUPPORTED) can_fuse = false;
+            else return rc;
+        }
+        if (!fused && (rc = launch_admm_update(a, sh.s <= 16, fuse, check, ugrid, ublk, S))) return rc;
         if (check) {
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));
@@ -423,6 +407,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
                                    s->rscale, s->rho, s->irho);
                 PDPLQR_HIP_TRY(hipGetLastError());
                 refactor = true;
+                fused = false;  // the fused backward used the old rho: refactor instead
                 ++rho_updates;
             }
         }

@@ -1,0 +1,52 @@
+// admm.hpp -- the ADMM outer loop's device arguments and termination /
+// adaptive-rho decision, shared by the stand-alone update kernel (admm.hip)
+// and the update fused into the streamed backward (kernels_nofact.hip).
+#pragma once
+#include "internal.hpp"
+
+namespace pdplqr {
+
+struct AdmmArgs {
+    Shape sh;
+    const double *D, *hv, *wt, *lb, *ub, *rho, *irho;
+    double *w, *y, *z, *hw, *gw;
+    const int32_t *d_off, *y_off;
+    int32_t *done, *iters, *conv, *active;
+    double *prim, *dual, *rscale;
+    double alpha, sigma, eps_abs, eps_rel, rho_tol;
+    int max_nc, it, adaptive;
+};
+
+// Termination test of iteration a.it for problem b from the five maxima
+// (r_prim, |Dw|, |z|, r_dual, |D^T y|), then OSQP's rho estimate when the
+// test fails (admm.hip header).  One thread per problem.
+__device__ __forceinline__ void admm_decide(const AdmmArgs &a, int b, double rp, double dwm, double zm, double rd,
+                                            double dty) {
+    a.iters[b] = a.it;
+    a.prim[b] = rp;
+    a.dual[b] = rd;
+    double f = 1.0;
+    if (rp <= a.eps_abs + a.eps_rel * fmax(dwm, zm) && rd <= a.eps_abs + a.eps_rel * dty) {
+        a.done[b] = 1;
+        a.conv[b] = 1;
+    } else {
+        atomicAdd(a.active, 1);
+        if (a.adaptive) {
+            // OSQP's compute_rho_estimate: the ratio of the normalised
+            // residuals, with its division guard 1e-30
+            const double pn = rp / (fmax(dwm, zm) + 1e-30), dn = rd / (dty + 1e-30);
+            const double e = sqrt(pn / (dn + 1e-30));
+            if (e > a.rho_tol || e < 1.0 / a.rho_tol) {
+                f = e;
+                atomicOr(a.active + 1, 1);
+            }
+        }
+    }
+    a.rscale[b] = f;
+}
+
+// Fused ADMM update + backward_without_factorization (kernels_nofact.hip):
+// PDPLQR_ERR_UNSUPPORTED when the shape / constraint layout is not covered.
+int launch_nofact_admm(const RiccatiArgs &r, const AdmmArgs &a, bool check, hipStream_t st);
+
+}  // namespace pdplqr

@@ -18,6 +18,7 @@
 // exactly NI DMA instructions and 2 stores, so "stage k - 1 has landed" is one
 // fixed vmcnt.  Output: lu' into the rollout record FR_k (its L part is
 // unchanged) and lp_k = [lu'; p_k] into the factor cache, as the generic kernel.
+#include "admm.hpp"
 #include "device_common.hpp"
 
 #include <stdint.h>
@@ -167,6 +168,247 @@ __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
         if (k > 0) q = offchain(ring[(k - 1) % D], Lk, s, m);
         wave_sync();
     }
+}
+
+// ---------------------------------------------------------------------------
+// ADMM iterations >= 2 (admm.hip): the z / y / w step of iteration it and the
+// backward_without_factorization of iteration it + 1 in ONE streamed pass.
+// The backward needs h~_k = h_k - sigma w_k^{it+1} - D_k^T (rho o g_k^{it+1}),
+// and everything that forms it -- w~_k (the rollout's output), w_k, D_k, z_k,
+// y_k, the bounds and rho of stage k -- is per stage.  So the stage record
+// grows by those (120 doubles at 12/4 with nc = 4: 476 doubles, 4 DMA
+// instructions) and the update of stage k - 1 runs while stage k is
+// processed, off the p-chain, right before its h~ enters q_{k-1}.  Lanes
+// (g, c): row g of D_k (nc = 4 rows), column c (s = 16); D w~ is a butterfly
+// over c, D^T (rho o g) a permlane sum over g.  The stand-alone update pass
+// (k_admm_update) and its w~ / w / h~ round trip through HBM disappear.
+// Requirements: nc_k = NC for k < N, nc_N = 0 (else admm.hip runs the
+// unfused path).  CHECK: the termination test of iteration it over the whole
+// problem (one wave = one problem: a wave-wide max, then admm_decide).
+// ---------------------------------------------------------------------------
+template <int NN, int MM, int NC>
+struct NofactAdmmShape {
+    static constexpr int n = NN, m = MM, s = NN + MM, ps = s * (s + 1) / 2;
+    static constexpr int OE = 0, OC = n * s, OH = OC + n, OL = OH + s, OWT = OL + ps, OW = OWT + s, OD = OW + s,
+                         OZ = OD + NC * s, OY = OZ + NC, OLB = OY + NC, OUB = OLB + NC, ORHO = OUB + NC,
+                         OIR = ORHO + NC, REC = OIR + NC;
+    static constexpr int CH = REC / 2, NI = (CH + 63) / 64, TAIL = CH - (NI - 1) * 64;
+    static constexpr bool ok = s == 16 && NC == 4 && n % 2 == 0 && (n * s) % 2 == 0 && ps % 2 == 0;
+};
+
+template <int NN, int MM, int NC, int D, bool CHECK>
+__global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs Q) {
+    using SH = NofactAdmmShape<NN, MM, NC>;
+    constexpr int n = SH::n, m = SH::m, s = SH::s, NI = SH::NI;
+    static_assert(SH::ok, "fused nofact / ADMM layout");
+    __shared__ __attribute__((aligned(16))) double ring[D][SH::REC];
+    __shared__ double sp[16], st[16], sw[16];
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
+    const Shape &sh = A.sh;
+    const long long b = blockIdx.x;
+    if (Q.done[b]) return;  // frozen problem: no update, no backward (wave-uniform)
+    const int N = sh.N;
+    const double al = Q.alpha, bl = 1.0 - Q.alpha;
+    const double *hb = Q.hv + b * sh.perh;  // the MODEL's h
+    const double *Lb = A.Lc + b * sh.perHw;
+    double *FRb = A.KD + b * sh.perKD;
+    double *lpb = A.lpc + b * sh.perh;
+    double *wb = Q.w + b * sh.perh, *hwb = Q.hw + b * sh.perh;
+    double *zb = Q.z + b * sh.ny, *yb = Q.y + b * sh.ny, *gb = Q.gw + b * sh.ny;
+    constexpr int frs = s * m + m;
+    // per-lane source of each DMA chunk: base at stage 0 + stage stride
+    const double *gbase[NI];
+    int gstride[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+        int ch = q * 64 + lane;
+        ch = ch < SH::CH ? ch : SH::CH - 1;
+        const int d = 2 * ch;
+        const long long pb = b * sh.perh, yb0 = b * sh.ny;
+        if (d < SH::OC) { gbase[q] = A.E + b * sh.perE + d; gstride[q] = n * s; }
+        else if (d < SH::OH) { gbase[q] = A.c + b * sh.perc + (d - SH::OC); gstride[q] = n; }
+        else if (d < SH::OL) { gbase[q] = Q.hv + pb + (d - SH::OH); gstride[q] = s; }
+        else if (d < SH::OWT) { gbase[q] = Lb + (d - SH::OL); gstride[q] = SH::ps; }
+        else if (d < SH::OW) { gbase[q] = Q.wt + pb + (d - SH::OWT); gstride[q] = s; }
+        else if (d < SH::OD) { gbase[q] = Q.w + pb + (d - SH::OW); gstride[q] = s; }
+        else if (d < SH::OZ) { gbase[q] = Q.D + b * sh.ndD + (d - SH::OD); gstride[q] = NC * s; }
+        else if (d < SH::OY) { gbase[q] = Q.z + yb0 + (d - SH::OZ); gstride[q] = NC; }
+        else if (d < SH::OLB) { gbase[q] = Q.y + yb0 + (d - SH::OY); gstride[q] = NC; }
+        else if (d < SH::OUB) { gbase[q] = Q.lb + yb0 + (d - SH::OLB); gstride[q] = NC; }
+        else if (d < SH::ORHO) { gbase[q] = Q.ub + yb0 + (d - SH::OUB); gstride[q] = NC; }
+        else if (d < SH::OIR) { gbase[q] = Q.rho + yb0 + (d - SH::ORHO); gstride[q] = NC; }
+        else { gbase[q] = Q.irho + yb0 + (d - SH::OIR); gstride[q] = NC; }
+    }
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+            if (q < NI - 1 || lane < SH::TAIL) dma16(gbase[q] + (long long)k * gstride[q], &ring[slot][q * 128]);
+    };
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
+    // The ADMM step of stage kk from its ring record; returns h~_kk[cl].
+    // Exactly 5 stores (z, y, g: lanes c == 0; w, h~: row group 0).
+    auto upd = [&](const double *R, int kk) -> double {
+        const double wt = R[SH::OWT + cl], wo = R[SH::OW + cl];
+        const double wn = al * wt + bl * wo;
+        const double d = R[SH::OD + g + cl * NC];  // D_kk[g][cl]
+        double v = d * wt, vw = d * wo;
+#pragma unroll
+        for (int msk = 1; msk < 16; msk <<= 1) {
+            v += __shfl_xor(v, msk, 64);
+            vw += __shfl_xor(vw, msk, 64);
+        }
+        const double zr = R[SH::OZ + g], yr = R[SH::OY + g], rr = R[SH::ORHO + g], ir = R[SH::OIR + g];
+        const double vrel = al * v + bl * zr;
+        const double zn = fmin(fmax(vrel + ir * yr, R[SH::OLB + g]), R[SH::OUB + g]);
+        const double yn = yr + rr * (vrel - zn);
+        const double gn = zn - ir * yn;
+        const long long yo = (long long)kk * NC + g;
+        if (cl == 0) gstore(zb + yo, zn);
+        if (cl == 0) gstore(yb + yo, yn);
+        if (cl == 0) gstore(gb + yo, gn);
+        const double ag = sum_groups(d * (rr * gn));  // (D^T (rho o g))[cl]
+        const double hj = (R[SH::OH + cl] - Q.sigma * wn) - ag;
+        if (g == 0) gstore(wb + (long long)kk * s + cl, wn);
+        if (g == 0) gstore(hwb + (long long)kk * s + cl, hj);
+        if (CHECK) {
+            const double dwn = al * v + bl * vw;
+            rp = fmax(rp, fabs(dwn - zn));
+            dwm = fmax(dwm, fabs(dwn));
+            zm = fmax(zm, fabs(zn));
+            rd = fmax(rd, fabs(sum_groups(d * (rr * (zn - zr)))));
+            dty = fmax(dty, fabs(sum_groups(d * yn)));
+        }
+        return hj;
+    };
+    // P c and q = h~ + E^T (P c) for record R with factor Lp (as k_nofact_dma)
+    auto offchain = [&](const double *R, const double *Lp, int dim, int off, double ht) -> double {
+        const int j = cl < n ? cl : n - 1;
+        double a = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+            const int i = 4 * qq + g;
+            const int ic = i < n ? i : n - 1;
+            const double l = Lp[pidx(off + (ic >= j ? ic : j), off + j, dim)];
+            a = __builtin_fma((i < n && i >= j) ? l : 0.0, R[SH::OC + ic], a);
+        }
+        a = sum_groups(a);
+        if (g == 0 && cl < n) st[cl] = a;
+        wave_sync();
+        double w = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+            const int jj = 4 * qq + g;
+            const int jc = jj < n ? jj : n - 1;
+            const double l = Lp[pidx(off + (j >= jc ? j : jc), off + jc, dim)];
+            w = __builtin_fma((jj < n && jj <= j) ? l : 0.0, st[jc], w);
+        }
+        w = sum_groups(w);
+        if (g == 0 && cl < n) sw[cl] = w;
+        wave_sync();
+        double qv = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+            const int i = 4 * qq + g;
+            const int ic = i < n ? i : n - 1;
+            qv = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sw[ic], qv);
+        }
+        return sum_groups(qv) + ht;
+    };
+
+    // ---- terminal (nc_N = 0): w_N relaxed, h~_N = h_N - sigma w_N; lp_N = h~_N ----
+    if (lane < n) {
+        const long long o = (long long)N * s + lane;
+        const double wn = al * Q.wt[b * sh.perh + o] + bl * wb[o];
+        const double hN = hb[o] - Q.sigma * wn;
+        wb[o] = wn;
+        hwb[o] = hN;
+        sp[lane] = hN;
+        lpb[o] = hN;
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) {
+        const int k = N - 1 - j;
+        dma(k >= 0 ? k : 0, ((k % D) + D) % D);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    double q;
+    {
+        const double *R = ring[(N - 1) % D];
+        const double ht = upd(R, N - 1);
+        q = offchain(R, Lb + (long long)N * SH::ps, n, 0, ht);  // q_{N-1} with Lxx_N
+    }
+    constexpr int VM = NI + 7;  // vm ops per iteration: NI DMA + 2 backward stores + 5 update stores
+    for (int k = N - 1; k >= 0; --k) {
+        const int kp = k - (D - 1);
+        dma(kp >= 0 ? kp : 0, ((kp % D) + D) % D);
+        if (k >= N - (D - 2)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM * (D - 2)) : "memory");
+        wave_sync();
+        const double *R = ring[k % D];
+        const double *Lk = R + SH::OL;
+        const int cm = cl < m ? cl : m - 1;
+        const double rdiag = 1.0 / Lk[pidx(cm, cm, s)];
+        double lcol[MM];
+#pragma unroll
+        for (int j = 0; j < MM; ++j) lcol[j] = (cl > j) ? Lk[pidx(cl > j ? cl : j, j, s)] : 0.0;
+        double a = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+            const int i = 4 * qq + g;
+            const int ic = i < n ? i : n - 1;
+            a = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sp[ic], a);
+        }
+        const double lp = sum_groups(a) + q;
+        double acc = 0.0, myu = 0.0;
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            const double uj = readlane_f64((lp - acc) * rdiag, j);
+            if (cl == j) myu = uj;
+            acc = __builtin_fma(lcol[j], uj, acc);
+        }
+        const double pk = lp - acc;
+        wave_sync();
+        if (g == 0 && cl >= m) sp[cl - m] = pk;
+        if (lane < m) gstore(FRb + (long long)k * frs + s * m + lane, myu);
+        if (lane < s) gstore(lpb + (long long)k * s + lane, lane < m ? myu : pk);
+        if (k > 0) {
+            const double *Rn = ring[(k - 1) % D];
+            const double ht = upd(Rn, k - 1);
+            q = offchain(Rn, Lk, s, m, ht);
+        }
+        wave_sync();
+    }
+    if (CHECK) {
+#pragma unroll
+        for (int msk = 32; msk >= 1; msk >>= 1) {
+            rp = fmax(rp, __shfl_xor(rp, msk, 64));
+            dwm = fmax(dwm, __shfl_xor(dwm, msk, 64));
+            zm = fmax(zm, __shfl_xor(zm, msk, 64));
+            rd = fmax(rd, __shfl_xor(rd, msk, 64));
+            dty = fmax(dty, __shfl_xor(dty, msk, 64));
+        }
+        if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty);
+    }
+}
+
+int launch_nofact_admm(const RiccatiArgs &a, const AdmmArgs &q, bool check, hipStream_t st) {
+    const Shape &sh = a.sh;
+    if (getenv("PDPLQR_NO_ADMM_FUSE") || !a.Lc || !a.lpc || sh.n != 12 || sh.m != 4 || sh.ny != 4 * sh.N)
+        return PDPLQR_ERR_UNSUPPORTED;
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (!al(a.E) || !al(a.c) || !al(a.Lc) || !al(q.hv) || !al(q.wt) || !al(q.w) || !al(q.D) || !al(q.z) ||
+        !al(q.y) || !al(q.lb) || !al(q.ub) || !al(q.rho) || !al(q.irho) || sh.perE % 2 || sh.perc % 2 ||
+        sh.perh % 2 || sh.perHw % 2 || sh.ndD % 2 || sh.ny % 2)
+        return PDPLQR_ERR_UNSUPPORTED;
+    if (check)
+        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st,
+                           a, q);
+    else
+        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_DEPTH, false>), dim3(sh.batch), dim3(64), 0,
+                           st, a, q);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
 }
 
 static bool nofact_aligned(const RiccatiArgs &a) {

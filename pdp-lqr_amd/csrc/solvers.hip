@@ -3,6 +3,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "admm.hpp"
 #include "parallel.hpp"
 #include "solvers.hpp"
 
@@ -418,6 +419,16 @@ int solver_backward_prepared(pdplqr_handle h) {
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1, fact);
     return fact ? launch_riccati_backward(riccati_args(h), h->stream)
                 : launch_riccati_backward_nofact(riccati_args(h), h->stream);
+}
+
+// ADMM: the update of iteration it fused into the backward of it + 1
+// (serial solver with cached factors; ERR_UNSUPPORTED otherwise)
+int solver_nofact_admm(pdplqr_handle h, const AdmmArgs &a, bool check) {
+    if (h->cfg.solver != PDPLQR_SOLVER_SERIAL) return PDPLQR_ERR_UNSUPPORTED;
+    for (int k = 0; k < h->sh.N; ++k)
+        if (h->ncs[k] != 4) return PDPLQR_ERR_UNSUPPORTED;
+    if (h->ncs[h->sh.N] != 0) return PDPLQR_ERR_UNSUPPORTED;
+    return launch_nofact_admm(riccati_args(h), a, check, h->stream);
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {

@@ -16,6 +16,8 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho);
 // factorizing kernels on the unchanged H~
 int solver_backward_prepared(pdplqr_handle h);
 void admm_release(pdplqr_handle h);  // admm.hip
+struct AdmmArgs;
+int solver_nofact_admm(pdplqr_handle h, const AdmmArgs &a, bool check);
 int solver_forward(pdplqr_handle h, const double *x0, double *ws);
 int solver_clear(pdplqr_handle h);
 int solver_status(pdplqr_handle h, int32_t *flags);  // per-problem status (host)

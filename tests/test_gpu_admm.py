@@ -250,3 +250,64 @@ def test_adaptive_rho_matches_oracle(solver):
         # iterates, so they carry the path's tolerance amplified (KKT: 1e-8)
         assert rel_err(info["rho"][b], oi["rho"]) < (1e-6 if solver == "kkt" else 1e-9), b
         assert rel_err(w[b], ow) < tol and rel_err(y[b], oy) < tol, b
+
+
+@pytest.mark.parametrize("check_every,adaptive", [(1, False), (5, True), (25, True)])
+def test_fused_update_equals_unfused(check_every, adaptive):
+    """At 12/4 with 4 rows per stage (C5's layout) the serial solver runs the
+    ADMM update inside the streamed backward (k_nofact_admm_dma).  Same
+    per-problem iteration counts, convergence flags and rho as the separate
+    update pass (PDPLQR_NO_ADMM_FUSE), iterates to 1e-8, and the oracle."""
+    import os
+
+    n, m, nc, N, B = 12, 4, 4, 60, 6
+    models, x0s = [], []
+    for b in range(B):
+        mod, x0 = random_model(n, m, N, seed=700 + b, nc=nc, D_kind="ubox")
+        for k, nd in enumerate(mod.nodes):
+            if nd.n_con:
+                nd.e_lb[:] = -0.4 - 0.1 * b
+                nd.e_ub[:] = 0.4 + 0.1 * b
+        models.append(mod)
+        x0s.append(x0)
+    # terminal stage without constraints (the fused layout): rebuild the models
+    from pdplqr.model import LQRModel
+
+    fixed = []
+    for mod in models:
+        nm = LQRModel(n, m, N)
+        for k, nd in enumerate(mod.nodes):
+            nm.add_node(n, m, nc if k < N else 0, k, k == N)
+            t = nm.nodes[k]
+            t.H[:] = nd.H
+            t.h[:] = nd.h
+            if k < N:
+                t.E[:] = nd.E
+                t.c[:] = nd.c
+                t.D_con[:] = nd.D_con
+                t.e_lb[:] = nd.e_lb
+                t.e_ub[:] = nd.e_ub
+        fixed.append(nm)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(fixed, x0s, seed=9)
+    rho = np.full(lb.shape, 0.3)
+    st = dict(max_iter=400, check_every=check_every, eps_abs=1e-6, eps_rel=1e-6, adaptive_rho=adaptive)
+    res = {}
+    for mode in ("fused", "separate"):
+        if mode == "separate":
+            os.environ["PDPLQR_NO_ADMM_FUSE"] = "1"
+        try:
+            res[mode] = _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, **st)
+        finally:
+            os.environ.pop("PDPLQR_NO_ADMM_FUSE", None)
+    (wf, yf, zf, fi), (wsep, ysep, zsep, si) = res["fused"], res["separate"]
+    assert np.array_equal(fi["iters"], si["iters"]) and np.array_equal(fi["converged"], si["converged"])
+    assert fi["converged"].any() or not adaptive  # fixed rho = 0.3 needs more than 400 iterations here
+    for a, b_ in ((wf, wsep), (yf, ysep), (zf, zsep), (fi["rho"], si["rho"])):
+        d = np.linalg.norm(a - b_, axis=1) / np.maximum(np.linalg.norm(b_, axis=1), 1e-300)
+        # rounding of the fused h~ sum (permlane tree vs k_penalty's sequential
+        # sum) carried through up to 400 contractive iterations and rho changes
+        assert float(d.max()) < 1e-8, float(d.max())
+    for b in (0, B - 1):
+        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial", **st)
+        assert oi["iters"] == fi["iters"][b]
+        assert rel_err(wf[b], ow) < 1e-9 and rel_err(yf[b], oy) < 1e-9, b
