@@ -186,6 +186,16 @@ __global__ void k_admm_init(long long ny_total, const double *__restrict__ rho, 
     if (t < ny_total) irho[t] = 1.0 / rho[t];
 }
 
+// input check: e_lb <= e_ub and 0 < rho < inf on every row (OSQP's
+// validate_data / validate_settings); flag[0] counts violations
+__global__ void k_admm_validate(long long ny_total, const double *__restrict__ lb, const double *__restrict__ ub,
+                                const double *__restrict__ rho, int32_t *flag) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ny_total) return;
+    const double r = rho[t];
+    if (!(lb[t] <= ub[t]) || !(r > 0.0 && r < 1.0e300)) atomicAdd(flag, 1);
+}
+
 // adaptive rho: every row of problem b scales by rscale[b], clamped to OSQP's
 // [RHO_MIN, RHO_MAX] = [1e-6, 1e6]
 __global__ void k_admm_rescale(long long ny_total, int ny, const double *__restrict__ rscale, double *__restrict__ rho,
@@ -312,8 +322,18 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         PDPLQR_HIP_TRY(hipMemcpyAsync(s->lb, lb, Y * sizeof(double), kin, S));
         PDPLQR_HIP_TRY(hipMemcpyAsync(s->ub, ub, Y * sizeof(double), kin, S));
         PDPLQR_HIP_TRY(hipMemcpyAsync(s->rho, rho, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
+        hipLaunchKernelGGL(k_admm_validate, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, s->lb, s->ub,
+                           s->rho, s->active);
         hipLaunchKernelGGL(k_admm_init, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, s->rho, s->irho);
         PDPLQR_HIP_TRY(hipGetLastError());
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, sizeof(int32_t), hipMemcpyDeviceToHost, S));
+        PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+        if (s->active_h[0] != 0) {
+            set_error("admm_solve: " + std::to_string(s->active_h[0]) +
+                      " constraint rows with e_lb > e_ub, or rho not in (0, inf)");
+            return PDPLQR_ERR_INVALID;
+        }
     }
     PDPLQR_HIP_TRY(hipMemsetAsync(s->done, 0, B * sizeof(int32_t), S));
     PDPLQR_HIP_TRY(hipMemsetAsync(s->conv, 0, B * sizeof(int32_t), S));

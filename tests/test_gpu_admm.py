@@ -311,3 +311,24 @@ def test_fused_update_equals_unfused(check_every, adaptive):
         ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial", **st)
         assert oi["iters"] == fi["iters"][b]
         assert rel_err(wf[b], ow) < 1e-9 and rel_err(yf[b], oy) < 1e-9, b
+
+
+def test_invalid_bounds_and_rho_are_rejected():
+    """e_lb > e_ub on a row, or rho <= 0, is an ERR_INVALID before any solve
+    (OSQP's validation); the C-ABI message names it."""
+    from pdplqr import PdplqrError
+
+    models, x0s = _ubox_models(2)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s)
+    rho = np.full(lb.shape, 1.0)
+    bad = lb.copy()
+    bad[1, 5] = ub[1, 5] + 1.0
+    with pytest.raises(PdplqrError) as e:
+        _run_gpu("serial", pms, ncs, A, bad, ub, x0, ws, ys, zs, rho, True, max_iter=5)
+    assert "e_lb > e_ub" in str(e.value)
+    r2 = rho.copy()
+    r2[0, 0] = 0.0
+    with pytest.raises(PdplqrError):
+        _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, r2, True, max_iter=5)
+    w, y, z, info = _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, max_iter=5)
+    assert info["iterations"] == 5
