@@ -231,6 +231,44 @@ def measured_copy_gbs(dev, nbytes=1 << 32, reps=5):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
+    """C3: batch 4096 independent LQRs, N = 256, 12/4 (MPC-style batched solve):
+    backward + forward of the serial solver, as the headline line, plus an
+    oracle check of two problems."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+
+    n, m = 12, 4
+    E, c, H, h, x0 = gen_batch_device(n, m, N, batch, seed=4321, device=dev)
+    ws0 = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False, device=local)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+
+    def step():
+        bs.backward()
+        bs.forward(x0, out)
+
+    t = _timed(step, steps, warmup, dev, dist)
+    ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
+    bs.close()
+    err = 0.0
+    for b in (0, batch - 1):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), *(a[b].cpu().numpy() for a in (E, c, H, h)),
+                         np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(np.zeros(N * (n + m) + n), None, None, None, 1e-6)
+        o.backward(None)
+        ref = o.forward(x0[b].cpu().numpy())
+        err = max(err, float(np.linalg.norm(out[b].cpu().numpy() - ref) / np.linalg.norm(ref)))
+    del E, c, H, h
+    torch.cuda.empty_cache()
+    return {"N": N, "nx": n, "nu": m, "batch": batch, "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
+            "status_ok": ok, "oracle_rel_err": err}
+
+
 def bench_single(local, dev, dist, steps=10, warmup=3):
     """C2: one N = 1024, 12/4 problem, LQRParallelSolver path (segments + scans).
     Latency-bound; stages/s = N / time of backward + forward (every rank runs a
@@ -593,6 +631,7 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_secondary:
         res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
+                            "C3_batched_N256": bench_batched_c3(local, dev, dist),
                             "C5_conic_kkt": bench_conic(local, dev, dist),
                             "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}
     if rank == 0 and world == 1 and not args.no_cpu:

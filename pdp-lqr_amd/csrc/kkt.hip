@@ -347,6 +347,96 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     tn_store(q + 1280, lane, Linv);
 }
 
+// P = 16: the per-stage work of k_kkt_stage + the primal half of k_kkt_pack16
+// on MFMA register tiles (one wave per (problem, stage), no LDS matrices):
+//   L = chol(H_k + sigma I) with [C_kk^T | C_{k+1,k}^T | I] carried through the
+//   blocked elimination (chol_blk4_aug): V = L^{-1} C_kk^T, U = L^{-1} C_{k+1,k}^T,
+//   L^{-1} come out directly; V^T V, U^T U, U^T V are one MFMA product each.
+// Writes the primal tiles ppk (L^{-T}, V, U, V^T, U^T, L^{-1}) and the three
+// dual blocks (tile-native, into blk's first three tiles) for k_kkt_pack16d,
+// which adds the neighbour's U^T U.  The generic LDS kernel took 15.4 ms + 3.4 ms
+// of packing per model at C5 (N = 512, batch 1024).
+__global__ __launch_bounds__(64) void k_kkt_stage16(KKTArgs A) {
+    __shared__ double tt[16 * 17];
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int p = A.prim_dim[k], gk = A.gdim[k], g1 = k < N ? A.gdim[k + 1] : 0;
+    const int nck = A.ncs[k];
+    const double *Hk = A.H + b * sh.perH + (long long)k * s * s;
+    const int ldH = k < N ? s : n;
+    const double *Ek = A.E + b * sh.perE + (long long)(k < N ? k : 0) * n * s;
+    const double *Dk = A.D + b * sh.ndD + A.d_off[k];
+    d4 M, B[3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;  // row (primal index in KKT order), column c
+        double h = (i == c) ? 1.0 : 0.0, v = 0.0, u = 0.0;
+        if (i < p && c < p) {
+            h = Hk[kref(k, N, n, m, i) + kref(k, N, n, m, c) * ldH];
+            if (i == c) h += A.sigma;
+        }
+        if (i < p && c < gk) {  // C_kk^T
+            if (k == 0) v = Dk[c + i * nck];                       // y0 rows: D0 u-columns
+            else if (c < n) v = (i == c) ? -1.0 : 0.0;             // lambda_k rows: -x_k
+            else v = Dk[(c - n) + kref(k, N, n, m, i) * nck];      // y_k rows
+        }
+        if (i < p && c < g1 && c < n) u = Ek[c + kref(k, N, n, m, i) * n];  // lambda_{k+1} rows: E_k
+        M[r] = h;
+        B[0][r] = v;
+        B[1][r] = u;
+        B[2][r] = (i == c) ? 1.0 : 0.0;
+    }
+    const bool ok = chol_blk4_aug<3>(M, B, g, c);  // B <- L^{-1} B
+    WM<1> V, U, VtV, UtU, UtV;
+    V.t[0][0] = B[0];
+    U.t[0][0] = B[1];
+    wm_tn<1>(VtV, V, V, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
+    wm_tn<1>(UtU, U, U, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
+    wm_tn<1>(UtV, U, V, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
+    double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
+    tn_store(q, lane, tile_transpose(B[2], tt, g, c));  // L^{-T}
+    tn_store(q + 256, lane, B[0]);                      // V
+    tn_store(q + 512, lane, B[1]);                      // U
+    tn_store(q + 768, lane, tile_transpose(B[0], tt, g, c));   // V^T
+    tn_store(q + 1024, lane, tile_transpose(B[1], tt, g, c));  // U^T
+    tn_store(q + 1280, lane, B[2]);                     // L^{-1}
+    double *o = A.blk + (b * (N + 1) + k) * 6LL * 256;
+    tn_store(o, lane, VtV.t[0][0]);
+    tn_store(o + 256, lane, UtU.t[0][0]);
+    tn_store(o + 512, lane, UtV.t[0][0]);
+    if (!ok && lane == 0) A.pstat[b] = 1;  // primal block not positive definite
+}
+
+// P = 16, after k_kkt_stage16: D_k = (V^T V)_k + (U^T U)_{k-1} + rho_dyn on the
+// lambda diagonal (identity padding) and (U^T V)_k^T, tile-native into dpk --
+// k_kkt_pack16's dual half on the tile-native blocks
+__global__ __launch_bounds__(64) void k_kkt_pack16d(KKTArgs A, double *__restrict__ dpk) {
+    __shared__ double tt[16 * 17];
+    const Shape &sh = A.sh;
+    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x / (N + 1);
+    const int k = blockIdx.x % (N + 1);
+    const int gk = A.gdim[k];
+    const double *o = A.blk + (b * (N + 1) + k) * 6LL * 256;
+    d4 D = tn_load(o, lane);
+    if (k > 0) {
+        const d4 P = tn_load(o - 6 * 256 + 256, lane);  // (U^T U)_{k-1}
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D[r] += P[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        if (i == c && k > 0 && i < sh.n) D[r] += A.rho_dyn;  // lambda rows: -rho_dyn I (frozen)
+        if (!(i < gk && c < gk)) D[r] = (i == c) ? 1.0 : 0.0;
+    }
+    double *out = dpk + (b * (N + 1) + k) * 512LL;
+    tn_store(out, lane, D);
+    tn_store(out + 256, lane, tile_transpose(tn_load(o + 512, lane), tt, g, c));  // (U^T V)^T
+}
+
 // forward phase 1, P = 16 (parallel over stages): w = L^{-1} r_p, t = V^T w,
 // t1 = U^T w as single-column MFMA products on the packed primal tiles
 __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
@@ -1145,12 +1235,15 @@ int kkt_on_model(pdplqr_handle h) {
     const Shape &sh = h->sh;
     KKTArgs a = kkt_args(h);
     const size_t smem = 4 * (size_t)ks->P * ks->P * sizeof(double);
-    hipLaunchKernelGGL(k_kkt_stage, dim3((unsigned)(sh.batch * (sh.N + 1))), dim3(64), smem, h->stream, a);
-    PDPLQR_HIP_TRY(hipGetLastError());
-    if (ks->P == 16) {
-        hipLaunchKernelGGL(k_kkt_pack16, dim3((unsigned)(sh.batch * (sh.N + 1))), dim3(64), 0, h->stream, a, ks->dpk);
-        PDPLQR_HIP_TRY(hipGetLastError());
+    const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), wave(64);
+    if (ks->P == 16 && !getenv("PDPLQR_KKT_STAGE_GENERIC")) {
+        hipLaunchKernelGGL(k_kkt_stage16, stages, wave, 0, h->stream, a);
+        hipLaunchKernelGGL(k_kkt_pack16d, stages, wave, 0, h->stream, a, ks->dpk);
+    } else {
+        hipLaunchKernelGGL(k_kkt_stage, stages, wave, smem, h->stream, a);
+        if (ks->P == 16) hipLaunchKernelGGL(k_kkt_pack16, stages, wave, 0, h->stream, a, ks->dpk);
     }
+    PDPLQR_HIP_TRY(hipGetLastError());
     ks->formed = true;
     return PDPLQR_OK;
 }

@@ -250,3 +250,44 @@ def test_twisted_factor_equals_natural_order(N):
         o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
         o.backward(irho[b])
         assert rel_err(outs["twist"][b], o.forward(x0[b])) < TOL, b
+
+
+def test_register_tile_stage_equals_generic():
+    """P = 16 model setup on register tiles (k_kkt_stage16 + k_kkt_pack16d, the
+    default) against the generic LDS kernels (PDPLQR_KKT_STAGE_GENERIC): the
+    same solution to 1e-12 on a batch with varying constraint counts."""
+    import os
+
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 37, 4
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 4242)
+    g = np.random.default_rng(7)
+    ncs = g.integers(0, 5, N + 1).astype(np.int32)
+    ncs[N] = min(int(ncs[N]), 4)
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    outs = {}
+    for mode in ("tiles", "generic"):
+        if mode == "generic":
+            os.environ["PDPLQR_KKT_STAGE_GENERIC"] = "1"
+        try:
+            bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+            bs.set_model(E, c, H, h, D)
+            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+            bs.backward(irho)
+            out = np.zeros((batch, N * s + n))
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            outs[mode] = out
+            bs.close()
+        finally:
+            os.environ.pop("PDPLQR_KKT_STAGE_GENERIC", None)
+    d = np.linalg.norm(outs["tiles"] - outs["generic"], axis=1) / np.linalg.norm(outs["generic"], axis=1)
+    assert float(d.max()) < 1e-12, float(d.max())
