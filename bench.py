@@ -269,6 +269,81 @@ def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
             "status_ok": ok, "oracle_rel_err": err}
 
 
+def bench_factor_reuse(local, dev, dist, steps=10, warmup=3, N=1024, batch=4096):
+    """SURVEY.md 8(f) rank 1 at the headline config: backward_without_factorization
+    + forward (lqr_solver.hpp:65-77) on factors cached by one factorising
+    backward, the per-iteration cost of an ADMM loop.  The right-hand side
+    changes between the factorisation and the timed calls (new w-bar), so the
+    oracle check (two problems, factorising OracleSerial on the new data) sees
+    the reused factors applied to new linear terms.  Roofline of the streamed
+    k_nofact_dma: it reads the per-stage record [E | c | h~ | L packed] and
+    writes lp (8 (n s + n + s + s(s+1)/2) + 8 s bytes per stage)."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+
+    n, m = 12, 4
+    s = n + m
+    E, c, H, h, x0 = gen_batch_device(n, m, N, batch, seed=2468, device=dev)
+    ws0 = torch.zeros(batch, N * s + n, dtype=torch.float64, device=dev)
+    ws1 = torch.randn(batch, N * s + n, dtype=torch.float64, device=dev,
+                      generator=torch.Generator(device=dev).manual_seed(5))
+    out = torch.empty_like(ws0)
+    sigma = 1e-3
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=True, device=local)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=sigma)
+    bs.backward()
+    bs.update_problem_data(ws1, sigma=sigma)  # same H~, new h~ = h - sigma w-bar
+    stream = torch.cuda.ExternalStream(bs.handle.stream(), device=dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    it = iter(evs)
+
+    def step():
+        e = next(it, None)
+        if e:
+            e[0].record(stream)
+        bs.backward_without_factorization()
+        if e:
+            e[1].record(stream)
+        bs.forward(x0, out)
+        if e:
+            e[2].record(stream)
+
+    for _ in range(warmup):
+        bs.backward_without_factorization()
+        bs.forward(x0, out)
+    t = _timed(step, steps, 0, dev, dist)
+    bs.synchronize()
+    ms_bwd = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    ms_fwd = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
+    bs.close()
+    err = 0.0
+    for b in (0, batch - 1):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), *(a[b].cpu().numpy() for a in (E, c, H, h)),
+                         np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws1[b].cpu().numpy(), None, None, None, sigma)
+        o.backward(None)
+        ref = o.forward(x0[b].cpu().numpy())
+        err = max(err, float(np.linalg.norm(out[b].cpu().numpy() - ref) / np.linalg.norm(ref)))
+    del E, c, H, h, ws0, ws1, out
+    torch.cuda.empty_cache()
+    stages = N * batch
+    bytes_stage = 8 * (n * s + n + s + s * (s + 1) // 2) + 8 * s
+    achieved = bytes_stage * stages / (ms_bwd * 1e-3) / 1e9
+    kern = "k_nofact_dma<12, 4, 4>"
+    pmc = load_pmc_traffic(f"nofact_N{N}_n{n}_m{m}_b{batch}", kern)
+    return {"N": N, "nx": n, "nu": m, "batch": batch, "ms_per_iteration": t * 1e3, "stages_per_s": stages / t,
+            "kernels_ms": {"backward_without_factorization": ms_bwd, "forward": ms_fwd},
+            "roofline": {"kernel": kern, "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (pmc["bytes_per_launch"] if pmc else None),
+                         "bytes_per_stage_algorithmic": bytes_stage},
+            "status_ok": ok, "oracle_rel_err": err}
+
+
 def bench_single(local, dev, dist, steps=10, warmup=3):
     """C2: one N = 1024, 12/4 problem, LQRParallelSolver path (segments + scans).
     Latency-bound; stages/s = N / time of backward + forward (every rank runs a
@@ -632,6 +707,7 @@ def main():
     if not args.no_secondary:
         res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
                             "C3_batched_N256": bench_batched_c3(local, dev, dist),
+                            "factor_reuse": bench_factor_reuse(local, dev, dist, N=N, batch=B),
                             "C5_conic_kkt": bench_conic(local, dev, dist),
                             "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -16,6 +16,7 @@ from collections import defaultdict
 
 def main():
     root, tag = sys.argv[1], sys.argv[2]
+    dom = sys.argv[3] if len(sys.argv) > 3 else "k_riccati_bwd"  # dominant-kernel substring
     per = defaultdict(lambda: defaultdict(list))
     rows = []
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
@@ -38,10 +39,10 @@ def main():
             continue
         out["kernels"][short] = {c: sum(v) / len(v) for c, v in d.items()}
     # dominant kernel of the bench step: the value-form backward when present
-    names = sorted(out["kernels"], key=lambda k: ("bwd_schur" not in k, "k_riccati_bwd" not in k))
-    bwd = [out["kernels"][k] for k in names if "k_riccati_bwd" in k]
+    names = sorted(out["kernels"], key=lambda k: ("bwd_schur" not in k, dom not in k))
+    bwd = [out["kernels"][k] for k in names if dom in k]
     if bwd:
-        out["dominant_kernel"] = [k for k in names if "k_riccati_bwd" in k][0]
+        out["dominant_kernel"] = [k for k in names if dom in k][0]
     if bwd and "FETCH_SIZE" in bwd[0] and "WRITE_SIZE" in bwd[0]:
         b = bwd[0]
         out["bytes_per_launch"] = b["FETCH_SIZE"] * 1024 * 2 + b["WRITE_SIZE"] * 1024
