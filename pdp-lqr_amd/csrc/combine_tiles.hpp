@@ -251,6 +251,39 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, d4 (&B)[T][TB], int n_rt, 
     return ok;
 }
 
+// The 4 x 4 block step of the blocked Cholesky applies T = L4^{-1} (lower,
+// wave-uniform) to a tile's rows j0..j0+3, which every lane (g, c) holds as
+// register j0/4 = X[j0 + g][c].  That register IS the B operand of
+// v_mfma_f64_16x16x4_f64 (B[k][n] = lane (k, n)), so with A[m][k] = T[m][k]
+// in rows m < 4 (zeros below) one MFMA leaves (T X_rows)[g][c] in register 0
+// of lane (g, c): the layout of the panel.  t4_operand builds that A operand
+// once per block (lane (g, c) supplies A[c][g]); each tile then costs one
+// MFMA instead of four row-group broadcasts, ten FMAs and a select chain.
+// PDPLQR_T4_MFMA=0 keeps the broadcast form (A/B diagnostics).
+#ifndef PDPLQR_T4_MFMA
+#define PDPLQR_T4_MFMA 1
+#endif
+
+// The lane picks are products with 0/1 weights (loop-invariant per lane), not
+// selects: a select chain over values used nowhere else was turned into
+// divergent branches that sank the 4 x 4 block arithmetic into them.
+__device__ __forceinline__ double t4_operand(const double (&Ti)[4][4], int g, int c) {
+    double a = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double r = 0.0;  // T[i][g], zero above the diagonal
+#pragma unroll
+        for (int k = 0; k <= i; ++k) r = __builtin_fma(Ti[i][k], (g == k) ? 1.0 : 0.0, r);
+        a = __builtin_fma(r, (c == i) ? 1.0 : 0.0, a);
+    }
+    return a;
+}
+
+__device__ __forceinline__ double t4_apply(double ta, double xrow) {
+    const d4 z = mfma_f64(ta, xrow, d4{0.0, 0.0, 0.0, 0.0});
+    return z[0];
+}
+
 // Blocked Cholesky of a full symmetric 16 x 16 tile M = C C^T (both
 // triangles held, as MFMA products leave them), carrying TB column tiles:
 // B <- C^{-1} B (final, no row scaling left).  Four pivots per block:
@@ -298,6 +331,13 @@ __device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) 
                 T[i][j] = -v * inv[i];
             }
         }
+#if PDPLQR_T4_MFMA
+        const double top = t4_operand(T, g, c);
+        const double v = t4_apply(top, M[blk]);
+        const double vt = (c >= j0 + 4) ? v : 0.0;  // panel, trailing rows only
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) B[tb][blk] = t4_apply(top, B[tb][blk]);  // T4 B_block
+#else
         // row-block values M[j0 + k][c] (register blk, row group k) -> V
         double ml[4];
 #pragma unroll
@@ -326,6 +366,7 @@ __device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) 
             }
             B[tb][blk] = s4;
         }
+#endif
         if (blk < 3) M = mfma_f64(-vt, vt, M);
 #pragma unroll
         for (int tb = 0; tb < TB; ++tb) B[tb] = mfma_f64(-vt, B[tb][blk], B[tb]);
@@ -375,10 +416,16 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
             }
         }
         double vt[T];
+#if PDPLQR_T4_MFMA
+        const double top = t4_operand(Ti, g, c);
+#endif
 #pragma unroll
         for (int ta = 0; ta < T; ++ta) {
             vt[ta] = 0.0;
             if (ta < tj) continue;
+#if PDPLQR_T4_MFMA
+            const double v = t4_apply(top, M.t[tj][ta][rj]);  // (T M_rows)[g][16 ta + c]
+#else
             double ml[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) ml[k] = bcast_group(M.t[tj][ta][rj], k);  // M[j0 + k][16 ta + c]
@@ -390,6 +437,7 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
                 for (int k = 0; k <= jj; ++k) s = __builtin_fma(Ti[jj][k], ml[k], s);
                 v = (g == jj) ? s : v;
             }
+#endif
             const int col = 16 * ta + c;
             vt[ta] = (col >= j0 + 4) ? v : 0.0;  // trailing rows of the panel
             if (!AUG) M.t[tj][ta][rj] = (col >= j0) ? v : 0.0;  // row block of C^T, final
@@ -397,6 +445,9 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
         if (AUG) {
 #pragma unroll
             for (int tb = 0; tb < TB; ++tb) {  // block rows of B: T4 B_block (register rj of tile row tj)
+#if PDPLQR_T4_MFMA
+                B[tj][tb][rj] = t4_apply(top, B[tj][tb][rj]);
+#else
                 double bl[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) bl[k] = bcast_group(B[tj][tb][rj], k);
@@ -409,6 +460,7 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
                     s4 = (g == jj) ? s : s4;
                 }
                 B[tj][tb][rj] = s4;
+#endif
             }
         }
 #pragma unroll
