@@ -109,6 +109,14 @@ struct SchurSmem {
 //     the A operand of lp_x -= W lu' (one 16x16x4 MFMA each).
 // The u block of the tile is left as Muu - Luu Luu^T (~0); only the x block
 // and the x rows of lp are read by the next stage.
+// PDPLQR_SCHUR_T4 = 1 forms W with one MFMA (t4_apply, as the blocked
+// Cholesky does): 32 fewer VALU and 18 fewer cross-lane ops per loop trip, but
+// the MFMA sits on the stage chain; same-box A/B (scripts/gpu_r2k.sh) 3.11 ->
+// 3.13 ms per backward, so it stays off.
+#ifndef PDPLQR_SCHUR_T4
+#define PDPLQR_SCHUR_T4 0
+#endif
+
 template <int MM>
 __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], double &w, double (&luq)[4], int g,
                                                    int c) {
@@ -151,6 +159,16 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         for (int j = 0; j <= i; ++j) v = __builtin_fma(T[i][j], lu[j], v);
         luq[i] = v;
     }
+#if PDPLQR_SCHUR_T4
+    // W = T times the u rows (register 0 of every lane: the B operand) as one
+    // MFMA (combine_tiles.hpp t4_apply); T zero-padded past m
+    double Tz[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Tz[i][j] = (i < MM) ? T[i < MM ? i : 0][j < MM ? j : 0] : 0.0;
+    w = t4_apply(t4_operand(Tz, g, c), M[0]);
+#else
     // column c of the u rows: m_l = M[l][c] (group l, register 0)
     double ml[4];
 #pragma unroll
@@ -163,6 +181,7 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         for (int l = 0; l <= j; ++l) v = __builtin_fma(T[j][l], ml[l], v);
         w = (g == j) ? v : w;  // W[c][g]; groups g >= m keep 0
     }
+#endif
 #if PDPLQR_LP_IN_P
     // lp -= W lu' rides in the same MFMA: column 0 of M (u column 0: dead
     // after this stage -- the next stage reads P's x rows through the x
