@@ -276,6 +276,69 @@ __device__ __forceinline__ void tn_store(double *tile, int lane, const d4 &v) {
     *(__attribute__((address_space(1))) d4 *)(tile + 4 * lane) = v;
 }
 
+// Triangular tiles (L^{-1} lower, L^{-T} upper: exact zeros on the other side,
+// the elimination that forms them only combines earlier rows) are stored
+// packed in tile-native order: lane (g, c) keeps its nonzero rows r0..r1 (a
+// contiguous range) at off.., lanes in order -- 136 doubles, so a solve reads
+// 1,088 B per triangular tile instead of 2 KB.  With F(d) = sum_{j<d}
+// (floor(j/4) + 1): lower (4r + g >= c) r0 = ceil((c - g)/4)+, off = sum_{g'<g}
+// (64 - F(15 - g')) + 4c - F(c - g - 1)+; upper (4r + g <= c) r1 = floor((c - g)/4),
+// off = sum_{g'<g} F(16 - g') + F(c - g)+.  Tile slots stay 256 doubles apart.
+struct TriLane {
+    int off, r0, r1;
+};
+
+__device__ __forceinline__ int tri_f(int d) {
+    const int q = d >> 2, t = d & 3;
+    return 2 * q * (q + 1) + t * (q + 1);
+}
+
+__device__ __forceinline__ TriLane tri_lane(int g, int c, bool upper) {
+    TriLane t;
+    int base = 0;
+#pragma unroll
+    for (int gg = 0; gg < 3; ++gg)
+        if (gg < g) base += upper ? tri_f(16 - gg) : 64 - tri_f(15 - gg);
+    if (!upper) {
+        t.r0 = c > g ? (c - g + 3) >> 2 : 0;
+        t.r1 = 3;
+        t.off = base + 4 * c - tri_f(c > g ? c - g - 1 : 0);
+    } else {
+        t.r0 = 0;
+        t.r1 = c >= g ? (c - g) >> 2 : -1;
+        t.off = base + tri_f(c > g ? c - g : 0);
+    }
+    return t;
+}
+
+// branch-free: rows outside r0..r1 read a valid slot and are masked to 0.
+// The raw / mask split lets a prefetching loop keep the raw values in its
+// buffer and mask at the point of use (masking at the load makes the compiler
+// wait for the load right there).
+__device__ __forceinline__ d4 tri_load_raw(const double *tile, const TriLane &t) {
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = tile[(r >= t.r0 && r <= t.r1) ? t.off + r - t.r0 : 0];
+    return v;
+}
+
+__device__ __forceinline__ d4 tri_mask(const d4 &raw, const TriLane &t) {
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (r >= t.r0 && r <= t.r1) ? raw[r] : 0.0;
+    return v;
+}
+
+__device__ __forceinline__ d4 tri_load(const double *tile, const TriLane &t) {
+    return tri_mask(tri_load_raw(tile, t), t);
+}
+
+__device__ __forceinline__ void tri_store(double *tile, const TriLane &t, const d4 &v) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (r >= t.r0 && r <= t.r1) tile[t.off + r - t.r0] = v[r];
+}
+
 // C/D-layout transpose of a 16 x 16 tile through LDS (t: 16 x 17 doubles)
 __device__ __forceinline__ d4 tile_transpose(const d4 &v, double *t, int g, int c) {
 #pragma unroll
@@ -339,12 +402,12 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
         U[r] = (i < p && c < g1) ? bk[512 + i + 16 * c] : 0.0;
     }
     double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    tn_store(q, lane, tile_transpose(Linv, tt, g, c));
+    tri_store(q, tri_lane(g, c, true), tile_transpose(Linv, tt, g, c));  // L^{-T}, packed
     tn_store(q + 256, lane, V);
     tn_store(q + 512, lane, U);
     tn_store(q + 768, lane, tile_transpose(V, tt, g, c));
     tn_store(q + 1024, lane, tile_transpose(U, tt, g, c));
-    tn_store(q + 1280, lane, Linv);
+    tri_store(q + 1280, tri_lane(g, c, false), Linv);  // L^{-1}, packed
 }
 
 // P = 16: the per-stage work of k_kkt_stage + the primal half of k_kkt_pack16
@@ -396,12 +459,12 @@ __global__ __launch_bounds__(64) void k_kkt_stage16(KKTArgs A) {
     wm_tn<1>(UtU, U, U, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
     wm_tn<1>(UtV, U, V, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
     double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    tn_store(q, lane, tile_transpose(B[2], tt, g, c));  // L^{-T}
+    tri_store(q, tri_lane(g, c, true), tile_transpose(B[2], tt, g, c));  // L^{-T}, packed
     tn_store(q + 256, lane, B[0]);                      // V
     tn_store(q + 512, lane, B[1]);                      // U
     tn_store(q + 768, lane, tile_transpose(B[0], tt, g, c));   // V^T
     tn_store(q + 1024, lane, tile_transpose(B[1], tt, g, c));  // U^T
-    tn_store(q + 1280, lane, B[2]);                     // L^{-1}
+    tri_store(q + 1280, tri_lane(g, c, false), B[2]);  // L^{-1}, packed
     double *o = A.blk + (b * (N + 1) + k) * 6LL * 256;
     tn_store(o, lane, VtV.t[0][0]);
     tn_store(o + 256, lane, UtU.t[0][0]);
@@ -447,7 +510,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
     const int p = A.prim_dim[k];
     const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
     WM<1> LiT, V, U;
-    LiT.t[0][0] = tn_load(q, lane);
+    LiT.t[0][0] = tri_load(q, tri_lane(g, c, true));
     V.t[0][0] = tn_load(q + 256, lane);
     U.t[0][0] = tn_load(q + 512, lane);
     const double *rp = A.rhs + b * A.dim + A.prim_off[k];
@@ -478,7 +541,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *_
     WM<1> VT, UT, Li;
     VT.t[0][0] = tn_load(q + 768, lane);
     UT.t[0][0] = tn_load(q + 1024, lane);
-    Li.t[0][0] = tn_load(q + 1280, lane);
+    Li.t[0][0] = tri_load(q + 1280, tri_lane(g, c, false));
     const double *wk = A.wv + (b * (N + 1) + k) * 64LL;
     const double *wn = A.wv + (b * (N + 1) + min(k + 1, N)) * 64LL;  // U_N = 0
     WV<1> w, lk, ln, v, z;
@@ -554,6 +617,7 @@ __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__
                                                      const double *__restrict__ dreg) {
     const Shape &sh = A.sh;
     const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
     const long long b = blockIdx.x;
     const double *tiles = dpk + b * (N + 1) * 512LL;
     const double *dg = dreg + b * (N + 1) * 16LL;
@@ -606,7 +670,7 @@ __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__
 #endif
         double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
         tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1} = L_{k+1,k}^T
-        tn_store(fk + 512, lane, Linv);       // Lkk^{-1}
+        tri_store(fk + 512, tl, Linv);        // Lkk^{-1}, packed
     }
     if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
 }
@@ -618,6 +682,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
     __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
     const long long b = blockIdx.x;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
     const double *fb = A.fac + b * (N + 1) * 3LL * 256;
@@ -629,7 +694,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
     // forward: X_k natural (stored by group k-1), Lkk^{-1} (transposed at use)
     auto fload = [&](In &in, int k) {
         in.X = tn_load(fb + (long long)max(k - 1, 0) * 768 + 256, lane);
-        in.L = tn_load(fb + (long long)k * 768 + 512, lane);
+        in.L = tri_load(fb + (long long)k * 768 + 512, tl);
 #pragma unroll
         for (int r = 0; r < 4; ++r) in.v[r] = bv[k * 16 + 4 * r + g];
     };
@@ -657,7 +722,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     auto bload = [&](In &in, int k) {
         in.X = tn_load(fb + (long long)min(k, N - 1) * 768 + 256, lane);
-        in.L = tn_load(fb + (long long)k * 768 + 512, lane);
+        in.L = tri_load(fb + (long long)k * 768 + 512, tl);
 #pragma unroll
         for (int r = 0; r < 4; ++r) in.v[r] = wvb[(long long)k * 64 + 48 + 4 * r + g];
     };
@@ -745,6 +810,7 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
     const Shape &sh = A.sh;
     const int N = sh.N, p = N / 2;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
     __builtin_assume(lane >= 0 && lane < 64);
     const long long b = blockIdx.x;
     const double *tiles = dpk + b * (N + 1) * 512LL;
@@ -782,7 +848,7 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
         X.t[0][0] = B[0];
         double *fk = fb + k * 768LL;
         tn_store(fk + 256, lane, B[0]);  // X_{k+1} (top) / Z_{k-1} (bottom)
-        tn_store(fk + 512, lane, B[1]);  // Lkk^{-1} / L'_kk^{-1}
+        tri_store(fk + 512, tl, B[1]);   // Lkk^{-1} / L'_kk^{-1}, packed
     };
     if (wv == 0) {
         sweep2<FacIn>(p, [&](FacIn &in, int i) { fload(in, i, i); },
@@ -808,7 +874,7 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
         B[0] = d4{0.0, 0.0, 0.0, 0.0};
         B[1] = tile_identity(g, c);
         const bool ok = chol_blk4_aug<2>(M.t[0][0], B, g, c);
-        tn_store(fb + p * 768LL + 512, lane, B[1]);  // L_pp^{-1}
+        tri_store(fb + p * 768LL + 512, tl, B[1]);  // L_pp^{-1}, packed
         int f = fail;
         if (!ok && (!f || p + 1 < f)) f = p + 1;
         if (wfail[1] && (!f || wfail[1] < f)) f = wfail[1];
@@ -824,38 +890,44 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     const Shape &sh = A.sh;
     const int N = sh.N, p = N / 2;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
     __builtin_assume(lane >= 0 && lane < 64);
     const long long b = blockIdx.x;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
     const double *fb = A.fac + b * (N + 1) * 3LL * 256;
     const double *bv = bvec + b * (N + 1) * 16LL;
     double *T = tt[wv];
-    auto vin = [&](const double *src) {  // a 16-vector into column 0 (lanes c == 0)
+    auto vin_raw = [&](const double *src) {  // a 16-vector, row 4 r + g in every lane (branch-free)
         WV<1> v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double x = src[4 * r + g];  // every lane loads (branch-free), column 0 keeps it
-            v.t[0][r] = (c == 0) ? x : 0.0;
-        }
+        for (int r = 0; r < 4; ++r) v.t[0][r] = src[4 * r + g];
         return v;
     };
+    auto vmask = [&](const WV<1> &raw) {  // column 0 keeps it
+        WV<1> v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? raw.t[0][r] : 0.0;
+        return v;
+    };
+    auto vin = [&](const double *src) { return vmask(vin_raw(src)); };
+    // raw loads into the prefetch buffer; the masks are applied in the step
     auto load = [&](SolveIn &in, long long xoff, int k, const double *vsrc) {
         in.X = tn_load(fb + xoff, lane);
-        in.L = tn_load(fb + k * 768LL + 512, lane);
-        in.v = vin(vsrc);
+        in.L = tri_load_raw(fb + k * 768LL + 512, tl);
+        in.v = vin_raw(vsrc);
     };
     WV<1> y;
     y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
     // forward step: y_k = Lkk^{-1} (bvec_k - C^T y_prev), C = X_k (top) or Z_k (bottom)
     auto fstep = [&](const SolveIn &in, int k, bool first) {
-        WV<1> v = in.v;
+        WV<1> v = vmask(in.v);
         if (!first) {
             WM<1> Ck;
             Ck.t[0][0] = in.X;
             wv_tn<1>(v, Ck, y, 16, -1.0, &v);
         }
         WM<1> LinvT;
-        LinvT.t[0][0] = tile_transpose(in.L, T, g, c);
+        LinvT.t[0][0] = tile_transpose(tri_mask(in.L, tl), T, g, c);
         wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
         wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
     };
@@ -886,7 +958,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         const WV<1> yb = vin(vmid);
         wv_tn<1>(v, Zp, yb, 16, -1.0, &v);
         WM<1> Linv, LinvT;
-        Linv.t[0][0] = tn_load(fb + p * 768LL + 512, lane);
+        Linv.t[0][0] = tri_load(fb + p * 768LL + 512, tl);
         LinvT.t[0][0] = tile_transpose(Linv.t[0][0], T, g, c);
         WV<1> yp, lam;
         wv_tn<1>(yp, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
@@ -902,11 +974,11 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     // (bottom), both stored by group k
     auto bload = [&](SolveIn &in, int k) { load(in, k * 768LL + 256, k, wvb + (long long)k * 64 + 48); };
     auto bstep = [&](const SolveIn &in, int k) {
-        WV<1> v = in.v;
+        WV<1> v = vmask(in.v);
         WM<1> CT, Linv;
         CT.t[0][0] = tile_transpose(in.X, T, g, c);
         wv_tn<1>(v, CT, lam, 16, -1.0, &v);
-        Linv.t[0][0] = in.L;
+        Linv.t[0][0] = tri_mask(in.L, tl);
         wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
         wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
     };
