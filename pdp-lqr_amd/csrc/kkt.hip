@@ -512,7 +512,8 @@ __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
     WM<1> LiT, V, U;
     LiT.t[0][0] = tri_load(q, tri_lane(g, c, true));
     V.t[0][0] = tn_load(q + 256, lane);
-    U.t[0][0] = tn_load(q + 512, lane);
+    U.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+    if (c < sh.n) U.t[0][0] = tn_load(q + 512, lane);  // columns c >= n (y_{k+1}) are zero
     const double *rp = A.rhs + b * A.dim + A.prim_off[k];
     WV<1> r, w, t, t1;
 #pragma unroll
