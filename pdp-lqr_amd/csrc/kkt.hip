@@ -848,7 +848,9 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
         if (!ok && (bottom || !fail)) fail = k + 1;  // bottom-up: the last one is the lowest
         X.t[0][0] = B[0];
         double *fk = fb + k * 768LL;
-        tn_store(fk + 256, lane, B[0]);  // X_{k+1} (top) / Z_{k-1} (bottom)
+        // X_{k+1} (top) / Z_{k-1} (bottom).  X = Lkk^{-1} (U^T V)_k^T keeps the
+        // zero columns c >= n of (U^T V)^T (U's y columns): those lanes store nothing
+        if (bottom || c < sh.n) tn_store(fk + 256, lane, B[0]);
         tri_store(fk + 512, tl, B[1]);   // Lkk^{-1} / L'_kk^{-1}, packed
     };
     if (wv == 0) {
@@ -912,8 +914,11 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     };
     auto vin = [&](const double *src) { return vmask(vin_raw(src)); };
     // raw loads into the prefetch buffer; the masks are applied in the step
+    // wave 0 reads X tiles (zero, unstored columns c >= n), wave 1 full Z tiles
+    const bool xcol = wv == 1 || c < sh.n;
+    auto xmask = [&](const d4 &x) { return xcol ? x : d4{0.0, 0.0, 0.0, 0.0}; };
     auto load = [&](SolveIn &in, long long xoff, int k, const double *vsrc) {
-        in.X = tn_load(fb + xoff, lane);
+        if (xcol) in.X = tn_load(fb + xoff, lane);  // raw; masked in the step
         in.L = tri_load_raw(fb + k * 768LL + 512, tl);
         in.v = vin_raw(vsrc);
     };
@@ -924,7 +929,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         WV<1> v = vmask(in.v);
         if (!first) {
             WM<1> Ck;
-            Ck.t[0][0] = in.X;
+            Ck.t[0][0] = xmask(in.X);
             wv_tn<1>(v, Ck, y, 16, -1.0, &v);
         }
         WM<1> LinvT;
@@ -951,7 +956,8 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         WV<1> v = vin(bv + p * 16);
         if (p > 0) {
             WM<1> Xp;
-            Xp.t[0][0] = tn_load(fb + (p - 1) * 768LL + 256, lane);
+            Xp.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+            if (c < sh.n) Xp.t[0][0] = tn_load(fb + (p - 1) * 768LL + 256, lane);
             wv_tn<1>(v, Xp, y, 16, -1.0, &v);
         }
         WM<1> Zp;
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     auto bstep = [&](const SolveIn &in, int k) {
         WV<1> v = vmask(in.v);
         WM<1> CT, Linv;
-        CT.t[0][0] = tile_transpose(in.X, T, g, c);
+        CT.t[0][0] = tile_transpose(xmask(in.X), T, g, c);
         wv_tn<1>(v, CT, lam, 16, -1.0, &v);
         Linv.t[0][0] = tri_mask(in.L, tl);
         wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
