@@ -378,7 +378,7 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     tn_store(o, lane, D);
     tn_store(o + 256, lane, Bt);
     // primal tiles for the parallel solve phases, ppk [b][N+1][6][256]:
-    // L_k^{-T}, V_k, U_k (solve1) and V_k^T, U_k^T, L_k^{-1} (solve3).
+    // L_k^{-T}, V_k, U_k (solve1) and V_k^T, L_k^{-1} (solve3, which also reads U_k).
     // L^{-1} by re-eliminating L L^T carrying I (identity padding past p).
     __shared__ double tt[16 * 17];
     const int p = A.prim_dim[k];
@@ -406,7 +406,6 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     tn_store(q + 256, lane, V);
     tn_store(q + 512, lane, U);
     tn_store(q + 768, lane, tile_transpose(V, tt, g, c));
-    tn_store(q + 1024, lane, tile_transpose(U, tt, g, c));
     tri_store(q + 1280, tri_lane(g, c, false), Linv);  // L^{-1}, packed
 }
 
@@ -415,7 +414,7 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
 //   L = chol(H_k + sigma I) with [C_kk^T | C_{k+1,k}^T | I] carried through the
 //   blocked elimination (chol_blk4_aug): V = L^{-1} C_kk^T, U = L^{-1} C_{k+1,k}^T,
 //   L^{-1} come out directly; V^T V, U^T U, U^T V are one MFMA product each.
-// Writes the primal tiles ppk (L^{-T}, V, U, V^T, U^T, L^{-1}) and the three
+// Writes the primal tiles ppk (L^{-T}, V, U, V^T, -, L^{-1}) and the three
 // dual blocks (tile-native, into blk's first three tiles) for k_kkt_pack16d,
 // which adds the neighbour's U^T U.  The generic LDS kernel took 15.4 ms + 3.4 ms
 // of packing per model at C5 (N = 512, batch 1024).
@@ -463,7 +462,6 @@ __global__ __launch_bounds__(64) void k_kkt_stage16(KKTArgs A) {
     tn_store(q + 256, lane, B[0]);                      // V
     tn_store(q + 512, lane, B[1]);                      // U
     tn_store(q + 768, lane, tile_transpose(B[0], tt, g, c));   // V^T
-    tn_store(q + 1024, lane, tile_transpose(B[1], tt, g, c));  // U^T
     tri_store(q + 1280, tri_lane(g, c, false), B[2]);  // L^{-1}, packed
     double *o = A.blk + (b * (N + 1) + k) * 6LL * 256;
     tn_store(o, lane, VtV.t[0][0]);
@@ -534,6 +532,7 @@ __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
 __global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *__restrict__ x0,
                                                       double *__restrict__ ws) {
     __shared__ double zs[16];
+    __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
@@ -541,7 +540,11 @@ __global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *_
     const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
     WM<1> VT, UT, Li;
     VT.t[0][0] = tn_load(q + 768, lane);
-    UT.t[0][0] = tn_load(q + 1024, lane);
+    // U^T from U through LDS: U's columns c >= n are zero, so those lanes load
+    // nothing (U^T's zero rows would not skip whole cache lines)
+    d4 u = d4{0.0, 0.0, 0.0, 0.0};
+    if (c < n) u = tn_load(q + 512, lane);
+    UT.t[0][0] = tile_transpose(u, tt, g, c);
     Li.t[0][0] = tri_load(q + 1280, tri_lane(g, c, false));
     const double *wk = A.wv + (b * (N + 1) + k) * 64LL;
     const double *wn = A.wv + (b * (N + 1) + min(k + 1, N)) * 64LL;  // U_N = 0
@@ -1190,7 +1193,7 @@ struct KKTState {
     double *dpk = nullptr;   // P = 16: D_k and (U^T V)_k^T tiles, tile-native [b][N+1][2][256]
     double *dreg = nullptr;  // P = 16: y diagonal per group [b][N+1][16]
     double *bvec = nullptr;  // P = 16: forward-substitution right-hand sides [b][N+1][16]
-    double *ppk = nullptr;   // P = 16: primal tiles L^{-T}, V, U, V^T, U^T, L^{-1} [b][N+1][6][256]
+    double *ppk = nullptr;   // P = 16: primal tiles L^{-T}, V, U, V^T, (unused), L^{-1} [b][N+1][6][256]
     bool formed = false;
 };
 
