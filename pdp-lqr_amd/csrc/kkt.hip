@@ -44,7 +44,7 @@ struct KKTArgs {
     double *fac;    // [b][N+1][3][P*P]: Lkk, L_{k+1,k} (P = 16: its transpose), Lkk^{-1} (P = 16)
     double *rhs;    // [b][dim]
     double *wv;     // [b][N+1][4][P]: w, t, t1, lam
-    double *ppk;    // P = 16: primal tiles [b][N+1][6][256] (tile-native)
+    double *ppk;    // P = 16: H^{-1} (packed) and G^T per stage [b][N+1][2][256] (PPK)
     int32_t *status;
     int32_t *pstat;  // per problem: a primal block H_k + sigma I was not positive definite
 };
@@ -339,6 +339,69 @@ __device__ __forceinline__ void tri_store(double *tile, const TriLane &t, const 
         if (r >= t.r0 && r <= t.r1) tile[t.off + r - t.r0] = v[r];
 }
 
+// Symmetric tiles (H_k^{-1} = L^{-T} L^{-1}: an MFMA product X^T X sums the same
+// products in the same order for (i, j) and (j, i), so it is exactly symmetric)
+// are stored as their packed lower triangle; lane (g, c) reads row 4r + g of
+// column c from its own lower slot or from the mirror (c, 4r + g), which lives
+// in lane (c & 3, 4r + g), row c >> 2.  Indices per lane, once.
+struct SymLane {
+    int idx[4];
+};
+
+__device__ __forceinline__ SymLane sym_lane(int g, int c) {
+    SymLane sl;
+    const TriLane own = tri_lane(g, c, false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        const TriLane mir = tri_lane(c & 3, i, false);
+        sl.idx[r] = i >= c ? own.off + r - own.r0 : mir.off + (c >> 2) - mir.r0;
+    }
+    return sl;
+}
+
+__device__ __forceinline__ d4 sym_load(const double *tile, const SymLane &sl) {
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = tile[sl.idx[r]];
+    return v;
+}
+
+// P = 16 primal data of the parallel solve phases, ppk [b][N+1][2][256]:
+//   slot 0: H_k^{-1} (symmetric, packed lower), slot 1: G_k^T, the coupling
+//   columns of stage k's primal block -- column c < n: C_{k+1,k}^T (lambda_{k+1}:
+//   E_k in KKT order), column n + j: the y_k column j of C_kk^T (D_k).  The
+//   lambda_k columns of C_kk^T are -I on x_k and are applied implicitly.
+// Then with z' = H^{-1} r_p:  t_k = C_kk z' = [-z'_x ; (G z')_y],
+// t1_k = C_{k+1,k} z' = (G z')_lambda, and the back substitution is
+// z = z' - H^{-1} (C_kk^T lam_k + C_{k+1,k}^T lam_{k+1}) = z' - H^{-1} (G^T q - [lam_k,x ; 0])
+// with q = [lam_{k+1,lambda} ; lam_{k,y}].  3 KB of tiles per stage and phase
+// instead of 4.5 (L^{-1} / L^{-T}, V, U).  Needs n + nc_0 <= 16 (kkt_init).
+constexpr long long PPK = 512;  // doubles per stage
+
+__device__ __forceinline__ d4 kkt_g_tile(const KKTArgs &A, long long b, int k, int g, int c) {
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N;
+    const int p = A.prim_dim[k], g1 = k < N ? A.gdim[k + 1] : 0, nck = A.ncs[k];
+    const double *Ek = A.E + b * sh.perE + (long long)(k < N ? k : 0) * n * s;
+    const double *Dk = A.D + b * sh.ndD + A.d_off[k];
+    d4 G;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;  // primal index in KKT order
+        double v = 0.0;
+        if (i < p) {
+            if (c < n) {
+                if (c < g1) v = Ek[c + kref(k, N, n, m, i) * n];  // lambda_{k+1} rows: E_k
+            } else if (c - n < nck) {
+                v = k == 0 ? Dk[(c - n) + i * nck] : Dk[(c - n) + kref(k, N, n, m, i) * nck];  // y_k rows
+            }
+        }
+        G[r] = v;
+    }
+    return G;
+}
+
 // C/D-layout transpose of a 16 x 16 tile through LDS (t: 16 x 17 doubles)
 __device__ __forceinline__ d4 tile_transpose(const d4 &v, double *t, int g, int c) {
 #pragma unroll
@@ -377,10 +440,8 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     double *o = dpk + (b * (N + 1) + k) * 512LL;
     tn_store(o, lane, D);
     tn_store(o + 256, lane, Bt);
-    // primal tiles for the parallel solve phases, ppk [b][N+1][6][256]:
-    // L_k^{-T}, V_k, U_k (solve1) and V_k^T, L_k^{-1} (solve3, which also reads U_k).
+    // primal data of the parallel solve phases (ppk, see PPK): H^{-1} and G^T.
     // L^{-1} by re-eliminating L L^T carrying I (identity padding past p).
-    __shared__ double tt[16 * 17];
     const int p = A.prim_dim[k];
     WM<1> Lt, M;
     wm_load<1>(Lt, bk, 16, p, true, 0.0, g, c);
@@ -393,20 +454,13 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
     for (int r = 0; r < 4; ++r) Bi[0][0][r] = (4 * r + g == c) ? 1.0 : 0.0;
     double colinv[1], rowinv[1][4];
     elim_regs<1, true, 1>(M, Bi, 16, colinv, rowinv, g, c);
-    d4 Linv, V, U;
+    WM<1> Li, Hi;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = 4 * r + g;
-        Linv[r] = Bi[0][0][r] * rowinv[0][r];
-        V[r] = (i < p && c < gk) ? bk[256 + i + 16 * c] : 0.0;
-        U[r] = (i < p && c < g1) ? bk[512 + i + 16 * c] : 0.0;
-    }
-    double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    tri_store(q, tri_lane(g, c, true), tile_transpose(Linv, tt, g, c));  // L^{-T}, packed
-    tn_store(q + 256, lane, V);
-    tn_store(q + 512, lane, U);
-    tn_store(q + 768, lane, tile_transpose(V, tt, g, c));
-    tri_store(q + 1280, tri_lane(g, c, false), Linv);  // L^{-1}, packed
+    for (int r = 0; r < 4; ++r) Li.t[0][0][r] = Bi[0][0][r] * rowinv[0][r];  // L^{-1}
+    wm_tn<1>(Hi, Li, Li, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);      // H^{-1} = L^{-T} L^{-1}
+    double *q = A.ppk + (b * (N + 1) + k) * PPK;
+    tri_store(q, tri_lane(g, c, false), Hi.t[0][0]);  // symmetric: packed lower
+    tn_store(q + 256, lane, kkt_g_tile(A, b, k, g, c));
 }
 
 // P = 16: the per-stage work of k_kkt_stage + the primal half of k_kkt_pack16
@@ -414,12 +468,11 @@ __global__ __launch_bounds__(64) void k_kkt_pack16(KKTArgs A, double *__restrict
 //   L = chol(H_k + sigma I) with [C_kk^T | C_{k+1,k}^T | I] carried through the
 //   blocked elimination (chol_blk4_aug): V = L^{-1} C_kk^T, U = L^{-1} C_{k+1,k}^T,
 //   L^{-1} come out directly; V^T V, U^T U, U^T V are one MFMA product each.
-// Writes the primal tiles ppk (L^{-T}, V, U, V^T, -, L^{-1}) and the three
+// Writes the primal data ppk (H^{-1} = L^{-T} L^{-1}, G^T; see PPK) and the three
 // dual blocks (tile-native, into blk's first three tiles) for k_kkt_pack16d,
 // which adds the neighbour's U^T U.  The generic LDS kernel took 15.4 ms + 3.4 ms
 // of packing per model at C5 (N = 512, batch 1024).
 __global__ __launch_bounds__(64) void k_kkt_stage16(KKTArgs A) {
-    __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
@@ -457,12 +510,12 @@ __global__ __launch_bounds__(64) void k_kkt_stage16(KKTArgs A) {
     wm_tn<1>(VtV, V, V, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
     wm_tn<1>(UtU, U, U, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
     wm_tn<1>(UtV, U, V, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
-    double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    tri_store(q, tri_lane(g, c, true), tile_transpose(B[2], tt, g, c));  // L^{-T}, packed
-    tn_store(q + 256, lane, B[0]);                      // V
-    tn_store(q + 512, lane, B[1]);                      // U
-    tn_store(q + 768, lane, tile_transpose(B[0], tt, g, c));   // V^T
-    tri_store(q + 1280, tri_lane(g, c, false), B[2]);  // L^{-1}, packed
+    WM<1> Li, Hi;
+    Li.t[0][0] = B[2];
+    wm_tn<1>(Hi, Li, Li, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);  // H^{-1} = L^{-T} L^{-1}
+    double *q = A.ppk + (b * (N + 1) + k) * PPK;
+    tri_store(q, tri_lane(g, c, false), Hi.t[0][0]);  // symmetric: packed lower
+    tn_store(q + 256, lane, kkt_g_tile(A, b, k, g, c));
     double *o = A.blk + (b * (N + 1) + k) * 6LL * 256;
     tn_store(o, lane, VtV.t[0][0]);
     tn_store(o + 256, lane, UtU.t[0][0]);
@@ -498,63 +551,75 @@ __global__ __launch_bounds__(64) void k_kkt_pack16d(KKTArgs A, double *__restric
     tn_store(out + 256, lane, tile_transpose(tn_load(o + 512, lane), tt, g, c));  // (U^T V)^T
 }
 
-// forward phase 1, P = 16 (parallel over stages): w = L^{-1} r_p, t = V^T w,
-// t1 = U^T w as single-column MFMA products on the packed primal tiles
+// forward phase 1, P = 16 (parallel over stages): z' = H^{-1} r_p and, by one
+// more single-column MFMA product, G z' -> t_k = C_kk z', t1_k = C_{k+1,k} z'
+// (see PPK).  wv [b][N+1][64]: z' | t | t1 | lam.
 __global__ __launch_bounds__(64) void k_kkt_solve1_16(KKTArgs A) {
+    __shared__ double sz[16], so[16];
     const Shape &sh = A.sh;
-    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const int n = sh.n, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
     const int p = A.prim_dim[k];
-    const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    WM<1> LiT, V, U;
-    LiT.t[0][0] = tri_load(q, tri_lane(g, c, true));
-    V.t[0][0] = tn_load(q + 256, lane);
-    U.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-    if (c < sh.n) U.t[0][0] = tn_load(q + 512, lane);  // columns c >= n (y_{k+1}) are zero
+    const double *q = A.ppk + (b * (N + 1) + k) * PPK;
+    WM<1> Hi, Gt;
+    Hi.t[0][0] = sym_load(q, sym_lane(g, c));
+    Gt.t[0][0] = tn_load(q + 256, lane);
     const double *rp = A.rhs + b * A.dim + A.prim_off[k];
-    WV<1> r, w, t, t1;
+    WV<1> r, z, o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i = 4 * j + g;
         r.t[0][j] = (c == 0 && i < p) ? rp[i] : 0.0;
     }
-    wv_tn<1>(w, LiT, r, 16, 1.0, (const WV<1> *)nullptr);
-    wv_tn<1>(t, V, w, 16, 1.0, (const WV<1> *)nullptr);
-    wv_tn<1>(t1, U, w, 16, 1.0, (const WV<1> *)nullptr);
-    double *o = A.wv + (b * (N + 1) + k) * 64LL;
-    wv_store<1>(w, o, 16, g, c);
-    wv_store<1>(t, o + 16, 16, g, c);
-    wv_store<1>(t1, o + 32, 16, g, c);
+    wv_tn<1>(z, Hi, r, 16, 1.0, (const WV<1> *)nullptr);  // H^{-1} r (symmetric)
+    wv_tn<1>(o, Gt, z, 16, 1.0, (const WV<1> *)nullptr);  // G z'
+    wv_store<1>(z, sz, 16, g, c);
+    wv_store<1>(o, so, 16, g, c);
+    wave_sync();
+    double *w = A.wv + (b * (N + 1) + k) * 64LL;
+    if (lane < 16) {
+        const int nck = A.ncs[k];
+        double t;
+        if (k == 0) t = lane < nck ? so[n + (lane < 16 - n ? lane : 0)] : 0.0;  // group 0 = y_0
+        else t = lane < n ? -sz[lane] : so[lane];                             // [lambda_k ; y_k]
+        w[lane] = sz[lane];
+        w[16 + lane] = t;
+        w[32 + lane] = lane < n ? so[lane] : 0.0;  // lambda_{k+1} part only
+    }
 }
 
-// forward phase 3, P = 16 (parallel): z_k = L^{-T}(w - V lam_k - U lam_{k+1}), unpacked into ws
+// forward phase 3, P = 16 (parallel): z_k = z' - H^{-1} (G^T q - [lam_k,x ; 0]),
+// q = [lam_{k+1} (lambda part) ; lam_k (y part)] (see PPK), unpacked into ws
 __global__ __launch_bounds__(64) void k_kkt_solve3_16(KKTArgs A, const double *__restrict__ x0,
                                                       double *__restrict__ ws) {
-    __shared__ double zs[16];
+    __shared__ double zs[16], qs[16];
     __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const long long b = blockIdx.x / (N + 1);
     const int k = blockIdx.x % (N + 1);
-    const double *q = A.ppk + (b * (N + 1) + k) * 1536LL;
-    WM<1> VT, UT, Li;
-    VT.t[0][0] = tn_load(q + 768, lane);
-    // U^T from U through LDS: U's columns c >= n are zero, so those lanes load
-    // nothing (U^T's zero rows would not skip whole cache lines)
-    d4 u = d4{0.0, 0.0, 0.0, 0.0};
-    if (c < n) u = tn_load(q + 512, lane);
-    UT.t[0][0] = tile_transpose(u, tt, g, c);
-    Li.t[0][0] = tri_load(q + 1280, tri_lane(g, c, false));
+    const double *q = A.ppk + (b * (N + 1) + k) * PPK;
+    WM<1> Hi, G;
+    Hi.t[0][0] = sym_load(q, sym_lane(g, c));
+    G.t[0][0] = tile_transpose(tn_load(q + 256, lane), tt, g, c);
     const double *wk = A.wv + (b * (N + 1) + k) * 64LL;
-    const double *wn = A.wv + (b * (N + 1) + min(k + 1, N)) * 64LL;  // U_N = 0
-    WV<1> w, lk, ln, v, z;
-    wv_load<1>(w, wk, 16, g, c);
-    wv_load<1>(lk, wk + 48, 16, g, c);
-    wv_load<1>(ln, wn + 48, 16, g, c);
-    wv_tn<1>(v, VT, lk, 16, -1.0, &w);
-    wv_tn<1>(v, UT, ln, 16, -1.0, &v);
-    wv_tn<1>(z, Li, v, 16, 1.0, (const WV<1> *)nullptr);
+    if (lane < 16) {
+        const int nck = A.ncs[k];
+        double v = 0.0;
+        if (lane < n) v = k < N ? wk[64 + 48 + lane] : 0.0;  // lam_{k+1}, lambda part
+        else if (lane - n < nck) v = wk[48 + (k == 0 ? lane - n : lane)];  // lam_k, y part
+        qs[lane] = v;
+    }
+    wave_sync();
+    WV<1> zp, lk, qv, sv, z;
+    wv_load<1>(zp, wk, 16, g, c);
+    wv_load<1>(lk, wk + 48, k == 0 ? 0 : n, g, c);  // lam_k, lambda part (x_k rows of -I)
+    wv_load<1>(qv, qs, 16, g, c);
+    wv_tn<1>(sv, G, qv, 16, 1.0, (const WV<1> *)nullptr);  // G^T q
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sv.t[0][r] -= lk.t[0][r];
+    wv_tn<1>(z, Hi, sv, 16, -1.0, &zp);  // z' - H^{-1} s
     wv_store<1>(z, zs, 16, g, c);
     wave_sync();
     double *wb = ws + b * sh.perh;
@@ -1193,7 +1258,7 @@ struct KKTState {
     double *dpk = nullptr;   // P = 16: D_k and (U^T V)_k^T tiles, tile-native [b][N+1][2][256]
     double *dreg = nullptr;  // P = 16: y diagonal per group [b][N+1][16]
     double *bvec = nullptr;  // P = 16: forward-substitution right-hand sides [b][N+1][16]
-    double *ppk = nullptr;   // P = 16: primal tiles L^{-T}, V, U, V^T, (unused), L^{-1} [b][N+1][6][256]
+    double *ppk = nullptr;   // P = 16: H^{-1} (packed) and G^T per stage [b][N+1][2][256]
     bool formed = false;
 };
 
@@ -1269,7 +1334,8 @@ int kkt_init(pdplqr_handle h) {
         set_error("KKT solver with n + m > 32 or n + nc > 32 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
-    ks->P = dmax <= 16 ? 16 : 32;
+    // P = 16 also needs stage 0's y columns beside the lambda_1 columns of G_0 (PPK)
+    ks->P = dmax <= 16 && n + h->ncs[0] <= 16 ? 16 : 32;
     // row descriptors (kind, stage, index)
     std::vector<int4> rows(ks->dim);
     for (int k = 0; k <= N; ++k) {
@@ -1291,7 +1357,7 @@ int kkt_init(pdplqr_handle h) {
         (rc = kalloc(h, &ks->rhs, B * ks->dim)) ||
         (ks->P == 16 && ((rc = kalloc(h, &ks->dpk, B * (N + 1) * 512)) || (rc = kalloc(h, &ks->dreg, B * (N + 1) * 16)) ||
                          (rc = kalloc(h, &ks->bvec, B * (N + 1) * 16)) ||
-                         (rc = kalloc(h, &ks->ppk, B * (N + 1) * 1536)))) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
+                         (rc = kalloc(h, &ks->ppk, B * (N + 1) * PPK)))) || (rc = kalloc(h, &ks->wv, B * (N + 1) * 4 * ks->P)))
         return rc;
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_off, ks->prim_off.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ks->d_prim_dim, ks->prim_dim.data(), (N + 1) * sizeof(int32_t), hipMemcpyHostToDevice));

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r2l
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kkt.py tests/test_gpu_admm.py tests/test_gpu_configs.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kkt.py tests/test_gpu_admm.py tests/test_gpu_configs.py tests/test_bench_contract.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
 i=0
