@@ -1,6 +1,7 @@
 """Phase breakdown of the segment combine (debug build libpdplqr_combprof.so,
 -DPDPLQR_COMB_PROFILE): runs one horizon-slice backward (segments + scans) and
-prints the median duration of each combine phase over the recorded blocks."""
+prints the median duration of each combine phase over the recorded blocks.
+usage: python scripts/comb_phases.py [N] [n] [m]"""
 import ctypes as C
 import os
 import sys
@@ -16,7 +17,8 @@ from pdplqr import _lib  # noqa: E402
 from pdplqr.horizon import HorizonShard  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-n, m = 24, 8
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+m = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 dev = torch.device("cuda", 0)
 E, c, H, h, x0 = bench.gen_batch_device(n, m, N, 1, seed=1, device=dev)
 sh = HorizonShard(n, m, N, 1, device=0)
