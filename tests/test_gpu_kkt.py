@@ -156,11 +156,14 @@ def test_batched_kkt_matches_oracle(n, m, N, batch, nc):
         assert rel_err(out[b], o.forward(x0[b])) < TOL, b
 
 
-@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 40, 3), (5, 3, 17, 2)])
-def test_batched_kkt_varying_constraints(n, m, N, batch):
+@pytest.mark.parametrize("n,m,N,batch,nc0", [(12, 4, 40, 3, 3), (5, 3, 17, 2, 3), (12, 4, 24, 2, 8)])
+def test_batched_kkt_varying_constraints(n, m, N, batch, nc0):
     """Per-stage constraint counts (kkt.hpp: ncs from time_step, lqr_model.hpp:87)
     vary 0..4 and the terminal has its own: exercises the y offsets of the
-    16-wide tile path (dual groups of mixed size, group 0 possibly empty)."""
+    16-wide tile path (dual groups of mixed size, group 0 possibly empty).
+    nc0 = 8 with n = 12: every dual group still fits 16, but stage 0's y columns
+    do not fit beside lambda_1's in the coupling tile G_0 (kkt.hip PPK), so the
+    build takes the P = 32 kernels."""
     from oracle.oracle import OracleKKT
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
@@ -170,7 +173,7 @@ def test_batched_kkt_varying_constraints(n, m, N, batch):
     s = n + m
     g = np.random.default_rng(5 + N)
     ncs = g.integers(0, 5, size=N + 1).astype(np.int32)
-    ncs[0] = 3
+    ncs[0] = nc0
     dims = [s] * N + [n]
     D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
     ny = int(ncs.sum())
