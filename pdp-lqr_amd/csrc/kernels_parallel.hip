@@ -261,6 +261,64 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
 }
 
+// Two Hillis-Steele rounds (distances d and 2 d) in one launch, two waves per
+// block: wave 0 forms a_i = e_i + e_{i+d}, wave 1 a_{i+2d} = e_{i+2d} + e_{i+3d}
+// (the a_{i+2d} of block i + 2d, formed again: idle CUs are cheap here), both
+// into the block's private scratch slots; after the block barrier wave 0
+// forms a_i + a_{i+2d}.  The result equals two radix-2 rounds exactly (the
+// same combines in the same order); a pair of rounds costs two combine
+// latencies but one dispatch, operand fetch and write-back less.  Each
+// combine's right operand covers [first, min(first + span - 1, S - 1)]; when
+// that range holds the real terminal, F = C = f = 0 (see k_seg_scan).
+template <int T, bool LU>
+__global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
+    __shared__ CombSmem<T> smv[2];
+    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // per wave: 2 operand images
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = A.n, S = A.S, d = A.dist;
+    const int es = 3 * n * n + 2 * n, nn = n * n, ol = op_stage_len(n);
+    const long long b = blockIdx.x / S;
+    const int i = blockIdx.x % S;
+    const long long is = A.istride ? A.istride : es;
+    const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
+    double *out = A.out + b * (long long)S * es;
+    double *scr = A.scratch + (b * S + i) * 2LL * es;
+    double *eb = ebuf + wv * 2 * ol;
+    CombSmem<T> &sm = smv[wv];
+    auto combine = [&](double *o, const double *left, const double *right, bool fcf) {
+        const ElemIn ea = stage_left(eb, left, n, lane);
+        const ElemIn er = stage_right(eb + ol, right, n, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_sync();
+        const bool ok = tcombine_parts<T, LU>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, er, n, fcf,
+                                              true, sm, lane);
+        if (!fcf)
+            for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
+        return ok;
+    };
+    auto fcf_of = [&](int last) { return !(A.terminal && last >= S - 1); };  // right operand's last segment
+    if (i + d >= S) {  // suf_i already reaches the last segment (block-uniform)
+        if (wv == 0) elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
+        return;
+    }
+    const bool two = i + 2 * d < S;  // block-uniform
+    bool ok = true;
+    if (wv == 0) {
+        ok = combine(two ? scr : out + (long long)i * es, in + (long long)i * is, in + (long long)(i + d) * is,
+                     fcf_of(i + 2 * d - 1));
+    } else if (two) {
+        if (i + 3 * d >= S) elem_copy(scr + es, in + (long long)(i + 2 * d) * is, n, lane);
+        else
+            ok = combine(scr + es, in + (long long)(i + 2 * d) * is, in + (long long)(i + 3 * d) * is,
+                         fcf_of(i + 4 * d - 1));
+    }
+    if (two) {
+        __syncthreads();  // the scratch slots are written and visible to the block
+        if (wv == 0) ok = combine(out + (long long)i * es, scr, scr + es, fcf_of(i + 4 * d - 1)) && ok;
+    }
+    if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
+}
+
 // ---------------------------------------------------------------------------
 // Boundary maps.  With the value function V_j = (P_j, p_j) at boundary j (the
 // suffix-scan entry j, right-folded with the global suffix of later shards),
@@ -465,6 +523,23 @@ int seg_scan_slots(const Shape &sh, int device) {
 static size_t elems_smem(int n, int elems) { return (size_t)elems * (3 * n * n + 2 * n) * sizeof(double); }
 
 static int tile_order(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 0); }
+
+// T = 1 only: at T = 2 two waves' combine LDS (~75 KB a block) halves the
+// resident blocks, and C4's scans need every slot.
+#ifndef PDPLQR_SCAN4
+#define PDPLQR_SCAN4 1
+#endif
+bool seg_scan4_supported(int n) { return PDPLQR_SCAN4 && tile_order(n) == 1; }
+
+int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
+    const dim3 grid((unsigned)(batch * a.S)), blk(128);
+    const size_t smem = 2 * op_stage_bytes(a.n);
+    if (!seg_scan4_supported(a.n) || !a.scratch) return PDPLQR_ERR_UNSUPPORTED;
+    if (a.lu) hipLaunchKernelGGL((k_seg_scan4<1, true>), grid, blk, smem, st, a);
+    else hipLaunchKernelGGL((k_seg_scan4<1, false>), grid, blk, smem, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(64);

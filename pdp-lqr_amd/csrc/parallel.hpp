@@ -25,6 +25,7 @@ struct ScanArgs {
     double *out;
     int *flag;                 // [b]: a combine was not positive definite
     int lu = 0;                // LU form of the combine (CondensedSystemSolverType::LU)
+    double *scratch = nullptr; // radix-4 rounds: two private element slots per block [b][S][2][es]
 };
 
 struct MapArgs {
@@ -63,6 +64,10 @@ int seg_backward_slots(const Shape &sh, int device);
 int seg_scan_slots(const Shape &sh, int device);
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
+// one launch = the two Hillis-Steele rounds at distances dist and 2 dist (two
+// waves per block); false when this shape keeps the radix-2 rounds
+bool seg_scan4_supported(int n);
+int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 // Composition radix of the boundary-map prefix scan (2 or 4).
 #ifndef PDPLQR_MAP_RADIX

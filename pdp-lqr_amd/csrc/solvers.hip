@@ -23,6 +23,7 @@ struct ParallelState {
     int S = 0;
     int32_t *seg_start = nullptr, *seg_len = nullptr, *seg_status = nullptr;
     double *G = nullptr, *elem = nullptr, *bufA = nullptr, *bufB = nullptr, *xhat = nullptr, *lam = nullptr;
+    double *scan4 = nullptr;  // radix-4 scan scratch [b][S][2][es] (T = 1 shapes)
     double *mapA = nullptr, *mapB = nullptr, *vfun = nullptr;  // boundary maps (ping-pong), value functions
     const double *suf_final = nullptr;
     int *flag = nullptr;
@@ -176,6 +177,7 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->seg_status, B * S)) || (rc = palloc(h, &ps->G, B * sh.N * sh.m * sh.n)) ||
         (rc = palloc(h, &ps->elem, B * S * es)) || (rc = palloc(h, &ps->bufA, B * S * es)) ||
         (rc = palloc(h, &ps->bufB, B * S * es)) || (rc = palloc(h, &ps->xhat, B * (S + 1) * sh.n)) ||
+        (seg_scan4_supported(sh.n) && !getenv("PDPLQR_NO_SCAN4") && (rc = palloc(h, &ps->scan4, B * S * 2 * es))) ||
         (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, B)) ||
         (rc = palloc(h, &ps->mapA, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->mapB, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
@@ -228,7 +230,8 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
     const double *sin = ps->elem;
     double *bufs[2] = {ps->bufA, ps->bufB};
     int round = 0;
-    for (int d = 1; d < ps->S; d <<= 1, ++round) {
+    const bool r4 = ps->scan4 != nullptr;  // two rounds per launch (k_seg_scan4)
+    for (int d = 1; d < ps->S; d <<= (r4 ? 2 : 1), ++round) {
         ScanArgs s;
         s.n = sh.n;
         s.S = ps->S;
@@ -238,7 +241,8 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
         s.out = bufs[round & 1];
         s.flag = ps->flag;
         s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
-        int rc = launch_seg_scan(s, sh.batch, h->stream);
+        s.scratch = ps->scan4;
+        int rc = r4 ? launch_seg_scan4(s, sh.batch, h->stream) : launch_seg_scan(s, sh.batch, h->stream);
         if (rc) return rc;
         sin = s.out;
     }

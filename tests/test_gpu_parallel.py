@@ -161,6 +161,38 @@ def test_parallel_backward_without_factorization(name, ns, condensed, seglen):
         ws2 = ws2 + 0.05 * g.standard_normal(ws2.shape)
 
 
+@pytest.mark.parametrize("N,batch,seglen,condensed", [(1024, 1, 0, "CHOLESKY"), (1024, 1, 0, "LU"),
+                                                      (96, 3, 5, "CHOLESKY"), (40, 2, 2, "LU"), (7, 2, 3, "CHOLESKY"),
+                                                      (12, 1, 4, "CHOLESKY")])
+def test_radix4_scan_equals_radix2(N, batch, seglen, condensed, monkeypatch):
+    """k_seg_scan4 (two Hillis-Steele rounds per launch, T = 1 shapes) performs
+    the same combines in the same order as two k_seg_scan rounds: the solutions
+    are bit-identical.  PDPLQR_NO_SCAN4 (read at handle creation) keeps radix 2.
+    Segment counts 1..~200 cover every case of the two-level round (i + d, i + 2d,
+    i + 3d past the end) and the terminal element's (P, p)-only combines."""
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    n, m = 12, 4
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 1000 + N)
+    ws0 = np.zeros((batch, N * (n + m) + n))
+    outs = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("PDPLQR_NO_SCAN4", "1")
+        bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=True,
+                              segment_len=seglen, condensed=condensed)
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+        bs.backward()
+        out = np.zeros_like(ws0)
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0)
+        outs.append(out)
+        bs.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_graph_replay_matches_direct():
     """Protocol calls replayed from a captured hipGraph (PDPLQR_GRAPH=1, read at
     library load: run in a child process) give the same trajectory as direct
