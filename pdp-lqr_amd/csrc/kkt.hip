@@ -855,6 +855,30 @@ struct FacIn {
     double dr[4];
 };
 
+// Branch-free store of a column-0 vector (lane (g, 0) holds entries 4r + g):
+// every lane of a row group stores the same value to the same address.  A
+// lane-predicated store is an exec-masked branch, and the compiler's wait-count
+// merge after it drains every load in flight -- the sweeps' prefetch.
+__device__ __forceinline__ void wv_store_rows(const WV<1> &v, double *p, int g) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double x = bcast_lane16(v.t[0][r], 0);
+        p[4 * r + g] = x;
+    }
+}
+
+// A scheduling barrier after each load group keeps the loads where they are
+// written (the machine scheduler would otherwise sink them towards their use,
+// shortening the prefetch distance).
+#ifndef PDPLQR_SWEEP_SCHED_BARRIER
+#define PDPLQR_SWEEP_SCHED_BARRIER 1
+#endif
+__device__ __forceinline__ void sweep_fence() {
+#if PDPLQR_SWEEP_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 template <class In, class LD, class ST>
 __device__ __forceinline__ void sweep2(int cnt, LD &&ld, ST &&step) {
     if (cnt <= 0) return;
@@ -864,9 +888,13 @@ __device__ __forceinline__ void sweep2(int cnt, LD &&ld, ST &&step) {
     int i = 0;
     for (; i + 1 < cnt; i += 2) {
         step(a, i);
+        sweep_fence();
         ld(a, min(i + 2, cnt - 1));  // past the end: re-loads the last step (harmless)
+        sweep_fence();
         step(b, i + 1);
+        sweep_fence();
         ld(b, min(i + 3, cnt - 1));
+        sweep_fence();
     }
     if (i < cnt) step(a, i);
 }
@@ -982,11 +1010,14 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     };
     auto vin = [&](const double *src) { return vmask(vin_raw(src)); };
     // raw loads into the prefetch buffer; the masks are applied in the step
-    // wave 0 reads X tiles (zero, unstored columns c >= n), wave 1 full Z tiles
+    // wave 0 reads X tiles (zero, unstored columns c >= n), wave 1 full Z tiles.
+    // Lanes c >= n of wave 0 re-read lane (g, n - 1)'s slot, a cache line fetched
+    // anyway (branch-free: a masked load would drain the prefetch at the merge).
     const bool xcol = wv == 1 || c < sh.n;
+    const int xl = xcol ? lane : (lane & 48) + sh.n - 1;
     auto xmask = [&](const d4 &x) { return xcol ? x : d4{0.0, 0.0, 0.0, 0.0}; };
     auto load = [&](SolveIn &in, long long xoff, int k, const double *vsrc) {
-        if (xcol) in.X = tn_load(fb + xoff, lane);  // raw; masked in the step
+        in.X = tn_load(fb + xoff, xl);  // raw; masked in the step
         in.L = tri_load_raw(fb + k * 768LL + 512, tl);
         in.v = vin_raw(vsrc);
     };
@@ -1003,7 +1034,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         WM<1> LinvT;
         LinvT.t[0][0] = tile_transpose(tri_mask(in.L, tl), T, g, c);
         wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-        wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+        wv_store_rows(y, wvb + (long long)k * 64 + 48, g);
     };
     // ---- forward substitution from both ends ----
     if (wv == 0) {  // steps k = 0 .. p-1: X_k stored by group k - 1
@@ -1055,7 +1086,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         wv_tn<1>(v, CT, lam, 16, -1.0, &v);
         Linv.t[0][0] = tri_mask(in.L, tl);
         wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
-        wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
+        wv_store_rows(lam, wvb + (long long)k * 64 + 48, g);
     };
     if (wv == 0)
         sweep2<SolveIn>(p, [&](SolveIn &in, int i) { bload(in, p - 1 - i); },
