@@ -48,6 +48,13 @@ __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
     __shared__ __attribute__((aligned(16))) double ring[D][SH::REC];
     __shared__ double sp[16], st[16], sw[16];
     const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
+    // E[i][c] reads (column-major, stride n = 12): lane (g, c) takes rows i = 4 q + ge.
+    // With ge = g the two row groups of a 32-lane half put columns c and c + 8 on
+    // the same ds_read_b64 bank (12 * 8 = 0 mod 32); swapping the row slice of the
+    // upper 8 columns spreads them over all 32 banks.  sum_groups still adds the
+    // same four partials in the same order (its butterfly is symmetric): the
+    // results are bit-identical.
+    const int ge = g ^ ((cl >> 3) << 1);
     const Shape &sh = A.sh;
     const long long b = blockIdx.x;
     const int N = sh.N;
@@ -102,7 +109,7 @@ __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
         double qv = 0.0;  // q_c = h_c + sum_i E[i][c] w_i   (c = cl)
 #pragma unroll
         for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + g;
+            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
             const int ic = i < n ? i : n - 1;
             qv = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sw[ic], qv);
         }
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
         double a = 0.0;
 #pragma unroll
         for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + g;
+            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
             const int ic = i < n ? i : n - 1;
             a = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sp[ic], a);
         }
@@ -204,6 +211,13 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
     __shared__ __attribute__((aligned(16))) double ring[D][SH::REC];
     __shared__ double sp[16], st[16], sw[16];
     const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
+    // E[i][c] reads (column-major, stride n = 12): lane (g, c) takes rows i = 4 q + ge.
+    // With ge = g the two row groups of a 32-lane half put columns c and c + 8 on
+    // the same ds_read_b64 bank (12 * 8 = 0 mod 32); swapping the row slice of the
+    // upper 8 columns spreads them over all 32 banks.  sum_groups still adds the
+    // same four partials in the same order (its butterfly is symmetric): the
+    // results are bit-identical.
+    const int ge = g ^ ((cl >> 3) << 1);
     const Shape &sh = A.sh;
     const long long b = blockIdx.x;
     if (Q.done[b]) return;  // frozen problem: no update, no backward (wave-uniform)
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
         double qv = 0.0;
 #pragma unroll
         for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + g;
+            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
             const int ic = i < n ? i : n - 1;
             qv = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sw[ic], qv);
         }
@@ -355,7 +369,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
         double a = 0.0;
 #pragma unroll
         for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + g;
+            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
             const int ic = i < n ? i : n - 1;
             a = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sp[ic], a);
         }
