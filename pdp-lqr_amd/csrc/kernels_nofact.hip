@@ -35,6 +35,49 @@ struct NofactShape {
                                n <= 12 && m <= 4;
 };
 
+// The off-chain part of a stage, shared by both streamed kernels:
+//     w = Lxx (Lxx^T c),  q = h~ + E^T w
+// for the stage record R (E column-major at oe, c at oc) and the packed factor
+// Lp (dimension dim, x block at offset off); h~ of lane column cl is ht, q
+// returns on lane column cl (all groups).  st, sw: 16-double LDS scratch.
+// ge: the bank-spread row slice of the E reads (see k_nofact_dma).
+template <int NN>
+__device__ __forceinline__ double nofact_q(const double *R, int oe, int oc, const double *Lp, int dim, int off,
+                                           double ht, double *st, double *sw, int g, int ge, int cl) {
+    constexpr int n = NN;
+    const int j = cl < n ? cl : n - 1;
+    double a = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < (n + 3) / 4; ++qq) {  // t_j = sum_{i >= j} Lxx[i][j] c_i
+        const int i = 4 * qq + g;
+        const int ic = i < n ? i : n - 1;
+        const double l = Lp[pidx(off + (ic >= j ? ic : j), off + j, dim)];
+        a = __builtin_fma((i < n && i >= j) ? l : 0.0, R[oc + ic], a);
+    }
+    a = sum_groups(a);
+    if (g == 0 && cl < n) st[cl] = a;
+    wave_sync();
+    double w = 0.0;  // w_i = sum_{j <= i} Lxx[i][j] t_j   (i = cl)
+#pragma unroll
+    for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+        const int jj = 4 * qq + g;
+        const int jc = jj < n ? jj : n - 1;
+        const double l = Lp[pidx(off + (j >= jc ? j : jc), off + jc, dim)];
+        w = __builtin_fma((jj < n && jj <= j) ? l : 0.0, st[jc], w);
+    }
+    w = sum_groups(w);
+    if (g == 0 && cl < n) sw[cl] = w;
+    wave_sync();
+    double qv = 0.0;  // q_c = h_c + sum_i E[i][c] w_i   (c = cl)
+#pragma unroll
+    for (int qq = 0; qq < (n + 3) / 4; ++qq) {
+        const int i = 4 * qq + ge;
+        const int ic = i < n ? i : n - 1;
+        qv = __builtin_fma(i < n ? R[oe + ic + cl * n] : 0.0, sw[ic], qv);
+    }
+    return sum_groups(qv) + ht;
+}
+
 #ifndef PDPLQR_NOFACT_DEPTH
 #define PDPLQR_NOFACT_DEPTH 4
 #endif
@@ -79,41 +122,8 @@ __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
             }
         }
     };
-    // w = Lxx (Lxx^T c) and q = h + E^T w for the stage record R (E, c, h) and
-    // the packed factor Lp (dimension dim, x block at offset off); q on lane
-    // column cl (all groups)
     auto offchain = [&](const double *R, const double *Lp, int dim, int off) -> double {
-        const int j = cl < n ? cl : n - 1;
-        double a = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {  // t_j = sum_{i >= j} Lxx[i][j] c_i
-            const int i = 4 * qq + g;
-            const int ic = i < n ? i : n - 1;
-            const double l = Lp[pidx(off + (ic >= j ? ic : j), off + j, dim)];
-            a = __builtin_fma((i < n && i >= j) ? l : 0.0, R[SH::OC + ic], a);
-        }
-        a = sum_groups(a);
-        if (g == 0 && cl < n) st[cl] = a;
-        wave_sync();
-        double w = 0.0;  // w_i = sum_{j <= i} Lxx[i][j] t_j   (i = cl)
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int jj = 4 * qq + g;
-            const int jc = jj < n ? jj : n - 1;
-            const double l = Lp[pidx(off + (j >= jc ? j : jc), off + jc, dim)];
-            w = __builtin_fma((jj < n && jj <= j) ? l : 0.0, st[jc], w);
-        }
-        w = sum_groups(w);
-        if (g == 0 && cl < n) sw[cl] = w;
-        wave_sync();
-        double qv = 0.0;  // q_c = h_c + sum_i E[i][c] w_i   (c = cl)
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
-            const int ic = i < n ? i : n - 1;
-            qv = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sw[ic], qv);
-        }
-        return sum_groups(qv) + R[SH::OH + cl];
+        return nofact_q<NN>(R, SH::OE, SH::OC, Lp, dim, off, R[SH::OH + cl], st, sw, g, ge, cl);
     };
 
     // ---- terminal (lqr_kernel.hpp:94-101): lp_N = h~_N ----
@@ -296,37 +306,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
     };
     // P c and q = h~ + E^T (P c) for record R with factor Lp (as k_nofact_dma)
     auto offchain = [&](const double *R, const double *Lp, int dim, int off, double ht) -> double {
-        const int j = cl < n ? cl : n - 1;
-        double a = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + g;
-            const int ic = i < n ? i : n - 1;
-            const double l = Lp[pidx(off + (ic >= j ? ic : j), off + j, dim)];
-            a = __builtin_fma((i < n && i >= j) ? l : 0.0, R[SH::OC + ic], a);
-        }
-        a = sum_groups(a);
-        if (g == 0 && cl < n) st[cl] = a;
-        wave_sync();
-        double w = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int jj = 4 * qq + g;
-            const int jc = jj < n ? jj : n - 1;
-            const double l = Lp[pidx(off + (j >= jc ? j : jc), off + jc, dim)];
-            w = __builtin_fma((jj < n && jj <= j) ? l : 0.0, st[jc], w);
-        }
-        w = sum_groups(w);
-        if (g == 0 && cl < n) sw[cl] = w;
-        wave_sync();
-        double qv = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < (n + 3) / 4; ++qq) {
-            const int i = 4 * qq + ge;  // bank-spread row slice (see ge)
-            const int ic = i < n ? i : n - 1;
-            qv = __builtin_fma(i < n ? R[SH::OE + ic + cl * n] : 0.0, sw[ic], qv);
-        }
-        return sum_groups(qv) + ht;
+        return nofact_q<NN>(R, SH::OE, SH::OC, Lp, dim, off, ht, st, sw, g, ge, cl);
     };
 
     // ---- terminal (nc_N = 0): w_N relaxed, h~_N = h_N - sigma w_N; lp_N = h~_N ----
