@@ -737,38 +737,46 @@ __global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__
             Linv[r] = B[0][1][r] * rowinv[0][r];
         }
 #endif
+        // block LDL^T form for the solve (see k_kkt_solve2_16): T_k = M_k^{-1} Bt_k
+        // = Lkk^{-T} X_{k+1}, and Lkk^{-1} (packed) for M_k^{-1} = Lkk^{-T} Lkk^{-1}
+        WM<1> Li, Tm;
+        Li.t[0][0] = Linv;
+        wm_tn<1>(Tm, Li, X, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
         double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
-        tn_store(fk + 256, lane, X.t[0][0]);  // X_{k+1} = L_{k+1,k}^T
-        tri_store(fk + 512, tl, Linv);        // Lkk^{-1}, packed
+        tn_store(fk + 256, lane, Tm.t[0][0]);
+        tri_store(fk + 512, tl, Linv);
     }
     if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
 }
 
-// forward phase 2, P = 16: L y = bvec, then L^T lam = y, with the stored
-// Lkk^{-1} and X_{k+1} = L_{k+1,k}^T (single-column MFMA products over the
-// full padded tile; inputs loaded two steps ahead)
+// forward phase 2, P = 16, in block LDL^T form -S = L~ D L~^T with unit lower
+// blocks L~_{k+1,k} = T_k^T (T_k = M_k^{-1} Bt_k) and D = diag(M_k):
+//     forward  z_k   = bvec_k - T_{k-1}^T z_{k-1}      (one product, no M^{-1})
+//     backward lam_k = M_k^{-1} z_k - T_k lam_{k+1}    (M^{-1} z off the chain)
+// the same solution as L y = bvec, L^T lam = y with the Cholesky blocks, with
+// one tile less read in the forward sweep (single-column MFMA products over
+// the full padded tile; inputs loaded two steps ahead)
 __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *__restrict__ bvec) {
     __shared__ double tt[16 * 17];
     const Shape &sh = A.sh;
     const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
-    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
+    const TriLane tl = tri_lane(g, c, false);  // packed Lkk^{-1} tiles
     const long long b = blockIdx.x;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
     const double *fb = A.fac + b * (N + 1) * 3LL * 256;
     const double *bv = bvec + b * (N + 1) * 16LL;
     struct In {
-        d4 X, L;
+        d4 T, L;
         double v[4];
     };
-    // forward: X_k natural (stored by group k-1), Lkk^{-1} (transposed at use)
+    // forward (unit lower block L~): z_k = bvec_k - T_{k-1}^T z_{k-1}, T_{k-1} stored by group k - 1
     auto fload = [&](In &in, int k) {
-        in.X = tn_load(fb + (long long)max(k - 1, 0) * 768 + 256, lane);
-        in.L = tri_load(fb + (long long)k * 768 + 512, tl);
+        in.T = tn_load(fb + (long long)max(k - 1, 0) * 768 + 256, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) in.v[r] = bv[k * 16 + 4 * r + g];
     };
-    WV<1> y;
-    y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    WV<1> z;
+    z.t[0] = d4{0.0, 0.0, 0.0, 0.0};
     In nx1, nx2;
     fload(nx1, 0);
     fload(nx2, min(1, N));
@@ -776,21 +784,20 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
         const In in = nx1;
         nx1 = nx2;
         fload(nx2, min(k + 2, N));
-        WM<1> Xk, LinvT;
-        Xk.t[0][0] = in.X;
-        LinvT.t[0][0] = tile_transpose(in.L, tt, g, c);
+        WM<1> Tk;
+        Tk.t[0][0] = in.T;
         WV<1> v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
-        if (k > 0) wv_tn<1>(v, Xk, y, 16, -1.0, &v);  // - L_{k,k-1} y_{k-1}
-        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-        wv_store<1>(y, wvb + (long long)k * 64 + 48, 16, g, c);
+        if (k > 0) wv_tn<1>(v, Tk, z, 16, -1.0, &v);
+        z = v;
+        wv_store<1>(z, wvb + (long long)k * 64 + 48, 16, g, c);
     }
-    // backward: X_{k+1} transposed, Lkk^{-1} natural; y_k was written by this
+    // backward: lam_k = M_k^{-1} z_k - T_k lam_{k+1}; z_k was written by this
     // wave above (same lanes: wv_store / the loads below touch lanes c == 0 only)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     auto bload = [&](In &in, int k) {
-        in.X = tn_load(fb + (long long)min(k, N - 1) * 768 + 256, lane);
+        in.T = tn_load(fb + (long long)min(k, N - 1) * 768 + 256, lane);
         in.L = tri_load(fb + (long long)k * 768 + 512, tl);
 #pragma unroll
         for (int r = 0; r < 4; ++r) in.v[r] = wvb[(long long)k * 64 + 48 + 4 * r + g];
@@ -803,14 +810,17 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
         const In in = nx1;
         nx1 = nx2;
         bload(nx2, max(k - 2, 0));
-        WM<1> XnT, Linv;
-        XnT.t[0][0] = tile_transpose(in.X, tt, g, c);
+        WM<1> TkT, Linv, LinvT;
+        TkT.t[0][0] = tile_transpose(in.T, tt, g, c);
         Linv.t[0][0] = in.L;
-        WV<1> v;
+        LinvT.t[0][0] = tile_transpose(in.L, tt, g, c);
+        WV<1> v, y, w;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
-        if (k < N) wv_tn<1>(v, XnT, lam, 16, -1.0, &v);  // - L_{k+1,k}^T lam_{k+1}
-        wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
+        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);  // Lkk^{-1} z_k
+        wv_tn<1>(w, Linv, y, 16, 1.0, (const WV<1> *)nullptr);   // M_k^{-1} z_k
+        if (k < N) wv_tn<1>(w, TkT, lam, 16, -1.0, &w);      // - T_k lam_{k+1}
+        lam = w;
         wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
     }
 }
@@ -946,8 +956,16 @@ __global__ __launch_bounds__(128) void k_kkt_factor16_tw(KKTArgs A, const double
         double *fk = fb + k * 768LL;
         // X_{k+1} (top) / Z_{k-1} (bottom).  X = Lkk^{-1} (U^T V)_k^T keeps the
         // zero columns c >= n of (U^T V)^T (U's y columns): those lanes store nothing
-        if (bottom || c < sh.n) tn_store(fk + 256, lane, B[0]);
-        tri_store(fk + 512, tl, B[1]);   // Lkk^{-1} / L'_kk^{-1}, packed
+        // block LDL^T form for the solve (k_kkt_solve2_16_tw): T = Lkk^{-T} X
+        // (= M^{-1} Bt_k top-down, M'^{-1} Bt_{k-1}^T bottom-up; the top chain's
+        // keeps the zero columns c >= n), and Lkk^{-1} (packed): the solve forms
+        // M^{-1} z = Lkk^{-T} Lkk^{-1} z itself (one product less in this chain)
+        WM<1> Li, Xc, Tm;
+        Li.t[0][0] = B[1];
+        Xc.t[0][0] = B[0];
+        wm_tn<1>(Tm, Li, Xc, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
+        if (bottom || c < sh.n) tn_store(fk + 256, lane, Tm.t[0][0]);
+        tri_store(fk + 512, tl, B[1]);  // Lkk^{-1} / L'_kk^{-1}, packed
     };
     if (wv == 0) {
         sweep2<FacIn>(p, [&](FacIn &in, int i) { fload(in, i, i); },
@@ -989,7 +1007,7 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
     const Shape &sh = A.sh;
     const int N = sh.N, p = N / 2;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
+    const TriLane tl = tri_lane(g, c, false);  // packed Lkk^{-1} tiles
     __builtin_assume(lane >= 0 && lane < 64);
     const long long b = blockIdx.x;
     double *wvb = A.wv + b * (N + 1) * 4LL * 16;
@@ -1009,83 +1027,87 @@ __global__ __launch_bounds__(128) void k_kkt_solve2_16_tw(KKTArgs A, const doubl
         return v;
     };
     auto vin = [&](const double *src) { return vmask(vin_raw(src)); };
-    // raw loads into the prefetch buffer; the masks are applied in the step
-    // wave 0 reads X tiles (zero, unstored columns c >= n), wave 1 full Z tiles.
-    // Lanes c >= n of wave 0 re-read lane (g, n - 1)'s slot, a cache line fetched
-    // anyway (branch-free: a masked load would drain the prefetch at the merge).
+    // raw loads into the prefetch buffer; the masks are applied in the step.
+    // Wave 0 reads T tiles with zero, unstored columns c >= n, wave 1 full T'
+    // tiles; lanes c >= n of wave 0 re-read lane (g, n - 1)'s slot, a cache
+    // line fetched anyway (branch-free: a masked load would drain the prefetch
+    // at the merge).  The forward sweep needs no M^{-1}.
     const bool xcol = wv == 1 || c < sh.n;
     const int xl = xcol ? lane : (lane & 48) + sh.n - 1;
     auto xmask = [&](const d4 &x) { return xcol ? x : d4{0.0, 0.0, 0.0, 0.0}; };
-    auto load = [&](SolveIn &in, long long xoff, int k, const double *vsrc) {
-        in.X = tn_load(fb + xoff, xl);  // raw; masked in the step
-        in.L = tri_load_raw(fb + k * 768LL + 512, tl);
+    auto fload = [&](SolveIn &in, long long toff, const double *vsrc) {
+        in.X = tn_load(fb + toff, xl);
         in.v = vin_raw(vsrc);
     };
-    WV<1> y;
-    y.t[0] = d4{0.0, 0.0, 0.0, 0.0};
-    // forward step: y_k = Lkk^{-1} (bvec_k - C^T y_prev), C = X_k (top) or Z_k (bottom)
+    auto bload = [&](SolveIn &in, int k) {
+        in.X = tn_load(fb + k * 768LL + 256, xl);
+        in.L = tri_load_raw(fb + k * 768LL + 512, tl);
+        in.v = vin_raw(wvb + (long long)k * 64 + 48);
+    };
+    WV<1> z;
+    z.t[0] = d4{0.0, 0.0, 0.0, 0.0};
+    // forward step: z_k = bvec_k - T^T z_prev, T = T_{k-1} (top) or T'_{k+1} (bottom)
     auto fstep = [&](const SolveIn &in, int k, bool first) {
         WV<1> v = vmask(in.v);
         if (!first) {
-            WM<1> Ck;
-            Ck.t[0][0] = xmask(in.X);
-            wv_tn<1>(v, Ck, y, 16, -1.0, &v);
+            WM<1> Tk;
+            Tk.t[0][0] = xmask(in.X);
+            wv_tn<1>(v, Tk, z, 16, -1.0, &v);
         }
-        WM<1> LinvT;
-        LinvT.t[0][0] = tile_transpose(tri_mask(in.L, tl), T, g, c);
-        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-        wv_store_rows(y, wvb + (long long)k * 64 + 48, g);
+        z = v;
+        wv_store_rows(z, wvb + (long long)k * 64 + 48, g);
     };
     // ---- forward substitution from both ends ----
-    if (wv == 0) {  // steps k = 0 .. p-1: X_k stored by group k - 1
-        sweep2<SolveIn>(p, [&](SolveIn &in, int i) { load(in, max(i - 1, 0) * 768LL + 256, i, bv + i * 16); },
+    if (wv == 0) {  // steps k = 0 .. p-1: T_{k-1} stored by group k - 1
+        sweep2<SolveIn>(p, [&](SolveIn &in, int i) { fload(in, max(i - 1, 0) * 768LL + 256, bv + i * 16); },
                [&](const SolveIn &in, int i) { fstep(in, i, i == 0); });
-    } else {  // steps k = N .. p+1: Z_k stored by group k + 1
+    } else {  // steps k = N .. p+1: T'_{k+1} stored by group k + 1
         sweep2<SolveIn>(N - p,
                [&](SolveIn &in, int i) {
                    const int k = N - i;
-                   load(in, min(k + 1, N) * 768LL + 256, k, bv + k * 16);
+                   fload(in, min(k + 1, N) * 768LL + 256, bv + k * 16);
                },
                [&](const SolveIn &in, int i) { fstep(in, N - i, i == 0); });
-        wv_store<1>(y, vmid, 16, g, c);  // y'_{p+1}
+        wv_store<1>(z, vmid, 16, g, c);  // z'_{p+1}
     }
     __syncthreads();
-    // ---- the middle group ----
+    // ---- the middle group: z_p = bvec_p - T_{p-1}^T z_{p-1} - T'_{p+1}^T z'_{p+1}, lam_p = M_p^{-1} z_p ----
     if (wv == 0) {
         WV<1> v = vin(bv + p * 16);
         if (p > 0) {
-            WM<1> Xp;
-            Xp.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-            if (c < sh.n) Xp.t[0][0] = tn_load(fb + (p - 1) * 768LL + 256, lane);
-            wv_tn<1>(v, Xp, y, 16, -1.0, &v);
+            WM<1> Tp;
+            Tp.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+            if (c < sh.n) Tp.t[0][0] = tn_load(fb + (p - 1) * 768LL + 256, lane);
+            wv_tn<1>(v, Tp, z, 16, -1.0, &v);
         }
-        WM<1> Zp;
-        Zp.t[0][0] = tn_load(fb + (p + 1) * 768LL + 256, lane);
-        const WV<1> yb = vin(vmid);
-        wv_tn<1>(v, Zp, yb, 16, -1.0, &v);
+        WM<1> Tq;
+        Tq.t[0][0] = tn_load(fb + (p + 1) * 768LL + 256, lane);
+        const WV<1> zb = vin(vmid);
+        wv_tn<1>(v, Tq, zb, 16, -1.0, &v);
         WM<1> Linv, LinvT;
         Linv.t[0][0] = tri_load(fb + p * 768LL + 512, tl);
         LinvT.t[0][0] = tile_transpose(Linv.t[0][0], T, g, c);
         WV<1> yp, lam;
         wv_tn<1>(yp, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);
-        wv_tn<1>(lam, Linv, yp, 16, 1.0, (const WV<1> *)nullptr);
+        wv_tn<1>(lam, Linv, yp, 16, 1.0, (const WV<1> *)nullptr);  // M_p^{-1} z_p
         wv_store<1>(lam, wvb + (long long)p * 64 + 48, 16, g, c);
         wv_store<1>(lam, lmid, 16, g, c);
     }
     __syncthreads();
-    // ---- back substitution outward; y_k was written by this wave (same lanes) ----
+    // ---- back substitution outward; z_k was written by this wave (same rows) ----
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     WV<1> lam = vin(lmid);
-    // step k: lam_k = Lkk^{-T} (y_k - C lam_prev), C = X_{k+1} (top) or Z_{k-1}
-    // (bottom), both stored by group k
-    auto bload = [&](SolveIn &in, int k) { load(in, k * 768LL + 256, k, wvb + (long long)k * 64 + 48); };
+    // step k: lam_k = M_k^{-1} z_k - T lam_prev, T = T_k (top) or T'_k (bottom),
+    // both stored by group k; M^{-1} z_k = Lkk^{-T} Lkk^{-1} z_k does not wait for lam_prev
     auto bstep = [&](const SolveIn &in, int k) {
-        WV<1> v = vmask(in.v);
-        WM<1> CT, Linv;
-        CT.t[0][0] = tile_transpose(xmask(in.X), T, g, c);
-        wv_tn<1>(v, CT, lam, 16, -1.0, &v);
+        WM<1> TT, Linv, LinvT;
         Linv.t[0][0] = tri_mask(in.L, tl);
-        wv_tn<1>(lam, Linv, v, 16, 1.0, (const WV<1> *)nullptr);
+        LinvT.t[0][0] = tile_transpose(Linv.t[0][0], T, g, c);
+        WV<1> y, w;
+        wv_tn<1>(y, LinvT, vmask(in.v), 16, 1.0, (const WV<1> *)nullptr);  // Lkk^{-1} z_k
+        wv_tn<1>(w, Linv, y, 16, 1.0, (const WV<1> *)nullptr);             // M_k^{-1} z_k
+        TT.t[0][0] = tile_transpose(xmask(in.X), T, g, c);
+        wv_tn<1>(lam, TT, lam, 16, -1.0, &w);
         wv_store_rows(lam, wvb + (long long)k * 64 + 48, g);
     };
     if (wv == 0)
