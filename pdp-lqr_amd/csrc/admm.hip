@@ -88,7 +88,11 @@ __device__ __forceinline__ double wave_max(double v) {
 // CHECK: the five maxima of the termination test reduce over the block and
 // thread 0 decides (OSQP's test, admm.hip header), so there is no separate
 // check launch and no atomics on the residuals.
-template <int LPS, bool FUSE, bool CHECK>
+// MNC > 0 (every stage has at most MNC constraint rows): the rows are a
+// compile-time loop whose loads are all issued before the arithmetic (a
+// runtime row loop waited for each row's loads in turn), and the row results
+// are stored after it.  Same operations in the same order either way.
+template <int LPS, bool FUSE, bool CHECK, int MNC>
 __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
     const Shape &sh = a.sh;
     const int b = blockIdx.x;
@@ -111,6 +115,54 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
         const double wtj = col ? a.wt[wo] : 0.0, wj = col ? a.w[wo] : 0.0;
         const double wn = al * wtj + bl * wj;
         double ag = 0.0, ad = 0.0, ay = 0.0;
+        if constexpr (MNC > 0) {
+            double dr[MNC], zr[MNC], yr[MNC], rr[MNC], ir[MNC], lo[MNC], hi[MNC], zs[MNC], ys[MNC], gs[MNC];
+            const long long y0 = (long long)b * sh.ny;  // a valid slot for rows past nc
+#pragma unroll
+            for (int r = 0; r < MNC; ++r) {
+                const bool row = r < nc;
+                const long long q = row ? yo + r : y0;
+                dr[r] = (row && col) ? Dk[r + j * nc] : 0.0;
+                zr[r] = a.z[q];
+                yr[r] = a.y[q];
+                rr[r] = a.rho[q];
+                ir[r] = a.irho[q];
+                lo[r] = a.lb[q];
+                hi[r] = a.ub[q];
+            }
+#pragma unroll
+            for (int r = 0; r < MNC; ++r) {
+                const bool row = r < nc;
+                const double d = dr[r];
+                const double v = stage_sum<LPS>(d * wtj);
+                const double vw = stage_sum<LPS>(d * wj);
+                const double vrel = al * v + bl * zr[r];
+                const double zn = fmin(fmax(vrel + ir[r] * yr[r], lo[r]), hi[r]);
+                const double yn = yr[r] + rr[r] * (vrel - zn);
+                const double gn = zn - ir[r] * yn;
+                zs[r] = zn;
+                ys[r] = yn;
+                gs[r] = gn;
+                if (row) {
+                    if (FUSE) ag += d * (rr[r] * gn);  // k_penalty's order: D[q][i] * (rho_q * g_q)
+                    if (CHECK) {
+                        const double dwn = al * v + bl * vw;  // D w^{k+1}
+                        rp = fmax(rp, fabs(dwn - zn));
+                        dwm = fmax(dwm, fabs(dwn));
+                        zm = fmax(zm, fabs(zn));
+                        ad += d * (rr[r] * (zn - zr[r]));
+                        ay += d * yn;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < MNC; ++r)
+                if (j == 0 && r < nc) {
+                    a.z[yo + r] = zs[r];
+                    a.y[yo + r] = ys[r];
+                    if (FUSE) a.gw[yo + r] = gs[r];
+                }
+        } else
         for (int r = 0; r < a.max_nc; ++r) {
             const bool row = r < nc;
             const double d = (row && col) ? Dk[r + j * nc] : 0.0;
@@ -211,8 +263,14 @@ __global__ void k_admm_rescale(long long ny_total, int ny, const double *__restr
 
 static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check, dim3 grid, dim3 blk,
                               hipStream_t S) {
-#define PDPLQR_ADMM_LAUNCH(L, F, C) hipLaunchKernelGGL((k_admm_update<L, F, C>), grid, blk, 0, S, a)
-    if (l16) {
+#define PDPLQR_ADMM_LAUNCH(L, F, C) hipLaunchKernelGGL((k_admm_update<L, F, C, 0>), grid, blk, 0, S, a)
+#define PDPLQR_ADMM_LAUNCH4(F, C) hipLaunchKernelGGL((k_admm_update<16, F, C, 4>), grid, blk, 0, S, a)
+    if (l16 && a.max_nc <= 4) {
+        if (fuse && check) PDPLQR_ADMM_LAUNCH4(true, true);
+        else if (fuse) PDPLQR_ADMM_LAUNCH4(true, false);
+        else if (check) PDPLQR_ADMM_LAUNCH4(false, true);
+        else PDPLQR_ADMM_LAUNCH4(false, false);
+    } else if (l16) {
         if (fuse && check) PDPLQR_ADMM_LAUNCH(16, true, true);
         else if (fuse) PDPLQR_ADMM_LAUNCH(16, true, false);
         else if (check) PDPLQR_ADMM_LAUNCH(16, false, true);
@@ -224,6 +282,7 @@ static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check
         else PDPLQR_ADMM_LAUNCH(32, false, false);
     }
 #undef PDPLQR_ADMM_LAUNCH
+#undef PDPLQR_ADMM_LAUNCH4
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
