@@ -48,6 +48,7 @@
 #include <algorithm>
 
 #include "admm.hpp"
+#include "device_common.hpp"
 #include "solvers.hpp"
 
 namespace pdplqr {
@@ -68,9 +69,13 @@ struct AdmmState {
 // the same bits)
 template <int LPS>
 __device__ __forceinline__ double stage_sum(double v) {
+    if constexpr (LPS == 16) {
+        return sum_row16(v);  // DPP form of the same butterfly
+    } else {
 #pragma unroll
-    for (int m = 1; m < LPS; m <<= 1) v += __shfl_xor(v, m, 64);
-    return v;
+        for (int m = 1; m < LPS; m <<= 1) v += __shfl_xor(v, m, 64);
+        return v;
+    }
 }
 
 __device__ __forceinline__ double wave_max(double v) {

@@ -80,6 +80,27 @@ __device__ __forceinline__ double sum_groups(double v) {
     return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
 }
 
+// Sum over the 16 lanes of a row (lanes 16 g .. 16 g + 15), returned on all of
+// them, with DPP moves (VALU) instead of the four ds_bpermute round trips of an
+// xor butterfly.  Bit-identical to v += shfl_xor(v, m) for m = 1, 2, 4, 8:
+// quad_perm [1,0,3,2] / [2,3,0,1] are xor 1 / xor 2; after them a quad holds
+// one value, and row_half_mirror (l -> 7 - l) / row_mirror (l -> 15 - l) flip
+// bit 2 / bit 3 of the lane like xor 4 / xor 8 (the fp add is commutative).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double sum_row16(double v) {
+    v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
+    return v;
+}
+
 // Status semantics of a value-function diagonal (P_k = Lxx Lxx^T): the
 // reference's Eigen LLT stops at the first non-positive pivot and the
 // remaining columns flow through unfactored (lqr_kernel.hpp:89,126 ignore

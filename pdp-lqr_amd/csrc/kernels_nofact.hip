@@ -275,12 +275,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
         const double wt = R[SH::OWT + cl], wo = R[SH::OW + cl];
         const double wn = al * wt + bl * wo;
         const double d = R[SH::OD + g + cl * NC];  // D_kk[g][cl]
-        double v = d * wt, vw = d * wo;
-#pragma unroll
-        for (int msk = 1; msk < 16; msk <<= 1) {
-            v += __shfl_xor(v, msk, 64);
-            vw += __shfl_xor(vw, msk, 64);
-        }
+        const double v = sum_row16(d * wt), vw = sum_row16(d * wo);
         const double zr = R[SH::OZ + g], yr = R[SH::OY + g], rr = R[SH::ORHO + g], ir = R[SH::OIR + g];
         const double vrel = al * v + bl * zr;
         const double zn = fmin(fmax(vrel + ir * yr, R[SH::OLB + g]), R[SH::OUB + g]);
