@@ -91,9 +91,10 @@ typedef struct {
 
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,
  * CHOLESKY, rho_dyn = kkt_sigma = 1e-6).
- * Hard limit of this build: nx + nu <= 32 (a stage matrix is at most 2 x 2 MFMA
- * tiles of 16 in one wavefront); pdplqr_create returns PDPLQR_ERR_UNSUPPORTED
- * for larger shapes (the reference is size-generic, lqr_kernel.hpp:104-147). */
+ * Shape limits of this build (the reference is size-generic, lqr_kernel.hpp:104-147):
+ * SERIAL nx + nu <= 64 (up to 32 on MFMA tiles in one wavefront, 33..64 on
+ * LDS-resident stage matrices, one 256-thread block per problem); PARALLEL and
+ * KKT nx + nu <= 32.  pdplqr_create returns PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 
 int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out);

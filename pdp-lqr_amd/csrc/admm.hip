@@ -85,7 +85,7 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 // One 256-thread block per problem.  A stage takes LPS lanes (one per entry
-// of w_k: LPS = 16 for s <= 16, 32 for s <= 32), so a wave covers 64 / LPS
+// of w_k: LPS = 16 for s <= 16, 32 for s <= 32, 64 for s <= 64), so a wave covers 64 / LPS
 // consecutive stages with coalesced w / w~ / h loads; the block strides over
 // the horizon.  Row r of D_k w~ is a butterfly sum over the stage's lanes;
 // every lane then holds the row's new z, y, g and adds its column's share of
@@ -266,10 +266,11 @@ __global__ void k_admm_rescale(long long ny_total, int ny, const double *__restr
     irho[t] = 1.0 / r;
 }
 
-static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check, dim3 grid, dim3 blk,
+static int launch_admm_update(const AdmmArgs &a, int lps, bool fuse, bool check, dim3 grid, dim3 blk,
                               hipStream_t S) {
 #define PDPLQR_ADMM_LAUNCH(L, F, C) hipLaunchKernelGGL((k_admm_update<L, F, C, 0>), grid, blk, 0, S, a)
 #define PDPLQR_ADMM_LAUNCH4(F, C) hipLaunchKernelGGL((k_admm_update<16, F, C, 4>), grid, blk, 0, S, a)
+    const bool l16 = lps == 16;
     if (l16 && a.max_nc <= 4) {
         if (fuse && check) PDPLQR_ADMM_LAUNCH4(true, true);
         else if (fuse) PDPLQR_ADMM_LAUNCH4(true, false);
@@ -280,11 +281,16 @@ static int launch_admm_update(const AdmmArgs &a, bool l16, bool fuse, bool check
         else if (fuse) PDPLQR_ADMM_LAUNCH(16, true, false);
         else if (check) PDPLQR_ADMM_LAUNCH(16, false, true);
         else PDPLQR_ADMM_LAUNCH(16, false, false);
-    } else {
+    } else if (lps == 32) {
         if (fuse && check) PDPLQR_ADMM_LAUNCH(32, true, true);
         else if (fuse) PDPLQR_ADMM_LAUNCH(32, true, false);
         else if (check) PDPLQR_ADMM_LAUNCH(32, false, true);
         else PDPLQR_ADMM_LAUNCH(32, false, false);
+    } else {
+        if (fuse && check) PDPLQR_ADMM_LAUNCH(64, true, true);
+        else if (fuse) PDPLQR_ADMM_LAUNCH(64, true, false);
+        else if (check) PDPLQR_ADMM_LAUNCH(64, false, true);
+        else PDPLQR_ADMM_LAUNCH(64, false, false);
     }
 #undef PDPLQR_ADMM_LAUNCH
 #undef PDPLQR_ADMM_LAUNCH4
@@ -481,7 +487,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             else if (rc == PDPLQR_ERR_UNSUPPORTED) can_fuse = false;
             else return rc;
         }
-        if (!fused && (rc = launch_admm_update(a, sh.s <= 16, fuse, check, ugrid, ublk, S))) return rc;
+        if (!fused && (rc = launch_admm_update(a, sh.s <= 16 ? 16 : (sh.s <= 32 ? 32 : 64), fuse, check, ugrid, ublk, S))) return rc;
         if (check) {
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));

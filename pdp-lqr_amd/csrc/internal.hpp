@@ -65,6 +65,11 @@ int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st);  // ERR
 int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                        double *ws, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
 int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st);
+// 32 < n + m <= 64 (kernels_big.hip): serial backward with factorization, forward
+bool big_shape(const Shape &sh);
+int launch_riccati_backward_big(const RiccatiArgs &a, hipStream_t st);
+int launch_riccati_forward_big(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                               double *ws, hipStream_t st);
 int launch_nofact_dma(const RiccatiArgs &a, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
 int launch_riccati_forward(const Shape &sh, const double *E, const double *c, const double *KD, const double *x0,
                            double *ws, hipStream_t st);

@@ -450,8 +450,10 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k_riccati_bwd<1>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (a.sh.s <= 32) {
         hipLaunchKernelGGL(k_riccati_bwd<2>, dim3(a.sh.batch), dim3(64), 0, st, a);
+    } else if (big_shape(a.sh)) {
+        return launch_riccati_backward_big(a, st);
     } else {
-        set_error("backward: n + m > 32 is not supported by this build");
+        set_error("backward: n + m > 64 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -463,8 +465,8 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
 // linear terms, reusing the cached factors L_k (keep_factors).  One wavefront
 // per problem; writes lp_k to the cache and lu'_k into the rollout record.
 // ---------------------------------------------------------------------------
+template <int P>  // P >= n + m: 32, or 64 for the shapes of kernels_big.hip
 __global__ __launch_bounds__(64) void k_riccati_bwd_nofact(RiccatiArgs A) {
-    constexpr int P = 32;
     __shared__ double Lk[P * P];  // this stage's L (packed -> dense, column-major, ld = s)
     __shared__ double Ln[P * P];  // next stage's Lxx (ld = n)
     __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P];
@@ -553,11 +555,12 @@ int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st) {
         const int rc = launch_nofact_dma(a, st);
         if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
     }
-    if (a.sh.s > 32) {
-        set_error("backward_without_factorization: n + m > 32 is not supported by this build");
+    if (a.sh.s > 64) {
+        set_error("backward_without_factorization: n + m > 64 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
-    hipLaunchKernelGGL(k_riccati_bwd_nofact, dim3(a.sh.batch), dim3(64), 0, st, a);
+    if (a.sh.s <= 32) hipLaunchKernelGGL(k_riccati_bwd_nofact<32>, dim3(a.sh.batch), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_riccati_bwd_nofact<64>, dim3(a.sh.batch), dim3(64), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -914,7 +917,9 @@ static int launch_fwd(const Shape &sh, const double *E, const double *c, const d
                       double *ws, const SegFwd &sf, hipStream_t st) {
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
     if (sh.s > 32) {
-        set_error("forward: n + m > 32 is not supported by this build");
+        if (!SEG && big_shape(sh)) return launch_riccati_forward_big(sh, E, c, FR, x0, ws, st);
+        set_error(SEG ? "segment forward: n + m > 32 is not supported by this build"
+                      : "forward: n + m > 64 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     const int R = sh.s <= 16 ? 1 : 2;

@@ -302,7 +302,7 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
 int solver_init(pdplqr_handle h) {
     switch (h->cfg.solver) {
         case PDPLQR_SOLVER_SERIAL:
-            if (h->sh.s > 32) return unsupported("SERIAL solver with n + m > 32");
+            if (h->sh.s > 64) return unsupported("SERIAL solver with n + m > 64");
             return PDPLQR_OK;
         case PDPLQR_SOLVER_PARALLEL:
             return parallel_init(h);
