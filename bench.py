@@ -584,7 +584,7 @@ def bwd_kernel_name(n, m, keep):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)  # ~0.5 s timed at the headline config
+    ap.add_argument("--steps", type=int, default=400)  # ~2 s timed at the headline config (visible to a busy sampler)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--nx", type=int, default=12)
