@@ -231,6 +231,54 @@ def measured_copy_gbs(dev, nbytes=1 << 32, reps=5):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def pattern_ceiling_ms(dev, n, m, N, batch, reps=5):
+    """Time of the serial kernels' own HBM access pattern with no arithmetic
+    (libpdplqr_probe.so, csrc/probe_pattern.hip): one wave per problem streams
+    the stage records the kernel reads and writes its per-stage output.
+    Returns {"backward": ms, "forward": ms}, or None when the probe library
+    is absent.  Backward: E | packed H~ + h~ | c in, rollout record out;
+    forward: E | c | record in, w_k out (all 16-byte chunks per stage)."""
+    import ctypes
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pdp-lqr_amd", "pdplqr",
+                        "libpdplqr_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    fn = lib.pdplqr_probe_pattern
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                         ctypes.c_void_p, ctypes.c_void_p]
+    s = n + m
+    ch = lambda doubles: (doubles + 1) // 2  # noqa: E731
+    rE, rH, rc, rR, rw = ch(n * s), ch(s * (s + 1) // 2 + s), ch(n), ch(s * m + m), ch(s)
+    st = N * batch
+    bufs = [torch.zeros(st * r * 2, dtype=torch.float64, device=dev) for r in (rE, rH, rc, rR)]
+    out = torch.empty(st * max(rR, rw) * 2, dtype=torch.float64, device=dev)
+    sink = torch.zeros(1, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for name, (a0, r0), (a1, r1), (a2, r2), r_out in (
+            ("backward", (bufs[0], rE), (bufs[1], rH), (bufs[2], rc), rR),
+            ("forward", (bufs[0], rE), (bufs[2], rc), (bufs[3], rR), rw)):
+        def launch():
+            rc_ = fn(a0.data_ptr(), r0, a1.data_ptr(), r1, a2.data_ptr(), r2, out.data_ptr(), r_out, batch, N,
+                     sink.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+            if rc_ != 0:
+                raise RuntimeError(f"pdplqr_probe_pattern: hip error {rc_}")
+        launch()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        for i in range(reps):
+            e[2 * i].record(stream)
+            launch()
+            e[2 * i + 1].record(stream)
+        torch.cuda.synchronize(dev)
+        res[name] = min(e[2 * i].elapsed_time(e[2 * i + 1]) for i in range(reps))
+    del bufs, out, sink
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
     """C3: batch 4096 independent LQRs, N = 256, 12/4 (MPC-style batched solve):
     backward + forward of the serial solver, as the headline line, plus an
@@ -699,6 +747,15 @@ def main():
     copy_gbs = measured_copy_gbs(dev)
     res["roofline"]["peak_measured_copy"] = copy_gbs
     res["roofline"]["frac_of_measured_copy"] = achieved / copy_gbs
+    pat = pattern_ceiling_ms(dev, n, m, N, B)
+    if pat is not None:
+        # the kernels' own access pattern with nothing on the chain: the time
+        # their data flow needs on this box (1.0 = at that ceiling)
+        res["roofline"]["pattern_ceiling"] = {
+            "backward_ms": pat["backward"], "forward_ms": pat["forward"],
+            "backward_frac": pat["backward"] / ms_bwd, "forward_frac": pat["forward"] / ms_fwd,
+            "solve_frac": (pat["backward"] + pat["forward"]) / (ms_bwd + ms_fwd),
+            "probe": "csrc/probe_pattern.hip"}
     if not args.no_secondary:
         res["end_to_end"] = bench_end_to_end(bs, E, c, Hk, h, x0, ws0, out, dev, dist, local)
     bs.close()

@@ -1,0 +1,64 @@
+// Bench-only probe (libpdplqr_probe.so, not part of the C ABI in pdplqr.h):
+// the HBM access pattern of the serial solver's streamed kernels with no
+// arithmetic on the chain.  One wave per problem walks N stage records of
+// three arrays (problem-major [b][N][rec], as the boundary and workspace lay
+// them out), four stages of loads in flight, and writes one small record per
+// stage.  Its time is the ceiling the backward / rollout kernels' data flow
+// allows on the box: bench.py reports each kernel's time against it
+// (scripts/ubench/stream_layout.hip sweeps layouts, depths and store kinds:
+// none of them moves this ceiling, profiles/r02/stream_*.log).
+#include <hip/hip_runtime.h>
+
+namespace {
+
+constexpr int kDepth = 4;
+
+__global__ __launch_bounds__(256) void k_probe_pattern(const double2 *__restrict__ a0, int r0,
+                                                       const double2 *__restrict__ a1, int r1,
+                                                       const double2 *__restrict__ a2, int r2,
+                                                       double2 *__restrict__ w, int rw, int P, int N,
+                                                       double *__restrict__ sink) {
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+    if (p >= P) return;
+    const size_t base = (size_t)p * N;
+    double2 buf[kDepth][6];
+    // record j of stage k of array a with r chunks per stage; lanes past the
+    // record re-read its last chunk (clamped: no exec-masked loads)
+    auto load = [&](int d, int k) {
+        k = k < N - 1 ? k : N - 1;
+        const size_t s = base + k;
+        buf[d][0] = a0[s * r0 + min(l, r0 - 1)];
+        buf[d][1] = a0[s * r0 + min(l + 64, r0 - 1)];
+        buf[d][2] = a1[s * r1 + min(l, r1 - 1)];
+        buf[d][3] = a1[s * r1 + min(l + 64, r1 - 1)];
+        buf[d][4] = a2[s * r2 + min(l, r2 - 1)];
+        buf[d][5] = a2[s * r2 + min(l + 64, r2 - 1)];
+    };
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) load(d, d);
+    double acc = 0.0;
+    for (int k = 0; k < N; k += kDepth) {
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) acc += buf[d][i].x * buf[d][i].y;
+            if (l < rw && k + d < N) w[(base + k + d) * rw + l] = make_double2(acc, (double)k);
+            load(d, k + kDepth + d);
+        }
+    }
+    if (acc == 1234.5) sink[0] = acc;  // keeps the loads live
+}
+
+}  // namespace
+
+// Chunks are 16 bytes; r0, r1, r2 in [1, 128], rw in [0, 64].  Returns 0 or a
+// hipError_t.  Buffers hold P * N records of their size.
+extern "C" int pdplqr_probe_pattern(const void *a0, int r0, const void *a1, int r1, const void *a2, int r2, void *w,
+                                    int rw, int P, int N, void *sink, void *stream) {
+    if (r0 < 1 || r0 > 128 || r1 < 1 || r1 > 128 || r2 < 1 || r2 > 128 || rw < 0 || rw > 64 || P < 1 || N < 1)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_probe_pattern, dim3((P + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                       (const double2 *)a0, r0, (const double2 *)a1, r1, (const double2 *)a2, r2, (double2 *)w, rw, P,
+                       N, (double *)sink);
+    return (int)hipGetLastError();
+}
