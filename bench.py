@@ -237,7 +237,8 @@ def pattern_ceiling_ms(dev, n, m, N, batch, reps=5):
     the stage records the kernel reads and writes its per-stage output.
     Returns {"backward": ms, "forward": ms}, or None when the probe library
     is absent.  Backward: E | packed H~ + h~ | c in, rollout record out;
-    forward: E | c | record in, w_k out (all 16-byte chunks per stage)."""
+    forward: E | c | record in, w_k out (all 16-byte chunks per stage; the record
+    in the form the backward leaves it)."""
     import ctypes
 
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pdp-lqr_amd", "pdplqr",
@@ -251,7 +252,9 @@ def pattern_ceiling_ms(dev, n, m, N, batch, reps=5):
                                                          ctypes.c_void_p, ctypes.c_void_p]
     s = n + m
     ch = lambda doubles: (doubles + 1) // 2  # noqa: E731
-    rE, rH, rc, rR, rw = ch(n * s), ch(s * (s + 1) // 2 + s), ch(n), ch(s * m + m), ch(s)
+    # rollout record: gain form [K~ | k~] on the 12/4 value-form path, else [L(:, 0:m) | lu']
+    gain = (n, m) == (12, 4) and not os.environ.get("PDPLQR_REC_L")
+    rE, rH, rc, rR, rw = ch(n * s), ch(s * (s + 1) // 2 + s), ch(n), ch(n * m + m if gain else s * m + m), ch(s)
     st = N * batch
     bufs = [torch.zeros(st * r * 2, dtype=torch.float64, device=dev) for r in (rE, rH, rc, rR)]
     out = torch.empty(st * max(rR, rw) * 2, dtype=torch.float64, device=dev)

@@ -62,8 +62,9 @@ int launch_penalty(const Shape &sh, const double *D, const double *rho, const do
                    const short2 *tab_n, int with_H, int max_nc, hipStream_t st);
 int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
+bool schur_gain_record(const RiccatiArgs &a);  // the backward leaves the gain-form record [K~ | k~]
 int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
-                       double *ws, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
+                       double *ws, hipStream_t st, bool gain = false);  // ERR_UNSUPPORTED: not applicable
 int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st);
 // 32 < n + m <= 64 (kernels_big.hip): serial backward with factorization, forward
 bool big_shape(const Shape &sh);
@@ -98,6 +99,8 @@ struct pdplqr_handle_s {
     // update_problem_data calls with the same sigma, re-formed after set_model
     // or clear_workspace
     bool hw_cached = false;
+    // the last serial backward left the gain-form rollout record (schur_gain_record)
+    bool rec_gain = false;
     double hw_sigma = 0.0;
     int32_t *status = nullptr;
     int32_t *d_off = nullptr, *y_off = nullptr;

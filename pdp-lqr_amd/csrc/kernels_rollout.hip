@@ -14,8 +14,13 @@
 //   u   = -Luu^{-T} v            back substitution, u_i broadcast by readlane;
 //                                B u accumulates on the fly (lanes g == 0)
 //   x+  = c + A x + B u          lanes cl < n, columns split over g, reduced over g
-// vmcnt accounting: each iteration issues exactly 3 DMA + 1 store instructions,
-// so "stage k has landed" is s_waitcnt vmcnt(4 (D - 1)).
+// vmcnt accounting: each iteration issues exactly NI DMA + 1 store instructions,
+// so "stage k has landed" is s_waitcnt vmcnt((NI + 1) (D - 1)).
+//
+// GAIN: the value-form backward's gain-form record FR_k = [K~ | k~]
+// (kernels_schur.hip, K~ = Luu^{-T} Lxu^T, k~ = Luu^{-T} lu'), so
+//   u = -(k~ + K~ x)                lanes cl < m, columns 4 q + g, reduced over g
+// with no back substitution; 256 doubles per stage = exactly 2 DMA instructions.
 #include "device_common.hpp"
 
 #include <stdint.h>
@@ -23,25 +28,26 @@
 
 namespace pdplqr {
 
-template <int NN, int MM>
+template <int NN, int MM, bool GAIN = false>
 struct RollShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
-    static constexpr int OE = 0, OC = n * s, OF = OC + n, FS = s * m + m, REC = OF + FS;  // doubles per stage
+    static constexpr int FS = GAIN ? n * m + m : s * m + m;            // record doubles per stage
+    static constexpr int OE = 0, OC = n * s, OF = OC + n, REC = OF + FS;  // doubles per stage
     static constexpr int CH = REC / 2;                                                  // 16-byte chunks
     static constexpr int NI = (CH + 63) / 64;
     static constexpr int TAIL = CH - (NI - 1) * 64;  // active lanes of the last DMA instruction
-    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FS % 2 == 0 && s <= 16 && NI == 3;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FS % 2 == 0 && s <= 16 && NI >= 2 && NI <= 3;
 };
 
 #ifndef PDPLQR_ROLL_DEPTH
 #define PDPLQR_ROLL_DEPTH 4
 #endif
 
-template <int NN, int MM, int D>
+template <int NN, int MM, int D, bool GAIN = false>
 __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
                                                     const double *__restrict__ x0, double *__restrict__ ws) {
-    using SH = RollShape<NN, MM>;
+    using SH = RollShape<NN, MM, GAIN>;
     constexpr int n = SH::n, m = SH::m, s = SH::s, NI = SH::NI;
     constexpr int NQ = (n + 3) / 4;  // row / column chunks of the x block over g
     static_assert(SH::ok, "rollout DMA layout");
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__re
         const int kp = k + D - 1;
         dma(kp < N ? kp : N - 1, kp % D);  // past the end: re-load into a consumed slot (keeps the count uniform)
         if (k < D - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (D - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NI + 1) * (D - 1)) : "memory");
         const double *R = ring[k % D];
         const double *F = R + SH::OF;
         // ---- record reads (independent of the chain).  Addresses are
@@ -92,17 +98,17 @@ __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__re
         for (int q = 0; q < NQ; ++q) {
             const int t = 4 * q + g, tc = t < n ? t : n - 1;
             const bool tv = (4 * q + 3 < n) || t < n;  // folds to true when n % 4 == 0
-            const double l = F[cm * s + m + tc], e = R[SH::OE + (m + tc) * n + cn];
+            const double l = GAIN ? F[cm * n + tc] : F[cm * s + m + tc], e = R[SH::OE + (m + tc) * n + cn];
             lxu[q] = tv ? l : 0.0;
             ex[q] = tv ? e : 0.0;
         }
 #pragma unroll
         for (int i = 0; i < MM; ++i) {
             eu[i] = g0 * R[SH::OE + i * n + cn];
-            luu[i] = F[cm * s + i];  // Luu[i][cl] (the record is zero above the diagonal)
+            luu[i] = GAIN ? 0.0 : F[cm * s + i];  // Luu[i][cl] (the record is zero above the diagonal)
         }
-        const double lu = F[s * m + cm];
-        const double rdiag = 1.0 / F[cm * s + cm];
+        const double lu = GAIN ? F[n * m + cm] : F[s * m + cm];  // k~ / lu'
+        const double rdiag = GAIN ? 1.0 : 1.0 / F[cm * s + cm];
         const double cc = R[SH::OC + cn];
         // ---- chain ----
         const int lx = (lane >= m && lane < s) ? lane - m : 0;
@@ -122,6 +128,14 @@ __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__re
         }
         v = sum_groups(v) + lu;
         double acc = 0.0, myu = 0.0;
+        if constexpr (GAIN) {
+#pragma unroll
+            for (int i = 0; i < MM; ++i) {
+                const double ui = readlane_f64(-v, i);  // u = -(k~ + K~ x), valid on lane cl == i
+                if (cl == i) myu = ui;
+                a = __builtin_fma(eu[i], ui, a);  // lanes g == 0: B[cl][i] u_i
+            }
+        } else
 #pragma unroll
         for (int i = m - 1; i >= 0; --i) {
             const double ui = readlane_f64(-(v + acc) * rdiag, i);  // valid on lane cl == i
@@ -145,8 +159,17 @@ static bool roll_aligned(const Shape &sh, const double *E, const double *c, cons
 }
 
 // PDPLQR_ERR_UNSUPPORTED: shape / alignment not covered, caller uses the generic rollout.
+// gain: FR holds the gain-form record (only the 12/4 value-form backward writes
+// it; no other rollout reads that format, so UNSUPPORTED is then an error).
 int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
-                       double *ws, hipStream_t st) {
+                       double *ws, hipStream_t st, bool gain) {
+    if (gain) {
+        if (!(sh.n == 12 && sh.m == 4 && roll_aligned(sh, E, c, FR))) return PDPLQR_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st, sh, E,
+                           c, FR, x0, ws);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     if (getenv("PDPLQR_NO_DMA") || !roll_aligned(sh, E, c, FR)) return PDPLQR_ERR_UNSUPPORTED;
     if (sh.n == 12 && sh.m == 4)
         hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH>), dim3(sh.batch), dim3(64), 0, st, sh, E, c, FR,

@@ -117,10 +117,21 @@ struct SchurSmem {
 #define PDPLQR_SCHUR_T4 0
 #endif
 
-template <int MM>
+// Gain-form rollout record (GAIN, 12/4 value-form path): the forward needs
+// u = -Luu^{-T}(lu' + Lxu^T x) = -(k~ + K~ x) with K~ = T^T Lxu^T (m x n) and
+// k~ = T^T lu' (T = Luu^{-1}): 52 instead of 68 doubles per stage, and the
+// forward loses its back substitution.  Off the P chain: every lane already
+// holds its whole row W[c][0..m) of the u columns.
+struct GainOut {
+    double kt;  // lane (g, c): K~[g][c - m] on x rows c >= m
+    double kq;  // k~[g] (every lane of group g)
+};
+
+template <int MM, bool GAIN = false>
 __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], double &w, double (&luq)[4], int g,
-                                                   int c) {
+                                                   int c, GainOut *go = nullptr) {
     static_assert(MM >= 1 && MM <= 4, "u block");
+    static_assert(!GAIN || !PDPLQR_SCHUR_T4, "gain record needs the VALU W");
     double a[4][4], lu[4], L[4][4], T[4][4], inv[4];
     bool ok = true;
 #pragma unroll
@@ -174,12 +185,30 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
 #pragma unroll
     for (int l = 0; l < MM; ++l) ml[l] = bcast_group(M[0], l);
     w = 0.0;
+    double Wc[4];  // W[c][j], j < m: this lane's row of the u columns
 #pragma unroll
     for (int j = 0; j < MM; ++j) {
         double v = 0.0;
 #pragma unroll
         for (int l = 0; l <= j; ++l) v = __builtin_fma(T[j][l], ml[l], v);
+        Wc[j] = v;
         w = (g == j) ? v : w;  // W[c][g]; groups g >= m keep 0
+    }
+    if constexpr (GAIN) {  // K~[i][c] = sum_{l >= i} T[l][i] W[c][l], k~[i] = sum_{l >= i} T[l][i] lu'[l]
+        double kt = 0.0, kq = 0.0;
+#pragma unroll
+        for (int i = 0; i < MM; ++i) {
+            double a = 0.0, q = 0.0;
+#pragma unroll
+            for (int l = i; l < MM; ++l) {
+                a = __builtin_fma(T[l][i], Wc[l], a);
+                q = __builtin_fma(T[l][i], luq[l], q);
+            }
+            kt = (g == i) ? a : kt;
+            kq = (g == i) ? q : kq;
+        }
+        go->kt = kt;
+        go->kq = kq;
     }
 #endif
 #if PDPLQR_LP_IN_P
@@ -209,9 +238,10 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
 // after the m u-pivots (trailing block P_k, u columns unscaled L).  prow:
 // p~ in row layout (prow[r] = p[4 r + g - m] on x rows).
-template <int MM, bool SYM = true>
+template <int MM, bool SYM = true, bool GAIN = false>
 __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const SchurIn &in, SchurSmem &sm, int m,
-                                            int s, int g, int c, double &w, double (&luq)[4], bool sym_rt = true) {
+                                            int s, int g, int c, double &w, double (&luq)[4], bool sym_rt = true,
+                                            GainOut *go = nullptr) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks that hold x rows
     d4 G = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -242,7 +272,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
     }
     bool ok;
     if constexpr (MM > 0) {
-        ok = schur_block_pivots<MM>(Mn, lpr[0], w, luq, g, c);
+        ok = schur_block_pivots<MM, GAIN>(Mn, lpr[0], w, luq, g, c, go);
         Pm = Mn;
     } else {
         d4 Mt[1][1];
@@ -318,6 +348,16 @@ __device__ __forceinline__ void schur_store_record_direct(double *FRk, double w,
     if (lane < M) gstore(FRk + S * M + lane, luq[lane < M ? lane : 0]);
 }
 
+// Gain-form record [K~ (m x n, row-major) | k~] in ONE store: lane (g, c >= M)
+// writes K~[g][c - M], lanes (g, c < M) write k~[g] (three of them a duplicate
+// of the same value to the same address).
+template <int M, int S>
+__device__ __forceinline__ void schur_store_record_gain(double *FRk, const GainOut &go, int g, int c) {
+    static_assert(M == 4 && S == 16, "one K~ row per row group");
+    constexpr int NX = S - M;
+    gstore(FRk + (c >= M ? g * NX + (c - M) : M * NX + g), c >= M ? go.kt : go.kq);
+}
+
 // Record from the tile (chol_tiles path): u columns of M scaled by 1/sqrt(d)
 // (sm.inv), lu' from sm.luq; staged in LDS, one coalesced store.
 template <int M, int S>
@@ -380,8 +420,9 @@ using SymOff = std::integral_constant<bool, false>;
 // NN = MM = 0: runtime shape, register prefetch of the next stage.
 // NN, MM > 0 : compile-time shape, stage records streamed by LDS-DMA
 //              (global_load_lds_dwordx4) into a double buffer.
-template <int NN, int MM>
+template <int NN, int MM, bool GAIN = false>
 __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_riccati_bwd_schur(RiccatiArgs A) {
+    static_assert(!GAIN || (NN == 12 && MM == 4 && PDPLQR_SCHUR_BLOCK), "gain-form record: 12/4 block path");
     constexpr bool CT = NN > 0;
     using SH = SchurShape<(CT ? NN : 2), (CT ? MM : 2)>;
     constexpr int NI = CT ? SH::NI : 1;
@@ -398,7 +439,7 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     const double *Hb = A.Hw + b * sh.perHw;
     const double *hb = A.hw + b * sh.perh;
     double *FRb = A.KD + b * sh.perKD;
-    const int frs = s * m + m;
+    const int frs = GAIN ? n * m + m : s * m + m;  // doubles per stage of the record
     int fail_stage = -1;
 
     // ---- terminal (lqr_kernel.hpp:80-91): P_N = H~_N, p_N = h~_N ----
@@ -458,11 +499,13 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // compiler copy R (still in flight) into other registers.
         auto vwait5 = [&](d2v(&R)[NI]) {  // steady state
             static_assert(NI == 3, "register staging");
-            if (PDPLQR_REC_DIRECT) asm volatile("s_waitcnt vmcnt(7)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if (PDPLQR_REC_DIRECT && !GAIN)
+                asm volatile("s_waitcnt vmcnt(7)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
             else asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
         };
         auto vwait4 = [&](d2v(&R)[NI]) {  // first step
-            if (PDPLQR_REC_DIRECT) asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if (PDPLQR_REC_DIRECT && !GAIN)
+                asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
             else asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
         };
         auto vwait0 = [&](d2v(&R)[NI]) {
@@ -499,10 +542,13 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::LOC, R + SH::LOP, R + SH::LOH, n, m, s, g, c, SH::LDE);
             double w, luq[4];
-            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value>(Pm, prow, in, sm, m, s,
-                                                                                              g, c, w, luq, sym_rt);
+            GainOut go;
+            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN>(
+                Pm, prow, in, sm, m, s, g, c, w, luq, sym_rt, &go);
             fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
-            if (PDPLQR_SCHUR_BLOCK && PDPLQR_REC_DIRECT)
+            if constexpr (GAIN)
+                schur_store_record_gain<SH::m, SH::s>(FRb + (long long)k * frs, go, g, c);
+            else if (PDPLQR_SCHUR_BLOCK && PDPLQR_REC_DIRECT)
                 schur_store_record_direct<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, g, c);
             else if (PDPLQR_SCHUR_BLOCK)
                 schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
@@ -571,11 +617,27 @@ static bool schur_aligned(const RiccatiArgs &a) {
            sh.perHw % 2 == 0 && sh.perh % 2 == 0;
 }
 
+static bool schur_ct(const RiccatiArgs &a) {  // the compile-time 12/4 kernel applies
+    const Shape &sh = a.sh;
+    return !a.Lc && !getenv("PDPLQR_NO_SCHUR") && sh.n == 12 && sh.m == 4 && schur_aligned(a) &&
+           !getenv("PDPLQR_NO_DMA");
+}
+
+// The backward for these arguments leaves the gain-form record [K~ | k~]
+// (the forward must then run launch_rollout_dma(..., gain = true)).
+// PDPLQR_REC_L: keep the [L(:, 0:m) | lu'] record (A/B).
+bool schur_gain_record(const RiccatiArgs &a) {
+    return PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4 && schur_ct(a) && !getenv("PDPLQR_REC_L");
+}
+
 // Returns PDPLQR_ERR_UNSUPPORTED when the shape / options need the full-factor kernels.
 int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st) {
     const Shape &sh = a.sh;
     if (a.Lc || sh.s > 16 || getenv("PDPLQR_NO_SCHUR")) return PDPLQR_ERR_UNSUPPORTED;
-    if (sh.n == 12 && sh.m == 4 && schur_aligned(a) && !getenv("PDPLQR_NO_DMA"))
+    if (schur_gain_record(a))
+        hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4>), dim3(sh.batch),
+                           dim3(64), 0, st, a);
+    else if (schur_ct(a))
         hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4>), dim3(sh.batch), dim3(64), 0, st, a);
     else
         hipLaunchKernelGGL((k_riccati_bwd_schur<0, 0>), dim3(sh.batch), dim3(64), 0, st, a);

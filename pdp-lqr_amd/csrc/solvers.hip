@@ -402,7 +402,9 @@ int solver_backward(pdplqr_handle h, const double *rho) {
                                 h->max_nc, h->stream);
         if (rc) return rc;
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1);
-        return launch_riccati_backward(riccati_args(h), h->stream);
+        const RiccatiArgs a = riccati_args(h);
+        h->rec_gain = schur_gain_record(a);
+        return launch_riccati_backward(a, h->stream);
     });
 }
 
@@ -414,6 +416,7 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho) {
         if (rc) return rc;
         // LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154)
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, last, false);
+        h->rec_gain = false;
         return launch_riccati_backward_nofact(riccati_args(h), h->stream);
     });
 }
@@ -421,8 +424,9 @@ int solver_backward_nofact(pdplqr_handle h, const double *rho) {
 int solver_backward_prepared(pdplqr_handle h) {
     const bool fact = h->Lc == nullptr || h->lpc == nullptr;
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1, fact);
-    return fact ? launch_riccati_backward(riccati_args(h), h->stream)
-                : launch_riccati_backward_nofact(riccati_args(h), h->stream);
+    const RiccatiArgs a = riccati_args(h);
+    h->rec_gain = fact && schur_gain_record(a);
+    return fact ? launch_riccati_backward(a, h->stream) : launch_riccati_backward_nofact(a, h->stream);
 }
 
 // ADMM: the update of iteration it fused into the backward of it + 1
@@ -432,6 +436,7 @@ int solver_nofact_admm(pdplqr_handle h, const AdmmArgs &a, bool check) {
     for (int k = 0; k < h->sh.N; ++k)
         if (h->ncs[k] != 4) return PDPLQR_ERR_UNSUPPORTED;
     if (h->ncs[h->sh.N] != 0) return PDPLQR_ERR_UNSUPPORTED;
+    h->rec_gain = false;
     return launch_nofact_admm(riccati_args(h), a, check, h->stream);
 }
 
@@ -439,6 +444,11 @@ int solver_forward(pdplqr_handle h, const double *x0, double *ws) {
     return run_graphed(h, 2, x0, ws, [&]() -> int {
         if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_forward(h, x0, ws);
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
+        if (h->rec_gain) {
+            const int rc = launch_rollout_dma(h->sh, h->E, h->c, h->KD, x0, ws, h->stream, true);
+            if (rc == PDPLQR_ERR_UNSUPPORTED) set_error("forward: the model changed layout since backward");
+            return rc;
+        }
         return launch_riccati_forward(h->sh, h->E, h->c, h->KD, x0, ws, h->stream);
     });
 }

@@ -18,9 +18,21 @@ def regs(op):
 def main(src, asm="/tmp/_schur_check.s"):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Iinclude",
                            "--cuda-device-only", "-S", src, "-o", asm], stderr=subprocess.DEVNULL)
-    lines = open(asm).read().split("\n")
-    end = next(i for i, l in enumerate(lines) if l.startswith(".Lfunc_end0"))
-    lines = lines[:end]
+    text = open(asm).read().split("\n")
+    # every compile-time 12/4 instantiation (L-form and gain-form record)
+    starts = [i for i, l in enumerate(text) if re.match(r"_Z\w*k_riccati_bwd_schurILi12ELi4E\w*:", l)]
+    if not starts:
+        print("no k_riccati_bwd_schur<12, 4> instantiation found")
+        return 1
+    rc = 0
+    for st in starts:
+        end = next(i for i in range(st, len(text)) if text[i].startswith(".Lfunc_end"))
+        print(text[st].rstrip(":"))
+        rc |= check(text[st:end])
+    return rc
+
+
+def check(lines):
     hdr = next(i for i, l in enumerate(lines) if "Inner Loop Header" in l)
     lab = lines[hdr].split(":")[0]
     back = max(i for i, l in enumerate(lines) if re.search(r"s_branch\s+" + re.escape(lab) + r"\b", l))
@@ -41,7 +53,7 @@ def main(src, asm="/tmp/_schur_check.s"):
                 # the set is consumed after this wait (its ds_write follows); stop at the first wait
                 # that precedes a ds_write of r
                 k, found = (j + 1) % L, False
-                for _ in range(12):
+                for _ in range(32):
                     if ins[k].startswith("ds_write_b128") and regs(ins[k].split()[2].rstrip(",")) & r:
                         found = True
                         break

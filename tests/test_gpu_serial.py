@@ -122,6 +122,49 @@ def test_value_form_batched_shapes(n, m, N, batch):
         assert rel_err(out[b], o.forward(x0[b])) < TOL, b
 
 
+@pytest.mark.parametrize("N,batch", [(1, 2), (2, 3), (5, 2), (64, 7), (301, 4)])
+def test_rollout_record_forms(N, batch):
+    """The 12/4 value-form backward writes the gain-form record [K~ | k~]
+    (K~ = Luu^-T Lxu^T, k~ = Luu^-T lu', 52 doubles per stage) read by the
+    gain rollout; PDPLQR_REC_L keeps the reference's [L(:, 0:m) | lu'] record
+    (68 doubles, back substitution in the rollout).  Both against the oracle
+    and against each other, horizons shorter and longer than the rings."""
+    import os
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m = 12, 4
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 7 + N)
+    ws0 = np.zeros((batch, N * (n + m) + n))
+    outs = {}
+    for form in ("gain", "L"):
+        if form == "L":
+            os.environ["PDPLQR_REC_L"] = "1"
+        try:
+            bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
+            bs.set_model(E, c, H, h)
+            bs.update_problem_data(ws0, sigma=1e-6)
+            bs.backward()
+            out = np.zeros_like(ws0)
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0), form
+            outs[form] = out
+        finally:
+            os.environ.pop("PDPLQR_REC_L", None)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        ref = o.forward(x0[b])
+        for form, out in outs.items():
+            assert rel_err(out[b], ref) < TOL, (form, b)
+        assert rel_err(outs["gain"][b], outs["L"][b]) < 1e-12, b
+
+
 @pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40"])
 def test_backward_without_factorization(name):
     """lqr_solver.hpp:65-70 after a full backward, with new linear data."""
