@@ -626,7 +626,9 @@ def bwd_kernel_name(n, m, keep):
     kernels_riccati.hip launch_riccati_backward)."""
     s = n + m
     if not keep and s <= 16:
-        return "k_riccati_bwd_schur<12, 4>" if (n, m) == (12, 4) else "k_riccati_bwd_schur<0, 0>"
+        if (n, m) == (12, 4):  # the record form rides in the template (kernels_schur.hip GAIN)
+            return f"k_riccati_bwd_schur<12, 4, {'false' if os.environ.get('PDPLQR_REC_L') else 'true'}>"
+        return "k_riccati_bwd_schur<0, 0, false>"
     if (n, m) == (12, 4):
         return f"k_riccati_bwd_fast<1, 12, 4, {str(bool(keep)).lower()}>"
     return "k_riccati_bwd<1>" if s <= 16 else "k_riccati_bwd<2>"
