@@ -165,6 +165,47 @@ def test_rollout_record_forms(N, batch):
         assert rel_err(outs["gain"][b], outs["L"][b]) < 1e-12, b
 
 
+def test_record_form_follows_last_backward():
+    """One handle alternating backward kernels: the forward must read the
+    record in the form the LAST backward left (gain form from the 12/4
+    value-form kernel, L form from the runtime-shape kernel under
+    PDPLQR_NO_DMA), and a forward repeated without a new backward is
+    idempotent."""
+    import os
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 40, 3
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 99)
+    ws0 = np.zeros((batch, N * (n + m) + n))
+    refs = []
+    for b in range(batch):
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(ws0[b], None, None, None, 1e-6)
+        o.backward(None)
+        refs.append(o.forward(x0[b]))
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    for generic in (False, True, False, True):
+        if generic:
+            os.environ["PDPLQR_NO_DMA"] = "1"
+        try:
+            bs.backward()
+        finally:
+            os.environ.pop("PDPLQR_NO_DMA", None)
+        for _ in range(2):
+            out = np.zeros_like(ws0)
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            for b in range(batch):
+                assert rel_err(out[b], refs[b]) < TOL, (generic, b)
+
+
 @pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40"])
 def test_backward_without_factorization(name):
     """lqr_solver.hpp:65-70 after a full backward, with new linear data."""
