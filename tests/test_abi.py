@@ -35,6 +35,22 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_lib.EXPORTS) == syms
 
 
+def test_bench_probe_library_loads():
+    """bench.py's pattern-ceiling probe (csrc/probe_pattern.hip) is its own
+    library, outside the C ABI: it loads, exports its one entry point, and
+    rejects bad sizes before any launch."""
+    path = os.path.join(ROOT, "pdp-lqr_amd", "pdplqr", "libpdplqr_probe.so")
+    if not os.path.exists(path):
+        pytest.skip("probe library not built")
+    L = C.CDLL(path)
+    fn = L.pdplqr_probe_pattern
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_void_p, C.c_int] * 3 + [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    assert fn(None, 0, None, 1, None, 1, None, 0, 1, 1, None, None) != 0  # r0 = 0: invalid
+    assert fn(None, 1, None, 1, None, 129, None, 0, 1, 1, None, None) != 0  # r2 > 128: invalid
+    assert not any(s.startswith("pdplqr_probe") for s in declared_symbols())
+
+
 def test_config_defaults_match_reference():
     from pdplqr import _lib
 
