@@ -101,6 +101,7 @@ struct pdplqr_handle_s {
     bool hw_cached = false;
     // the last serial backward left the gain-form rollout record (schur_gain_record)
     bool rec_gain = false;
+    bool graph_rec_gain = false;  // record form the captured forward graph reads
     double hw_sigma = 0.0;
     int32_t *status = nullptr;
     int32_t *d_off = nullptr, *y_off = nullptr;

@@ -396,27 +396,27 @@ static int run_graphed(pdplqr_handle h, int slot, const void *k1, const void *k2
 
 int solver_backward(pdplqr_handle h, const double *rho) {
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) h->shard_last = 1;
+    // the record form is host state: set outside the (replayable) launch sequence
+    h->rec_gain = h->cfg.solver == PDPLQR_SOLVER_SERIAL && schur_gain_record(riccati_args(h));
     return run_graphed(h, 0, rho, nullptr, [&]() -> int {
         if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
         int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                                 h->max_nc, h->stream);
         if (rc) return rc;
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, 1);
-        const RiccatiArgs a = riccati_args(h);
-        h->rec_gain = schur_gain_record(a);
-        return launch_riccati_backward(a, h->stream);
+        return launch_riccati_backward(riccati_args(h), h->stream);
     });
 }
 
 int solver_backward_nofact(pdplqr_handle h, const double *rho) {
     const int last = h->shard_last;
+    h->rec_gain = false;  // the nofact kernels write lu' into the L-form record
     return run_graphed(h, 1, rho, reinterpret_cast<const void *>((intptr_t)(last + 1)), [&]() -> int {
         int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 0,
                                 h->max_nc, h->stream);
         if (rc) return rc;
         // LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154)
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_backward(h, last, false);
-        h->rec_gain = false;
         return launch_riccati_backward_nofact(riccati_args(h), h->stream);
     });
 }
@@ -441,6 +441,13 @@ int solver_nofact_admm(pdplqr_handle h, const AdmmArgs &a, bool check) {
 }
 
 int solver_forward(pdplqr_handle h, const double *x0, double *ws) {
+    // a forward sequence captured for the other record form is stale
+    auto &g = h->graphs[2];
+    if (g.exec && h->graph_rec_gain != h->rec_gain) {
+        (void)hipGraphExecDestroy(g.exec);
+        g = pdplqr_handle_s::Graph{};
+    }
+    h->graph_rec_gain = h->rec_gain;
     return run_graphed(h, 2, x0, ws, [&]() -> int {
         if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_forward(h, x0, ws);
         if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) return parallel_forward(h, x0, ws, nullptr, nullptr, 1);
