@@ -318,7 +318,8 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
     at a test that does not terminate, rho scales by
     e = sqrt((r_prim / max(|Dw|, |z|)) / (r_dual / |D^T y|)) (guards 1e-30, rows
     clamped to [1e-6, 1e6]) when e leaves [1/tol, tol], and the next x-update
-    re-forms and refactors.  One problem (PackedModel arrays of one batch
+    re-forms and refactors; no rescale while |D^T y| <= eps_abs (no active row:
+    the dual normalisation is undefined).  One problem (PackedModel arrays of one batch
     entry).  Returns (ws, ys, zs, info)."""
     n, m, N = pm.n, pm.m, pm.N
     s = n + m
@@ -383,7 +384,7 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
         if check and rp <= eps_abs + eps_rel * max(dwm, zm) and rd <= eps_abs + eps_rel * dty:
             conv = True
             break
-        if check and adaptive_rho and it < max_iter:
+        if check and adaptive_rho and it < max_iter and dty > eps_abs:
             e = np.sqrt((rp / (max(dwm, zm) + 1e-30)) / (rd / (dty + 1e-30) + 1e-30))
             if e > adaptive_rho_tolerance or e < 1.0 / adaptive_rho_tolerance:
                 rho = np.minimum(np.maximum(rho * e, 1e-6), 1e6)

@@ -31,7 +31,10 @@ __device__ __forceinline__ void admm_decide(const AdmmArgs &a, int b, double rp,
         a.conv[b] = 1;
     } else {
         atomicAdd(a.active, 1);
-        if (a.adaptive) {
+        // no rescale while |D^T y| is below eps_abs (every row inactive: y = 0
+        // and the dual normalisation is undefined -- the estimate would
+        // collapse to ~1e-14 and pin rho at its lower clamp)
+        if (a.adaptive && dty > a.eps_abs) {
             // OSQP's compute_rho_estimate: the ratio of the normalised
             // residuals, with its division guard 1e-30
             const double pn = rp / (fmax(dwm, zm) + 1e-30), dn = rd / (dty + 1e-30);

@@ -230,6 +230,57 @@ __device__ __forceinline__ constexpr int colpos(int i) {
     return (i & 3) * (4 * T) + ((i >> 4) << 2) + ((i >> 2) & 3);
 }
 
+// Eigen's LLT stop, restated for the right-looking elimination below.  Eigen
+// factors small matrices left-looking (llt_inplace::unblocked; the oracle's
+// llt_lower, pdplqr_oracle.c:97-116): when the reduced pivot of column j is
+// <= 0 it returns with column j and every later column still holding their
+// ORIGINAL values, and the reference uses that lower triangle as L
+// (lqr_kernel.hpp:89,126 ignore info()).  The right-looking loop has already
+// applied the rank-1 updates of the live pivots p < j to that trailing block,
+// so they are undone here, in reverse order, with the same products: row p of
+// the matrix is still the raw (unscaled) pivot row, 1/d_p = sinv[p]^2.  Only
+// the block (i, l >= j) is restored; columns < j keep their factor values.
+template <int T>
+__device__ __forceinline__ void chol_restore_tail(d4 (&M)[T][T], double *cb, const double *sinv, int jbeg,
+                                                            int jdead, int g, int c) {
+    double *myslot = cb + g * 16 * T;
+#pragma unroll
+    for (int tr = T - 1; tr >= 0; --tr)
+#pragma unroll
+        for (int rr = 3; rr >= 0; --rr) {
+#pragma unroll 1
+            for (int gj = 3; gj >= 0; --gj) {
+                const int p = 16 * tr + 4 * rr + gj;
+                if (p < jbeg || p >= jdead) continue;
+#pragma unroll
+                for (int b = 0; b < T; ++b) {
+                    const int jc = 16 * b + c;
+                    myslot[colpos<T>(jc)] = (jc > p) ? M[tr][b][rr] : 0.0;
+                }
+                wave_sync();
+                const double *slot = cb + gj * 16 * T;
+                const double inv = sinv[p];
+                const double inv2 = inv * inv;
+                double lc[T];
+#pragma unroll
+                for (int b = 0; b < T; ++b) {
+                    const int jc = 16 * b + c;
+                    lc[b] = (jc >= jdead) ? slot[colpos<T>(jc)] * inv2 : 0.0;
+                }
+#pragma unroll
+                for (int a = 0; a < T; ++a)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g;
+                        const double li = (i >= jdead) ? slot[colpos<T>(i)] : 0.0;
+#pragma unroll
+                        for (int b = 0; b < T; ++b) M[a][b][r] = __builtin_fma(li, lc[b], M[a][b][r]);
+                    }
+                wave_sync();
+            }
+        }
+}
+
 // Right-looking Cholesky of the symmetric padded matrix in C/D layout, pivots
 // jbeg..jend-1.  Column j is broadcast through LDS from row j (the row group
 // that owns row j holds M[j][*] = M[*][j]; M stays exactly symmetric because
@@ -248,6 +299,7 @@ template <int T>
 __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], double *cb, double *sinv, double *luq,
                                            int jbeg, int jend, int m, bool aug, int g, int c) {
     bool ok = true, live = true;
+    int jdead = jend;  // first state pivot <= 0 (wave-uniform)
     // cb holds one 16 T slot per row group: every group writes its own row
     // (no exec-mask branch), readers take the pivot's group slot
     double *myslot = cb + g * 16 * T;
@@ -276,6 +328,7 @@ __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], d
                 // columns stay unfactored, unscaled), flagged only if clearly
                 // negative or not finite (psd_bad)
                 ok = ok && (j < m ? djj > 0.0 : !psd_bad(djj));
+                if (live && !(j < m || djj > 0.0)) jdead = j;
                 live = live && (j < m || djj > 0.0);
                 const double inv = live ? rsqrt_f64(djj) : 0.0;
                 const double inv2 = inv * inv;
@@ -306,6 +359,7 @@ __device__ __forceinline__ bool chol_tiles(d4 (&M)[T][T], double (&lpr)[T][4], d
                 wave_sync();
             }
         }
+    if (jdead < jend) chol_restore_tail<T>(M, cb, sinv, jbeg, jdead, g, c);  // rare, wave-uniform
     return ok;
 }
 

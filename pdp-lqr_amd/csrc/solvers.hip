@@ -398,7 +398,10 @@ int solver_backward(pdplqr_handle h, const double *rho) {
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) h->shard_last = 1;
     // the record form is host state: set outside the (replayable) launch sequence
     h->rec_gain = h->cfg.solver == PDPLQR_SOLVER_SERIAL && schur_gain_record(riccati_args(h));
-    return run_graphed(h, 0, rho, nullptr, [&]() -> int {
+    // the record form selects the backward kernel: it is part of the graph key
+    // (a replay of the other form's capture would leave the record in the
+    // layout the forward does not read)
+    return run_graphed(h, 0, rho, reinterpret_cast<const void *>((intptr_t)(h->rec_gain ? 2 : 1)), [&]() -> int {
         if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
         int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                                 h->max_nc, h->stream);

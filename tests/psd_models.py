@@ -4,7 +4,14 @@ P_k = 0, only the linear costate survives) and a zero terminal cost only
 (Q_N = 0).  With sigma = 0 the reference's serial solver handles both (Eigen's
 LLT stops at the first non-positive pivot, lqr_kernel.hpp:89,126), the LU
 condensed system combines P = 0, and the CHOLESKY one fails (llt of P,
-condensed_system.hpp:217-226)."""
+condensed_system.hpp:217-226).
+
+"coupled_dead_terminal" (ADVICE r2): Q_N is the identity except that state 1
+has no cost and states 0 and 2 are coupled (Q_N[0,2] = 0.8).  Its second
+pivot is exactly 0 AFTER the first pivot has reduced the trailing block, so
+Eigen's left-looking LLT stops there with columns >= 1 at their ORIGINAL
+values: the reference's L_N is not a factor of Q_N (L_N L_N^T has 1.64 at
+(2, 2)), and every L-form path must reproduce that L_N."""
 import numpy as np
 
 
@@ -14,9 +21,29 @@ def psd_model(kind, n=12, m=4, N=64, seed=0):
 
     model, x0 = random_model(n, m, N, seed=seed)
     for k, nd in enumerate(model.nodes):
-        if k == N:
+        if k == N and kind == "coupled_dead_terminal":
+            nd.H[:] = np.eye(n)
+            nd.H[1, 1] = 0.0
+            nd.H[0, 2] = nd.H[2, 0] = 0.8
+        elif k == N:
             nd.H[:] = 0.0
         elif kind == "zero_state_cost":
             nd.H[m:, :] = 0.0
             nd.H[:, m:] = 0.0
     return pack_model(model), model, x0
+
+
+def eigen_stop_factor(Q):
+    """Eigen's llt_inplace::unblocked on Q (left-looking): the lower triangle it
+    leaves, including the untouched columns after a pivot <= 0 (the restated
+    semantics the tests pin; the reference ignores info())."""
+    Q = np.array(Q, dtype=np.float64)
+    n = Q.shape[0]
+    L = np.tril(Q).copy()
+    for k in range(n):
+        x = Q[k, k] - L[k, :k] @ L[k, :k]
+        if x <= 0.0:
+            return L
+        L[k, k] = np.sqrt(x)
+        L[k + 1:, k] = (Q[k + 1:, k] - L[k + 1:, :k] @ L[k, :k]) / L[k, k]
+    return L

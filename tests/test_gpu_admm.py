@@ -334,3 +334,18 @@ def test_invalid_bounds_and_rho_are_rejected():
         _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, r2, True, max_iter=5)
     w, y, z, info = _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, max_iter=5)
     assert info["iterations"] == 5
+
+
+def test_adaptive_rho_no_active_row_keeps_rho():
+    """No row active at any check (bounds +-1e6): |D^T y| = 0, the rescale is
+    skipped on the device as in the oracle, and rho stays at its start value."""
+    models, x0s = _ubox_models(3, bound=1e6)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s, warm=False)
+    rho = np.full(lb.shape, 0.1)
+    st = dict(max_iter=100, check_every=5, eps_abs=1e-12, eps_rel=1e-12)
+    w, y, z, info = _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, **st)
+    for b in range(len(pms)):
+        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], solver="serial", **st)
+        assert oi["rho_updates"] == 0
+        assert np.all(info["rho"][b] == 0.1), info["rho"][b]
+        assert rel_err(w[b], ow) < 1e-9

@@ -185,3 +185,46 @@ def test_horizon_shards_both_forms(condensed):
         o.update_problem_data(np.zeros(N * s + n), None, None, None, 1e-6)
         o.backward(None)
         assert rel_err(full[b], o.forward(x0[b])) < TOL
+
+
+@pytest.mark.parametrize("shape", [(12, 4), (6, 3), (24, 8)])
+@pytest.mark.parametrize("solver", ["serial_fullfactor", "batched_value_form", "parallel_LU"])
+def test_coupled_dead_terminal_pivot(shape, solver):
+    """Q_N's second pivot is exactly 0 after the first pivot has
+    reduced the trailing block (tests/psd_models.py coupled_dead_terminal).
+    The L-form (full-factor) kernels restore Eigen's stopped factor -- columns
+    >= 1 at their ORIGINAL values (device_common.hpp chol_restore_tail) -- and
+    equal the oracle, i.e. the reference.  The value-form kernels never factor
+    P (the 12/4 / s <= 16 batched backward and the parallel segment kernel
+    carry P_N = Q_N itself), so they return the exact optimum of the stated
+    problem instead: the documented deviation."""
+    from dense_ref import riccati_optimum
+    from pdplqr import BatchedLQRSolver, CondensedSystemSolverType, LQRParallelSolver, LQRSolver
+
+    n, m = shape
+    pm, model, x0 = psd_model("coupled_dead_terminal", n=n, m=m, N=40)
+    N = pm.N
+    ref = _oracle(pm, x0)
+    z0 = np.zeros(0)
+    exact = riccati_optimum(pm, x0, np.zeros(N * (n + m) + n), z0, z0, z0, z0, 0.0)
+    assert rel_err(ref, exact) > 1e-6  # the stop changes the answer
+    if solver == "serial_fullfactor":
+        w, st = _run(LQRSolver(model), model, x0)
+        target = ref
+    elif solver == "parallel_LU":
+        w, st = _run(LQRParallelSolver(model, 4, True, CondensedSystemSolverType.LU), model, x0)
+        target = exact
+    else:
+        bs = BatchedLQRSolver(n, m, N, 2, keep_factors=False)
+        rep = lambda a: np.ascontiguousarray(np.stack([a, a]))
+        bs.set_model(rep(pm.E), rep(pm.c), rep(pm.H), rep(pm.h))
+        bs.update_problem_data(np.zeros((2, N * (n + m) + n)), sigma=0.0)
+        bs.backward()
+        out = np.zeros((2, N * (n + m) + n))
+        bs.forward(rep(x0), out)
+        w, st = out[1], int(np.max(bs.status()))
+        # s > 16 has no value-form kernel: the full-factor kernel runs
+        target = exact if n + m <= 16 else ref
+    assert st == 0
+    assert np.all(np.isfinite(w))
+    assert rel_err(w, target) < TOL

@@ -206,6 +206,64 @@ def test_record_form_follows_last_backward():
                 assert rel_err(out[b], refs[b]) < TOL, (generic, b)
 
 
+def test_record_form_follows_last_backward_graph():
+    """The same alternation with protocol calls replayed from captured hipGraphs
+    (PDPLQR_GRAPH=1 is read at library load: child process).  The backward
+    graph is keyed on the record form, so a replay never runs the other form's
+    captured kernel; PDPLQR_NO_DMA is read per call, so it is toggled in the
+    child around each backward."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    code = textwrap.dedent(r"""
+        import os, sys, numpy as np
+        sys.path[:0] = [os.environ["ROOT"], os.path.join(os.environ["ROOT"], "pdp-lqr_amd")]
+        import torch
+        from oracle.oracle import OracleSerial
+        from pdplqr import BatchedLQRSolver
+        from pdplqr.model import PackedModel
+        from pdplqr.problems import random_batch_arrays
+        n, m, N, batch = 12, 4, 40, 3
+        E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 99)
+        ws0 = np.zeros((batch, N * (n + m) + n))
+        refs = []
+        for b in range(batch):
+            pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
+            o = OracleSerial(pm)
+            o.update_problem_data(ws0[b], None, None, None, 1e-6)
+            o.backward(None)
+            refs.append(o.forward(x0[b]))
+        dev = torch.device("cuda", 0)
+        t = lambda a: torch.as_tensor(a, device=dev)
+        bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
+        bs.set_model(t(E), t(c), t(H), t(h))
+        bs.update_problem_data(t(ws0), sigma=1e-6)
+        worst = 0.0
+        for generic in (False, True, False, True, False):
+            if generic:
+                os.environ["PDPLQR_NO_DMA"] = "1"
+            try:
+                bs.backward()
+            finally:
+                os.environ.pop("PDPLQR_NO_DMA", None)
+            for _ in range(2):
+                out = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev)
+                bs.forward(t(x0), out)
+                torch.cuda.synchronize()
+                o = out.cpu().numpy()
+                assert np.all(bs.status() == 0)
+                for b in range(batch):
+                    worst = max(worst, np.linalg.norm(o[b] - refs[b]) / np.linalg.norm(refs[b]))
+        print("worst", worst)
+        assert worst < 1e-9, worst
+    """)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ROOT=root, PDPLQR_GRAPH="1")
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
+
+
 @pytest.mark.parametrize("name", ["random_n12_m4_N64_nc4", "quadrotor_N30_constrained", "random_n24_m8_N40"])
 def test_backward_without_factorization(name):
     """lqr_solver.hpp:65-70 after a full backward, with new linear data."""

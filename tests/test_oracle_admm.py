@@ -124,3 +124,17 @@ def test_adaptive_rho_recovers_a_poor_rho():
     assert not fixed["converged"]
     assert info["converged"] and info["rho_updates"] >= 1 and info["rho"][0] > 0.5, info
     assert _certificate(pm, x0, w, y, lb, ub, 1e-6) < 1e-6
+
+
+def test_adaptive_rho_keeps_rho_when_no_row_is_active():
+    """Bounds so loose that no row is ever active: y stays exactly 0 and
+    |D^T y| = 0, where OSQP's estimate (normalised by |D^T y| alone) would
+    collapse to ~1e-14 and pin rho at its 1e-6 clamp.  The rule
+    skips the rescale while |D^T y| <= eps_abs, so rho is untouched."""
+    model, pm, x0, lb, ub = _case("ubox")
+    ny = int(np.sum(pm.ncs))
+    lb, ub = np.full(ny, -1e6), np.full(ny, 1e6)
+    rho = np.full(ny, 0.1)
+    w, y, z, info = admm_solve(pm, x0, lb, ub, rho, max_iter=100, check_every=5, eps_abs=1e-12, eps_rel=1e-12)
+    assert np.all(y == 0.0)
+    assert info["rho_updates"] == 0 and np.all(info["rho"] == 0.1), info

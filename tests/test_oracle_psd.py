@@ -53,3 +53,26 @@ def test_parallel_cholesky_oracle_zero_terminal_only():
     ok, w = _solve(OracleParallel(pm, 4, True, "CHOLESKY"), pm, x0)
     assert ok
     assert rel_err(w, _dense(pm, x0)) < 1e-9
+
+
+def test_oracle_eigen_stop_coupled_dead_terminal():
+    """Q_N's second pivot is exactly 0 after the first has reduced the trailing
+    block (tests/psd_models.py).  The reference's L_N is Eigen's stopped
+    factor (original values from column 1 on), so its solve equals the dense
+    optimum of the model whose terminal cost is L_N L_N^T -- not of Q_N."""
+    from psd_models import eigen_stop_factor
+
+    pm, model, x0 = psd_model("coupled_dead_terminal")
+    n, m, N = pm.n, pm.m, pm.N
+    s = n + m
+    _, w = _solve(OracleSerial(pm), pm, x0)
+    QN = pm.H[N * s * s:].reshape(n, n, order="F")
+    L = eigen_stop_factor(QN)
+    assert abs((L @ L.T)[2, 2] - 1.64) < 1e-15
+    H2 = pm.H.copy()
+    H2[N * s * s:] = (L @ L.T).ravel(order="F")
+    from pdplqr.model import PackedModel
+
+    pm2 = PackedModel(n, m, N, pm.ncs, pm.E, pm.c, H2, pm.h, pm.D)
+    assert rel_err(w, _dense(pm2, x0)) < 1e-9
+    assert rel_err(w, _dense(pm, x0)) > 1e-6  # the stop changes the answer
