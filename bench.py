@@ -36,6 +36,7 @@ import torch  # noqa: E402
 
 METRIC = "LQR stages/sec (N*batch) at nx=12,nu=4; wall-clock/solve; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TF = 78.6    # MI355X fp64 (vector = matrix)
 
 
 def gen_batch_device(n, m, N, batch, seed, device):
@@ -83,6 +84,60 @@ def load_pmc_traffic(workload_tag, kernel=None):
                     and (kernel is None or d.get("dominant_kernel", "").endswith(kernel))):
                 best = d
     return best
+
+
+def pmc_traffic(workload_tag, kernels):
+    """HBM bytes per solve of a secondary workload from a committed PMC summary
+    (profiles/**/*_pmc.json with this workload tag): the sum over the solve's
+    kernels (name substrings) of FETCH_SIZE x 2 + WRITE_SIZE (KB; gfx950
+    correction of MI355X_MICROARCH.md), or None."""
+    pdir = os.path.join(ROOT, "profiles")
+    found = None
+    for dp, _, fs in os.walk(pdir):
+        for f in sorted(fs):
+            if not f.endswith("_pmc.json"):
+                continue
+            try:
+                d = json.load(open(os.path.join(dp, f)))
+            except Exception:
+                continue
+            if d.get("workload") == workload_tag:
+                found = d
+    if not found:
+        return None
+    tot, seen = 0.0, []
+    for sub in kernels:
+        ks = [k for k in found.get("kernels", {}) if sub in k]
+        if not ks:
+            return None
+        c = found["kernels"][ks[0]]
+        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            return None
+        tot += c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        seen.append(ks[0])
+    return {"bytes": tot, "kernels": seen}
+
+
+def roofline_block(bytes_stage, stages, ms, workload_tag=None, kernels=(), flops_stage=None, kernel_desc=None):
+    """roofline of a secondary line: SURVEY.md 8(d) algorithmic bytes per stage x
+    stages over the measured solve time, against the 8 TB/s HBM spec; traffic =
+    counter bytes of the same workload from a committed profile (profiles/),
+    frac_moved = traffic / time / peak; flops (if given) against fp64 peak."""
+    achieved = bytes_stage * stages / (ms * 1e-3) / 1e9
+    r = {"kernel": kernel_desc, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "bytes_per_stage_algorithmic": bytes_stage, "ms": ms}
+    t = pmc_traffic(workload_tag, kernels) if workload_tag else None
+    r["traffic"] = t["bytes"] if t else None
+    r["traffic_source"] = (f"committed PMC summary, workload {workload_tag}: {', '.join(t['kernels'])}" if t
+                           else "no committed PMC summary for this workload")
+    if t:
+        r["frac_moved"] = t["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        r["traffic_over_algorithmic"] = t["bytes"] / (bytes_stage * stages)
+    if flops_stage:
+        tf = flops_stage * stages / (ms * 1e-3) / 1e12
+        r["fp64_tflops"] = tf
+        r["fp64_frac"] = tf / FP64_PEAK_TF
+    return r
 
 
 def cpu_baseline(n, m, N, seconds=12.0, sample_batch=64, threads=None):
@@ -316,8 +371,11 @@ def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
         err = max(err, float(np.linalg.norm(out[b].cpu().numpy() - ref) / np.linalg.norm(ref)))
     del E, c, H, h
     torch.cuda.empty_cache()
+    bst = 8 * (n * (n + m) + n + (n + m) ** 2 + (n + m)) + 8 * (n + m)  # 3,936 B at 12/4
     return {"N": N, "nx": n, "nu": m, "batch": batch, "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
-            "status_ok": ok, "oracle_rel_err": err}
+            "status_ok": ok, "oracle_rel_err": err,
+            "roofline": roofline_block(bst, N * batch, t * 1e3, f"C3_N{N}_b{batch}",
+                                       ("k_riccati_bwd_schur", "k_rollout_dma"), kernel_desc="backward + forward")}
 
 
 def bench_factor_reuse(local, dev, dist, steps=10, warmup=3, N=1024, batch=4096):
@@ -464,11 +522,15 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
         step()
         torch.cuda.synchronize(dev)
         ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
-        res["kkt" if solver == "kkt" else "riccati"] = {"ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
-                                                        "status_ok": ok,
-                                                        "oracle_rel_err": _conic_oracle_err(solver, n, m, N, ncs, E, c,
-                                                                                            H, h, D, x0, ws, ys, zs,
-                                                                                            irho, rho, out)}
+        # C5 = 4,704 B per stage (E, c, H, h, w + D, y, z, inv_rho, rho, w-bar)
+        bst = 8 * (n * s + n + s * s + s) + 8 * s + 8 * (nc * s + 4 * nc + s)
+        kern = ("k_kkt_ric_bwd", "k_kkt_ric_fwd") if solver == "kkt" else ("k_penalty", "k_riccati_bwd_schur",
+                                                                              "k_rollout_dma")
+        res["kkt" if solver == "kkt" else "riccati"] = {
+            "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t, "status_ok": ok,
+            "oracle_rel_err": _conic_oracle_err(solver, n, m, N, ncs, E, c, H, h, D, x0, ws, ys, zs, irho, rho, out),
+            "roofline": roofline_block(bst, N * batch, t * 1e3, f"C5_{solver}_N{N}_b{batch}", kern,
+                                       kernel_desc="backward + forward")}
         bs.close()
     # the ADMM outer loop on the same data (pdplqr_admm_solve): |u| <= 0.5,
     # rho = 1, from a cold start.  (a) 100 fixed iterations (eps = 0, one
@@ -578,9 +640,32 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
         oerr = float(np.linalg.norm(out[0].cpu().numpy() - ref) / np.linalg.norm(ref))
         del pm, o, ref
     del E0, H0
+    bst = 8 * (n * s + n + s * s + s) + 8 * s  # 15,040 B per stage at 24/8
+    # SURVEY 8(d) flop model: 103,235 per stage (backward + forward) + 59,968 for the segment element
     return {"N": Ntot, "nx": n, "nu": m, "n_gpus": world, "ms_per_solve": t * 1e3, "stages_per_s": Ntot / t,
             "scaling": "strong", "finite": ok, "oracle_rel_err": oerr,
-            "exchange": "all-gather of 3n^2+2n doubles per rank"}
+            "exchange": "all-gather of 3n^2+2n doubles per rank",
+            "roofline": roofline_block(bst, Ntot, t * 1e3, None, (), flops_stage=103235 + 59968,
+                                       kernel_desc="whole horizon solve (latency-bound: see DESIGN.md section 6)")}
+
+
+def headline_oracle_err(E, c, Hs, h, x0, out, n, m, N, probs):
+    """Max relative error of the timed output against the CPU oracle on a few
+    problems of the headline batch (test infrastructure, outside the timed
+    region).  Hs: the sampled problems' H (the handle keeps its own copy)."""
+    from oracle.oracle import OracleSerial
+    from pdplqr.model import PackedModel
+
+    err = 0.0
+    for b in probs:
+        pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b].cpu().numpy(), c[b].cpu().numpy(), Hs[b],
+                         h[b].cpu().numpy(), np.zeros(0))
+        o = OracleSerial(pm)
+        o.update_problem_data(np.zeros(N * (n + m) + n), None, None, None, 1e-6)
+        o.backward(None)
+        ref = o.forward(x0[b].cpu().numpy())
+        err = max(err, float(np.linalg.norm(out[b].cpu().numpy() - ref) / np.linalg.norm(ref)))
+    return err
 
 
 def bench_end_to_end(bs, E, c, H, h, x0, ws0, out, dev, dist, local, steps=3, warmup=1, host_batch=256):
@@ -682,6 +767,7 @@ def main():
     bs.set_model(E, c, H, h)
     # the handle holds its own copy; a sub-batch is kept for the host-memory (PCIe) line
     Hk = H[:256].clone() if not args.no_secondary else None
+    Hk_full_sample = {b: H[b].cpu().numpy() for b in (0, B // 2, B - 1)}  # the oracle check's problems
     del H
     bs.update_problem_data(ws0, sigma=1e-6)
     bs.synchronize()
@@ -713,8 +799,15 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     st = bs.status()
+    # outside the timed region: the timed batch's output is finite and agrees
+    # with the CPU oracle on sampled problems (a wrong-but-finite answer would
+    # pass the status flags alone)
+    finite = bool(torch.isfinite(out).all().item())
+    oracle_err = headline_oracle_err(E, c, Hk_full_sample, h, x0, out, n, m, N, (0, B // 2, B - 1))
+    status_ok = bool(np.all(st == 0)) and finite and oracle_err < 1e-9
     if dist:
         el = _max_over_ranks(dist, el, dev)
+        status_ok = _max_over_ranks(dist, 0.0 if status_ok else 1.0, dev) == 0.0  # every rank's batch
     ms_bwd = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     ms_fwd = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     stages = N * B
@@ -747,8 +840,19 @@ def main():
                      "bytes_per_stage_algorithmic": bytes_bwd_stage, "ms_per_launch": ms_bwd},
         "kernels_ms": {"backward": ms_bwd, "forward": ms_fwd},
         "solve_hbm_frac": bytes_stage * stages / ((ms_bwd + ms_fwd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        "status_ok": bool(np.all(st == 0)),
+        "status_ok": status_ok,
+        "checks": {"factor_status_clean": bool(np.all(st == 0)), "finite": finite,
+                   "oracle_rel_err_sampled": oracle_err, "sampled_problems": [0, B // 2, B - 1],
+                   "all_ranks": bool(dist)},
     }
+    if pmc:
+        # bytes the kernel actually moves (counter bytes of the committed profile
+        # of this workload) over the same time: the value-form backward reads
+        # the PACKED H~ that update_problem_data writes (136 of 256 doubles at
+        # 12/4), so it moves fewer bytes than the 3,808 B algorithmic figure and
+        # `frac_of_measured_copy` (algorithmic bytes) can exceed 1
+        res["roofline"]["frac_moved"] = pmc["bytes_per_launch"] / (ms_bwd * 1e-3) / 1e9 / HBM_PEAK_GBS
+        res["roofline"]["traffic_source"] = "committed PMC summary (profiles/), same workload and kernel; not this run"
     copy_gbs = measured_copy_gbs(dev)
     res["roofline"]["peak_measured_copy"] = copy_gbs
     res["roofline"]["frac_of_measured_copy"] = achieved / copy_gbs
@@ -781,9 +885,11 @@ def main():
     if dist:
         dist.destroy_process_group()
     if not res["status_ok"]:
-        # a solve that flagged a failed factorisation on the timed batch does
-        # not back its number: report it, then fail the run
-        print("bench: status_ok is false (non-SPD pivot or non-finite value on the timed batch)", file=sys.stderr)
+        # a solve that flagged a failed factorisation, a non-finite output or an
+        # oracle mismatch on any rank's timed batch does not back its number:
+        # report it, then fail the run
+        print("bench: status_ok is false (factor status, finiteness or oracle check on the timed batch)",
+              file=sys.stderr)
         sys.exit(3)
 
 

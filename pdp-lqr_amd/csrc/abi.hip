@@ -258,6 +258,10 @@ int pdplqr_set_model(pdplqr_handle h, const double *E, const double *c, const do
     const Shape &sh = h->sh;
     const long long B = sh.batch;
     const hipMemcpyKind kind = mem == PDPLQR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (h->cfg.solver == PDPLQR_SOLVER_KKT) {
+        const int rc = kkt_before_model(h);
+        if (rc) return rc;
+    }
     PDPLQR_HIP_TRY(hipMemcpyAsync(h->E, E, B * sh.perE * sizeof(double), kind, h->stream));
     PDPLQR_HIP_TRY(hipMemcpyAsync(h->c, c, B * sh.perc * sizeof(double), kind, h->stream));
     PDPLQR_HIP_TRY(hipMemcpyAsync(h->H, H, B * sh.perH * sizeof(double), kind, h->stream));

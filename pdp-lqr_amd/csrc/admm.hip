@@ -457,7 +457,9 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             if ((rc = solver_update(h, s->w, s->y, s->z, irho_or_null, st->sigma))) return rc;
             h->updated = true;
         }
-        if (refactor) {
+        // the Riccati-ordered KKT path folds the right-hand side into its
+        // elimination (kkt_riccati.hip): it re-runs the backward on every rhs
+        if (refactor || (kkt && kkt_ric_active(h))) {
             if ((rc = solver_backward(h, kkt ? s->irho : s->rho))) return rc;
             h->factored = true;
             refactor = false;

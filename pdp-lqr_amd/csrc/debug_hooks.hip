@@ -1,6 +1,7 @@
 // debug_hooks.hip -- test-only entry points (not part of include/pdplqr.h):
 // device kernels exercised directly by the GPU unit tests
 // (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
+#include "combine_mw.hpp"
 #include "combine_tiles.hpp"
 
 // out = a (x) b on the device (one wave), elements in host memory; LU: the
@@ -29,6 +30,43 @@ extern "C" int pdplqr_debug_combine_form(int n, const double *a, const double *b
     else if (T == 1) hipLaunchKernelGGL((k_debug_combine<1, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     else if (lu) hipLaunchKernelGGL((k_debug_combine<2, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     else hipLaunchKernelGGL((k_debug_combine<2, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    (void)hipFree(dok);
+    return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
+}
+
+// the 4-wave combine of the horizon scan (combine_mw.hpp); fcf = 0: only P, p
+template <int T>
+__global__ __launch_bounds__(256) void k_debug_combine_mw(const double *a, const double *b, double *out, int n, int fcf,
+                                                          int *ok) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const pdplqr::MwSmem sm = pdplqr::mw_smem(mwbuf, n);
+    const int nn = n * n;
+    const bool good = pdplqr::mw_combine<T>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n,
+                                            pdplqr::elem_in(a, n), pdplqr::elem_in(b, n), n, fcf != 0, sm);
+    if (threadIdx.x == 0) *ok = good ? 1 : 0;
+}
+
+extern "C" int pdplqr_debug_combine_mw(int n, const double *a, const double *b, double *out, int fcf) {
+    using namespace pdplqr;
+    const int T = n <= 16 ? 1 : (n <= 32 ? 2 : 0);
+    if (!T) return PDPLQR_ERR_UNSUPPORTED;
+    const size_t es = (size_t)(3 * n * n + 2 * n) * sizeof(double);
+    double *d = nullptr;
+    int *dok = nullptr, okh = 0;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 3 * es));
+    PDPLQR_HIP_TRY(hipMalloc(&dok, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, a, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + 2 * es, out, es, hipMemcpyHostToDevice));  // untouched blocks kept
+    const double *da = d, *db = (const double *)((char *)d + es);
+    double *dout = (double *)((char *)d + 2 * es);
+    const size_t sm = mw_smem_bytes(n);
+    if (T == 1) hipLaunchKernelGGL(k_debug_combine_mw<1>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
+    else hipLaunchKernelGGL(k_debug_combine_mw<2>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
     PDPLQR_HIP_TRY(hipDeviceSynchronize());
     PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
     PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));

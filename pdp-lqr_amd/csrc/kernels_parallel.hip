@@ -25,6 +25,7 @@
 //   * the rollout reuses k_riccati_fwd with the G_k u_hat coupling
 //     (lqr_kernel_parallel.hpp:195-198), u_hat from lambda_{i+1}.
 #define PDPLQR_COMB_PROFILE_TU 1  // the combine phase marks live in this translation unit
+#include "combine_mw.hpp"
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
@@ -319,6 +320,34 @@ __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
     if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
 }
 
+// One Hillis-Steele round with the 4-wave combine (combine_mw.hpp; CHOLESKY
+// form): the same operands, output and terminal rule as k_seg_scan.
+template <int T>
+__global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = A.n, S = A.S, d = A.dist;
+    const int es = 3 * n * n + 2 * n, nn = n * n;
+    const long long b = blockIdx.x / S;
+    const int i = blockIdx.x % S;
+    const long long is = A.istride ? A.istride : es;
+    const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
+    double *out = A.out + b * (long long)S * es;
+    if (i + d >= S) {  // block-uniform
+        if (wv == 0) elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
+        return;
+    }
+    const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    const MwSmem sm = mw_smem(mwbuf, n);
+    double *o = out + (long long)i * es;
+    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n,
+                                  elem_in(in + (long long)i * is, n), elem_in(in + (long long)(i + d) * is, n), n, fcf,
+                                  sm);
+    if (!fcf && wv == 1)
+        for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
+    if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
+}
+
 // ---------------------------------------------------------------------------
 // Boundary maps.  With the value function V_j = (P_j, p_j) at boundary j (the
 // suffix-scan entry j, right-folded with the global suffix of later shards),
@@ -509,13 +538,27 @@ __global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
     wv_store(pacc, out + (long long)j * mw + nn, n, g, c);
 }
 
-// Resident scan waves (one combine each) the device holds for this shape.
+static int tile_order(int n);
+
+// the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
+// one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
+bool seg_scan_mw(int n, bool lu) {
+    if (lu || getenv("PDPLQR_SCAN_1WAVE")) return false;
+    return tile_order(n) == 2 || (tile_order(n) == 1 && getenv("PDPLQR_SCAN_MW"));
+}
+
+// Resident scan combines the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const size_t smem = op_stage_bytes(sh.n);
-    hipError_t e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1, false>, 64, smem)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2, false>, 64, smem);
+    hipError_t e;
+    if (seg_scan_mw(sh.n, false))
+        e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<1>, 256, mw_smem_bytes(sh.n))
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<2>, 256, mw_smem_bytes(sh.n));
+    else
+        e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1, false>, 64, smem)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2, false>, 64, smem);
     if (e != hipSuccess || per <= 0) per = 1;
     return cus * per;
 }
@@ -545,6 +588,13 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
+    if (seg_scan_mw(a.n, a.lu)) {
+        const size_t sm = mw_smem_bytes(a.n);
+        if (T == 1) hipLaunchKernelGGL(k_seg_scan_mw<1>, grid, dim3(256), sm, st, a);
+        else hipLaunchKernelGGL(k_seg_scan_mw<2>, grid, dim3(256), sm, st, a);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_scan<1, true>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_scan<1, false>), grid, blk, smem, st, a);
     else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_scan<2, true>), grid, blk, smem, st, a);

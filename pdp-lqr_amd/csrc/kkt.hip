@@ -1313,6 +1313,12 @@ struct KKTState {
     double *bvec = nullptr;  // P = 16: forward-substitution right-hand sides [b][N+1][16]
     double *ppk = nullptr;   // P = 16: H^{-1} (packed) and G^T per stage [b][N+1][2][256]
     bool formed = false;
+    // Riccati-ordered elimination (kkt_riccati.hip): the uniform row count nc,
+    // or -1 where the block LDL^T kernels below run
+    int ric = -1;
+    double *rec = nullptr;    // rollout records [b][N][FS]
+    double *x0acc = nullptr;  // sum of the x0s since update_problem_data [b][n]
+    double *Ef = nullptr, *Df = nullptr;  // frozen E, D once set_model re-runs (else the model's)
 };
 
 template <typename X>
@@ -1383,6 +1389,14 @@ int kkt_init(pdplqr_handle h) {
         dmax = std::max(dmax, ks->gdim[k]);
     }
     ks->dim = dof;
+    const long long B = sh.batch, PP = (long long)ks->P * ks->P;
+    int rc;
+    ks->ric = kkt_ric_nc(sh, h->ncs);
+    if (ks->ric >= 0) {  // Riccati-ordered path: no tile buffers
+        if ((rc = kalloc(h, &ks->rec, B * kkt_ric_rec_doubles(sh))) || (rc = kalloc(h, &ks->x0acc, B * n))) return rc;
+        PDPLQR_HIP_TRY(hipMemset(ks->x0acc, 0, B * n * sizeof(double)));
+        return PDPLQR_OK;
+    }
     if (dmax > 32) {
         set_error("KKT solver with n + m > 32 or n + nc > 32 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
@@ -1401,8 +1415,6 @@ int kkt_init(pdplqr_handle h) {
             for (int q = 0; q < h->ncs[k]; ++q) rows[base + n + q] = make_int4(1, k, q, 0);
         }
     }
-    const long long B = sh.batch, PP = (long long)ks->P * ks->P;
-    int rc;
     if ((rc = kalloc(h, &ks->d_prim_off, N + 1)) || (rc = kalloc(h, &ks->d_prim_dim, N + 1)) ||
         (rc = kalloc(h, &ks->d_dual_off, N + 1)) || (rc = kalloc(h, &ks->d_gdim, N + 1)) ||
         (rc = kalloc(h, &ks->d_ncs, N + 1)) || (rc = kalloc(h, &ks->rows, ks->dim)) || (rc = kalloc(h, &ks->pstat, B)) ||
@@ -1434,6 +1446,16 @@ int kkt_on_model(pdplqr_handle h) {
     KKTState *ks = h->kkt;
     if (ks->formed) return PDPLQR_OK;
     const Shape &sh = h->sh;
+    if (ks->ric >= 0) {  // H + sigma_f I, packed: the matrix part that is formed once
+        Shape hs = sh;
+        hs.perh = 0;  // only the H~ part of the update kernel
+        hs.ny = 0;
+        const int rc = launch_update_problem_data(hs, h->H, h->h, nullptr, nullptr, nullptr, nullptr, h->cfg.kkt_sigma,
+                                                  h->Hw, h->hw, h->gw, h->tab_s, h->tab_n, h->stream, false);
+        if (rc) return rc;
+        ks->formed = true;
+        return PDPLQR_OK;
+    }
     KKTArgs a = kkt_args(h);
     const size_t smem = 4 * (size_t)ks->P * ks->P * sizeof(double);
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), wave(64);
@@ -1449,10 +1471,38 @@ int kkt_on_model(pdplqr_handle h) {
     return PDPLQR_OK;
 }
 
+// A later set_model keeps the matrix frozen (qdldl_solver.hpp:36-45 forms it in
+// the constructor only): the Riccati path snapshots E and D once, before the
+// first overwrite (H + sigma_f I already lives in Hw).  The right-hand side
+// keeps reading the current model (form_rhs re-reads model_, kkt.hpp:224-300).
+// Deviation: the x0 terms of update_rhs_initial_stage use the CURRENT S0, A0 in
+// the reference, the frozen ones here.
+int kkt_before_model(pdplqr_handle h) {
+    KKTState *ks = h->kkt;
+    if (!ks || ks->ric < 0 || !ks->formed || ks->Ef) return PDPLQR_OK;
+    const Shape &sh = h->sh;
+    int rc;
+    if ((rc = kalloc(h, &ks->Ef, sh.batch * sh.perE)) ||
+        (sh.ndD > 0 && (rc = kalloc(h, &ks->Df, sh.batch * (long long)sh.ndD))))
+        return rc;
+    PDPLQR_HIP_TRY(hipMemcpyAsync(ks->Ef, h->E, sh.batch * sh.perE * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    if (sh.ndD > 0)
+        PDPLQR_HIP_TRY(hipMemcpyAsync(ks->Df, h->D, sh.batch * (long long)sh.ndD * sizeof(double),
+                                      hipMemcpyDeviceToDevice, h->stream));
+    return PDPLQR_OK;
+}
+
 int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
                double sigma) {
     KKTState *ks = h->kkt;
     const Shape &sh = h->sh;
+    if (ks->ric >= 0) {  // h - sigma w, z - inv_rho o y; the x0 sum restarts
+        const int rc = launch_update_problem_data(sh, h->H, h->h, ws, ys, zs, irho, sigma, h->Hw, h->hw, h->gw,
+                                                  h->tab_s, h->tab_n, h->stream, true);
+        if (rc) return rc;
+        PDPLQR_HIP_TRY(hipMemsetAsync(ks->x0acc, 0, sh.batch * sh.n * sizeof(double), h->stream));
+        return PDPLQR_OK;
+    }
     KKTArgs a = kkt_args(h);
     const long long total = (long long)ks->dim * sh.batch;
     const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
@@ -1464,6 +1514,14 @@ int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double
 int kkt_backward(pdplqr_handle h, const double *inv_rho) {
     KKTState *ks = h->kkt;
     const Shape &sh = h->sh;
+    if (ks->ric >= 0) {
+        const int rc = launch_kkt_ric_backward(sh, ks->ric, ks->Ef ? ks->Ef : h->E, h->c, ks->Df ? ks->Df : h->D, h->Hw,
+                                               h->hw, h->gw, inv_rho, h->d_off, h->y_off, h->ncs[sh.N], h->cfg.rho_dyn,
+                                               ks->rec, h->status, h->stream);
+        if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
+        set_error("KKT backward: unaligned buffers for the Riccati-ordered path");
+        return rc;
+    }
     KKTArgs a = kkt_args(h);
     const size_t smem = 3 * (size_t)ks->P * ks->P * sizeof(double);
     if (ks->P == 16) {
@@ -1484,6 +1542,9 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     KKTState *ks = h->kkt;
     const Shape &sh = h->sh;
+    if (ks->ric >= 0)
+        return launch_kkt_ric_forward(sh, ks->Ef ? ks->Ef : h->E, h->c, ks->rec, x0, ks->x0acc, ws, h->cfg.rho_dyn,
+                                      h->stream);
     KKTArgs a = kkt_args(h);
     const size_t P = ks->P, PP = P * P;
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
@@ -1507,5 +1568,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
 }
 
 int kkt_dim(pdplqr_handle h) { return h->kkt ? h->kkt->dim : 0; }
+
+bool kkt_ric_active(pdplqr_handle h) { return h->kkt && h->kkt->ric >= 0; }
 
 }  // namespace pdplqr

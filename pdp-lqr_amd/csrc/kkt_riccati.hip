@@ -1,0 +1,500 @@
+// kkt_riccati.hip -- QDLDLSolver's KKT system (kkt.hpp:124-300) eliminated in
+// REVERSE stage order: a Riccati-ordered block LDL^T of the same matrix, with
+// its frozen regularisation carried exactly.
+//
+// The reference assembles (kkt.hpp:124-205, qdldl_solver.hpp:36-45)
+//     [ H_k + sigma_f I   C^T        ]   sigma_f = kkt_sigma (1e-6, frozen),
+//     [ C                -Reg        ]   Reg = rho_dyn I on every lambda_k,
+//                                              diag(inv_rho) on every y_k
+// and factors it with QDLDL in natural order (primal pivots first).  The
+// solution of a nonsingular quasi-definite system does not depend on the
+// elimination order, so eliminating it stage by stage from the END gives the
+// same (w, y, lambda) to rounding, and each step is a value-function update:
+//   * y_k (row D_k w_k - inv_rho y_k = g_k, g = z - inv_rho o y_in):
+//       y_k = rho (D_k w_k - g_k)  ->  H~ += D^T rho D,  h~ -= D^T rho g
+//     (rho = 1 / inv_rho of backward(), g from update_problem_data: exactly the
+//      Riccati solvers' penalty, lqr_kernel.hpp:106-112; stage 0 keeps only the
+//      u columns of D_0, as the KKT drops D_x0 x0, kkt.hpp:218-221);
+//   * lambda_{k+1} (row E_k w_k + c_k - x_{k+1} - rho_dyn lambda_{k+1} = 0):
+//       eliminating lambda and x_{k+1} against the value function V_{k+1} =
+//       (P, p) leaves the Moreau envelope of V_{k+1} at v = E_k w_k + c_k,
+//         P~ = (P^{-1} + rho_dyn I)^{-1} = P (I + rho_dyn P)^{-1},
+//         p~ = (I + rho_dyn P)^{-1} p,
+//       and the minimiser x_{k+1} = v - rho_dyn (P~ v + p~)  (the costate
+//       lambda_{k+1} = P~ v + p~);
+//   * (u_k, x_k): the value-form stage of kernels_schur.hip on
+//       M_k = H~_k + E~^T P~ E~ (+ D^T rho D),  lp = h~ + E^T (P~ c + p~).
+// P~ is formed by the Neumann series P~ = sum_j (-rho_dyn P)^j P, one MFMA
+// product per term (A operand = P's own registers, B = the previous term), with
+// as many terms as the trace bound e = rho_dyn tr(P) >= rho_dyn ||P|| asks:
+// terms until e^{J+1} <= 1e-16 (rho_dyn = 1e-6 and ||P|| ~ 10..100: 2 or 3).
+// p~ never appears alone: lp = h~ + G^T (c - rho_dyn p) + E~^T p with
+// G = P~ E~, and the forward uses x+ = v - rho_dyn (P~ (v - rho_dyn p) + p).
+//
+// Per stage this reads E, c, h~, packed H~ = H + sigma_f I, D, inv_rho, g
+// (428 doubles at 12/4 with 4 rows) once and writes the rollout record
+// [K~ | k~ | p_{k+1} | P~_{k+1} (fp32)] -- against the natural-order path's
+// once-per-model H^{-1} / G tiles and its three solve phases over explicit
+// fp64 tiles (kkt.hip).  P~ is stored in fp32: it only enters
+// rho_dyn P~ v, a 1e-6-relative correction of the state, so its 6e-8 rounding
+// is ~1e-13 of x.
+//
+// update_rhs_initial_stage ACCUMULATES -S0 x0 and -A0 x0 into the right-hand
+// side on every forward (kkt.hpp:207-222): the solve then uses the sum of every
+// x0 passed since the last update_problem_data (x0acc here), while ws[0]'s x
+// part is the x0 of the call (qdldl_solver.hpp:129-131).
+#include "schur_stage.hpp"
+#include "solvers.hpp"
+
+#include <stdint.h>
+#include <stdlib.h>
+
+namespace pdplqr {
+
+struct KKTRicArgs {
+    Shape sh;
+    const double *E, *c, *D;  // model
+    const double *Hw, *hw;    // H + sigma_f I (packed), h - sigma w
+    const double *gw;         // z - inv_rho o y (update_problem_data)
+    const double *irho;       // backward's inv_rho
+    const int32_t *d_off, *y_off;
+    double *rec;              // [b][N][KKT_FS] rollout records
+    int32_t *status;
+    double rho_dyn;
+    int nc_last;              // constraint rows of the terminal stage
+};
+
+// record per stage: K~ (m x n row-major) | k~ (m) | p_{k+1} (n) | P~_{k+1} fp32
+// (float3 per lane (g, c >= m): P~[4 + g][c], P~[8 + g][c], P~[12 + g][c])
+template <int NN, int MM>
+struct KRecShape {
+    static constexpr int n = NN, m = MM, s = NN + MM;
+    static constexpr int OK = 0, OKQ = n * m, OPV = OKQ + m, OPT = OPV + n;
+    static constexpr int PTF = 3 * 4 * n;             // floats of P~ (48 lanes x 3)
+    static constexpr int FS = OPT + (PTF + 1) / 2;    // doubles per stage
+};
+
+// Stage record streamed by the backward: E | c | h~ | packed H~ | D | inv_rho | g
+template <int NN, int MM, int NC>
+struct KBwdShape {
+    static constexpr int n = NN, m = MM, s = NN + MM, nc = NC;
+    static constexpr int ps = s * (s + 1) / 2;
+    static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, OD = OP + ps, OI = OD + nc * s,
+                         OG = OI + nc, Q = OG + nc;
+    static constexpr int CH = Q / 2, NI = (CH + 63) / 64, SLOT = NI * 128;
+    static_assert(Q % 2 == 0 && OC % 2 == 0 && OH % 2 == 0 && OP % 2 == 0 && OD % 2 == 0 && OI % 2 == 0, "chunks");
+};
+
+// sum of a value over the whole wave (every lane gets it)
+__device__ __forceinline__ double wave_sum(double v) { return sum_groups(sum_row16(v)); }
+
+template <int NC>
+__global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
+    constexpr int NN = 12, MM = 4;
+    using SH = KBwdShape<NN, MM, NC>;
+    using RS = KRecShape<NN, MM>;
+    constexpr int NI = SH::NI, n = NN, m = MM, s = NN + MM;
+    constexpr int ST = 3;  // record stores per stage: [K~ | k~], p_{k+1}, P~_{k+1}
+    __shared__ SchurSmem sm;
+    __shared__ __attribute__((aligned(16))) double stg[2][SH::SLOT];
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const Shape &sh = A.sh;
+    const int N = sh.N;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    const double *Db = A.D + b * (long long)sh.ndD;
+    const double *gb = A.gw + b * (long long)sh.ny;
+    const double *ib = A.irho + b * (long long)sh.ny;
+    double *RB = A.rec + b * (long long)N * RS::FS;
+    const double rd = A.rho_dyn;
+    int fail_stage = -1;
+
+    // ---- terminal: P_N = H~_N + D_N^T rho D_N, p_N = h~_N - D_N^T rho g_N ----
+    d4 Pm;
+    double prow[4];
+    {
+        d4 Mt[1][1];
+        load_M<1>(Mt, Hb + (long long)N * sh.ps, n, m, m, s, g, c);
+        Pm = Mt[0][0];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            prow[r] = i >= m ? hb[(long long)N * s + (i - m)] : 0.0;
+        }
+        const int ncN = A.nc_last;
+        if (ncN > 0) {  // rare: plain loops (nc_N <= 4, D_N is nc_N x n)
+            const double *DN = Db + A.d_off[N];
+            const double *gN = gb + A.y_off[N], *iN = ib + A.y_off[N];
+            for (int q = 0; q < ncN; ++q) {
+                const double rq = 1.0 / iN[q], gq = gN[q];
+                const double dc = c >= m ? DN[q + (c - m) * ncN] : 0.0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 4 * r + g;
+                    const double di = i >= m ? DN[q + (i - m) * ncN] : 0.0;
+                    Pm[r] = __builtin_fma(di * rq, dc, Pm[r]);
+                    prow[r] = __builtin_fma(-di * rq, gq, prow[r]);
+                }
+            }
+        }
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            if (i == c && i >= m && psd_bad(Pm[r])) bad = true;
+        }
+        if (__any(bad)) fail_stage = N;
+    }
+
+    // ---- stage records: HBM -> registers (two sets in flight) -> LDS, as the
+    // 12/4 value-form backward (kernels_schur.hip) ----
+    d2v RA[NI], RB2[NI];
+    const double *gbase[NI];
+    int gstride[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+        int ch = q * 64 + lane;
+        ch = ch < SH::CH ? ch : SH::CH - 1;
+        const int d = 2 * ch;
+        gbase[q] = d < SH::OC   ? Eb + d
+                   : d < SH::OH ? cb + (d - SH::OC)
+                   : d < SH::OP ? hb + (d - SH::OH)
+                   : d < SH::OD ? Hb + (d - SH::OP)
+                   : d < SH::OI ? Db + (d - SH::OD)
+                   : d < SH::OG ? ib + (d - SH::OI)
+                                : gb + (d - SH::OG);
+        gstride[q] = d < SH::OC ? n * s : d < SH::OH ? n : d < SH::OP ? s : d < SH::OD ? sh.ps : d < SH::OI ? NC * s : NC;
+    }
+    auto gload = [&](d2v(&R)[NI], int k) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            const double *src = gbase[q] + (long long)k * gstride[q];
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[q]) : "v"(src) : "memory");
+        }
+    };
+    // "set X has landed": the younger vm ops are the other set's NI loads and
+    // two steps' ST stores (steady state), one step's stores (first step)
+    auto vwait_steady = [&](d2v(&R)[NI]) {
+        if constexpr (NI == 4)
+            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) : "n"(NI + 2 * ST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%3)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]) : "n"(NI + 2 * ST) : "memory");
+    };
+    auto vwait_first = [&](d2v(&R)[NI]) {
+        if constexpr (NI == 4)
+            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) : "n"(NI + ST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%3)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]) : "n"(NI + ST) : "memory");
+    };
+    auto vwait0 = [&](d2v(&R)[NI]) {
+        if constexpr (NI == 4)
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3])::"memory");
+        else asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+    };
+    auto lput = [&](const d2v(&R)[NI], int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) *reinterpret_cast<d2v *>(&stg[slot][2 * (q * 64 + lane)]) = R[q];
+    };
+
+    auto process = [&](int k, bool sym) {
+        const double *R = stg[k & 1];
+        double *Rk = RB + (long long)k * RS::FS;
+        SchurIn in;
+        schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c, n);
+        // ---- the lambda_{k+1} elimination: P~ = sum_j (-rho_dyn P)^j P ----
+        const double diag = [&] {
+            double d = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d = (4 * r + g == c && c >= m) ? Pm[r] : d;
+            return wave_sum(d);
+        }();
+        const double e = rd * fabs(diag);
+        d4 Pt = Pm, T = Pm;
+        {
+            d4 Pneg;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
+            double ej = e;
+            for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // wave-uniform
+                d4 Tn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 1; kk < 4; ++kk) Tn = mfma_f64(Pneg[kk], T[kk], Tn);  // (-rho_dyn P) T (x rows)
+                T = Tn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Pt[r] += T[r];
+                ej *= e;
+            }
+        }
+        // ---- record part 1: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]) and P~_{k+1} ----
+        {
+            // every lane stores (duplicates carry the same value): one store
+            // instruction per part, no exec-mask branch
+            const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
+            // (a select chain on cp became a dynamically indexed private array)
+            const double pv = __builtin_fma(prow[1], (double)(cp == 1), __builtin_fma(prow[2], (double)(cp == 2),
+                                                                                       prow[3] * (double)(cp == 3)));
+            gstore(Rk + RS::OPV + (4 * cp + g - m), pv);
+            // P~ (fp32): lanes c >= m only -- lanes c < m hold u-column values
+            if (c >= m) {
+                float *dst = reinterpret_cast<float *>(Rk + RS::OPT) + 3 * (12 * g + (c - m));
+                typedef float f3v __attribute__((ext_vector_type(3)));
+                *(__attribute__((address_space(1))) f3v *)dst = f3v{(float)Pt[1], (float)Pt[2], (float)Pt[3]};
+            }
+        }
+        // ---- G = P~ E~, M = H~ + E~^T G + D^T rho D ----
+        d4 G = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 1; kk < 4; ++kk) G = mfma_f64(Pt[kk], in.E[kk], G);
+        d4 Mn = in.H;
+#pragma unroll
+        for (int kk = 1; kk < 4; ++kk) Mn = mfma_f64(in.E[kk], G[kk], Mn);
+        double part = 0.0;
+        if constexpr (NC > 0) {
+            // lane (g, c): D[g][c] (rows g < NC); stage 0 keeps only the u columns
+            const bool dv = g < NC && (k > 0 || c < m);
+            const double dgc = dv ? R[SH::OD + (g < NC ? g : 0) + c * NC] : 0.0;
+            const double rq = (g < NC) ? rcp_f64(R[SH::OI + (g < NC ? g : 0)]) : 0.0;
+            const double gq = (g < NC) ? R[SH::OG + (g < NC ? g : 0)] : 0.0;
+            Mn = mfma_f64(dgc, rq * dgc, Mn);      // D^T diag(rho) D
+            part = -dgc * rq * gq;                 // -(D^T rho g)[c]
+        }
+#pragma unroll
+        for (int kk = 1; kk < 4; ++kk) {
+            part = __builtin_fma(G[kk], __builtin_fma(-rd, prow[kk], in.ct[kk]), part);  // G^T (c - rho_dyn p)
+            part = __builtin_fma(in.E[kk], prow[kk], part);                             // E~^T p
+        }
+        part = sum_groups(part);
+        sm.lpt[colpos<1>(c)] = in.h + part;
+        wave_sync();
+        double lpr[4];
+        {
+            const double2 *q = reinterpret_cast<const double2 *>(sm.lpt + 4 * g);
+            const double2 a = q[0], bb = q[1];
+            lpr[0] = a.x;
+            lpr[1] = a.y;
+            lpr[2] = bb.x;
+            lpr[3] = bb.y;
+        }
+        double w, luq[4];
+        GainOut go;
+        bool ok = schur_block_pivots<MM, true>(Mn, lpr, w, luq, g, c, &go);
+        Pm = Mn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) prow[r] = lpr[r];
+        if (sym) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm.tp[(4 * r + g) * PDPLQR_TP_LD + c] = Pm[r];
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pm[r] = 0.5 * (Pm[r] + sm.tp[c * PDPLQR_TP_LD + 4 * r + g]);
+        }
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            if (i == c && i >= m && psd_bad(Pm[r])) bad = true;
+        }
+        ok = (int)ok & (int)!__any(bad);
+        fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
+        schur_store_record_gain<MM, s>(Rk, go, g, c);  // [K~ | k~]
+        wave_sync();  // stage k's LDS reads retire before slot reuse
+    };
+    auto step = [&](int k, d2v(&X)[NI], bool first, bool sym) {
+        process(k, sym);
+        if (first) vwait_first(X);
+        else vwait_steady(X);
+        if (k >= 1) lput(X, (k - 1) & 1);
+        gload(X, k >= 3 ? k - 3 : 0);
+        wave_sync();
+    };
+    auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+    gload(RA, N - 1);
+    vwait0(RA);
+    lput(RA, (N - 1) & 1);
+    gload(RA, N >= 2 ? N - 2 : 0);
+    gload(RB2, N >= 3 ? N - 3 : 0);
+    wave_sync();
+    step(N - 1, RA, true, true);
+    if (N < 3) drain();
+    int k = N - 2;
+    for (; k >= 1; k -= 2) {
+        step(k, RB2, false, ((N - 2 - k) & 2) == 0);
+        step(k - 1, RA, false, false);
+        if (k < 3) drain();
+    }
+    if (k == 0) process(0, true);
+    if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+// ---------------------------------------------------------------------------
+// forward: the gain-form rollout of kernels_rollout.hip plus the lambda
+// correction x+ = v - rho_dyn (P~ (v - rho_dyn p) + p), v = A x + B u + c.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
+                                                    const double *__restrict__ c, const double *__restrict__ FR,
+                                                    const double *__restrict__ x0, double *__restrict__ x0acc,
+                                                    double *__restrict__ ws, double rho_dyn) {
+    constexpr int n = 12, m = 4, s = 16;
+    using RS = KRecShape<n, m>;
+    constexpr int FS = RS::FS;
+    constexpr int OE = 0, OC = n * s, OF = OC + n, REC = OF + FS, CH = REC / 2, NI = (CH + 63) / 64;
+    constexpr int TAIL = CH - (NI - 1) * 64;
+    constexpr int NQ = 3;
+    static_assert(REC % 2 == 0 && NI == 3, "record layout");
+    __shared__ __attribute__((aligned(16))) double ring[D][REC];
+    __shared__ double sx[16], sz[16], sx0[16];
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
+    const long long b = blockIdx.x;
+    const int N = sh.N;
+    const double *Eb = E + b * sh.perE;
+    const double *cb = c + b * sh.perc;
+    const double *Fb = FR + b * (long long)N * FS;
+    double *wb = ws + b * sh.perh;
+
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            if (q < NI - 1 || lane < TAIL) {
+                const int d = 2 * (q * 64 + lane);
+                const double *src = d < OC   ? Eb + (long long)k * (n * s) + d
+                                    : d < OF ? cb + (long long)k * n + (d - OC)
+                                             : Fb + (long long)k * FS + (d - OF);
+                dma16(src, &ring[slot][q * 128]);
+            }
+        }
+    };
+
+    // update_rhs_initial_stage accumulates: the solve sees the sum of the x0s
+    double x0own = 0.0;
+    if (lane < n) {
+        x0own = x0[b * n + lane];
+        const double xa = x0acc[b * n + lane] + x0own;
+        x0acc[b * n + lane] = xa;
+        sx[lane] = xa;
+        sx0[lane] = x0own;
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) dma(j < N ? j : N - 1, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+
+    for (int k = 0; k < N; ++k) {
+        const int kp = k + D - 1;
+        dma(kp < N ? kp : N - 1, kp % D);
+        if (k < D - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NI + 1) * (D - 1)) : "memory");
+        const double *R = ring[k % D];
+        const double *F = R + OF;
+        const int cm = cl < m ? cl : m - 1, cn = cl < n ? cl : n - 1;
+        const double g0 = (g == 0) ? 1.0 : 0.0;
+        double kx[NQ], ex[NQ], eu[m], xt[NQ];
+        float pt[NQ];
+        {
+            const float *P3 = reinterpret_cast<const float *>(F + RS::OPT) + 3 * (12 * g + cn);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int t = 4 * q + g;
+                kx[q] = F[RS::OK + cm * n + t];
+                ex[q] = R[OE + (m + t) * n + cn];
+                pt[q] = P3[q];  // P~[4 q + g][cl] (= P~[cl][4 q + g])
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < m; ++i) eu[i] = g0 * R[OE + i * n + cn];
+        const double kq = F[RS::OKQ + cm];
+        const double cc = R[OC + cn];
+        const double pv = F[RS::OPV + cn];
+        // ---- chain ----
+        const int lx = (lane >= m && lane < s) ? lane - m : 0;
+        const double xk = k == 0 ? sx0[lx] : sx[lx];  // ws[0]'s x part is the call's x0
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) xt[q] = sx[4 * q + g];
+        double v = 0.0, a = 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            v = __builtin_fma(kx[q], xt[q], v);
+            a = __builtin_fma(ex[q], xt[q], a);
+        }
+        v = sum_groups(v) + kq;
+        double myu = 0.0;
+#pragma unroll
+        for (int i = 0; i < m; ++i) {
+            const double ui = readlane_f64(-v, i);  // u = -(k~ + K~ x)
+            if (cl == i) myu = ui;
+            a = __builtin_fma(eu[i], ui, a);
+        }
+        a = sum_groups(a) + cc;  // v = A x + B u + c (every group)
+        if (lane < s) gstore(wb + (long long)k * s + lane, (lane < m) ? myu : xk);
+        // ---- lambda correction: x+ = v - rho_dyn (P~ (v - rho_dyn p) + p) ----
+        if (g == 0 && cl < n) sz[cl] = __builtin_fma(-rho_dyn, pv, a);
+        wave_sync();
+        double y = 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) y = __builtin_fma((double)pt[q], sz[4 * q + g], y);
+        y = sum_groups(y);
+        const double xn = __builtin_fma(-rho_dyn, y + pv, a);
+        wave_sync();  // all reads of x_k done before it is overwritten
+        if (g == 0 && cl < n) sx[cl] = xn;
+        wave_sync();
+    }
+    if (lane < n) wb[(long long)N * s + lane] = sx[lane];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static bool kric_al(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// The Riccati-ordered KKT path applies: 12/4, the same row count nc in {0, 4}
+// on every stage k < N (nc_N <= 4), 16-byte aligned per-problem blocks.
+int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs) {
+    if (sh.n != 12 || sh.m != 4 || getenv("PDPLQR_KKT_LDL")) return -1;
+    const int nc = ncs[0];
+    if (nc != 0 && nc != 4) return -1;
+    for (int k = 0; k < sh.N; ++k)
+        if (ncs[k] != nc) return -1;
+    if (ncs[sh.N] > 4) return -1;
+    if (sh.perE % 2 || sh.perc % 2 || sh.perHw % 2 || sh.perh % 2 || (nc && (sh.ny % 2 || sh.ndD % 2))) return -1;
+    return nc;
+}
+
+size_t kkt_ric_rec_doubles(const Shape &sh) { return (size_t)sh.N * KRecShape<12, 4>::FS; }
+
+int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
+                            const double *Hw, const double *hw, const double *gw, const double *irho,
+                            const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
+                            int32_t *status, hipStream_t st) {
+    if (!kric_al(E) || !kric_al(c) || !kric_al(Hw) || !kric_al(hw) || (nc && (!kric_al(D) || !kric_al(gw) || !kric_al(irho))))
+        return PDPLQR_ERR_UNSUPPORTED;
+    KKTRicArgs a;
+    a.sh = sh;
+    a.E = E;
+    a.c = c;
+    a.D = D;
+    a.Hw = Hw;
+    a.hw = hw;
+    a.gw = gw;
+    a.irho = irho;
+    a.d_off = d_off;
+    a.y_off = y_off;
+    a.rec = rec;
+    a.status = status;
+    a.rho_dyn = rho_dyn;
+    a.nc_last = nc_last;
+    if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_bwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_kkt_ric_bwd<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
+                           double *x0acc, double *ws, double rho_dyn, hipStream_t st) {
+    hipLaunchKernelGGL(k_kkt_ric_fwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
+                       rho_dyn);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+}  // namespace pdplqr

@@ -54,6 +54,32 @@ def test_device_combine_matches_numpy(n, zero_b):
         assert np.linalg.norm(x - y) <= 1e-12 * max(1.0, np.linalg.norm(y)), name
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 12, 13, 16, 17, 20, 24, 31, 32])
+@pytest.mark.parametrize("zero_b", [False, True])
+@pytest.mark.parametrize("fcf", [True, False])
+def test_multiwave_combine_matches_numpy(n, zero_b, fcf):
+    """The 4-wave combine of the horizon scan (combine_mw.hpp): the same element
+    as seg_ref.combine (1e-12).  fcf = False: only P, p are formed (the right
+    operand holds the real terminal) and F, C, f are left untouched."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_mw.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(500 + n)
+    a, b = _elem(n, rng), _elem(n, rng, zero_fcf=zero_b or not fcf)
+    va, vb = _pack(a), _pack(b)
+    sentinel = 12345.0
+    out = np.full_like(va, sentinel)
+    rc = L.pdplqr_debug_combine_mw(n, va.ctypes.data, vb.ctypes.data, out.ctypes.data, int(fcf))
+    assert rc == 0
+    got, ref = _unpack(out, n), combine(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        if not fcf and name in "FCf":
+            assert np.all(x == sentinel), name
+            continue
+        assert np.linalg.norm(x - y) <= 1e-12 * max(1.0, np.linalg.norm(y)), name
+
+
 def test_rsq_f64_accuracy_allows_one_newton_step():
     """rsqrt_f64 (device_common.hpp) refines v_rsq_f64 by Newton steps; record
     the hardware estimate's accuracy (one step squares the relative error)."""
