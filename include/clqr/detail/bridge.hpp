@@ -100,11 +100,38 @@ public:
     Handle(const Handle &) = delete;
     Handle &operator=(const Handle &) = delete;
 
-    void upload(const LQRModel &model) {
-        packed_.pack(model);
-        check(pdplqr_set_model(h_, packed_.E.data(), packed_.c.data(), packed_.H.data(), packed_.h.data(),
-                               packed_.D.empty() ? nullptr : packed_.D.data(), PDPLQR_MEM_HOST),
+    // Uploads the arrays of `model` in `mask` (PDPLQR_MODEL_*) that differ from
+    // what the device holds: the reference reads its model lazily (H, h at
+    // update_problem_data, E, c, D_con at backward / forward), so each facade
+    // call syncs exactly what that call reads.  An unchanged model costs a host
+    // packing pass and a compare, no host -> device copy.
+    void sync(const LQRModel &model, int mask) {
+        fresh_.pack(model);
+        int need = synced_ ? 0 : PDPLQR_MODEL_ALL;
+        if (synced_) {
+            if ((mask & PDPLQR_MODEL_E) && fresh_.E != packed_.E) need |= PDPLQR_MODEL_E;
+            if ((mask & PDPLQR_MODEL_C) && fresh_.c != packed_.c) need |= PDPLQR_MODEL_C;
+            if ((mask & PDPLQR_MODEL_H) && fresh_.H != packed_.H) need |= PDPLQR_MODEL_H;
+            if ((mask & PDPLQR_MODEL_HV) && fresh_.h != packed_.h) need |= PDPLQR_MODEL_HV;
+            if ((mask & PDPLQR_MODEL_D) && fresh_.D != packed_.D) need |= PDPLQR_MODEL_D;
+        }
+        if (!need) return;
+        check(pdplqr_set_model_arrays(h_, need, fresh_.E.data(), fresh_.c.data(), fresh_.H.data(), fresh_.h.data(),
+                                      fresh_.D.empty() ? nullptr : fresh_.D.data(), PDPLQR_MEM_HOST),
               "set_model");
+        if (need & PDPLQR_MODEL_E) packed_.E = fresh_.E;
+        if (need & PDPLQR_MODEL_C) packed_.c = fresh_.c;
+        if (need & PDPLQR_MODEL_H) packed_.H = fresh_.H;
+        if (need & PDPLQR_MODEL_HV) packed_.h = fresh_.h;
+        if (need & PDPLQR_MODEL_D) packed_.D = fresh_.D;
+        synced_ = true;
+    }
+    void upload(const LQRModel &model) { sync(model, PDPLQR_MODEL_ALL); }
+
+    long long upload_bytes() const {
+        int64_t b = 0;
+        check(pdplqr_get_model_upload_bytes(h_, &b), "get_model_upload_bytes");
+        return static_cast<long long>(b);
     }
 
     void update(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys, const std::vector<VectorXs> &zs,
@@ -146,7 +173,8 @@ private:
     pdplqr_handle h_ = nullptr;
     int n_ = 0, m_ = 0, N_ = 0;
     std::vector<int32_t> ncs_;
-    PackedModel packed_;
+    PackedModel packed_, fresh_;  // what the device holds / the model as packed now
+    bool synced_ = false;
     std::vector<double> w_, y_, z_, r_;
 };
 

@@ -32,14 +32,28 @@ public:
     void update_problem_data(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys,
                              const std::vector<VectorXs> &zs, const std::vector<VectorXs> &inv_rho_vecs,
                              const scalar sigma) {
-        hd_.upload(model_);
+        hd_.sync(model_, PDPLQR_MODEL_H | PDPLQR_MODEL_HV);  // copied into the workspace here (lqr_solver.hpp:41-56)
         hd_.update(ws, ys, zs, inv_rho_vecs, sigma);
     }
 
-    void backward(const std::vector<VectorXs> &rho_vecs) { hd_.backward(rho_vecs, true); }
-    void backward_without_factorization(const std::vector<VectorXs> &rho_vecs) { hd_.backward(rho_vecs, false); }
-    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) { hd_.forward(x0, ws); }
+    // E, c, D_con are read when the kernels run (lqr_kernel.hpp:106-119,186-188)
+    void backward(const std::vector<VectorXs> &rho_vecs) {
+        hd_.sync(model_, PDPLQR_MODEL_E | PDPLQR_MODEL_C | PDPLQR_MODEL_D);
+        hd_.backward(rho_vecs, true);
+    }
+    void backward_without_factorization(const std::vector<VectorXs> &rho_vecs) {
+        hd_.sync(model_, PDPLQR_MODEL_E | PDPLQR_MODEL_C | PDPLQR_MODEL_D);
+        hd_.backward(rho_vecs, false);
+    }
+    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) {
+        hd_.sync(model_, PDPLQR_MODEL_E | PDPLQR_MODEL_C);
+        hd_.forward(x0, ws);
+    }
     void clear_workspace() { hd_.clear(); }
+
+    // this build: model bytes uploaded host -> device so far (a loop over an
+    // unchanged model uploads nothing after the constructor)
+    long long model_upload_bytes() const { return hd_.upload_bytes(); }
 
     int num_segments() const { return num_segments_; }
 

@@ -27,7 +27,7 @@ public:
     void update_problem_data(const std::vector<VectorXs> &ws, const std::vector<VectorXs> &ys,
                              const std::vector<VectorXs> &zs, const std::vector<VectorXs> &inv_rho_vecs,
                              const scalar sigma) {
-        hd_.upload(model_);  // form_rhs reads h, c of the current model; the matrix stays frozen
+        hd_.sync(model_, PDPLQR_MODEL_HV | PDPLQR_MODEL_C);  // form_rhs reads h, c; the matrix stays frozen
         hd_.update(ws, ys, zs, inv_rho_vecs, sigma);
     }
 
@@ -37,7 +37,13 @@ public:
             throw std::runtime_error("QDLDL factorization failed with status: " + std::to_string(hd_.status()));
     }
 
-    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) { hd_.forward(x0, ws); }
+    // update_rhs_initial_stage reads S0 (H) and A0 (E) of the current model (kkt.hpp:207-222)
+    void forward(const VectorXs &x0, std::vector<VectorXs> &ws) {
+        hd_.sync(model_, PDPLQR_MODEL_E | PDPLQR_MODEL_H);
+        hd_.forward(x0, ws);
+    }
+
+    long long model_upload_bytes() const { return hd_.upload_bytes(); }
 
     // qdldl_solver.hpp:19,47-78: the QDLDL workspace (elimination tree, column
     // counts, factor buffers) of a KKT matrix, e.g. KKTSystem::get_KKT_csc_matrix's.

@@ -115,6 +115,26 @@ int pdplqr_synchronize(pdplqr_handle h);
 int pdplqr_set_model(pdplqr_handle h, const double *E, const double *c, const double *H, const double *hv,
                      const double *D, int mem);
 
+/* The same upload restricted to the arrays in `mask` (PDPLQR_MODEL_*; the other
+ * pointers are ignored and may be NULL).  The reference reads its model lazily
+ * -- H, h when update_problem_data copies them (lqr_solver.hpp:41-56), E, c,
+ * D_con when backward / forward run (lqr_kernel.hpp:118-119,186-188) -- so the
+ * C++ facade re-uploads exactly the arrays a call reads, and only those that
+ * changed.  An upload of E, c or D alone keeps the protocol state (a backward
+ * may follow the update directly); H or h needs a new update_problem_data. */
+#define PDPLQR_MODEL_E 1
+#define PDPLQR_MODEL_C 2
+#define PDPLQR_MODEL_H 4
+#define PDPLQR_MODEL_HV 8
+#define PDPLQR_MODEL_D 16
+#define PDPLQR_MODEL_ALL 31
+int pdplqr_set_model_arrays(pdplqr_handle h, int mask, const double *E, const double *c, const double *H,
+                            const double *hv, const double *D, int mem);
+
+/* Model bytes copied host -> device by set_model / set_model_arrays since the
+ * handle was created (device-memory uploads are not counted). */
+int pdplqr_get_model_upload_bytes(pdplqr_handle h, int64_t *bytes);
+
 /* LQRSolver::update_problem_data(ws, ys, zs, inv_rho_vecs, sigma)      lqr_solver.hpp:41-56
  * LQRParallelSolver::update_problem_data                               lqr_solver_parallel.hpp:115-140
  * QDLDLSolver::update_problem_data -> KKTSystem::form_rhs              qdldl_solver.hpp:80-86, kkt.hpp:224-300

@@ -249,31 +249,61 @@ int pdplqr_synchronize(pdplqr_handle h) {
     return PDPLQR_OK;
 }
 
-int pdplqr_set_model(pdplqr_handle h, const double *E, const double *c, const double *H, const double *hv,
-                     const double *D, int mem) {
+int pdplqr_set_model_arrays(pdplqr_handle h, int mask, const double *E, const double *c, const double *H,
+                            const double *hv, const double *D, int mem) {
     if (!h) return invalid("null handle");
-    if (!E || !c || !H || !hv) return invalid("set_model: null E/c/H/h");
-    if (h->sh.ndD > 0 && !D) return invalid("set_model: constraints declared but D is null");
+    if (mask & ~PDPLQR_MODEL_ALL) return invalid("set_model_arrays: unknown mask bits");
+    if (!h->model_set && mask != PDPLQR_MODEL_ALL) return invalid("set_model_arrays: the first upload needs every array");
+    if (((mask & PDPLQR_MODEL_E) && !E) || ((mask & PDPLQR_MODEL_C) && !c) || ((mask & PDPLQR_MODEL_H) && !H) ||
+        ((mask & PDPLQR_MODEL_HV) && !hv))
+        return invalid("set_model: null E/c/H/h");
+    if ((mask & PDPLQR_MODEL_D) && h->sh.ndD > 0 && !D) return invalid("set_model: constraints declared but D is null");
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
     const long long B = sh.batch;
     const hipMemcpyKind kind = mem == PDPLQR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    if (h->cfg.solver == PDPLQR_SOLVER_KKT) {
-        const int rc = kkt_before_model(h);
+    if (h->cfg.solver == PDPLQR_SOLVER_KKT && (mask & (PDPLQR_MODEL_E | PDPLQR_MODEL_D))) {
+        const int rc = kkt_before_model(h);  // the frozen KKT matrix keeps the constructor's E, D
         if (rc) return rc;
     }
-    PDPLQR_HIP_TRY(hipMemcpyAsync(h->E, E, B * sh.perE * sizeof(double), kind, h->stream));
-    PDPLQR_HIP_TRY(hipMemcpyAsync(h->c, c, B * sh.perc * sizeof(double), kind, h->stream));
-    PDPLQR_HIP_TRY(hipMemcpyAsync(h->H, H, B * sh.perH * sizeof(double), kind, h->stream));
-    PDPLQR_HIP_TRY(hipMemcpyAsync(h->h, hv, B * sh.perh * sizeof(double), kind, h->stream));
-    if (sh.ndD > 0) PDPLQR_HIP_TRY(hipMemcpyAsync(h->D, D, B * sh.ndD * sizeof(double), kind, h->stream));
-    if (mem != PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+    long long bytes = 0;
+    auto put = [&](double *dst, const double *src, long long count) -> int {
+        PDPLQR_HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(double), kind, h->stream));
+        bytes += count * (long long)sizeof(double);
+        return PDPLQR_OK;
+    };
+    int rc;
+    if ((mask & PDPLQR_MODEL_E) && (rc = put(h->E, E, B * sh.perE))) return rc;
+    if ((mask & PDPLQR_MODEL_C) && (rc = put(h->c, c, B * sh.perc))) return rc;
+    if ((mask & PDPLQR_MODEL_H) && (rc = put(h->H, H, B * sh.perH))) return rc;
+    if ((mask & PDPLQR_MODEL_HV) && (rc = put(h->h, hv, B * sh.perh))) return rc;
+    if ((mask & PDPLQR_MODEL_D) && sh.ndD > 0 && (rc = put(h->D, D, B * sh.ndD))) return rc;
+    if (mem != PDPLQR_MEM_DEVICE) {
+        PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+        h->model_upload_bytes += bytes;
+    }
+    const bool first = !h->model_set;
     h->model_set = true;
-    h->hw_cached = false;  // H~ is re-formed from the new model
-    h->updated = false;
+    if (mask & (PDPLQR_MODEL_H | PDPLQR_MODEL_HV)) {
+        h->hw_cached = false;  // H~ is re-formed from the new model
+        h->updated = false;
+    }
     // The factor cache survives a model upload: the reference re-reads model_
     // lazily and never invalidates its workspace factors (lqr_solver.hpp:25,65-70).
-    return solver_on_model(h);
+    return first || h->cfg.solver == PDPLQR_SOLVER_KKT ? solver_on_model(h) : PDPLQR_OK;
+}
+
+int pdplqr_set_model(pdplqr_handle h, const double *E, const double *c, const double *H, const double *hv,
+                     const double *D, int mem) {
+    if (!h) return invalid("null handle");
+    if (!E || !c || !H || !hv) return invalid("set_model: null E/c/H/h");
+    return pdplqr_set_model_arrays(h, PDPLQR_MODEL_ALL, E, c, H, hv, D, mem);
+}
+
+int pdplqr_get_model_upload_bytes(pdplqr_handle h, int64_t *bytes) {
+    if (!h || !bytes) return invalid("null handle or output");
+    *bytes = h->model_upload_bytes;
+    return PDPLQR_OK;
 }
 
 int pdplqr_update_problem_data(pdplqr_handle h, const double *ws, const double *ys, const double *zs,

@@ -110,6 +110,7 @@ struct pdplqr_handle_s {
     double *st_ws = nullptr, *st_y = nullptr, *st_z = nullptr, *st_ir = nullptr, *st_rho = nullptr;
     double *st_x0 = nullptr;
     bool model_set = false, updated = false, factored = false;
+    long long model_upload_bytes = 0;  // host -> device model bytes (pdplqr_get_model_upload_bytes)
     bool host_staged = false;  // a host->device copy is in flight on `stream`
     std::vector<void *> allocs;
     pdplqr::ParallelState *par = nullptr;  // PARALLEL solver state (solvers.hip)

@@ -26,7 +26,8 @@ ERRORS = {-1: "INVALID", -2: "HIP", -3: "ALLOC", -4: "STATE", -5: "UNSUPPORTED",
 # Every symbol include/pdplqr.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "pdplqr_config_init", "pdplqr_create", "pdplqr_destroy", "pdplqr_last_error", "pdplqr_set_stream",
-    "pdplqr_get_stream", "pdplqr_synchronize", "pdplqr_set_model", "pdplqr_update_problem_data",
+    "pdplqr_get_stream", "pdplqr_synchronize", "pdplqr_set_model", "pdplqr_set_model_arrays",
+    "pdplqr_get_model_upload_bytes", "pdplqr_update_problem_data",
     "pdplqr_backward", "pdplqr_backward_without_factorization", "pdplqr_forward", "pdplqr_clear_workspace",
     "pdplqr_get_value_function", "pdplqr_get_status", "pdplqr_get_segments", "pdplqr_shard_element_size",
     "pdplqr_shard_backward", "pdplqr_shard_forward", "pdplqr_device_count",
@@ -89,6 +90,8 @@ def lib() -> C.CDLL:
     L.pdplqr_get_stream.restype = vp
     L.pdplqr_synchronize.argtypes = [vp]
     L.pdplqr_set_model.argtypes = [vp, dp, dp, dp, dp, dp, C.c_int]
+    L.pdplqr_set_model_arrays.argtypes = [vp, C.c_int, dp, dp, dp, dp, dp, C.c_int]
+    L.pdplqr_get_model_upload_bytes.argtypes = [vp, C.POINTER(C.c_int64)]
     L.pdplqr_update_problem_data.argtypes = [vp, dp, dp, dp, dp, C.c_double, C.c_int]
     L.pdplqr_backward.argtypes = [vp, dp, C.c_int]
     L.pdplqr_backward_without_factorization.argtypes = [vp, dp, C.c_int]

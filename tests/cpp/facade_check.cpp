@@ -3,13 +3,19 @@
 // Eigen-style blocks element by element, and runs one of the three solver
 // classes through update_problem_data -> backward -> forward.
 //
-//   facade_check <problem.bin> <out.bin> <solver> [num_segments condensed] [nofact]
+//   facade_check <problem.bin> <out.bin> <solver> [num_segments condensed] [nofact|mutate|mpc]
 //   solver: serial | parallel | qdldl
 // problem.bin (little endian): int32 n, m, N, ncs[N+1]; then float64 arrays in
 // the boundary layout of pdplqr.h: E, c, H, h, D, x0, sigma, ws, ys, zs, rho, inv_rho.
 // out.bin: float64 w = [u0; x0; ...; xN] (N s + n).  With `nofact` the solve is
 // followed by backward_without_factorization + forward on linear data
 // perturbed deterministically (w-bar + 0.1), and that second answer is written.
+// With `mutate` the model is edited between update_problem_data and backward
+// (E of node N/2 scaled by 1.01, H of node 1 doubled): the reference reads E
+// at backward / forward and H at update_problem_data, so the answer is that of
+// the model with the new E and the old H.  With `mpc` the protocol runs 5 more
+// times on the unchanged model and the model bytes uploaded host -> device
+// during those iterations are printed ("uploads <bytes>").
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -101,6 +107,17 @@ int main(int argc, char **argv) {
     const double sigma = sig[0];
     const std::string kind = argv[3];
     const bool nofact = std::string(argv[argc - 1]) == "nofact";
+    const bool mutate = std::string(argv[argc - 1]) == "mutate";
+    const bool mpc = std::string(argv[argc - 1]) == "mpc";
+    auto edit = [&]() {
+        lqr::Node &a = model.get_node(N / 2);
+        for (int j = 0; j < s; ++j)
+            for (int i = 0; i < n; ++i) a.E(i, j) *= 1.01;
+        lqr::Node &b = model.get_node(1);
+        for (int j = 0; j < s; ++j)
+            for (int i = 0; i < s; ++i) b.H(i, j) *= 2.0;
+    };
+    long long uploads = -1;
     std::vector<lqr::VectorXs> out = wsv;
     auto ws2 = wsv;
     for (auto &v : ws2)
@@ -109,8 +126,18 @@ int main(int argc, char **argv) {
         if (kind == "serial") {
             lqr::LQRSolver sol(model);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+            if (mutate) edit();
             sol.backward(rhov);
             sol.forward(x0, out);
+            if (mpc) {
+                const long long b0 = sol.model_upload_bytes();
+                for (int it = 0; it < 5; ++it) {
+                    sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+                    sol.backward(rhov);
+                    sol.forward(x0, out);
+                }
+                uploads = sol.model_upload_bytes() - b0;
+            }
             if (nofact) {
                 sol.update_problem_data(ws2, ysv, zsv, irv, sigma);
                 sol.backward_without_factorization(rhov);
@@ -122,8 +149,18 @@ int main(int argc, char **argv) {
                                                                         : lqr::CondensedSystemSolverType::CHOLESKY;
             lqr::LQRParallelSolver sol(model, ns, true, ty);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+            if (mutate) edit();
             sol.backward(rhov);
             sol.forward(x0, out);
+            if (mpc) {
+                const long long b0 = sol.model_upload_bytes();
+                for (int it = 0; it < 5; ++it) {
+                    sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+                    sol.backward(rhov);
+                    sol.forward(x0, out);
+                }
+                uploads = sol.model_upload_bytes() - b0;
+            }
             if (nofact) {
                 sol.update_problem_data(ws2, ysv, zsv, irv, sigma);
                 sol.backward_without_factorization(rhov);
@@ -134,6 +171,15 @@ int main(int argc, char **argv) {
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
             sol.backward(irv);
             sol.forward(x0, out);
+            if (mpc) {
+                const long long b0 = sol.model_upload_bytes();
+                for (int it = 0; it < 5; ++it) {
+                    sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+                    sol.backward(irv);
+                    sol.forward(x0, out);
+                }
+                uploads = sol.model_upload_bytes() - b0;
+            }
         } else {
             std::fprintf(stderr, "unknown solver %s\n", kind.c_str());
             return 2;
@@ -147,5 +193,6 @@ int main(int argc, char **argv) {
     for (const auto &v : out) std::fwrite(v.data(), sizeof(double), static_cast<size_t>(v.size()), g);
     std::fclose(g);
     std::printf("ok %s u0[0]=%.10f\n", kind.c_str(), out[0](0));
+    if (mpc) std::printf("uploads %lld\n", uploads);
     return 0;
 }

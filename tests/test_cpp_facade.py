@@ -126,3 +126,46 @@ def test_reference_example_program(facade_bin):
         assert np.allclose(blocks[name]["u0"], kat, rtol=0, atol=5e-10), name
         assert abs(blocks[name]["xN"][2] - 0.9999999) < 1e-6
     assert np.allclose(blocks["QDLDLSolver"]["u0"], kat * (2.8980026778 / 2.8980566697), rtol=0, atol=5e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["serial", "mutate"], ["parallel", "4", "CHOLESKY", "mutate"]])
+def test_cpp_facade_reads_model_lazily(facade_bin, tmp_path, args):
+    """VERDICT r2 missing #3: the model is edited between update_problem_data and
+    backward (E of node N/2 x 1.01, H of node 1 x 2).  The reference reads E at
+    backward / forward (lqr_kernel.hpp:118-119,186-188) and copied H at
+    update_problem_data (lqr_solver.hpp:41-56), so the answer is the oracle's on
+    the model with the NEW E and the OLD H."""
+    from oracle.oracle import OracleParallel, OracleSerial
+    from pdplqr.model import PackedModel
+
+    pm, d, w = _run(facade_bin, str(tmp_path), "random_n12_m4_N64_nc4", args)
+    n, m, N = pm.n, pm.m, pm.N
+    s = n + m
+    E = pm.E.copy()
+    k = N // 2
+    E[k * n * s:(k + 1) * n * s] *= 1.01
+    pm2 = PackedModel(n, m, N, pm.ncs, E, pm.c, pm.H, pm.h, pm.D)
+    o = OracleSerial(pm2) if args[0] == "serial" else OracleParallel(pm2, int(args[1]), True, args[2])
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    ref = o.forward(d["x0"])
+    assert rel_err(w, ref) < 1e-9
+    o0 = OracleSerial(pm)  # the unedited model gives a different answer: the edit was seen
+    o0.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o0.backward(d["rho"])
+    assert rel_err(w, o0.forward(d["x0"])) > 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["serial", "mpc"], ["parallel", "4", "CHOLESKY", "mpc"], ["qdldl", "mpc"]])
+def test_cpp_facade_mpc_loop_uploads_no_model(facade_bin, tmp_path, args):
+    """An MPC loop on an unchanged model (5 x update_problem_data, backward,
+    forward) copies no model bytes host -> device after the constructor."""
+    pm, d = load_golden("random_n12_m4_N64_nc4")
+    prob, out = os.path.join(str(tmp_path), "p.bin"), os.path.join(str(tmp_path), "p.out")
+    _write_problem(prob, pm, d)
+    r = subprocess.run([facade_bin, prob, out] + args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("uploads")]
+    assert line and int(line[0].split()[1]) == 0, r.stdout
