@@ -443,6 +443,201 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     }
 }
 
+// k_seg_maps on a 4-wave block (CHOLESKY form, combine_mw.hpp): the same
+// outputs.  V_j = suf_j (x) right is the P-only 4-wave combine; the map is
+//     R = chol(P_j), S = I + R^T C R = Q Q^T,  X1 = Q^{-1} R^T F,
+//     X2 = Q^{-1} R^T C,  x3 = Q^{-1} R^T (f - C p_j)
+//     Phi = Z F = F - X2^T X1,   phi = Z (f - C p_j) = v - X2^T x3
+// (Z = (I + C P_j)^{-1} = I - C R S^{-1} R^T), with the products after the
+// factorisations one deep and split over the waves by output tile.
+template <int T>
+__global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int n = A.n, S = A.S, J = S + 1, nn = n * n;
+    const int es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    const MwSmem sm = mw_smem(mwbuf, n);
+    const int PL = sm.ld;
+    const double *right = A.right ? A.right + b * (A.rstride ? A.rstride : (long long)es) : nullptr;
+    double *vo = A.vfun + (b * J + j) * (long long)mw;
+    double *mo = A.maps + (b * J + j) * (long long)mw;
+    bool ok = true;
+    const double *vP = nullptr, *vp = nullptr;
+    if (j < S && right) {  // block-uniform
+        ok = mw_combine<T>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(A.suf + (b * S + j) * (long long)es, n),
+                           elem_in(right, n), n, false, sm);
+        __syncthreads();  // vo (written by waves 0 and 3) is read by every wave below
+        vP = vo;
+        vp = vo + nn;
+    } else {
+        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : right;
+        if (src) {
+            vP = src + 2 * nn + n;
+            vp = src + 3 * nn + n;
+        }
+        if (wv == 0) {
+            if (src)
+                for (int q = lane; q < mw; q += 64) vo[q] = q < nn ? vP[q] : vp[q - nn];
+            else
+                for (int q = lane; q < mw; q += 64) vo[q] = 0.0;
+        }
+    }
+    const double *src = j > 0 ? A.elem + (b * S + j - 1) * (long long)es : A.left ? A.left + b * (long long)es
+                                                                                 : nullptr;
+    WV<T> phi, x;
+    bool have_x = false;  // j = 0: x_0 formed (wave 0)
+    if (src && vP) {
+        const ElemIn e = elem_in(src, n);
+        WM<T> R;
+        // ---- phase A: R = chol(P_j) (w0..w2); v = f - C p_j (w3) ----
+        if (wv < 3) {
+            ok = mw_chol_R<T>(R, vP, sm.S + wv * (n * PL), PL, n, g, c) && ok;
+        } else {
+            WM<T> Cs;
+            WV<T> pv, fs, v;
+            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+            wv_load(pv, vp, n, g, c);
+            wv_load(fs, e.f, n, g, c);
+            wv_tn(v, Cs, pv, n, -1.0, &fs);
+            wv_store(v, sm.fv, n, g, c);
+        }
+        // ---- phase B ----
+        if (wv == 0) {
+            WM<T> Cs, T1, Sm;
+            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+            wm_tn(T1, Cs, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C R
+            wm_tn(Sm, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);  // I + R^T C R
+            wm_store(Sm, sm.S, PL, n, g, c);
+            if (lane == 0) sm.ok[0] = ok;
+        } else if (wv == 1) {
+            WM<T> Fs, B;
+            wm_load(Fs, e.F, n, n, false, 0.0, g, c);
+            wm_tn(B, R, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F
+            wm_store(B, sm.B1, PL, n, g, c);
+            WM<T> Cs;
+            WV<T> pv, fs, v, y;
+            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+            wv_load(pv, vp, n, g, c);
+            wv_load(fs, e.f, n, g, c);
+            wv_tn(v, Cs, pv, n, -1.0, &fs);
+            wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
+            wv_store(y, sm.bv, n, g, c);
+        } else if (wv == 2) {
+            WM<T> Cs, B;
+            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+            wm_tn(B, R, Cs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T C
+            wm_store(B, sm.B2, PL, n, g, c);
+        }
+        __syncthreads();
+        ok = ok && sm.ok[0];
+        // ---- phase C: chol(S) carrying one column tile per wave ----
+        {
+            WM<T> Sm;
+            wm_load(Sm, sm.S, PL, n, false, 1.0, g, c);
+            d4 B[T][1], V[T][1];
+            int kind, tile = 0;  // 0: X1, 1: X2, 2: x3
+            if (T == 2) {
+                kind = wv < 2 ? 0 : 1;
+                tile = wv & 1;
+            } else {
+                kind = wv == 0 ? 2 : (wv == 1 ? 0 : (wv == 2 ? 1 : -1));
+            }
+            const bool vec3 = T == 2 && wv == 3;
+            if (kind == 0) mw_col_load<T>(B, sm.B1, PL, tile, n, g, c);
+            else if (kind == 1) mw_col_load<T>(B, sm.B2, PL, tile, n, g, c);
+            else if (kind == 2) mw_vec2_load<T>(B, sm.bv, n, g, c);
+            if (vec3) mw_vec2_load<T>(V, sm.bv, n, g, c);
+            bool okS = true;
+            if (vec3) {
+                d4 BV[T][2];
+#pragma unroll
+                for (int a = 0; a < T; ++a) {
+                    BV[a][0] = B[a][0];
+                    BV[a][1] = V[a][0];
+                }
+                okS = chol_blk4<T, true, 2>(Sm, BV, n, g, c);
+#pragma unroll
+                for (int a = 0; a < T; ++a) {
+                    B[a][0] = BV[a][0];
+                    V[a][0] = BV[a][1];
+                }
+            } else if (kind >= 0) {
+                okS = chol_blk4<T, true, 1>(Sm, B, n, g, c);
+            }
+            __syncthreads();
+            if (kind == 0) mw_col_store<T>(B, sm.B1, PL, tile, n, g, c);
+            else if (kind == 1) mw_col_store<T>(B, sm.B2, PL, tile, n, g, c);
+            else if (kind == 2) mw_vec2_store<T>(B, sm.bv, n, g, c);
+            if (vec3) mw_vec2_store<T>(V, sm.bv, n, g, c);
+            if (wv == 0 && lane == 0) sm.ok[1] = okS;
+        }
+        __syncthreads();
+        ok = ok && sm.ok[1];
+        // ---- phase D: phi = v - X2^T x3 (every wave: it is needed below); Phi ----
+        {
+            WM<T> X2;
+            WV<T> x3, v;
+            wm_load(X2, sm.B2, PL, n, false, 0.0, g, c);
+            wv_load(x3, sm.bv, n, g, c);
+            wv_load(v, sm.fv, n, g, c);
+            wv_tn(phi, X2, x3, n, -1.0, &v);
+            if (j > 0) {
+                if (wv == 0) {
+                    WM<T> X1, Fs, Phi;
+                    wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
+                    wm_load(Fs, e.F, n, n, false, 0.0, g, c);
+                    wm_tn(Phi, X2, X1, n, -1.0, 0.0, &Fs, g, c);  // F - X2^T X1
+                    wm_store(Phi, mo, n, n, g, c);
+                    wv_store(phi, mo + nn, n, g, c);
+                }
+            } else if (wv == 0) {
+                WM<T> X1, FsT, PhiT;
+                WV<T> x0v;
+                wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
+                wm_load(FsT, e.F, n, n, true, 0.0, g, c);
+                wm_tn(PhiT, X1, X2, n, -1.0, 0.0, &FsT, g, c);  // Phi^T = F^T - X1^T X2
+                wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
+                wv_tn(x, PhiT, x0v, n, 1.0, &phi);
+                have_x = true;
+            }
+        }
+    } else if (wv == 0 && src) {  // no value function after this boundary: the map is the element's (F, f)
+        const ElemIn e = elem_in(src, n);
+        wv_load(phi, e.f, n, g, c);
+        if (j > 0) {
+            WM<T> Fs;
+            wm_load(Fs, e.F, n, n, false, 0.0, g, c);
+            wm_store(Fs, mo, n, n, g, c);
+            wv_store(phi, mo + nn, n, g, c);
+        } else {
+            WM<T> PhiT;
+            WV<T> x0v;
+            wm_load(PhiT, src, n, n, true, 0.0, g, c);
+            wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
+            wv_tn(x, PhiT, x0v, n, 1.0, &phi);
+            have_x = true;
+        }
+    } else if (wv == 0 && j == 0) {  // x_0 itself
+        wv_load(x, A.x0 + b * (long long)n, n, g, c);
+        have_x = true;
+    }
+    if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 2);
+    if (j > 0 || wv != 0 || !have_x) return;
+    // j = 0: x_0 = Phi x0 + phi, lambda_0 = P_0 x_0 + p_0
+    wv_store(x, mo + nn, n, g, c);
+    wv_store(x, A.xhat + b * (long long)J * n, n, g, c);
+    if (vP) {
+        WM<T> Pv;
+        WV<T> pv, lam;
+        wm_load(Pv, vP, n, n, false, 0.0, g, c);
+        wv_load(pv, vp, n, g, c);
+        wv_tn(lam, Pv, x, n, 1.0, &pv);
+        wv_store(lam, A.lam + b * (long long)J * n, n, g, c);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // One Hillis-Steele round of the prefix composition of the boundary maps:
 // m_j <- m_j o m_{j-d}.  Map 0 is the constant x_0, so after the round with
@@ -607,6 +802,13 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
+    if (seg_scan_mw(a.n, a.lu) && !getenv("PDPLQR_MAPS_1WAVE")) {
+        const size_t sm = mw_smem_bytes(a.n);
+        if (T == 1) hipLaunchKernelGGL(k_seg_maps_mw<1>, grid, dim3(256), sm, st, a);
+        else hipLaunchKernelGGL(k_seg_maps_mw<2>, grid, dim3(256), sm, st, a);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     const size_t smem = a.right ? op_stage_bytes(a.n) : 0;
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_maps<1, true>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_maps<1, false>), grid, blk, smem, st, a);

@@ -67,6 +67,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 // one launch = the two Hillis-Steele rounds at distances dist and 2 dist (two
 // waves per block); false when this shape keeps the radix-2 rounds
 bool seg_scan4_supported(int n);
+bool seg_scan_mw(int n, bool lu);  // the 4-wave combine runs the scan rounds
 int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 // Composition radix of the boundary-map prefix scan (2 or 4).

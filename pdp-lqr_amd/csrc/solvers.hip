@@ -597,6 +597,9 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
     int lgR = 0;
     while ((1 << lgR) < R) ++lgR;
     bool use_scan = lgR + (r > 0 ? 1 : 0) < std::max(r - 1, R - r - 2);
+    // with the 4-wave scan rounds (seg_scan_mw) a round costs about half a
+    // one-wave chain combine: the log-depth form wins for every rank
+    if (R > 1 && seg_scan_mw(sh.n, h->cfg.condensed_type == PDPLQR_CONDENSED_LU)) use_scan = true;
     if (const char *f = getenv("PDPLQR_SHARD_FOLD")) use_scan = R > 1 && f[0] == 's';
     int rc;
     const double *left = nullptr, *right = nullptr;
