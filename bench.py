@@ -529,7 +529,7 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
         res["kkt" if solver == "kkt" else "riccati"] = {
             "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t, "status_ok": ok,
             "oracle_rel_err": _conic_oracle_err(solver, n, m, N, ncs, E, c, H, h, D, x0, ws, ys, zs, irho, rho, out),
-            "roofline": roofline_block(bst, N * batch, t * 1e3, f"C5_{solver}_N{N}_b{batch}", kern,
+            "roofline": roofline_block(bst, N * batch, t * 1e3, f"C5_N{N}_b{batch}", kern,
                                        kernel_desc="backward + forward")}
         bs.close()
     # the ADMM outer loop on the same data (pdplqr_admm_solve): |u| <= 0.5,
@@ -645,7 +645,9 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     return {"N": Ntot, "nx": n, "nu": m, "n_gpus": world, "ms_per_solve": t * 1e3, "stages_per_s": Ntot / t,
             "scaling": "strong", "finite": ok, "oracle_rel_err": oerr,
             "exchange": "all-gather of 3n^2+2n doubles per rank",
-            "roofline": roofline_block(bst, Ntot, t * 1e3, None, (), flops_stage=103235 + 59968,
+            "roofline": roofline_block(bst, Ntot, t * 1e3, f"C4_N{Ntot}_R{world}",
+                                       ("k_seg_bwd_aug", "k_seg_scan", "k_seg_maps", "k_map_scan", "k_seg_fwd_dma"),
+                                       flops_stage=103235 + 59968,
                                        kernel_desc="whole horizon solve (latency-bound: see DESIGN.md section 6)")}
 
 

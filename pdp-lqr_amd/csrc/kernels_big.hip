@@ -38,10 +38,12 @@ constexpr int BT = 256;      // threads per problem
 __device__ __forceinline__ bool chol_big(double *M, double *sinv, int j0, int j1, int m) {
     const int tid = threadIdx.x, ri = tid & 63, cg = tid >> 6;
     bool ok = true, live = true;
+    int jdead = j1;
     for (int j = j0; j < j1; ++j) {
         __syncthreads();
         const double d = M[j + j * BLD];
         ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
+        if (live && !(j < m || d > 0.0)) jdead = j;
         live = live && (j < m || d > 0.0);
         const double inv = live ? rsqrt_f64(d) : 0.0;
         const double inv2 = inv * inv;
@@ -53,6 +55,20 @@ __device__ __forceinline__ bool chol_big(double *M, double *sinv, int j0, int j1
         }
     }
     __syncthreads();
+    // Eigen's left-looking stop (device_common.hpp chol_restore_tail): columns
+    // >= jdead back to their original values -- undo the live pivots' updates
+    // of that block, in reverse order, with the same products
+    if (jdead < j1) {  // block-uniform, rare
+        for (int p = jdead - 1; p >= j0; --p) {
+            const double inv2 = sinv[p] * sinv[p];
+            const int i = ri;
+            if (i >= jdead && i < j1) {
+                const double lip = M[i + p * BLD] * inv2;
+                for (int l = jdead + cg; l <= i; l += 4) M[i + l * BLD] = __builtin_fma(lip, M[l + p * BLD], M[i + l * BLD]);
+            }
+            __syncthreads();
+        }
+    }
     for (int q = tid; q < (j1 - j0) * (j1 - j0); q += BT) {
         const int i = j0 + q % (j1 - j0), j = j0 + q / (j1 - j0);
         M[i + j * BLD] = i >= j ? M[i + j * BLD] * sinv[j] : 0.0;

@@ -12,6 +12,7 @@
 #   trace:<script args, comma separated>                 rocprofv3 --kernel-trace --stats of that script
 #   bench:<bench.py args, comma separated>               e.g. bench:--no-cpu,--steps,20
 #   lat                                                  scripts/ubench/lat_bench
+#   pmc:<tag>,<dominant kernel>,<script args...>         PMC passes of one workload (scripts/collect_pmc.sh)
 # outputs: gpurun_out/TAG/<step index>_<kind>.{log,json}, trace dirs under gpurun_out/TAG/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,6 +43,10 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py $args > "$log" 2>&1 ;;
     lat)
       timeout -k 10 60 ./scripts/ubench/lat_bench > "$log" 2>&1 ;;
+    pmc)
+      set -- $args
+      ptag=$1; pdom=$2; shift 2
+      TAG=$ptag DOM=$pdom OUT=$O/pmc_$ptag timeout -k 10 1200 scripts/collect_pmc.sh python3 "$@" > "$log" 2>&1 ;;
     *)
       echo "unknown step $kind" | tee -a "$O/steps.log"; exit 2 ;;
   esac

@@ -187,7 +187,7 @@ def test_horizon_shards_both_forms(condensed):
         assert rel_err(full[b], o.forward(x0[b])) < TOL
 
 
-@pytest.mark.parametrize("shape", [(12, 4), (6, 3), (24, 8)])
+@pytest.mark.parametrize("shape", [(12, 4), (6, 3), (24, 8), (36, 8)])
 @pytest.mark.parametrize("solver", ["serial_fullfactor", "batched_value_form", "parallel_LU"])
 def test_coupled_dead_terminal_pivot(shape, solver):
     """Q_N's second pivot is exactly 0 after the first pivot has
@@ -202,6 +202,8 @@ def test_coupled_dead_terminal_pivot(shape, solver):
     from pdplqr import BatchedLQRSolver, CondensedSystemSolverType, LQRParallelSolver, LQRSolver
 
     n, m = shape
+    if solver == "parallel_LU" and n + m > 32:
+        pytest.skip("the parallel solver stops at n + m <= 32 (include/pdplqr.h)")
     pm, model, x0 = psd_model("coupled_dead_terminal", n=n, m=m, N=40)
     N = pm.N
     ref = _oracle(pm, x0)
