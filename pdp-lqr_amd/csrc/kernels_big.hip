@@ -19,6 +19,7 @@
 // problem per block, stage inputs read straight from HBM); the shapes the
 // benchmarks use run on the tiled / streamed kernels.
 #include "device_common.hpp"
+#include "parallel.hpp"
 
 #include <stdint.h>
 
@@ -182,33 +183,55 @@ __global__ __launch_bounds__(BT) void k_riccati_bwd_big(RiccatiArgs A) {
     if (tid == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
 }
 
-// forward_step (lqr_kernel.hpp:181-205) for s <= 64: one wave per problem.
+// forward_step (lqr_kernel.hpp:181-205) for s <= 64: one wave per problem
+// (SEG: per (problem, segment) of the parallel solver, with the coupling
+// u_hat = lambda of the next boundary through G_k, lqr_kernel_parallel.hpp:
+// 195-198, and update_x_next, lqr_solver_parallel.hpp:231, as k_seg_fwd_dma).
 // ws[k s .. k s + s) = [u_k; x_k], ws[N s .. N s + n) = x_N.
+template <bool SEG>
 __global__ __launch_bounds__(64) void k_riccati_fwd_big(Shape sh, const double *__restrict__ E,
                                                        const double *__restrict__ c, const double *__restrict__ FR,
-                                                       const double *__restrict__ x0, double *__restrict__ ws) {
-    __shared__ double w[BS];
+                                                       const double *__restrict__ x0, double *__restrict__ ws,
+                                                       SegFwd sf) {
+    __shared__ double w[BS], uh[BS];
     const int lane = wave_lane();
-    const long long b = blockIdx.x;
+    const long long b = SEG ? blockIdx.x / sf.S : blockIdx.x;
+    const int seg = SEG ? blockIdx.x % sf.S : 0;
     const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
+    const int K0 = SEG ? sf.seg_start[seg] : 0, K1 = SEG ? K0 + sf.seg_len[seg] : N;
+    const bool last = !SEG || (seg == sf.S - 1 && sf.last_is_terminal);
     const long long frs = (long long)s * m + m;
     const double *Eb = E + b * sh.perE;
     const double *cb = c + b * sh.perc;
     const double *Fb = FR + b * sh.perKD;
+    const double *Gb = SEG ? sf.G + b * (long long)N * m * n : nullptr;
     double *wb = ws + b * sh.perh;
     if (lane < n) {
-        const double v = x0[b * n + lane];
-        w[m + lane] = v;
-        wb[(long long)(N > 0 ? m : 0) + lane] = v;
+        if (SEG) {
+            const double *xh = sf.xhat + b * (sf.S + 1) * (long long)n;
+            const double v = xh[(long long)seg * n + lane];
+            w[m + lane] = v;
+            uh[lane] = last ? 0.0 : sf.lam[(b * (sf.S + 1) + seg + 1) * n + lane];
+            wb[(long long)K0 * s + m + lane] = v;  // ws[N0].tail(n) = x_hat
+            if (!last && seg == sf.S - 1) wb[(long long)K1 * s + lane] = xh[(long long)sf.S * n + lane];
+        } else {
+            const double v = x0[b * n + lane];
+            w[m + lane] = v;
+            wb[(long long)(N > 0 ? m : 0) + lane] = v;
+        }
     }
     wave_sync();
-    for (int k = 0; k < N; ++k) {
+    for (int k = K0; k < K1; ++k) {
         const double *Fk = Fb + (long long)k * frs;
-        // v_j = -lu'_j - sum_i Lxu(i, j) x_i  (lane j < m)
+        // v_j = -lu'_j - sum_i Lxu(i, j) x_i (+ sum_t G(j, t) u_hat_t)  (lane j < m)
         double v = 0.0;
         if (lane < m) {
             double a = Fk[(long long)s * m + lane];
             for (int i = 0; i < n; ++i) a = __builtin_fma(Fk[(long long)lane * s + m + i], w[m + i], a);
+            if (SEG && !last) {
+                const double *Gk = Gb + (long long)k * m * n;
+                for (int t = 0; t < n; ++t) a = __builtin_fma(-Gk[lane + t * m], uh[t], a);
+            }
             v = -a;
         }
         // u = Luu^{-T} v (back substitution, column j of Luu^T = row j of Luu)
@@ -222,6 +245,7 @@ __global__ __launch_bounds__(64) void k_riccati_fwd_big(Shape sh, const double *
             wb[(long long)k * s + lane] = v;
         }
         wave_sync();
+        const bool upd = last || (k < K1 - 1);  // update_x_next
         // x+ = c + E [u; x]
         double xn = 0.0;
         if (lane < n) {
@@ -231,7 +255,7 @@ __global__ __launch_bounds__(64) void k_riccati_fwd_big(Shape sh, const double *
             xn = a;
         }
         wave_sync();
-        if (lane < n) {
+        if (lane < n && upd) {
             w[m + lane] = xn;
             wb[(long long)(k + 1) * s + ((k + 1 < N) ? m : 0) + lane] = xn;
         }
@@ -249,7 +273,15 @@ int launch_riccati_backward_big(const RiccatiArgs &a, hipStream_t st) {
 
 int launch_riccati_forward_big(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                                double *ws, hipStream_t st) {
-    hipLaunchKernelGGL(k_riccati_fwd_big, dim3(sh.batch), dim3(64), 0, st, sh, E, c, FR, x0, ws);
+    hipLaunchKernelGGL(k_riccati_fwd_big<false>, dim3(sh.batch), dim3(64), 0, st, sh, E, c, FR, x0, ws, SegFwd{});
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_riccati_forward_seg_big(const Shape &sh, const double *E, const double *c, const double *FR,
+                                   const SegFwd &sf, double *ws, hipStream_t st) {
+    hipLaunchKernelGGL(k_riccati_fwd_big<true>, dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c, FR,
+                       nullptr, ws, sf);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

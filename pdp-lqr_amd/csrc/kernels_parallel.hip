@@ -69,8 +69,8 @@ __device__ __forceinline__ void elem_copy(double *dst, const double *src, int n,
 // F, C, P of the element are unchanged (update_segment_data(p, f, id),
 // condensed_system.hpp:76-80).
 // ---------------------------------------------------------------------------
+template <int P>  // P >= n + m: 32, or 64 for the wide shapes
 __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
-    constexpr int P = 32;
     __shared__ double Pn[P * P];  // P_{k+1} (dense, ld n) from the factor cache
     __shared__ double cvec[P], va[P], vb[P], lp[P], pn[P], xs[P], us[P];
     const int lane = wave_lane();
@@ -178,11 +178,12 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
 }
 
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
-    if (a.sh.s > 32 || !a.Lc) {
-        set_error("PARALLEL backward_without_factorization needs keep_factors = 1 and n + m <= 32");
+    if (a.sh.s > 64 || !a.Lc) {
+        set_error("PARALLEL backward_without_factorization needs keep_factors = 1 and n + m <= 64");
         return PDPLQR_ERR_UNSUPPORTED;
     }
-    hipLaunchKernelGGL(k_seg_bwd_nofact, dim3((unsigned)(a.sh.batch * a.S)), dim3(64), 0, st, a);
+    if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd_nofact<32>, dim3((unsigned)(a.sh.batch * a.S)), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_seg_bwd_nofact<64>, dim3((unsigned)(a.sh.batch * a.S)), dim3(64), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -744,6 +745,7 @@ bool seg_scan_mw(int n, bool lu) {
 
 // Resident scan combines the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
+    if (wide_state(sh.n)) return wide_scan_slots(sh.n, device);
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const size_t smem = op_stage_bytes(sh.n);
@@ -780,6 +782,7 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
+    if (wide_state(a.n)) return launch_seg_scan_wide(a, batch, st);
     const dim3 grid((unsigned)(batch * a.S)), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
@@ -800,6 +803,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
+    if (wide_state(a.n)) return launch_seg_maps_wide(a, batch, st);
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     if (seg_scan_mw(a.n, a.lu) && !getenv("PDPLQR_MAPS_1WAVE")) {
@@ -820,6 +824,10 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
+    if (wide_state(a.n)) {
+        static_assert(PDPLQR_MAP_RADIX == 4, "k_map_scan_wide composes radix-4 rounds");
+        return launch_map_scan_wide(a, batch, st);
+    }
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     if (PDPLQR_MAP_RADIX == 4) {

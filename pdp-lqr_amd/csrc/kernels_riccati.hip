@@ -918,6 +918,7 @@ static int launch_fwd(const Shape &sh, const double *E, const double *c, const d
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
     if (sh.s > 32) {
         if (!SEG && big_shape(sh)) return launch_riccati_forward_big(sh, E, c, FR, x0, ws, st);
+        if (SEG && big_shape(sh)) return launch_riccati_forward_seg_big(sh, E, c, FR, sf, ws, st);
         set_error(SEG ? "segment forward: n + m > 32 is not supported by this build"
                       : "forward: n + m > 64 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;

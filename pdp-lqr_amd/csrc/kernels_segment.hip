@@ -428,6 +428,7 @@ static const void *aug_kernel(const Shape &sh) {
 }
 
 int seg_backward_slots(const Shape &sh, int device) {
+    if (wide_stage(sh)) return wide_seg_backward_slots(sh, device);
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const void *k = aug_kernel(sh);
@@ -436,6 +437,7 @@ int seg_backward_slots(const Shape &sh, int device) {
 }
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st) {
+    if (wide_stage(a.sh)) return launch_seg_backward_wide(a, st);
     const void *k = aug_kernel(a.sh);
     if (!k) {
         set_error("parallel solver: n + m > 32 is not supported by this build");

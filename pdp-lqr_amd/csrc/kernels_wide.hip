@@ -1,0 +1,498 @@
+// kernels_wide.hip -- the PARALLEL solver for the wide shapes 32 < n + m <= 64
+// (and state sizes 32 < n <= 63), one 256-thread block per segment / element
+// with the matrices in LDS (blk_la.hpp).
+//
+// Same algorithm and outputs as the tiled kernels (kernels_segment.hip,
+// kernels_parallel.hip), restating the same reference code:
+//   * k_seg_bwd_wide: ParallelLQRKernel::step_with_factorization
+//     (lqr_kernel_parallel.hpp:88-136) over a segment in the augmented value
+//     form of kernels_segment.hip: per stage
+//         PE = P E~,  YE = F E~,  M = H~ + E~^T PE,
+//         eliminate the m u-pivots of [[M, YE^T], [YE, -C]] with the aug
+//         column [h~ + E~^T (P c + p); F c + f]
+//     which leaves P_k, F_k, C_k, p_k, f_k (no x pivots, no n^3 recursion).
+//     Records: FR_k = [L(:, 0:m) | lu'], G_k, the factor cache P_k / lp_k.
+//   * wide_combine: the element combine (condensed_system.hpp
+//     :203-290 Cholesky form, :82-137 LU form) in the formulas of
+//     combine_tiles.hpp (Y = P_b (I + C_a P_b)^{-1}, Z = I - C_a Y).
+//   * k_seg_scan_wide / k_seg_maps_wide / k_map_scan_wide: one scan round,
+//     the boundary maps and one radix-4 composition round, as k_seg_scan,
+//     k_seg_maps, k_map_scan4.
+// Every blk_* call is a block-wide step bracketed by barriers (blk_la.hpp).
+#include "blk_la.hpp"
+#include "combine_tiles.hpp"  // ElemIn, elem_in
+#include "parallel.hpp"
+
+namespace pdplqr {
+
+namespace {
+constexpr int VL = 64;  // vector slot length (doubles)
+}
+
+// ---------------------------------------------------------------------------
+// element kernels: LDS = 4 n x n matrices (B0..B3, B1 | B2 contiguous for the
+// Gauss-Jordan [A | R]), 8 vectors, pivot scratch
+// ---------------------------------------------------------------------------
+struct WideSmem {
+    double *B[4];
+    double *v[8];
+    double *prow, *mul, *sinv;
+    int *piv;
+};
+
+static size_t wide_elem_smem_bytes(int n) {
+    return (size_t)(4 * n * n + 8 * VL + 2 * VL + VL + VL) * sizeof(double) + VL * sizeof(int);
+}
+
+__device__ __forceinline__ WideSmem wide_smem(double *base, int n) {
+    WideSmem s;
+    for (int q = 0; q < 4; ++q) s.B[q] = base + q * n * n;
+    double *v = base + 4 * n * n;
+    for (int q = 0; q < 8; ++q) s.v[q] = v + q * VL;
+    s.prow = v + 8 * VL;
+    s.mul = s.prow + 2 * VL;
+    s.sinv = s.mul + VL;
+    s.piv = reinterpret_cast<int *>(s.sinv + VL);
+    return s;
+}
+
+// Y = P_b (I + C_a P_b)^{-1}, Z = I - C_a Y with C_a in B0 (LDS) and P_b a
+// global n x n block.  Returns the buffers holding Y, Z and the free one.
+// Cholesky form: R = chol(P_b), S = I + R^T C_a R = Q Q^T, U = Q^{-1} R^T
+// (R^T carried through the elimination of S), Y = U^T U.  LU form:
+// Gauss-Jordan with partial pivoting on [I + P_b C_a | P_b], Y symmetrised.
+__device__ __noinline__ bool wide_core(const WideSmem &sm, const double *Pb, int n, bool lu, double **Y, double **Z,
+                                       double **Fr) {
+    double *B0 = sm.B[0], *B1 = sm.B[1], *B2 = sm.B[2], *B3 = sm.B[3];
+    bool ok;
+    if (!lu) {
+        blk_copy(B1, n, mv_n(Pb, n), n, n);
+        ok = blk_chol(B1, n, n, n, sm.sinv);                                         // R
+        blk_mm(B2, n, mv_n(B0, n), mv_n(B1, n), n, n, n, 1.0, 0.0, mv_none(), false);  // C_a R
+        blk_mm(B3, n, mv_t(B1, n), mv_n(B2, n), n, n, n, 1.0, 1.0, mv_none(), true);   // I + R^T C_a R
+        blk_copy(B2, n, mv_t(B1, n), n, n);                                          // R^T
+        ok = blk_chol(B3, n, n, n, sm.sinv, B2, n, n) && ok;                         // U = Q^{-1} R^T
+        blk_mm(B1, n, mv_t(B2, n), mv_n(B2, n), n, n, n, 1.0, 0.0, mv_none(), true);   // Y = U^T U
+        blk_mm(B3, n, mv_n(B0, n), mv_n(B1, n), n, n, n, -1.0, 1.0, mv_none(), false);  // Z = I - C_a Y
+        *Y = B1;
+        *Z = B3;
+        *Fr = B2;
+    } else {
+        blk_mm(B1, n, mv_n(Pb, n), mv_n(B0, n), n, n, n, 1.0, 1.0, mv_none(), false);  // I + P_b C_a
+        blk_copy(B2, n, mv_n(Pb, n), n, n);                                           // P_b
+        ok = blk_gauss_jordan(B1, n, sm.piv, sm.prow, sm.mul);
+        for (int q = threadIdx.x; q < n * n; q += BLK_THREADS) {
+            const int i = q % n, j = q / n;
+            B3[q] = 0.5 * (B2[sm.piv[i] + j * n] + B2[sm.piv[j] + i * n]);
+        }
+        blk_mm(B1, n, mv_n(B0, n), mv_n(B3, n), n, n, n, -1.0, 1.0, mv_none(), false);  // Z = I - C_a Y
+        *Y = B3;
+        *Z = B1;
+        *Fr = B2;
+    }
+    return ok;
+}
+
+// out = a (x) b, the output blocks addressed separately (see tcombine_parts);
+// fcf: form F, C, f; pp: form P, p.  Outputs must not alias the inputs.
+__device__ __noinline__ bool wide_combine(double *oF, double *oC, double *of, double *oP, double *op, ElemIn ea,
+                                          ElemIn eb, int n, bool fcf, bool pp, bool lu, const WideSmem &sm) {
+    double *B0 = sm.B[0];
+    double *pb = sm.v[0], *fa = sm.v[1], *v1 = sm.v[2], *v3 = sm.v[3], *t4 = sm.v[4], *t5 = sm.v[5];
+    blk_copy(B0, n, mv_n(ea.C, n), n, n);  // C_a
+    blk_vcopy(pb, eb.p, n);
+    blk_vcopy(fa, ea.f, n);
+    if (fcf) blk_mv(v1, mv_n(B0, n), pb, n, n, -1.0, fa);  // f_a - C_a p_b
+    if (pp) blk_mv(v3, mv_n(eb.P, n), fa, n, n, 1.0, pb);  // p_b + P_b f_a
+    double *Y, *Z, *Fr;
+    const bool ok = wide_core(sm, eb.P, n, lu, &Y, &Z, &Fr);
+    if (pp) {
+        blk_copy(Fr, n, mv_n(ea.F, n), n, n);                                                 // F_a
+        blk_mm(Y, n, mv_n(Y, n), mv_n(Fr, n), n, n, n, 1.0, 0.0, mv_none(), false);             // Y F_a
+        blk_mm(Y, n, mv_t(Fr, n), mv_n(Y, n), n, n, n, 1.0, 0.0, mv_n(ea.P, n), false);         // P_a + F_a^T Y F_a
+        blk_store_sym(oP, n, Y, n, n);
+        blk_mv(t4, mv_t(Z, n), v3, n, n, 1.0, nullptr);                                        // Z^T v3
+        blk_mv(op, mv_t(Fr, n), t4, n, n, 1.0, ea.p);                                          // p_a + F_a^T Z^T v3
+    }
+    if (fcf) {
+        if (!pp) blk_copy(Fr, n, mv_n(ea.F, n), n, n);
+        blk_mm(Y, n, mv_n(Z, n), mv_n(Fr, n), n, n, n, 1.0, 0.0, mv_none(), false);   // Z F_a (Y is free)
+        blk_copy(Fr, n, mv_n(eb.F, n), n, n);                                         // F_b
+        blk_mm(oF, n, mv_n(Fr, n), mv_n(Y, n), n, n, n, 1.0, 0.0, mv_none(), false);  // F_b Z F_a
+        blk_mm(Y, n, mv_n(Z, n), mv_n(B0, n), n, n, n, 1.0, 0.0, mv_none(), false);   // Z C_a
+        blk_mm(Y, n, mv_n(Y, n), mv_t(Fr, n), n, n, n, 1.0, 0.0, mv_none(), false);   // Z C_a F_b^T
+        blk_mv(t5, mv_n(Z, n), v1, n, n, 1.0, nullptr);                              // Z v1
+        blk_mm(Z, n, mv_n(Fr, n), mv_n(Y, n), n, n, n, 1.0, 0.0, mv_n(eb.C, n), false);  // F_b Z C_a F_b^T + C_b
+        blk_store_sym(oC, n, Z, n, n);
+        blk_mv(of, mv_n(Fr, n), t5, n, n, 1.0, eb.f);  // F_b Z v1 + f_b
+    }
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// one Hillis-Steele round of the suffix scan (k_seg_scan)
+// ---------------------------------------------------------------------------
+template <bool LU>
+__global__ __launch_bounds__(256) void k_seg_scan_wide(ScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int n = A.n, S = A.S, d = A.dist;
+    const int es = 3 * n * n + 2 * n, nn = n * n;
+    const long long b = blockIdx.x / S;
+    const int i = blockIdx.x % S;
+    const long long is = A.istride ? A.istride : es;
+    const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
+    double *out = A.out + b * (long long)S * es;
+    double *o = out + (long long)i * es;
+    if (i + d >= S) {  // block-uniform
+        const double *src = in + (long long)i * is;
+        for (int q = threadIdx.x; q < es; q += BLK_THREADS) o[q] = src[q];
+        return;
+    }
+    const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    const WideSmem sm = wide_smem(wbuf, n);
+    const bool ok = wide_combine(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n,
+                                 elem_in(in + (long long)i * is, n), elem_in(in + (long long)(i + d) * is, n), n, fcf,
+                                 true, LU, sm);
+    if (!fcf)
+        for (int q = threadIdx.x; q < 2 * nn + n; q += BLK_THREADS) o[q] = 0.0;  // [F | C | f]
+    if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
+}
+
+// ---------------------------------------------------------------------------
+// boundary maps (k_seg_maps): x_j = Phi_j x_{j-1} + phi_j, Phi = Z F,
+// phi = Z (f - C p_j), Z = (I + C P_j)^{-1}
+// ---------------------------------------------------------------------------
+template <bool LU>
+__global__ __launch_bounds__(256) void k_seg_maps_wide(MapArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int tid = threadIdx.x;
+    const int n = A.n, S = A.S, J = S + 1, nn = n * n;
+    const int es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    const WideSmem sm = wide_smem(wbuf, n);
+    const double *right = A.right ? A.right + b * (A.rstride ? A.rstride : (long long)es) : nullptr;
+    double *vo = A.vfun + (b * J + j) * (long long)mw;
+    double *mo = A.maps + (b * J + j) * (long long)mw;
+    bool ok = true;
+    const double *vP = nullptr, *vp = nullptr;
+    if (j < S && right) {  // V_j = suf_j (x) right: (P, p) only
+        ok = wide_combine(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(A.suf + (b * S + j) * (long long)es, n),
+                          elem_in(right, n), n, false, true, LU, sm);
+        __threadfence_block();
+        __syncthreads();
+        vP = vo;
+        vp = vo + nn;
+    } else {
+        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : right;
+        if (src) {
+            vP = src + 2 * nn + n;
+            vp = src + 3 * nn + n;
+        }
+        for (int q = tid; q < mw; q += BLK_THREADS) vo[q] = src ? (q < nn ? vP[q] : vp[q - nn]) : 0.0;
+    }
+    const double *src = j > 0 ? A.elem + (b * S + j - 1) * (long long)es : A.left ? A.left + b * (long long)es
+                                                                                 : nullptr;
+    double *phi = sm.v[5], *x = sm.v[6];
+    double *Phi = nullptr;  // LDS n x n (j = 0 with a value function) or null
+    const double *PhiG = nullptr;  // the map's matrix in global memory (no value function)
+    if (src && vP) {
+        const ElemIn e = elem_in(src, n);
+        double *B0 = sm.B[0];
+        blk_copy(B0, n, mv_n(e.C, n), n, n);
+        double *pv = sm.v[0], *v = sm.v[2];
+        blk_vcopy(pv, vp, n);
+        blk_mv(v, mv_n(B0, n), pv, n, n, -1.0, e.f);  // f - C p_j
+        double *Y, *Z, *Fr;
+        ok = wide_core(sm, vP, n, LU, &Y, &Z, &Fr) && ok;
+        blk_mv(phi, mv_n(Z, n), v, n, n, 1.0, nullptr);  // Z (f - C p_j)
+        if (j > 0) {
+            blk_mm(mo, n, mv_n(Z, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);  // Z F
+            for (int q = tid; q < n; q += BLK_THREADS) mo[nn + q] = phi[q];
+        } else {
+            blk_mm(Y, n, mv_n(Z, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);
+            Phi = Y;
+        }
+    } else if (src) {
+        const ElemIn e = elem_in(src, n);
+        blk_vcopy(phi, e.f, n);
+        if (j > 0)
+            for (int q = tid; q < mw; q += BLK_THREADS) mo[q] = q < nn ? e.F[q] : e.f[q - nn];
+        else PhiG = e.F;
+    }
+    if (!ok && tid == 0) atomicOr(A.flag + b, 2);
+    if (j > 0) return;
+    // j = 0: x_0 = Phi x0 + phi (x0 itself without a global prefix), lambda_0 = P_0 x_0 + p_0
+    double *x0 = sm.v[7];
+    blk_vcopy(x0, A.x0 + b * (long long)n, n);
+    if (Phi) blk_mv(x, mv_n(Phi, n), x0, n, n, 1.0, phi);
+    else if (PhiG) blk_mv(x, mv_n(PhiG, n), x0, n, n, 1.0, phi);
+    else blk_vcopy(x, x0, n);
+    for (int q = tid; q < n; q += BLK_THREADS) {
+        mo[nn + q] = x[q];
+        A.xhat[b * (long long)J * n + q] = x[q];
+    }
+    if (vP) blk_mv(A.lam + b * (long long)J * n, mv_n(vP, n), x, n, n, 1.0, vp);
+}
+
+// ---------------------------------------------------------------------------
+// one radix-4 round of the prefix composition of the boundary maps (k_map_scan4)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_map_scan_wide(MapScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int tid = threadIdx.x;
+    const int n = A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
+    const long long b = blockIdx.x / J;
+    const int j = blockIdx.x % J;
+    const double *in = A.in + b * (long long)J * mw;
+    double *out = A.out + b * (long long)J * mw;
+    if (j < d) {  // anchored earlier: keep x_j for this round's partners
+        for (int q = tid; q < n; q += BLK_THREADS) out[(long long)j * mw + nn + q] = in[(long long)j * mw + nn + q];
+        return;
+    }
+    double *Pacc = wbuf, *pacc = wbuf + nn, *po = pacc + VL;
+    blk_copy(Pacc, n, mv_n(in + (long long)j * mw, n), n, n);
+    blk_vcopy(pacc, in + (long long)j * mw + nn, n);
+#pragma unroll 1
+    for (int k = 1; k <= 3; ++k) {
+        const int ia = j - k * d;  // >= 0: the previous partner was not anchored (>= d)
+        const double *ea = in + (long long)ia * mw;
+        blk_mv(po, mv_n(Pacc, n), ea + nn, n, n, 1.0, pacc);  // Phi_acc phi_a + phi_acc
+        if (ia < d) {  // anchored partner: po = x_j
+            for (int q = tid; q < n; q += BLK_THREADS) {
+                out[(long long)j * mw + nn + q] = po[q];
+                A.xhat[(b * J + j) * (long long)n + q] = po[q];
+            }
+            const double *v = A.vfun + (b * J + j) * (long long)mw;
+            blk_mv(A.lam + (b * J + j) * (long long)n, mv_n(v, n), po, n, n, 1.0, v + nn);
+            return;
+        }
+        blk_mm(Pacc, n, mv_n(Pacc, n), mv_n(ea, n), n, n, n, 1.0, 0.0, mv_none(), false);  // Phi_acc Phi_a
+        blk_vcopy(pacc, po, n);
+    }
+    for (int q = tid; q < mw; q += BLK_THREADS) out[(long long)j * mw + q] = q < nn ? Pacc[q] : pacc[q - nn];
+}
+
+// ---------------------------------------------------------------------------
+// segment backward (k_seg_bwd_aug) for n + m > 32
+// LDS: XA (n x s: P, then P E~), XB (n x s: F at column offset 0 or m, then
+// F E~), Mb (s x s: E~, then the stage matrix), Cm (n x n), vectors.
+// ---------------------------------------------------------------------------
+static size_t wide_seg_smem_bytes(int n, int s) {
+    return (size_t)(2 * n * s + s * s + n * n + 8 * VL) * sizeof(double);
+}
+
+__global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int tid = threadIdx.x;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = n + m, S = A.S;
+    const long long bi = blockIdx.x / S;
+    const int seg = blockIdx.x % S;
+    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
+    const bool last = (seg == S - 1) && A.last_is_terminal;
+    const long long frs = (long long)s * m + m;
+    const int ps = sh.ps;
+    const double *Eb = A.E + bi * sh.perE;
+    const double *cb = A.c + bi * sh.perc;
+    const double *Hb = A.Hw + bi * sh.perHw;
+    const double *hb = A.hw + bi * sh.perh;
+    double *FRb = A.FR + bi * sh.perKD;
+    double *Gb = A.G + bi * (long long)sh.N * m * n;
+    double *Lcb = A.Lc ? A.Lc + bi * sh.perHw : nullptr;
+    double *lpb = A.lpc ? A.lpc + bi * sh.perh : nullptr;
+    double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Cm = Mb + s * s, *vec = Cm + n * n;
+    double *pv = vec, *fv = vec + VL, *cv = vec + 2 * VL, *hv = vec + 3 * VL, *pc = vec + 4 * VL,
+           *fy = vec + 5 * VL, *lp = vec + 6 * VL, *sinv = vec + 7 * VL;
+    __shared__ int s_bad;
+    int fail_stage = -1;
+    // ---- segment terminal: the real one (P = H~_N, p = h~_N, F = 0) or the
+    //      dummy (P = 0, p = 0, F = I, C = 0, f = 0) ----
+    {
+        const double *HN = Hb + (long long)sh.N * ps;
+        if (tid == 0) s_bad = 0;
+        __syncthreads();
+        for (int q = tid; q < n * n; q += BLK_THREADS) {
+            const int i = q % n, j = q / n;
+            XA[q] = last ? HN[i >= j ? pidx(i, j, n) : pidx(j, i, n)] : 0.0;
+            XB[q] = (!last && i == j) ? 1.0 : 0.0;
+            Cm[q] = 0.0;
+            if (last && i == j && psd_bad(XA[q])) s_bad = 1;
+        }
+        for (int q = tid; q < n; q += BLK_THREADS) {
+            pv[q] = last ? hb[(long long)sh.N * s + q] : 0.0;
+            fv[q] = 0.0;
+        }
+        if (last) {
+            const int pn = n * (n + 1) / 2;
+            if (Lcb)
+                for (int t = tid; t < pn; t += BLK_THREADS) Lcb[(long long)sh.N * ps + t] = HN[t];
+            if (lpb)
+                for (int t = tid; t < n; t += BLK_THREADS) lpb[(long long)sh.N * s + t] = hb[(long long)sh.N * s + t];
+        }
+        __syncthreads();
+        if (s_bad) fail_stage = sh.N;
+    }
+    const double *Fp = XB;  // F (n x n, ld n) inside XB
+    const bool yon = !last;  // the y block (F, C, f) is identically zero on the last segment
+    for (int k = N1 - 1; k >= N0; --k) {
+        const double *Ek = Eb + (long long)k * n * s;
+        blk_copy(Mb, n, mv_n(Ek, n), n, s);  // E~ (n x s)
+        for (int q = tid; q < s; q += BLK_THREADS) {
+            hv[q] = hb[(long long)k * s + q];
+            if (q < n) cv[q] = cb[(long long)k * n + q];
+        }
+        if (tid == 0) s_bad = 0;
+        __syncthreads();
+        blk_mv(pc, mv_n(XA, n), cv, n, n, 1.0, pv);  // P c + p
+        if (yon) blk_mv(fy, mv_n(Fp, n), cv, n, n, 1.0, fv);  // F c + f
+        blk_mm(XA, n, mv_n(XA, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // P E~
+        if (yon) blk_mm(XB, n, mv_n(Fp, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // F E~
+        blk_mv(lp, mv_t(Mb, n), pc, s, n, 1.0, hv);  // h~ + E~^T (P c + p)
+        blk_mm(Mb, s, mv_t(Mb, n), mv_n(XA, n), s, s, n, 1.0, 0.0, mv_pk(Hb + (long long)k * ps, s), true);
+        // ---- eliminate the u pivots of [[M, YE^T], [YE, -C]] (one barrier per pivot) ----
+        double *FRk = FRb + (long long)k * frs;
+        double *Gk = Gb + (long long)k * m * n;
+        const int rr = tid & 127, hh = tid >> 7;
+        bool ok = true;
+        for (int j = 0; j < m; ++j) {
+            const double d = Mb[j + j * s];
+            ok = ok && d > 0.0;
+            const double inv2 = 1.0 / d, invs = rsqrt_f64(d);
+            const double lpj = lp[j];
+            // column j is final: rollout record, coupling gain
+            if (tid < s) FRk[(long long)j * s + tid] = tid >= j ? Mb[tid + j * s] * invs : 0.0;
+            if (yon && tid >= 128 && tid < 128 + n) Gk[j + (tid - 128) * m] = -XB[(tid - 128) + j * n] * invs;
+            if (tid == 255) {
+                FRk[(long long)s * m + j] = lpj * invs;
+                sinv[j] = invs;
+            }
+            if (rr < s) {
+                const int i = rr;
+                if (i > j) {
+                    const double lij = Mb[i + j * s] * inv2;
+                    for (int l = j + 1 + hh; l <= i; l += 2) Mb[i + l * s] = __builtin_fma(-lij, Mb[l + j * s], Mb[i + l * s]);
+                    if (hh == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
+                }
+            } else if (yon && rr < s + n) {
+                const int r = rr - s;
+                const double yrj = XB[r + j * n] * inv2;
+                for (int l = j + 1 + hh; l < s; l += 2) XB[r + l * n] = __builtin_fma(-yrj, Mb[l + j * s], XB[r + l * n]);
+                for (int q = hh; q <= r; q += 2) Cm[r + q * n] = __builtin_fma(yrj, XB[q + j * n], Cm[r + q * n]);
+                if (hh == 0) fy[r] = __builtin_fma(-yrj, lpj, fy[r]);
+            }
+            __syncthreads();
+        }
+        // ---- P_k (lower block, symmetric by construction), p_k, f_k; F_k stays in XB at column m ----
+        for (int q = tid; q < n * n; q += BLK_THREADS) {
+            const int i = q % n, j = q / n;
+            const int hi = i > j ? i : j, lo = i > j ? j : i;
+            const double v = Mb[(m + hi) + (m + lo) * s];
+            XA[q] = v;
+            if (i == j && psd_bad(v)) s_bad = 1;
+            if (Lcb && i >= j) Lcb[(long long)k * ps + pidx(i, j, n)] = v;
+        }
+        for (int q = tid; q < s; q += BLK_THREADS) {
+            const double v = q < m ? lp[q] * sinv[q] : lp[q];  // [lu'; p_k]
+            if (lpb) lpb[(long long)k * s + q] = v;
+            if (q >= m) pv[q - m] = v;
+        }
+        if (yon)
+            for (int q = tid; q < n; q += BLK_THREADS) fv[q] = fy[q];
+        Fp = XB + m * n;
+        __syncthreads();
+        if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
+    }
+    // ---- export the element (update_segment_data, lqr_solver_parallel.hpp:182-187) ----
+    double *eo = A.elem + (bi * S + seg) * (long long)(3 * n * n + 2 * n);
+    double *eF = eo, *eC = eo + n * n, *ef = eo + 2 * n * n, *eP = ef + n, *ep = eP + n * n;
+    for (int q = tid; q < n * n; q += BLK_THREADS) {
+        const int i = q % n, j = q / n;
+        eP[q] = XA[q];
+        eF[q] = last ? 0.0 : Fp[q];
+        eC[q] = last ? 0.0 : Cm[i >= j ? i + j * n : j + i * n];
+    }
+    for (int q = tid; q < n; q += BLK_THREADS) {
+        ep[q] = pv[q];
+        ef[q] = last ? 0.0 : fv[q];
+    }
+    if (tid == 0) A.seg_status[bi * S + seg] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static bool wide_attr_set(const void *k, size_t bytes) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
+}
+
+bool wide_state(int n) { return n > 32 && n <= 64; }
+bool wide_stage(const Shape &sh) { return sh.s > 32 && sh.s <= 64; }
+
+size_t wide_seg_smem(const Shape &sh) { return wide_seg_smem_bytes(sh.n, sh.s); }
+size_t wide_elem_smem(int n) { return wide_elem_smem_bytes(n); }
+
+int wide_seg_backward_slots(const Shape &sh, int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    const size_t sm = wide_seg_smem_bytes(sh.n, sh.s);
+    wide_attr_set(reinterpret_cast<const void *>(&k_seg_bwd_wide), sm);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd_wide, 256, sm) != hipSuccess || per <= 0) per = 1;
+    return cus * per;
+}
+
+int wide_scan_slots(int n, int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    const size_t sm = wide_elem_smem_bytes(n);
+    wide_attr_set(reinterpret_cast<const void *>(&k_seg_scan_wide<false>), sm);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_wide<false>, 256, sm) != hipSuccess || per <= 0)
+        per = 1;
+    return cus * per;
+}
+
+int launch_seg_backward_wide(const SegArgs &a, hipStream_t st) {
+    const size_t sm = wide_seg_smem_bytes(a.sh.n, a.sh.s);
+    if (!wide_attr_set(reinterpret_cast<const void *>(&k_seg_bwd_wide), sm)) {
+        set_error("segment backward (n + m > 32): LDS request too large");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL(k_seg_bwd_wide, dim3((unsigned)(a.sh.batch * a.S)), dim3(256), sm, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_seg_scan_wide(const ScanArgs &a, int batch, hipStream_t st) {
+    const size_t sm = wide_elem_smem_bytes(a.n);
+    const void *k = a.lu ? reinterpret_cast<const void *>(&k_seg_scan_wide<true>)
+                         : reinterpret_cast<const void *>(&k_seg_scan_wide<false>);
+    if (!wide_attr_set(k, sm)) {
+        set_error("suffix scan (n > 32): LDS request too large");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    void *args[] = {const_cast<ScanArgs *>(&a)};
+    PDPLQR_HIP_TRY(hipLaunchKernel(k, dim3((unsigned)(batch * a.S)), dim3(256), args, sm, st));
+    return PDPLQR_OK;
+}
+
+int launch_seg_maps_wide(const MapArgs &a, int batch, hipStream_t st) {
+    const size_t sm = wide_elem_smem_bytes(a.n);
+    const void *k = a.lu ? reinterpret_cast<const void *>(&k_seg_maps_wide<true>)
+                         : reinterpret_cast<const void *>(&k_seg_maps_wide<false>);
+    if (!wide_attr_set(k, sm)) {
+        set_error("boundary maps (n > 32): LDS request too large");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    void *args[] = {const_cast<MapArgs *>(&a)};
+    PDPLQR_HIP_TRY(hipLaunchKernel(k, dim3((unsigned)(batch * (a.S + 1))), dim3(256), args, sm, st));
+    return PDPLQR_OK;
+}
+
+int launch_map_scan_wide(const MapScanArgs &a, int batch, hipStream_t st) {
+    const size_t sm = (size_t)(a.n * a.n + 2 * VL) * sizeof(double);
+    hipLaunchKernelGGL(k_map_scan_wide, dim3((unsigned)(batch * (a.S + 1))), dim3(256), sm, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+}  // namespace pdplqr

@@ -1391,14 +1391,14 @@ int kkt_init(pdplqr_handle h) {
     ks->dim = dof;
     const long long B = sh.batch, PP = (long long)ks->P * ks->P;
     int rc;
-    ks->ric = kkt_ric_nc(sh, h->ncs);
+    ks->ric = kkt_ric_nc(sh, h->ncs, dmax <= 32);
     if (ks->ric >= 0) {  // Riccati-ordered path: no tile buffers
-        if ((rc = kalloc(h, &ks->rec, B * kkt_ric_rec_doubles(sh))) || (rc = kalloc(h, &ks->x0acc, B * n))) return rc;
+        if ((rc = kalloc(h, &ks->rec, B * kkt_ric_rec_doubles(sh, ks->ric))) || (rc = kalloc(h, &ks->x0acc, B * n))) return rc;
         PDPLQR_HIP_TRY(hipMemset(ks->x0acc, 0, B * n * sizeof(double)));
         return PDPLQR_OK;
     }
     if (dmax > 32) {
-        set_error("KKT solver with n + m > 32 or n + nc > 32 is not supported by this build");
+        set_error("KKT solver with n + m > 64 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     // P = 16 also needs stage 0's y columns beside the lambda_1 columns of G_0 (PPK)
@@ -1544,7 +1544,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     const Shape &sh = h->sh;
     if (ks->ric >= 0)
         return launch_kkt_ric_forward(sh, ks->Ef ? ks->Ef : h->E, h->c, ks->rec, x0, ks->x0acc, ws, h->cfg.rho_dyn,
-                                      h->stream);
+                                      h->stream, ks->ric);
     KKTArgs a = kkt_args(h);
     const size_t P = ks->P, PP = P * P;
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);

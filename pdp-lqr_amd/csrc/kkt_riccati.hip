@@ -43,6 +43,7 @@
 // side on every forward (kkt.hpp:207-222): the solve then uses the sum of every
 // x0 passed since the last update_problem_data (x0acc here), while ws[0]'s x
 // part is the x0 of the call (qdldl_solver.hpp:129-131).
+#include "blk_la.hpp"
 #include "schur_stage.hpp"
 #include "solvers.hpp"
 
@@ -442,14 +443,234 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
     if (lane < n) wb[(long long)N * s + lane] = sx[lane];
 }
 
+
+// ---------------------------------------------------------------------------
+// Wide shapes (n + m <= 64, any per-stage constraint counts): the same
+// elimination on one 256-thread block per problem with the matrices in LDS
+// (blk_la.hpp).  Per stage k (value function (P, p) of stage k + 1):
+//     P~ = sum_j (-rho_dyn P)^j P   (the same trace-bounded Neumann series),
+//     G = P~ E~,  M = H~ + E~^T G + D^T rho D,
+//     lp = h~ + G^T (c - rho_dyn p) + E~^T p - D^T rho g   (stage 0: D's u columns),
+// then the m u-pivots of M (L-form record, as the serial solver's FR_k) leave
+// P_k, p_k.  Record per stage: [L(:, 0:m) | lu' | p_{k+1} | P~_{k+1}] (fp64).
+// LDS: XA (n x s: P, then G), XB (n x s: the Neumann term), Mb (s x s: E~,
+// then M), Pt (n x n: P~), vectors.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int KW_VL = 64;
+}
+
+__device__ __forceinline__ int kw_fs(int n, int m) { return (n + m) * m + m + n + n * n; }
+
+static size_t kw_smem_bytes(int n, int s) { return (size_t)(2 * n * s + s * s + n * n + 8 * KW_VL) * sizeof(double); }
+
+__global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    __shared__ int s_bad;
+    const int tid = threadIdx.x;
+    const long long b = blockIdx.x;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, FS = kw_fs(n, m);
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    const double *Db = A.D ? A.D + b * (long long)sh.ndD : nullptr;
+    const double *gb = A.gw + b * (long long)sh.ny;
+    const double *ib = A.irho ? A.irho + b * (long long)sh.ny : nullptr;
+    double *RB = A.rec + b * (long long)N * FS;
+    const double rd = A.rho_dyn;
+    double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Pt = Mb + s * s, *vec = Pt + n * n;
+    double *pv = vec, *cv = vec + KW_VL, *lp = vec + 2 * KW_VL, *t1 = vec + 3 * KW_VL, *rq = vec + 4 * KW_VL,
+           *gq = vec + 5 * KW_VL;
+    int fail_stage = -1;
+    // ---- terminal: P_N = H~_N + D_N^T rho D_N, p_N = h~_N - D_N^T rho g_N ----
+    {
+        const int ncN = A.y_off[N + 1] - A.y_off[N];
+        const double *DN = Db ? Db + A.d_off[N] : nullptr;
+        const double *gN = gb + A.y_off[N], *iN = ib ? ib + A.y_off[N] : nullptr;
+        if (tid == 0) s_bad = 0;
+        for (int q = tid; q < ncN; q += BLK_THREADS) {
+            rq[q] = 1.0 / iN[q];
+            gq[q] = gN[q];
+        }
+        __syncthreads();
+        const double *HN = Hb + (long long)N * sh.ps;
+        for (int q = tid; q < n * n; q += BLK_THREADS) {
+            const int i = q % n, j = q / n;
+            double v = HN[i >= j ? pidx(i, j, n) : pidx(j, i, n)];
+            for (int r = 0; r < ncN; ++r) v = __builtin_fma(DN[r + i * ncN] * rq[r], DN[r + j * ncN], v);
+            XA[q] = v;
+            if (i == j && psd_bad(v)) s_bad = 1;
+        }
+        for (int i = tid; i < n; i += BLK_THREADS) {
+            double v = hb[(long long)N * s + i];
+            for (int r = 0; r < ncN; ++r) v = __builtin_fma(-DN[r + i * ncN] * rq[r], gq[r], v);
+            pv[i] = v;
+        }
+        __syncthreads();
+        if (s_bad) fail_stage = N;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+        double *Rk = RB + (long long)k * FS;
+        const int nck = A.y_off[k + 1] - A.y_off[k];
+        const double *Dk = Db ? Db + A.d_off[k] : nullptr;
+        // ---- P~ = sum_j (-rho_dyn P)^j P, terms while (rho_dyn |tr P|)^(j+1) > 1e-16 ----
+        double tr = 0.0;
+        for (int i = 0; i < n; ++i) tr += XA[i + i * n];  // every thread (LDS broadcast)
+        const double e = rd * fabs(tr);
+        blk_copy(Pt, n, mv_n(XA, n), n, n);
+        blk_copy(XB, n, mv_n(XA, n), n, n);
+        double ej = e;
+        for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // block-uniform
+            blk_mm(XB, n, mv_n(XA, n), mv_n(XB, n), n, n, n, -rd, 0.0, mv_none(), false);
+            for (int q = tid; q < n * n; q += BLK_THREADS) Pt[q] += XB[q];
+            ej *= e;
+        }
+        // ---- record: p_{k+1}, P~_{k+1}; stage inputs ----
+        for (int q = tid; q < n; q += BLK_THREADS) Rk[s * m + m + q] = pv[q];
+        for (int q = tid; q < n * n; q += BLK_THREADS) Rk[s * m + m + n + q] = Pt[q];
+        for (int q = tid; q < n; q += BLK_THREADS) {
+            cv[q] = cb[(long long)k * n + q];
+            t1[q] = __builtin_fma(-rd, pv[q], cb[(long long)k * n + q]);  // c - rho_dyn p
+        }
+        for (int q = tid; q < nck; q += BLK_THREADS) {
+            rq[q] = 1.0 / ib[A.y_off[k] + q];
+            gq[q] = gb[A.y_off[k] + q];
+        }
+        blk_copy(Mb, n, mv_n(Eb + (long long)k * n * s, n), n, s);  // E~
+        blk_mm(XA, n, mv_n(Pt, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // G = P~ E~
+        // lp = h~ + G^T (c - rho_dyn p) + E~^T p - D^T rho g
+        if (tid < s) {
+            const int j = tid;
+            double a = hb[(long long)k * s + j];
+            for (int i = 0; i < n; ++i) {
+                a = __builtin_fma(XA[i + j * n], t1[i], a);
+                a = __builtin_fma(Mb[i + j * n], pv[i], a);
+            }
+            if (k > 0 || j < m)
+                for (int r = 0; r < nck; ++r) a = __builtin_fma(-Dk[r + j * nck] * rq[r], gq[r], a);
+            lp[j] = a;
+        }
+        // M = H~ + E~^T G (in place over E~), then + D^T rho D
+        blk_mm(Mb, s, mv_t(Mb, n), mv_n(XA, n), s, s, n, 1.0, 0.0, mv_pk(Hb + (long long)k * sh.ps, s), true);
+        if (nck > 0) {
+            for (int q = tid; q < s * s; q += BLK_THREADS) {
+                const int i = q % s, j = q / s;
+                if (i < j || (k == 0 && i >= m)) continue;  // lower; stage 0: u columns only
+                double v = Mb[q];
+                for (int r = 0; r < nck; ++r) v = __builtin_fma(Dk[r + i * nck] * rq[r], Dk[r + j * nck], v);
+                Mb[q] = v;
+            }
+            __syncthreads();
+        }
+        // ---- the m u-pivots (one barrier per pivot), L-form record ----
+        bool ok = true;
+        if (tid == 0) s_bad = 0;
+        for (int j = 0; j < m; ++j) {
+            const double d = Mb[j + j * s];
+            ok = ok && d > 0.0;
+            const double inv2 = 1.0 / d, invs = rsqrt_f64(d);
+            const double lpj = lp[j];
+            if (tid < s) Rk[j * s + tid] = tid >= j ? Mb[tid + j * s] * invs : 0.0;
+            if (tid == 255) Rk[s * m + j] = lpj * invs;
+            const int i = tid & 127, hh = tid >> 7;
+            if (i > j && i < s) {
+                const double lij = Mb[i + j * s] * inv2;
+                for (int l = j + 1 + hh; l <= i; l += 2) Mb[i + l * s] = __builtin_fma(-lij, Mb[l + j * s], Mb[i + l * s]);
+                if (hh == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
+            }
+            __syncthreads();
+        }
+        // ---- P_k, p_k ----
+        for (int q = tid; q < n * n; q += BLK_THREADS) {
+            const int i = q % n, j = q / n;
+            const int hi = i > j ? i : j, lo = i > j ? j : i;
+            const double v = Mb[(m + hi) + (m + lo) * s];
+            XA[q] = v;
+            if (i == j && psd_bad(v)) s_bad = 1;
+        }
+        for (int q = tid; q < n; q += BLK_THREADS) pv[q] = lp[m + q];
+        __syncthreads();
+        if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
+    }
+    if (tid == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+// forward: the L-form rollout (k_riccati_fwd_big) plus the lambda correction
+// x+ = v - rho_dyn (P~ (v - rho_dyn p) + p), v = A x + B u + c; one wave per problem
+__global__ __launch_bounds__(64) void k_kkt_ric_fwd_wide(Shape sh, const double *__restrict__ E,
+                                                        const double *__restrict__ c, const double *__restrict__ RB,
+                                                        const double *__restrict__ x0, double *__restrict__ x0acc,
+                                                        double *__restrict__ ws, double rho_dyn) {
+    __shared__ double w[64], sz[64], sx0[64];
+    const int lane = wave_lane();
+    const long long b = blockIdx.x;
+    const int n = sh.n, m = sh.m, N = sh.N, s = sh.s, FS = kw_fs(n, m);
+    const double *Eb = E + b * sh.perE;
+    const double *cb = c + b * sh.perc;
+    const double *Rb = RB + b * (long long)N * FS;
+    double *wb = ws + b * sh.perh;
+    if (lane < n) {  // update_rhs_initial_stage accumulates: the solve sees the sum of the x0s
+        const double x = x0[b * n + lane];
+        const double xa = x0acc[b * n + lane] + x;
+        x0acc[b * n + lane] = xa;
+        w[m + lane] = xa;
+        sx0[lane] = x;
+    }
+    wave_sync();
+    for (int k = 0; k < N; ++k) {
+        const double *Fk = Rb + (long long)k * FS;
+        double v = 0.0;
+        if (lane < m) {
+            double a = Fk[(long long)s * m + lane];
+            for (int i = 0; i < n; ++i) a = __builtin_fma(Fk[(long long)lane * s + m + i], w[m + i], a);
+            v = -a;
+        }
+        for (int j = m - 1; j >= 0; --j) {
+            const double uj = readlane_f64(v, j) / Fk[(long long)j * s + j];
+            if (lane == j) v = uj;
+            else if (lane < j) v = __builtin_fma(-Fk[(long long)lane * s + j], uj, v);
+        }
+        if (lane < m) w[lane] = v;
+        wave_sync();
+        if (lane < s) wb[(long long)k * s + lane] = lane < m ? v : (k == 0 ? sx0[lane - m] : w[lane]);
+        const double *pk = Fk + s * m + m, *Ptk = pk + n;
+        double a = 0.0;
+        if (lane < n) {
+            const double *Ek = Eb + (long long)k * n * s;
+            a = cb[(long long)k * n + lane];
+            for (int j = 0; j < s; ++j) a = __builtin_fma(Ek[lane + (long long)j * n], w[j], a);
+            sz[lane] = __builtin_fma(-rho_dyn, pk[lane], a);  // v - rho_dyn p
+        }
+        wave_sync();
+        if (lane < n) {
+            double y = 0.0;
+            for (int t = 0; t < n; ++t) y = __builtin_fma(Ptk[lane + t * n], sz[t], y);
+            a = __builtin_fma(-rho_dyn, y + pk[lane], a);
+        }
+        wave_sync();
+        if (lane < n) w[m + lane] = a;
+        wave_sync();
+    }
+    if (lane < n) wb[(long long)N * s + lane] = w[m + lane];
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static bool kric_al(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // The Riccati-ordered KKT path applies: 12/4, the same row count nc in {0, 4}
-// on every stage k < N (nc_N <= 4), 16-byte aligned per-problem blocks.
-int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs) {
+// on every stage k < N (nc_N <= 4), 16-byte aligned per-problem blocks; the
+// LDS kernels where the block LDL^T tiles do not fit (n + m or n + nc_k > 32,
+// ldl_fits false) up to n + m <= 64, any ncs.
+int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs, bool ldl_fits) {
+    if (!ldl_fits && sh.s <= 64) {
+        for (int k = 0; k <= sh.N; ++k)
+            if (ncs[k] > 64) return -1;  // the per-stage rho / g slots of k_kkt_ric_bwd_wide
+        return KKT_RIC_WIDE;
+    }
     if (sh.n != 12 || sh.m != 4 || getenv("PDPLQR_KKT_LDL")) return -1;
     const int nc = ncs[0];
     if (nc != 0 && nc != 4) return -1;
@@ -460,12 +681,41 @@ int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs) {
     return nc;
 }
 
-size_t kkt_ric_rec_doubles(const Shape &sh) { return (size_t)sh.N * KRecShape<12, 4>::FS; }
+size_t kkt_ric_rec_doubles(const Shape &sh, int ric) {
+    if (ric == KKT_RIC_WIDE) return (size_t)sh.N * ((size_t)sh.s * sh.m + sh.m + sh.n + (size_t)sh.n * sh.n);
+    return (size_t)sh.N * KRecShape<12, 4>::FS;
+}
 
 int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
                             int32_t *status, hipStream_t st) {
+    if (nc == KKT_RIC_WIDE) {
+        KKTRicArgs a;
+        a.sh = sh;
+        a.E = E;
+        a.c = c;
+        a.D = sh.ndD > 0 ? D : nullptr;
+        a.Hw = Hw;
+        a.hw = hw;
+        a.gw = gw;
+        a.irho = sh.ny > 0 ? irho : nullptr;
+        a.d_off = d_off;
+        a.y_off = y_off;
+        a.rec = rec;
+        a.status = status;
+        a.rho_dyn = rho_dyn;
+        a.nc_last = nc_last;
+        const size_t sm = kw_smem_bytes(sh.n, sh.s);
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_kkt_ric_bwd_wide),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm) != hipSuccess) {
+            set_error("KKT backward (wide): LDS request too large");
+            return PDPLQR_ERR_HIP;
+        }
+        hipLaunchKernelGGL(k_kkt_ric_bwd_wide, dim3((unsigned)sh.batch), dim3(256), sm, st, a);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     if (!kric_al(E) || !kric_al(c) || !kric_al(Hw) || !kric_al(hw) || (nc && (!kric_al(D) || !kric_al(gw) || !kric_al(irho))))
         return PDPLQR_ERR_UNSUPPORTED;
     KKTRicArgs a;
@@ -490,7 +740,13 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
 }
 
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
-                           double *x0acc, double *ws, double rho_dyn, hipStream_t st) {
+                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric) {
+    if (ric == KKT_RIC_WIDE) {
+        hipLaunchKernelGGL(k_kkt_ric_fwd_wide, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc,
+                           ws, rho_dyn);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     hipLaunchKernelGGL(k_kkt_ric_fwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
                        rho_dyn);
     PDPLQR_HIP_TRY(hipGetLastError());

@@ -79,6 +79,17 @@ int launch_fold_shards(const double *elems, int R, int r, int n, int batch, doub
                        int *has_suf, int *flag, bool lu, hipStream_t st);
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
                           double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
+// wide shapes (kernels_wide.hip): 32 < n + m <= 64 stage kernels, 32 < n element kernels
+bool wide_state(int n);
+bool wide_stage(const Shape &sh);
+int wide_seg_backward_slots(const Shape &sh, int device);
+int wide_scan_slots(int n, int device);
+int launch_seg_backward_wide(const SegArgs &a, hipStream_t st);
+int launch_seg_scan_wide(const ScanArgs &a, int batch, hipStream_t st);
+int launch_seg_maps_wide(const MapArgs &a, int batch, hipStream_t st);
+int launch_map_scan_wide(const MapScanArgs &a, int batch, hipStream_t st);
+int launch_riccati_forward_seg_big(const Shape &sh, const double *E, const double *c, const double *FR,
+                                   const SegFwd &sf, double *ws, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st);
 

@@ -82,7 +82,7 @@ static RiccatiArgs riccati_args(pdplqr_handle h) {
 
 static int parallel_init(pdplqr_handle h) {
     const Shape &sh = h->sh;
-    if (sh.s > 32) return unsupported("PARALLEL solver with n + m > 32");
+    if (sh.s > 64) return unsupported("PARALLEL solver with n + m > 64");
     ParallelState *ps = new ParallelState();
     h->par = ps;
     const int ns = h->cfg.num_segments;

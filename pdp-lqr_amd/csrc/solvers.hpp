@@ -31,15 +31,17 @@ int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double
 int kkt_backward(pdplqr_handle h, const double *inv_rho);
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws);
 int kkt_dim(pdplqr_handle h);
-int kkt_before_model(pdplqr_handle h);
-bool kkt_ric_active(pdplqr_handle h);  // the Riccati-ordered path serves this handle  // set_model on a formed KKT handle: keep the frozen matrix
-// Riccati-ordered KKT path (kkt_riccati.hip): nc of the uniform row layout, or -1
-int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs);
-size_t kkt_ric_rec_doubles(const Shape &sh);  // rollout record doubles per problem
+int kkt_before_model(pdplqr_handle h);  // set_model on a formed KKT handle: keep the frozen matrix
+bool kkt_ric_active(pdplqr_handle h);  // the Riccati-ordered path serves this handle
+// Riccati-ordered KKT path (kkt_riccati.hip): nc of the uniform 12/4 row
+// layout, KKT_RIC_WIDE for the LDS kernels (any ncs, n + m <= 64), or -1
+constexpr int KKT_RIC_WIDE = 1000;
+int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs, bool ldl_fits);
+size_t kkt_ric_rec_doubles(const Shape &sh, int ric);  // rollout record doubles per problem
 int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
                             int32_t *status, hipStream_t st);
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
-                           double *x0acc, double *ws, double rho_dyn, hipStream_t st);
+                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric);
 }  // namespace pdplqr
