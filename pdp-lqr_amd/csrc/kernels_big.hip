@@ -22,6 +22,7 @@
 #include "parallel.hpp"
 
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace pdplqr {
 
@@ -265,7 +266,11 @@ __global__ __launch_bounds__(64) void k_riccati_fwd_big(Shape sh, const double *
 
 bool big_shape(const Shape &sh) { return sh.s > 32 && sh.s <= BS; }
 
+int launch_riccati_backward_value_wide(const RiccatiArgs &r, hipStream_t st);  // kernels_wide.hip
+
 int launch_riccati_backward_big(const RiccatiArgs &a, hipStream_t st) {
+    // keep_factors = 0: the value form (m pivots a stage, MFMA products)
+    if (!a.Lc && !getenv("PDPLQR_BIG_LFORM")) return launch_riccati_backward_value_wide(a, st);
     hipLaunchKernelGGL(k_riccati_bwd_big, dim3(a.sh.batch), dim3(BT), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;

@@ -970,6 +970,7 @@ __global__ __launch_bounds__(64) void k_rank_chain(const double *maps, const dou
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
                           double *maps, double *out_pre, int *flag, bool lu, hipStream_t st) {
     if (r <= 0) return PDPLQR_OK;
+    if (wide_state(n)) return launch_rank_fold_maps_wide(elems, suf, x0, R, r, n, batch, maps, out_pre, flag, lu, st);
     const int T = tile_order(n);
     const dim3 gm(batch * r), blk(64);
     if (T == 1) {

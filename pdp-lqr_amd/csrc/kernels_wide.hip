@@ -274,6 +274,74 @@ __global__ __launch_bounds__(256) void k_map_scan_wide(MapScanArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// horizon shards, log-depth prefix (k_rank_maps / k_rank_chain): the boundary
+// map of rank element e_j under V_{j+1} (suffix entry j + 1 of the rank scan),
+// then their application to x0 in turn
+// ---------------------------------------------------------------------------
+template <bool LU>
+__global__ __launch_bounds__(256) void k_rank_maps_wide(const double *elems_all, const double *suf, int R, int r,
+                                                        int n, int batch, double *maps, int *flag) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / r;
+    const int j = blockIdx.x % r;
+    const ElemIn e = elem_in(elems_all + ((long long)j * batch + b) * es, n);  // rank-major all-gather
+    const double *v = suf + (b * R + j + 1) * (long long)es;                  // V_{j+1}
+    const WideSmem sm = wide_smem(wbuf, n);
+    double *B0 = sm.B[0], *pv = sm.v[0], *v2 = sm.v[2];
+    double *mo = maps + (b * r + j) * (long long)mw;
+    blk_copy(B0, n, mv_n(e.C, n), n, n);
+    blk_vcopy(pv, v + 3 * nn + n, n);
+    blk_mv(v2, mv_n(B0, n), pv, n, n, -1.0, e.f);  // f - C p
+    double *Y, *Z, *Fr;
+    const bool ok = wide_core(sm, v + 2 * nn + n, n, LU, &Y, &Z, &Fr);
+    blk_mv(mo + nn, mv_n(Z, n), v2, n, n, 1.0, nullptr);                               // Z (f - C p)
+    blk_mm(mo, n, mv_n(Z, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);  // Z F
+    if (!ok && threadIdx.x == 0) atomicOr(flag + b, 4);
+}
+
+__global__ __launch_bounds__(64) void k_rank_chain_wide(const double *maps, const double *x0, int r, int n,
+                                                        double *out_pre_all) {
+    __shared__ double xa[64], xb[64];
+    const int lane = threadIdx.x;
+    const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x;
+    if (lane < n) xa[lane] = x0[b * n + lane];
+    wave_sync();
+    double *x = xa, *y = xb;
+    for (int j = 0; j < r; ++j) {  // x <- Phi_j x + phi_j
+        const double *mo = maps + (b * r + j) * (long long)mw;
+        if (lane < n) {
+            double a = mo[nn + lane];
+            for (int t = 0; t < n; ++t) a = __builtin_fma(mo[lane + t * n], x[t], a);
+            y[lane] = a;
+        }
+        wave_sync();
+        double *t = x;
+        x = y;
+        y = t;
+    }
+    double *out = out_pre_all + b * es;
+    for (int q = lane; q < es; q += 64) out[q] = (q >= 2 * nn && q < 2 * nn + n) ? x[q - 2 * nn] : 0.0;
+}
+
+int launch_rank_fold_maps_wide(const double *elems, const double *suf, const double *x0, int R, int r, int n,
+                               int batch, double *maps, double *out_pre, int *flag, bool lu, hipStream_t st) {
+    const size_t sm = wide_elem_smem_bytes(n);
+    const void *k = lu ? reinterpret_cast<const void *>(&k_rank_maps_wide<true>)
+                       : reinterpret_cast<const void *>(&k_rank_maps_wide<false>);
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm) != hipSuccess) {
+        set_error("rank maps (n > 32): LDS request too large");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    void *args[] = {const_cast<double **>(&elems), const_cast<double **>(&suf), &R, &r, &n, &batch, &maps, &flag};
+    PDPLQR_HIP_TRY(hipLaunchKernel(k, dim3((unsigned)(batch * r)), dim3(256), args, sm, st));
+    hipLaunchKernelGGL(k_rank_chain_wide, dim3((unsigned)batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // segment backward (k_seg_bwd_aug) for n + m > 32
 // LDS: XA (n x s: P, then P E~), XB (n x s: F at column offset 0 or m, then
 // F E~), Mb (s x s: E~, then the stage matrix), Cm (n x n), vectors.
@@ -289,8 +357,8 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     const int n = sh.n, m = sh.m, s = n + m, S = A.S;
     const long long bi = blockIdx.x / S;
     const int seg = blockIdx.x % S;
-    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
-    const bool last = (seg == S - 1) && A.last_is_terminal;
+    const int N0 = A.serial ? 0 : A.seg_start[seg], N1 = A.serial ? sh.N : N0 + A.seg_len[seg];
+    const bool last = A.serial || ((seg == S - 1) && A.last_is_terminal);
     const long long frs = (long long)s * m + m;
     const int ps = sh.ps;
     const double *Eb = A.E + bi * sh.perE;
@@ -298,7 +366,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     const double *Hb = A.Hw + bi * sh.perHw;
     const double *hb = A.hw + bi * sh.perh;
     double *FRb = A.FR + bi * sh.perKD;
-    double *Gb = A.G + bi * (long long)sh.N * m * n;
+    double *Gb = A.G ? A.G + bi * (long long)sh.N * m * n : nullptr;
     double *Lcb = A.Lc ? A.Lc + bi * sh.perHw : nullptr;
     double *lpb = A.lpc ? A.lpc + bi * sh.perh : nullptr;
     double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Cm = Mb + s * s, *vec = Cm + n * n;
@@ -403,6 +471,10 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         __syncthreads();
         if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
     }
+    if (A.serial) {
+        if (tid == 0) A.seg_status[bi] = fail_stage < 0 ? 0 : fail_stage + 1;
+        return;
+    }
     // ---- export the element (update_segment_data, lqr_solver_parallel.hpp:182-187) ----
     double *eo = A.elem + (bi * S + seg) * (long long)(3 * n * n + 2 * n);
     double *eF = eo, *eC = eo + n * n, *ef = eo + 2 * n * n, *eP = ef + n, *ep = eP + n * n;
@@ -449,6 +521,35 @@ int wide_scan_slots(int n, int device) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_wide<false>, 256, sm) != hipSuccess || per <= 0)
         per = 1;
     return cus * per;
+}
+
+// the serial backward in value form (keep_factors = 0: no L_k cache to fill):
+// the m u-pivots per stage instead of the full s-pivot factorisation of
+// k_riccati_bwd_big; the same rollout record [L(:, 0:m) | lu'].
+int launch_riccati_backward_value_wide(const RiccatiArgs &r, hipStream_t st) {
+    SegArgs a{};
+    a.sh = r.sh;
+    a.S = 1;
+    a.last_is_terminal = 1;
+    a.E = r.E;
+    a.c = r.c;
+    a.Hw = r.Hw;
+    a.hw = r.hw;
+    a.FR = r.KD;
+    a.G = nullptr;
+    a.Lc = nullptr;
+    a.lpc = r.lpc;
+    a.elem = nullptr;
+    a.seg_status = r.status;
+    a.serial = 1;
+    const size_t sm = wide_seg_smem_bytes(a.sh.n, a.sh.s);
+    if (!wide_attr_set(reinterpret_cast<const void *>(&k_seg_bwd_wide), sm)) {
+        set_error("backward (n + m > 32): LDS request too large");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL(k_seg_bwd_wide, dim3((unsigned)a.sh.batch), dim3(256), sm, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
 }
 
 int launch_seg_backward_wide(const SegArgs &a, hipStream_t st) {

@@ -1389,7 +1389,7 @@ int kkt_init(pdplqr_handle h) {
         dmax = std::max(dmax, ks->gdim[k]);
     }
     ks->dim = dof;
-    const long long B = sh.batch, PP = (long long)ks->P * ks->P;
+    const long long B = sh.batch;
     int rc;
     ks->ric = kkt_ric_nc(sh, h->ncs, dmax <= 32);
     if (ks->ric >= 0) {  // Riccati-ordered path: no tile buffers
@@ -1403,6 +1403,7 @@ int kkt_init(pdplqr_handle h) {
     }
     // P = 16 also needs stage 0's y columns beside the lambda_1 columns of G_0 (PPK)
     ks->P = dmax <= 16 && n + h->ncs[0] <= 16 ? 16 : 32;
+    const long long PP = (long long)ks->P * ks->P;
     // row descriptors (kind, stage, index)
     std::vector<int4> rows(ks->dim);
     for (int k = 0; k <= N; ++k) {

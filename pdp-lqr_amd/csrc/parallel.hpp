@@ -15,6 +15,8 @@ struct SegArgs {
     double *Lc, *lpc;          // factor cache (nullable)
     double *elem;              // [b][S][3 n^2 + 2 n]
     int32_t *seg_status;       // [b][S]
+    int serial = 0;            // k_seg_bwd_wide as the serial value-form backward: one segment [0, N),
+                               // no element, status per problem (seg_start / seg_len unused)
 };
 
 struct ScanArgs {
@@ -88,6 +90,8 @@ int launch_seg_backward_wide(const SegArgs &a, hipStream_t st);
 int launch_seg_scan_wide(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps_wide(const MapArgs &a, int batch, hipStream_t st);
 int launch_map_scan_wide(const MapScanArgs &a, int batch, hipStream_t st);
+int launch_rank_fold_maps_wide(const double *elems, const double *suf, const double *x0, int R, int r, int n,
+                               int batch, double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
 int launch_riccati_forward_seg_big(const Shape &sh, const double *E, const double *c, const double *FR,
                                    const SegFwd &sf, double *ws, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,

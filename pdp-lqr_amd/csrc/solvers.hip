@@ -601,6 +601,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
     // one-wave chain combine: the log-depth form wins for every rank
     if (R > 1 && seg_scan_mw(sh.n, h->cfg.condensed_type == PDPLQR_CONDENSED_LU)) use_scan = true;
     if (const char *f = getenv("PDPLQR_SHARD_FOLD")) use_scan = R > 1 && f[0] == 's';
+    if (wide_state(sh.n)) use_scan = R > 1;  // the n > 32 element kernels fold by the scan form only
     int rc;
     const double *left = nullptr, *right = nullptr;
     long long rstride = 0;
@@ -641,7 +642,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
                 return rc;
             left = ps->left;
         }
-    } else {
+    } else if (R > 1) {
         rc = launch_fold_shards(delems, num_shards, shard_id, sh.n, sh.batch, ps->left, ps->right, ps->has_suf,
                                 ps->flag, h->cfg.condensed_type == PDPLQR_CONDENSED_LU, h->stream);
         if (rc) return rc;

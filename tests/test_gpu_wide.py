@@ -163,3 +163,15 @@ def test_wide_kkt_matches_oracle(n, m, nc):
         o.update_problem_data(p["ws"][b], p["ys"][b], p["zs"][b], p["irho"][b], 1e-6)
         o.backward(p["irho"][b])
         assert rel_err(out[b], o.forward(p["x0"][b])) < TOL, b
+
+
+@pytest.mark.parametrize("n,m,N,batch,R,seglen", [(40, 20, 60, 2, 3, 4), (32, 16, 48, 1, 4, 0), (20, 30, 40, 2, 2, 3)])
+def test_wide_horizon_shards_match_oracle(n, m, N, batch, R, seglen):
+    """Horizon shards (pdplqr_shard_backward / shard_forward) on the wide
+    shapes: virtual ranks in one process against the serial oracle (the n > 32
+    element kernels fold the gathered rank elements by the scan form)."""
+    from test_gpu_horizon import _run_virtual
+
+    got, ref = _run_virtual(n, m, N, batch, R, seglen)
+    for b in range(batch):
+        assert rel_err(got[b], ref[b]) < TOL, b
