@@ -337,15 +337,16 @@ def pattern_ceiling_ms(dev, n, m, N, batch, reps=5):
     return res
 
 
-def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
+def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096, n=12, m=4):
     """C3: batch 4096 independent LQRs, N = 256, 12/4 (MPC-style batched solve):
     backward + forward of the serial solver, as the headline line, plus an
-    oracle check of two problems."""
+    oracle check of two problems.  Also the wide-shape line (VERDICT r2 item 5:
+    24/16, batch 1024 -- kernels_wide.hip's value-form backward on 256-thread
+    blocks and k_riccati_fwd_big)."""
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
 
-    n, m = 12, 4
     E, c, H, h, x0 = gen_batch_device(n, m, N, batch, seed=4321, device=dev)
     ws0 = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev)
     out = torch.empty_like(ws0)
@@ -372,10 +373,16 @@ def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096):
     del E, c, H, h
     torch.cuda.empty_cache()
     bst = 8 * (n * (n + m) + n + (n + m) ** 2 + (n + m)) + 8 * (n + m)  # 3,936 B at 12/4
+    wide = n + m > 32
+    kern = ("k_seg_bwd_wide", "k_riccati_fwd_big") if wide else ("k_riccati_bwd_schur", "k_rollout_dma")
+    tag = f"C3_N{N}_b{batch}" if (n, m) == (12, 4) else f"W_n{n}_m{m}_N{N}_b{batch}"
+    s_ = n + m
+    # value-form stage flops: P E (2 n^2 s), E^T (P E) lower (n s (s + 1)), u-pivots (~m s^2)
+    fl = 2 * n * n * s_ + n * s_ * (s_ + 1) + m * s_ * s_
     return {"N": N, "nx": n, "nu": m, "batch": batch, "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t,
             "status_ok": ok, "oracle_rel_err": err,
-            "roofline": roofline_block(bst, N * batch, t * 1e3, f"C3_N{N}_b{batch}",
-                                       ("k_riccati_bwd_schur", "k_rollout_dma"), kernel_desc="backward + forward")}
+            "roofline": roofline_block(bst, N * batch, t * 1e3, tag, kern, flops_stage=fl if wide else None,
+                                       kernel_desc="backward + forward")}
 
 
 def bench_factor_reuse(local, dev, dist, steps=10, warmup=3, N=1024, batch=4096):
@@ -875,6 +882,8 @@ def main():
     if not args.no_secondary:
         res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
                             "C3_batched_N256": bench_batched_c3(local, dev, dist),
+                            "wide_24x16_N256_b1024": bench_batched_c3(local, dev, dist, steps=5, warmup=2, N=256,
+                                                                      batch=1024, n=24, m=16),
                             "factor_reuse": bench_factor_reuse(local, dev, dist, N=N, batch=B),
                             "C5_conic_kkt": bench_conic(local, dev, dist),
                             "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}

@@ -92,9 +92,11 @@ typedef struct {
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,
  * CHOLESKY, rho_dyn = kkt_sigma = 1e-6).
  * Shape limits of this build (the reference is size-generic, lqr_kernel.hpp:104-147):
- * SERIAL nx + nu <= 64 (up to 32 on MFMA tiles in one wavefront, 33..64 on
- * LDS-resident stage matrices, one 256-thread block per problem); PARALLEL and
- * KKT nx + nu <= 32.  pdplqr_create returns PDPLQR_ERR_UNSUPPORTED past them. */
+ * nx + nu <= 64 for every solver: up to 32 on MFMA tiles in one wavefront,
+ * 33..64 on LDS-resident stage matrices, one 256-thread block per problem /
+ * segment / element (kernels_big.hip, kernels_wide.hip); KKT rows per stage
+ * <= 64 past the block LDL^T tiles.  pdplqr_create returns
+ * PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 
 int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out);

@@ -1,5 +1,5 @@
 """One secondary bench workload on its own (for rocprofv3 kernel traces and PMC
-passes of exactly that workload): c2 | c3 | c5 | c4 | c4slice [N].
+passes of exactly that workload): c2 | c3 | c5 | c4 [N] | wide.
 Prints the bench's JSON for it."""
 import json
 import os
@@ -26,6 +26,8 @@ def main():
     elif which == "c4":
         r = bench.bench_horizon(0, dev, None, 1, 0, int(sys.argv[2]) if len(sys.argv) > 2 else 65536, steps=3,
                                 warmup=1)
+    elif which == "wide":
+        r = bench.bench_batched_c3(0, dev, None, steps=3, warmup=1, N=256, batch=1024, n=24, m=16)
     else:
         raise SystemExit(f"unknown workload {which}")
     print(json.dumps(r), flush=True)
