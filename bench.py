@@ -865,6 +865,9 @@ def main():
     copy_gbs = measured_copy_gbs(dev)
     res["roofline"]["peak_measured_copy"] = copy_gbs
     res["roofline"]["frac_of_measured_copy"] = achieved / copy_gbs
+    res["roofline"]["note"] = ("achieved/frac count the SURVEY 8(d) algorithmic bytes (dense s x s H~); the kernel "
+                               "reads the packed H~ (s(s+1)/2 doubles), so it moves fewer bytes than that figure and "
+                               "frac_of_measured_copy can exceed 1; frac_moved uses the counter bytes")
     pat = pattern_ceiling_ms(dev, n, m, N, B)
     if pat is not None:
         # the kernels' own access pattern with nothing on the chain: the time

@@ -3,6 +3,7 @@
 // (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
 #include "combine_mw.hpp"
 #include "combine_tiles.hpp"
+#include "parallel.hpp"
 
 // out = a (x) b on the device (one wave), elements in host memory; LU: the
 // LU form of the combine (CondensedSystemSolverType::LU).
@@ -15,7 +16,7 @@ __global__ __launch_bounds__(64) void k_debug_combine(const double *a, const dou
 
 extern "C" int pdplqr_debug_combine_form(int n, const double *a, const double *b, double *out, int lu) {
     using namespace pdplqr;
-    const int T = n <= 16 ? 1 : (n <= 32 ? 2 : 0);
+    const int T = n <= 16 ? 1 : (n <= 32 ? 2 : (n <= 64 ? 4 : 0));  // 4: the LDS kernels (kernels_wide.hip)
     if (!T) return PDPLQR_ERR_UNSUPPORTED;
     const size_t es = (size_t)(3 * n * n + 2 * n) * sizeof(double);
     double *d = nullptr;
@@ -26,7 +27,10 @@ extern "C" int pdplqr_debug_combine_form(int n, const double *a, const double *b
     PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
     const double *da = d, *db = (const double *)((char *)d + es);
     double *dout = (double *)((char *)d + 2 * es);
-    if (T == 1 && lu) hipLaunchKernelGGL((k_debug_combine<1, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
+    if (T == 4) {
+        const int rc = launch_debug_combine_wide(da, db, dout, n, dok, lu != 0);
+        if (rc) return rc;
+    } else if (T == 1 && lu) hipLaunchKernelGGL((k_debug_combine<1, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     else if (T == 1) hipLaunchKernelGGL((k_debug_combine<1, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     else if (lu) hipLaunchKernelGGL((k_debug_combine<2, true>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);
     else hipLaunchKernelGGL((k_debug_combine<2, false>), dim3(1), dim3(64), 0, 0, da, db, dout, n, dok);

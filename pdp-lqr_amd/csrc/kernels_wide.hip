@@ -347,7 +347,48 @@ int launch_rank_fold_maps_wide(const double *elems, const double *suf, const dou
 // F E~), Mb (s x s: E~, then the stage matrix), Cm (n x n), vectors.
 // ---------------------------------------------------------------------------
 static size_t wide_seg_smem_bytes(int n, int s) {
-    return (size_t)(2 * n * s + s * s + n * n + 8 * VL) * sizeof(double);
+    return (size_t)(2 * n * s + s * s + n * n + s * (s + 1) / 2 + 8 * VL) * sizeof(double);
+}
+
+// Stage inputs of stage k in flight in registers (issued before the pivot
+// loop of stage k + 1, written to LDS after it): E~ (<= 16 per thread), packed
+// H~ (<= 9), c, h~.
+struct WideIn {
+    double E[16], H[9], c, h;
+};
+
+__device__ __forceinline__ void wide_in_load(WideIn &in, const double *Ek, const double *Hk, const double *ck,
+                                             const double *hk, int n, int s, int ps) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = tid + q * BLK_THREADS;
+        in.E[q] = i < n * s ? Ek[i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const int i = tid + q * BLK_THREADS;
+        in.H[q] = i < ps ? Hk[i] : 0.0;
+    }
+    in.c = tid < n ? ck[tid] : 0.0;
+    in.h = tid < s ? hk[tid] : 0.0;
+}
+
+__device__ __forceinline__ void wide_in_store(const WideIn &in, double *Es, double *Hs, double *cv, double *hv, int n,
+                                              int s, int ps) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = tid + q * BLK_THREADS;
+        if (i < n * s) Es[i] = in.E[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const int i = tid + q * BLK_THREADS;
+        if (i < ps) Hs[i] = in.H[q];
+    }
+    if (tid < n) cv[tid] = in.c;
+    if (tid < s) hv[tid] = in.h;
 }
 
 __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
@@ -369,11 +410,16 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     double *Gb = A.G ? A.G + bi * (long long)sh.N * m * n : nullptr;
     double *Lcb = A.Lc ? A.Lc + bi * sh.perHw : nullptr;
     double *lpb = A.lpc ? A.lpc + bi * sh.perh : nullptr;
-    double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Cm = Mb + s * s, *vec = Cm + n * n;
+    double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Cm = Mb + s * s, *Hs = Cm + n * n,
+           *vec = Hs + s * (s + 1) / 2;
     double *pv = vec, *fv = vec + VL, *cv = vec + 2 * VL, *hv = vec + 3 * VL, *pc = vec + 4 * VL,
            *fy = vec + 5 * VL, *lp = vec + 6 * VL, *sinv = vec + 7 * VL;
     __shared__ int s_bad;
     int fail_stage = -1;
+    WideIn nxt;
+    if (N1 > N0)  // stage N1 - 1's inputs, in flight during the terminal
+        wide_in_load(nxt, Eb + (long long)(N1 - 1) * n * s, Hb + (long long)(N1 - 1) * ps, cb + (long long)(N1 - 1) * n,
+                     hb + (long long)(N1 - 1) * s, n, s, ps);
     // ---- segment terminal: the real one (P = H~_N, p = h~_N, F = 0) or the
     //      dummy (P = 0, p = 0, F = I, C = 0, f = 0) ----
     {
@@ -398,26 +444,25 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
             if (lpb)
                 for (int t = tid; t < n; t += BLK_THREADS) lpb[(long long)sh.N * s + t] = hb[(long long)sh.N * s + t];
         }
+        if (N1 > N0) wide_in_store(nxt, Mb, Hs, cv, hv, n, s, ps);
         __syncthreads();
         if (s_bad) fail_stage = sh.N;
     }
     const double *Fp = XB;  // F (n x n, ld n) inside XB
     const bool yon = !last;  // the y block (F, C, f) is identically zero on the last segment
     for (int k = N1 - 1; k >= N0; --k) {
-        const double *Ek = Eb + (long long)k * n * s;
-        blk_copy(Mb, n, mv_n(Ek, n), n, s);  // E~ (n x s)
-        for (int q = tid; q < s; q += BLK_THREADS) {
-            hv[q] = hb[(long long)k * s + q];
-            if (q < n) cv[q] = cb[(long long)k * n + q];
-        }
-        if (tid == 0) s_bad = 0;
-        __syncthreads();
+        // Mb = E~_k, Hs = H~_k (packed), cv = c_k, hv = h~_k (written at the end of stage k + 1)
         blk_mv(pc, mv_n(XA, n), cv, n, n, 1.0, pv);  // P c + p
+        if (tid == 0) s_bad = 0;  // every thread has read the previous stage's flag (blk_mv's barrier)
         if (yon) blk_mv(fy, mv_n(Fp, n), cv, n, n, 1.0, fv);  // F c + f
         blk_mm(XA, n, mv_n(XA, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // P E~
         if (yon) blk_mm(XB, n, mv_n(Fp, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // F E~
         blk_mv(lp, mv_t(Mb, n), pc, s, n, 1.0, hv);  // h~ + E~^T (P c + p)
-        blk_mm(Mb, s, mv_t(Mb, n), mv_n(XA, n), s, s, n, 1.0, 0.0, mv_pk(Hb + (long long)k * ps, s), true);
+        blk_mm(Mb, s, mv_t(Mb, n), mv_n(XA, n), s, s, n, 1.0, 0.0, mv_pk(Hs, s), true);
+        // stage k - 1's inputs in flight during the pivots
+        if (k > N0)
+            wide_in_load(nxt, Eb + (long long)(k - 1) * n * s, Hb + (long long)(k - 1) * ps, cb + (long long)(k - 1) * n,
+                         hb + (long long)(k - 1) * s, n, s, ps);
         // ---- eliminate the u pivots of [[M, YE^T], [YE, -C]] (one barrier per pivot) ----
         double *FRk = FRb + (long long)k * frs;
         double *Gk = Gb + (long long)k * m * n;
@@ -468,6 +513,10 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         if (yon)
             for (int q = tid; q < n; q += BLK_THREADS) fv[q] = fy[q];
         Fp = XB + m * n;
+        if (k > N0) {
+            __syncthreads();  // every read of M is done
+            wide_in_store(nxt, Mb, Hs, cv, hv, n, s, ps);
+        }
         __syncthreads();
         if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
     }
@@ -593,6 +642,27 @@ int launch_map_scan_wide(const MapScanArgs &a, int batch, hipStream_t st) {
     const size_t sm = (size_t)(a.n * a.n + 2 * VL) * sizeof(double);
     hipLaunchKernelGGL(k_map_scan_wide, dim3((unsigned)(batch * (a.S + 1))), dim3(256), sm, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// test hook (debug_hooks.hip pdplqr_debug_combine_form): out = a (x) b on one block
+template <bool LU>
+__global__ __launch_bounds__(256) void k_debug_combine_wide(const double *a, const double *b, double *out, int n,
+                                                            int *ok) {
+    extern __shared__ __attribute__((aligned(16))) double wbuf[];
+    const int nn = n * n;
+    const bool good = wide_combine(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n, elem_in(a, n),
+                                   elem_in(b, n), n, true, true, LU, wide_smem(wbuf, n));
+    if (threadIdx.x == 0) *ok = good ? 1 : 0;
+}
+
+int launch_debug_combine_wide(const double *a, const double *b, double *out, int n, int *ok, bool lu) {
+    const size_t sm = wide_elem_smem_bytes(n);
+    const void *k = lu ? reinterpret_cast<const void *>(&k_debug_combine_wide<true>)
+                       : reinterpret_cast<const void *>(&k_debug_combine_wide<false>);
+    if (!wide_attr_set(k, sm)) return PDPLQR_ERR_UNSUPPORTED;
+    void *args[] = {const_cast<double **>(&a), const_cast<double **>(&b), &out, &n, &ok};
+    PDPLQR_HIP_TRY(hipLaunchKernel(k, dim3(1), dim3(256), args, sm, 0));
     return PDPLQR_OK;
 }
 

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         }
         double w, luq[4];
         GainOut go;
-        bool ok = schur_block_pivots<MM, true>(Mn, lpr, w, luq, g, c, &go);
+        bool ok = schur_block_pivots<MM, true>(Mn, lpr, w, luq, g, c, &go, sm.col, sm.lu4);
         Pm = Mn;
 #pragma unroll
         for (int r = 0; r < 4; ++r) prow[r] = lpr[r];

@@ -90,6 +90,7 @@ int launch_seg_backward_wide(const SegArgs &a, hipStream_t st);
 int launch_seg_scan_wide(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps_wide(const MapArgs &a, int batch, hipStream_t st);
 int launch_map_scan_wide(const MapScanArgs &a, int batch, hipStream_t st);
+int launch_debug_combine_wide(const double *a, const double *b, double *out, int n, int *ok, bool lu);
 int launch_rank_fold_maps_wide(const double *elems, const double *suf, const double *x0, int R, int r, int n,
                                int batch, double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
 int launch_riccati_forward_seg_big(const Shape &sh, const double *E, const double *c, const double *FR,

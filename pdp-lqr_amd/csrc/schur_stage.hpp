@@ -67,6 +67,7 @@ struct SchurSmem {
     alignas(16) double lpt[16];  // lp_k, column -> row redistribution (colpos order)
     double inv[16];              // 1 / sqrt(pivot), u columns
     double luq[16];              // lu' = Luu^{-1} lu
+    alignas(16) double lu4[4];   // lu of the u rows (PDPLQR_SCHUR_LDSU)
     union {
         double tp[16 * PDPLQR_TP_LD];  // transpose of P_k (leading dimension: see PDPLQR_TP_LD)
         alignas(16) double rec[128];  // rollout record staging (one coalesced store per stage)
@@ -107,18 +108,56 @@ struct GainOut {
     double kq;  // k~[g] (every lane of group g)
 };
 
+// PDPLQR_SCHUR_LDSU = 1: the u rows reach the lanes through LDS instead of
+// v_readlane / permlane broadcasts -- one ds_write and 12 ds_read_b128 (LDS
+// pipe) for 14 f64 readlanes and 4 row-group broadcasts (44 VALU).
+#ifndef PDPLQR_SCHUR_LDSU
+#define PDPLQR_SCHUR_LDSU 0
+#endif
+
 template <int MM, bool GAIN = false>
 __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], double &w, double (&luq)[4], int g,
-                                                   int c, GainOut *go = nullptr) {
+                                                   int c, GainOut *go = nullptr, double *ldsu = nullptr,
+                                                   double *ldsl = nullptr) {
     static_assert(MM >= 1 && MM <= 4, "u block");
     static_assert(!GAIN || !PDPLQR_SCHUR_T4, "gain record needs the VALU W");
     double a[4][4], lu[4], L[4][4], T[4][4], inv[4];
     bool ok = true;
+#if PDPLQR_SCHUR_LDSU
+    double ml[4];  // column c of the u rows: m_l = M[l][c]
+    if constexpr (MM == 4) {
+        // lane (g, c) holds M[g][c] (register 0): stored at [c][g]; lu[g] by lanes (g, 0)
+        ldsu[4 * c + g] = M[0];
+        if (c == 0) ldsl[g] = lpr[0];
+        wave_sync();
+        const double2 *q = reinterpret_cast<const double2 *>(ldsu);
 #pragma unroll
-    for (int i = 0; i < MM; ++i) {
-        lu[i] = readlane_f64(lpr[0], 16 * i);
+        for (int j = 0; j < 4; ++j) {  // column j of Muu (uniform address: broadcast reads)
+            const double2 v0 = q[2 * j], v1 = q[2 * j + 1];
+            a[0][j] = v0.x;
+            a[1][j] = v0.y;
+            a[2][j] = v1.x;
+            a[3][j] = v1.y;
+        }
+        const double2 l0 = reinterpret_cast<const double2 *>(ldsl)[0], l1 = reinterpret_cast<const double2 *>(ldsl)[1];
+        lu[0] = l0.x;
+        lu[1] = l0.y;
+        lu[2] = l1.x;
+        lu[3] = l1.y;
+        const double2 c0 = q[2 * c], c1 = q[2 * c + 1];
+        ml[0] = c0.x;
+        ml[1] = c0.y;
+        ml[2] = c1.x;
+        ml[3] = c1.y;
+    } else
+#endif
+    {
 #pragma unroll
-        for (int j = 0; j <= i; ++j) a[i][j] = readlane_f64(M[0], 16 * i + j);  // M[i][j]: group i, lane j
+        for (int i = 0; i < MM; ++i) {
+            lu[i] = readlane_f64(lpr[0], 16 * i);
+#pragma unroll
+            for (int j = 0; j <= i; ++j) a[i][j] = readlane_f64(M[0], 16 * i + j);  // M[i][j]: group i, lane j
+        }
     }
 #pragma unroll
     for (int j = 0; j < MM; ++j) {  // right-looking Cholesky of Muu (uniform values)
@@ -161,9 +200,13 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
     w = t4_apply(t4_operand(Tz, g, c), M[0]);
 #else
     // column c of the u rows: m_l = M[l][c] (group l, register 0)
+#if PDPLQR_SCHUR_LDSU
+    if constexpr (MM != 4)
+#else
     double ml[4];
+#endif
 #pragma unroll
-    for (int l = 0; l < MM; ++l) ml[l] = bcast_group(M[0], l);
+        for (int l = 0; l < MM; ++l) ml[l] = bcast_group(M[0], l);
     w = 0.0;
     double Wc[4];  // W[c][j], j < m: this lane's row of the u columns
 #pragma unroll
@@ -252,7 +295,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
     }
     bool ok;
     if constexpr (MM > 0) {
-        ok = schur_block_pivots<MM, GAIN>(Mn, lpr[0], w, luq, g, c, go);
+        ok = schur_block_pivots<MM, GAIN>(Mn, lpr[0], w, luq, g, c, go, sm.col, sm.lu4);
         Pm = Mn;
     } else {
         d4 Mt[1][1];

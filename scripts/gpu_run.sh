@@ -15,6 +15,8 @@
 #   bench:<bench.py args, comma separated>               e.g. bench:--no-cpu,--steps,20
 #   lat                                                  scripts/ubench/lat_bench
 #   pmc:<tag>,<dominant kernel>,<script args...>         PMC passes of one workload (scripts/collect_pmc.sh)
+#   env:NAME=VALUE / unenv:NAME                          set / clear an environment variable for the later steps
+#                                                        (A/B of a variant library: env:PDPLQR_LIB=<path>)
 # outputs: gpurun_out/TAG/<step index>_<kind>.{log,json}, trace dirs under gpurun_out/TAG/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -49,6 +51,10 @@ for step in "$@"; do
       set -- $args
       ptag=$1; pdom=$2; shift 2
       TAG=$ptag DOM=$pdom OUT=$O/pmc_$ptag timeout -k 10 1200 scripts/collect_pmc.sh python3 "$@" > "$log" 2>&1 ;;
+    env)
+      export "$arg"; echo "rc=0" >> "$O/steps.log"; continue ;;
+    unenv)
+      unset "$arg"; echo "rc=0" >> "$O/steps.log"; continue ;;
     *)
       echo "unknown step $kind" | tee -a "$O/steps.log"; exit 2 ;;
   esac

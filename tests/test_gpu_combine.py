@@ -36,9 +36,10 @@ def _unpack(v, n):
             v[2 * nn + n:3 * nn + n].reshape(n, n, order="F"), v[3 * nn + n:])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 8, 12, 13, 16, 17, 20, 24, 31, 32])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 8, 12, 13, 16, 17, 20, 24, 31, 32, 33, 40, 50, 63])
 @pytest.mark.parametrize("zero_b", [False, True])
 def test_device_combine_matches_numpy(n, zero_b):
+    """n > 32: the LDS combine of kernels_wide.hip (256-thread block)."""
     from pdplqr import _lib
 
     L = _lib.lib()
@@ -112,3 +113,21 @@ def test_rsqrt_f64_full_precision():
     err = np.abs(y - ref) / ulp
     print(f"rsqrt_f64 max error {err.max():.2f} ulp")
     assert err.max() <= 2.0
+
+
+@pytest.mark.parametrize("n", [5, 24, 33, 40, 63])
+def test_device_combine_lu_form_matches_numpy(n):
+    """The LU form (Gauss-Jordan with partial pivoting, CondensedSystemLUSolver)
+    gives the same element (1e-12): tiles for n <= 32, LDS past that."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_form.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(900 + n)
+    a, b = _elem(n, rng), _elem(n, rng)
+    va, vb = _pack(a), _pack(b)
+    out = np.zeros_like(va)
+    assert L.pdplqr_debug_combine_form(n, va.ctypes.data, vb.ctypes.data, out.ctypes.data, 1) == 0
+    got, ref = _unpack(out, n), combine(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        assert np.linalg.norm(x - y) <= 1e-12 * max(1.0, np.linalg.norm(y)), name
