@@ -3,7 +3,8 @@
 // The tiled kernels hold a stage matrix in at most 2 x 2 MFMA tiles of one
 // wavefront (n + m <= 32).  Past that, a problem takes a 256-thread block whose
 // stage matrices live in LDS (3 x 64 x 65 doubles, about 100 KB):
-//   * k_riccati_bwd_big: terminal_step_with_factorization + step_with_factorization
+//   * k_riccati_bwd_big (keep_factors = 1; without a factor cache the value
+//     form of kernels_wide.hip runs): terminal_step_with_factorization + step_with_factorization
 //     (reference include/clqr/lqr/lqr_kernel.hpp:80-91, 104-147):
 //         V = E^T Lxx_next,  M = H~ + V V^T,  L = chol(M),
 //         Pb = Lxx_next (Lxx_next^T c) + p_next,  lp = h~ + E^T Pb,
@@ -15,9 +16,10 @@
 //     FR_k = [L(:, 0:m) | lu'], optionally the packed L_k and lp_k.
 //   * k_riccati_fwd_big: forward_step (lqr_kernel.hpp:181-205), one wave per
 //     problem: u = -Luu^{-T}(lu' + Lxu^T x), x+ = c + A x + B u.
-// These are correctness kernels for shapes outside the tiled range (one
-// problem per block, stage inputs read straight from HBM); the shapes the
-// benchmarks use run on the tiled / streamed kernels.
+// V and M are MFMA products split over the 4 waves (blk_la.hpp); the next
+// stage's E~, H~, c, h~ are loaded into registers during the Cholesky and
+// stored to LDS after it.
+#include "blk_la.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
 
@@ -79,15 +81,58 @@ __device__ __forceinline__ bool chol_big(double *M, double *sinv, int j0, int j1
     return ok;
 }
 
+// Stage inputs of stage k - 1 in flight in registers during stage k's
+// Cholesky (kernels_wide.hip's scheme): E~ (<= 16 doubles per thread), packed
+// H~ (<= 9), c, h~.
+struct BigIn {
+    double E[16], H[9], c, h;
+};
+
+__device__ __forceinline__ void big_in_load(BigIn &in, const double *Ek, const double *Hk, const double *ck,
+                                            const double *hk, int n, int s, int ps) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = tid + q * BT;
+        in.E[q] = i < n * s ? Ek[i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const int i = tid + q * BT;
+        in.H[q] = i < ps ? Hk[i] : 0.0;
+    }
+    in.c = tid < n ? ck[tid] : 0.0;
+    in.h = tid < s ? hk[tid] : 0.0;
+}
+
+// E~ into Es (ld BLD), H~ packed into Hs, c, h~
+__device__ __forceinline__ void big_in_store(const BigIn &in, double *Es, double *Hs, double *cv, double *hv, int n,
+                                             int s, int ps) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = tid + q * BT;
+        if (i < n * s) Es[(i % n) + (i / n) * BLD] = in.E[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const int i = tid + q * BT;
+        if (i < ps) Hs[i] = in.H[q];
+    }
+    if (tid < n) cv[tid] = in.c;
+    if (tid < s) hv[tid] = in.h;
+}
+
 __global__ __launch_bounds__(BT) void k_riccati_bwd_big(RiccatiArgs A) {
     __shared__ double M[BS * BLD];   // L_{k+1} at the start of stage k, then H~_k + V V^T -> L_k
     __shared__ double V[BS * BLD];   // V = E_k^T Lxx_{k+1}  (s x n)
     __shared__ double Es[BS * BLD];  // E_k (n x s)
+    __shared__ double Hs[BS * (BS + 1) / 2];  // H~_k, packed lower
     __shared__ double cv[BS], hv[BS], pbt[BS], pb[BS], pn[BS], lp[BS], sinv[BS];
     const int tid = threadIdx.x;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
-    const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
+    const int n = sh.n, m = sh.m, N = sh.N, s = sh.s, ps = sh.ps;
     const long long frs = (long long)s * m + m;
     const double *Eb = A.E + b * sh.perE;
     const double *cb = A.c + b * sh.perc;
@@ -98,6 +143,10 @@ __global__ __launch_bounds__(BT) void k_riccati_bwd_big(RiccatiArgs A) {
     double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
     auto Lxx = [&](int i, int t) -> double { return M[(m + i) + (m + t) * BLD]; };
     int fail_stage = -1;
+    BigIn nxt;
+    if (N > 0)
+        big_in_load(nxt, Eb + (long long)(N - 1) * n * s, Hb + (long long)(N - 1) * ps, cb + (long long)(N - 1) * n,
+                    hb + (long long)(N - 1) * s, n, s, ps);
 
     // ---- terminal (lqr_kernel.hpp:80-91): L_N = chol(H~_N) at offset m, lp_N = h~_N ----
     for (int q = tid; q < n * n; q += BT) {
@@ -115,47 +164,35 @@ __global__ __launch_bounds__(BT) void k_riccati_bwd_big(RiccatiArgs A) {
             const short2 ij = A.tab_n[q];
             Lcb[(long long)N * sh.ps + q] = Lxx(ij.x, ij.y);
         }
+    if (N > 0) big_in_store(nxt, Es, Hs, cv, hv, n, s, ps);
+    __syncthreads();
 
     for (int k = N - 1; k >= 0; --k) {
-        const double *Ek = Eb + (long long)k * n * s;
-        for (int q = tid; q < n * s; q += BT) Es[(q % n) + (q / n) * BLD] = Ek[q];
-        if (tid < n) cv[tid] = cb[(long long)k * n + tid];
-        if (tid < s) hv[tid] = hb[(long long)k * s + tid];
-        __syncthreads();
-        // V(j, t) = sum_{i >= t} E(i, j) Lxx(i, t);  Pb_tmp = Lxx^T c
-        for (int q = tid; q < s * n; q += BT) {
-            const int j = q % s, t = q / s;
-            double a = 0.0;
-            for (int i = t; i < n; ++i) a = __builtin_fma(Es[i + j * BLD], Lxx(i, t), a);
-            V[j + t * BLD] = a;
-        }
-        if (tid < n) {
+        // Es = E_k, Hs = H~_k, cv = c_k, hv = h~_k (stored at the end of stage k + 1)
+        // V = E^T Lxx (s x n; Lxx lower, zeros above: chol_big's finalisation)
+        blk_mm(V, BLD, mv_t(Es, BLD), mv_n(M + m + m * BLD, BLD), s, n, n, 1.0, 0.0, mv_none(), false);
+        if (tid < n) {  // Pb_tmp = Lxx^T c
             double a = 0.0;
             for (int i = tid; i < n; ++i) a = __builtin_fma(Lxx(i, tid), cv[i], a);
             pbt[tid] = a;
         }
         __syncthreads();
-        // Pb = Lxx Pb_tmp + p_next
-        if (tid < n) {
+        if (tid < n) {  // Pb = Lxx Pb_tmp + p_next
             double a = 0.0;
             for (int t = 0; t <= tid; ++t) a = __builtin_fma(Lxx(tid, t), pbt[t], a);
             pb[tid] = a + pn[tid];
         }
         __syncthreads();
-        // M = H~ + V V^T (lower), lp = h~ + E^T Pb  (M no longer holds L_{k+1})
-        const double *Hk = Hb + (long long)k * sh.ps;
-        for (int q = tid; q < sh.ps; q += BT) {
-            const short2 ij = A.tab_s[q];
-            const int i = ij.x, j = ij.y;
-            double a = Hk[q];
-            for (int t = 0; t < n; ++t) a = __builtin_fma(V[i + t * BLD], V[j + t * BLD], a);
-            M[i + j * BLD] = a;
-        }
-        if (tid < s) {
+        if (tid < s) {  // lp = h~ + E^T Pb
             double a = hv[tid];
             for (int i = 0; i < n; ++i) a = __builtin_fma(Es[i + tid * BLD], pb[i], a);
             lp[tid] = a;
         }
+        // M = H~ + V V^T (lower; M no longer holds L_{k+1})
+        blk_mm(M, BLD, mv_n(V, BLD), mv_t(V, BLD), s, s, n, 1.0, 0.0, mv_pk(Hs, s), true);
+        if (k > 0)  // stage k - 1's inputs in flight during the factorisation
+            big_in_load(nxt, Eb + (long long)(k - 1) * n * s, Hb + (long long)(k - 1) * ps,
+                        cb + (long long)(k - 1) * n, hb + (long long)(k - 1) * s, n, s, ps);
         if (!chol_big(M, sinv, 0, s, m) && fail_stage < 0) fail_stage = k;
         // lu <- Luu^{-1} lu ; p -= Lxu lu  (wave 0, lane i holds lp_i)
         if (tid < 64) {
@@ -179,6 +216,7 @@ __global__ __launch_bounds__(BT) void k_riccati_bwd_big(RiccatiArgs A) {
                 const short2 ij = A.tab_s[q];
                 Lcb[(long long)k * sh.ps + q] = M[ij.x + ij.y * BLD];
             }
+        if (k > 0) big_in_store(nxt, Es, Hs, cv, hv, n, s, ps);  // Es, Hs, cv, hv are free since M was formed
         __syncthreads();
     }
     if (tid == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;

@@ -230,6 +230,30 @@ __device__ __forceinline__ ElemIn stage_right(double *dst, const double *e, int 
 
 static size_t op_stage_bytes(int n) { return 2 * (size_t)((2 * n * n + 2 * n + 1) & ~1) * sizeof(double); }
 
+// Block-wide (256 threads) LDS[dst, dst + len) <- src[0, len): one LDS-DMA burst
+// per wave (global_load_lds_dwordx4, 1 KB per instruction) when both are
+// 16-byte aligned, a plain copy otherwise.  The caller waits on vmcnt(0) and
+// then __syncthreads().  The 4-wave combines stage BOTH operands up front this
+// way: every later read is an LDS read, so the combine pays one memory latency
+// instead of one per dependent global load of its phases.
+__device__ __forceinline__ void stage_range_blk(double *dst, const double *src, int len) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+        const int chunks = len >> 1;
+        for (int q = wv; q * 64 < chunks; q += 4) {
+            const int ch = q * 64 + lane;
+            if (ch < chunks) dma16(src + 2 * ch, dst + 2 * q * 64);
+        }
+        if ((len & 1) && threadIdx.x == 0) dst[len - 1] = src[len - 1];
+    } else {
+        for (int q = threadIdx.x; q < len; q += 256) dst[q] = src[q];
+    }
+}
+
+// doubles of the 4-wave combine's own LDS, rounded up to a 16-byte boundary
+__host__ __device__ inline int mw_smem_doubles(int n) { return (int)((mw_smem_bytes(n) + 15) / 16 * 2); }
+__host__ __device__ inline int elem_slot(int n) { return (3 * n * n + 2 * n + 1) & ~1; }
+
 template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
@@ -340,10 +364,14 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     }
     const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
     const MwSmem sm = mw_smem(mwbuf, n);
+    double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
+    stage_range_blk(ea, in + (long long)i * is, es);
+    stage_range_blk(eb, in + (long long)(i + d) * is, es);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     double *o = out + (long long)i * es;
-    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n,
-                                  elem_in(in + (long long)i * is, n), elem_in(in + (long long)(i + d) * is, n), n, fcf,
-                                  sm);
+    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
+                                  elem_in(eb, n), n, fcf, sm);
     if (!fcf && wv == 1)
         for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
     if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
@@ -466,27 +494,36 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     double *mo = A.maps + (b * J + j) * (long long)mw;
     bool ok = true;
     const double *vP = nullptr, *vp = nullptr;
-    if (j < S && right) {  // block-uniform
-        ok = mw_combine<T>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(A.suf + (b * S + j) * (long long)es, n),
-                           elem_in(right, n), n, false, sm);
-        __syncthreads();  // vo (written by waves 0 and 3) is read by every wave below
-        vP = vo;
-        vp = vo + nn;
-    } else {
-        const double *src = j < S ? A.suf + (b * S + j) * (long long)es : right;
-        if (src) {
-            vP = src + 2 * nn + n;
-            vp = src + 3 * nn + n;
-        }
-        if (wv == 0) {
-            if (src)
-                for (int q = lane; q < mw; q += 64) vo[q] = q < nn ? vP[q] : vp[q - nn];
-            else
-                for (int q = lane; q < mw; q += 64) vo[q] = 0.0;
-        }
+    // every global operand staged into LDS up front (one memory latency):
+    // slot 0 the source element; slots 1, 2 suf_j and right when V_j is a
+    // combine, else slot 1 the [P | p] of V_j (suf_j's or right's)
+    double *es0 = mwbuf + mw_smem_doubles(n), *es1 = es0 + elem_slot(n), *es2 = es1 + elem_slot(n);
+    const double *src_g = j > 0 ? A.elem + (b * S + j - 1) * (long long)es : A.left ? A.left + b * (long long)es
+                                                                                   : nullptr;
+    const bool vcomb = j < S && right;
+    const double *vsrc = j < S ? A.suf + (b * S + j) * (long long)es : right;  // element holding V_j (or null)
+    if (src_g) stage_range_blk(es0, src_g, es);
+    if (vcomb) {
+        stage_range_blk(es1, vsrc, es);
+        stage_range_blk(es2, right, es);
+    } else if (vsrc) {
+        stage_range_blk(es1, vsrc + 2 * nn + n, mw);  // [P | p]
     }
-    const double *src = j > 0 ? A.elem + (b * S + j - 1) * (long long)es : A.left ? A.left + b * (long long)es
-                                                                                 : nullptr;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (vcomb) {  // block-uniform
+        ok = mw_combine<T>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(es1, n), elem_in(es2, n), n, false, sm);
+        __syncthreads();  // vo (written by waves 0 and 3) is complete; es1 is free
+        for (int q = threadIdx.x; q < mw; q += 256) es1[q] = vo[q];
+        __syncthreads();
+    } else if (wv == 0) {
+        for (int q = lane; q < mw; q += 64) vo[q] = vsrc ? es1[q] : 0.0;
+    }
+    if (vsrc) {
+        vP = es1;
+        vp = es1 + nn;
+    }
+    const double *src = src_g ? es0 : nullptr;
     WV<T> phi, x;
     bool have_x = false;  // j = 0: x_0 formed (wave 0)
     if (src && vP) {
@@ -736,6 +773,10 @@ __global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
 
 static int tile_order(int n);
 
+// dynamic LDS of the 4-wave kernels: the combine's own + staged operand elements
+static size_t mw_scan_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 2 * elem_slot(n)) * sizeof(double); }
+static size_t mw_maps_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 3 * elem_slot(n)) * sizeof(double); }
+
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
 bool seg_scan_mw(int n, bool lu) {
@@ -751,8 +792,8 @@ int seg_scan_slots(const Shape &sh, int device) {
     const size_t smem = op_stage_bytes(sh.n);
     hipError_t e;
     if (seg_scan_mw(sh.n, false))
-        e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<1>, 256, mw_smem_bytes(sh.n))
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<2>, 256, mw_smem_bytes(sh.n));
+        e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<1>, 256, mw_scan_bytes(sh.n))
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<2>, 256, mw_scan_bytes(sh.n));
     else
         e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<1, false>, 64, smem)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan<2, false>, 64, smem);
@@ -787,7 +828,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
     if (seg_scan_mw(a.n, a.lu)) {
-        const size_t sm = mw_smem_bytes(a.n);
+        const size_t sm = mw_scan_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_scan_mw<1>, grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_scan_mw<2>, grid, dim3(256), sm, st, a);
         PDPLQR_HIP_TRY(hipGetLastError());
@@ -807,7 +848,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     if (seg_scan_mw(a.n, a.lu) && !getenv("PDPLQR_MAPS_1WAVE")) {
-        const size_t sm = mw_smem_bytes(a.n);
+        const size_t sm = mw_maps_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_maps_mw<1>, grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_maps_mw<2>, grid, dim3(256), sm, st, a);
         PDPLQR_HIP_TRY(hipGetLastError());

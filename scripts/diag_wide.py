@@ -102,6 +102,13 @@ def main():
     o.backward((1.0 / p["irho"][b]) if nc else None)
     ref = o.forward(x0)
     print("w err", rel(out[b], ref))
+    # boundary states and costates against the serial oracle's trajectory
+    for j, (k0, k1) in enumerate(segs):
+        xt = ref[k0 * s + (m if k0 < N else 0):k0 * s + (m if k0 < N else 0) + n]
+        Pt, pt = o.value_function(k0)
+        lt = Pt @ xt + pt
+        print(f"boundary {j} (stage {k0}) x vs oracle {rel(xhat[b][j * n:(j + 1) * n], xt):.2e}"
+              f"  lambda vs oracle {rel(lam[b][j * n:(j + 1) * n], lt):.2e}  |lambda| {np.linalg.norm(lt):.2e}")
     for k0, k1 in segs:
         print(f"  stages {k0}..{k1} err", rel(out[b][k0 * s:k1 * s], ref[k0 * s:k1 * s]))
 
