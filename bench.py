@@ -113,7 +113,10 @@ def pmc_traffic(workload_tag, kernels):
         c = found["kernels"][ks[0]]
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             return None
-        tot += c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        # dispatches per solve: counted when the profile made only this workload's
+        # solves (PMC_SOLVES), else one per solve
+        mult = c.get("dispatches", 1) / found["solves"] if found.get("solves") else 1.0
+        tot += (c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024) * mult
         seen.append(ks[0])
     return {"bytes": tot, "kernels": seen}
 

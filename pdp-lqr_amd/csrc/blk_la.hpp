@@ -178,13 +178,66 @@ __device__ __noinline__ bool blk_chol(double *M, int ld, int n, int m, double *s
     return ok;
 }
 
+// Triangular solves with the lower factor L (n x n, ld) of blk_chol, in place
+// on nb right-hand-side columns B (ld ldb) and optionally one more column v:
+//   blk_trsm_l:  L X = B      blk_trsm_lt:  L^T X = B
+// One barrier per row: the row of step i is final before step i and only
+// read in it (the other rows are updated with L(k, i) / L(i, i) times it, the
+// division by L(i, i) applied to every row at the end).
+__device__ __noinline__ void blk_trsm_l(const double *L, int ld, int n, double *B, int ldb, int nb, double *v) {
+    const int tid = threadIdx.x, nc = nb + (v ? 1 : 0);
+    for (int i = 0; i < n; ++i) {
+        __syncthreads();
+        const int rows = n - 1 - i;
+        const double inv = 1.0 / L[i + i * ld];
+        for (int q = tid; q < rows * nc; q += BLK_THREADS) {
+            const int k = i + 1 + q % rows, col = q / rows;
+            const double lk = L[k + i * ld] * inv;
+            if (col < nb) B[k + col * ldb] = __builtin_fma(-lk, B[i + col * ldb], B[k + col * ldb]);
+            else v[k] = __builtin_fma(-lk, v[i], v[k]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * nc; q += BLK_THREADS) {
+        const int k = q % n, col = q / n;
+        const double inv = 1.0 / L[k + k * ld];
+        if (col < nb) B[k + col * ldb] *= inv;
+        else v[k] *= inv;
+    }
+    __syncthreads();
+}
+
+__device__ __noinline__ void blk_trsm_lt(const double *L, int ld, int n, double *B, int ldb, int nb, double *v) {
+    const int tid = threadIdx.x, nc = nb + (v ? 1 : 0);
+    for (int i = n - 1; i >= 0; --i) {
+        __syncthreads();
+        const int rows = i;  // k = 0 .. i - 1
+        if (rows == 0) continue;
+        const double inv = 1.0 / L[i + i * ld];
+        for (int q = tid; q < rows * nc; q += BLK_THREADS) {
+            const int k = q % rows, col = q / rows;
+            const double lk = L[i + k * ld] * inv;  // L^T(k, i)
+            if (col < nb) B[k + col * ldb] = __builtin_fma(-lk, B[i + col * ldb], B[k + col * ldb]);
+            else v[k] = __builtin_fma(-lk, v[i], v[k]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * nc; q += BLK_THREADS) {
+        const int k = q % n, col = q / n;
+        const double inv = 1.0 / L[k + k * ld];
+        if (col < nb) B[k + col * ldb] *= inv;
+        else v[k] *= inv;
+    }
+    __syncthreads();
+}
+
 // Gauss-Jordan elimination with partial (row) pivoting of W = [A | R]
-// (n x 2n, ld n; the LU form of the combine): the same pivot rows as
+// (n x ncol, ld n; the LU form of the combine): the same pivot rows as
 // PartialPivLU (largest |a| among the rows not yet used, lowest row on ties),
-// kept in place.  On return row piv[k] of the right half holds row k of
-// A^{-1} R.  prow: 2n doubles, mul: n doubles, piv: n ints of LDS scratch.
+// kept in place.  On return row piv[k] of the right part holds row k of
+// A^{-1} R.  prow: ncol doubles, mul: n doubles, piv: n ints of LDS scratch.
 // False if a pivot is zero or not finite.
-__device__ __noinline__ bool blk_gauss_jordan(double *W, int n, int *piv, double *prow, double *mul) {
+__device__ __noinline__ bool blk_gauss_jordan(double *W, int n, int *piv, double *prow, double *mul, int ncol) {
     const int tid = threadIdx.x, lane = tid & 63;
     bool used = false, ok = true;  // used: wave 0, lane = row
     for (int k = 0; k < n; ++k) {
@@ -209,10 +262,10 @@ __device__ __noinline__ bool blk_gauss_jordan(double *W, int n, int *piv, double
         const double pv = W[p + k * n];
         ok = ok && pv != 0.0 && fabs(pv) <= 1.7976931348623157e308;
         const double inv = 1.0 / pv;
-        for (int j = tid; j < 2 * n; j += BLK_THREADS) prow[j] = W[p + j * n];
+        for (int j = tid; j < ncol; j += BLK_THREADS) prow[j] = W[p + j * n];
         for (int i = tid; i < n; i += BLK_THREADS) mul[i] = W[i + k * n] * inv;
         __syncthreads();
-        for (int q = tid; q < 2 * n * n; q += BLK_THREADS) {
+        for (int q = tid; q < ncol * n; q += BLK_THREADS) {
             const int i = q % n, j = q / n;
             W[q] = (i == p) ? prow[j] * inv : __builtin_fma(-mul[i], prow[j], W[q]);
         }

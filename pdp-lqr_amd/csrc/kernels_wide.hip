@@ -80,7 +80,7 @@ __device__ __noinline__ bool wide_core(const WideSmem &sm, const double *Pb, int
     } else {
         blk_mm(B1, n, mv_n(Pb, n), mv_n(B0, n), n, n, n, 1.0, 1.0, mv_none(), false);  // I + P_b C_a
         blk_copy(B2, n, mv_n(Pb, n), n, n);                                           // P_b
-        ok = blk_gauss_jordan(B1, n, sm.piv, sm.prow, sm.mul);
+        ok = blk_gauss_jordan(B1, n, sm.piv, sm.prow, sm.mul, 2 * n);
         for (int q = threadIdx.x; q < n * n; q += BLK_THREADS) {
             const int i = q % n, j = q / n;
             B3[q] = 0.5 * (B2[sm.piv[i] + j * n] + B2[sm.piv[j] + i * n]);
@@ -197,21 +197,57 @@ __global__ __launch_bounds__(256) void k_seg_maps_wide(MapArgs A) {
     double *Phi = nullptr;  // LDS n x n (j = 0 with a value function) or null
     const double *PhiG = nullptr;  // the map's matrix in global memory (no value function)
     if (src && vP) {
+        // Phi = Z F, phi = Z (f - C p_j) with Z = (I + C P_j)^{-1} as a SOLVE of
+        // (I + C P_j) [Phi | phi] = [F | f - C p_j] -- not I - C Y times the
+        // right-hand side: when C P_j is large (|CP| ~ 1e4 at 50/10 with
+        // penalties) Z is small and I - C Y cancels, costing ~4 digits per map
+        // (boundary states 1e-10 off instead of 1e-12, tests/test_gpu_wide.py).
+        //   CHOLESKY: R = chol(P_j), S = I + R^T C R = Q Q^T,
+        //             [Phi | phi] = R^{-T} Q^{-T} Q^{-1} R^T [F | v]
+        //   LU:       Gauss-Jordan with partial pivoting on [I + C P_j | F | v]
+        //             (the reference LU form factors I + C P with PartialPivLU)
         const ElemIn e = elem_in(src, n);
-        double *B0 = sm.B[0];
-        blk_copy(B0, n, mv_n(e.C, n), n, n);
+        double *B0 = sm.B[0], *B1 = sm.B[1], *B2 = sm.B[2], *B3 = sm.B[3];
         double *pv = sm.v[0], *v = sm.v[2];
+        blk_copy(B0, n, mv_n(e.C, n), n, n);
         blk_vcopy(pv, vp, n);
         blk_mv(v, mv_n(B0, n), pv, n, n, -1.0, e.f);  // f - C p_j
-        double *Y, *Z, *Fr;
-        ok = wide_core(sm, vP, n, LU, &Y, &Z, &Fr) && ok;
-        blk_mv(phi, mv_n(Z, n), v, n, n, 1.0, nullptr);  // Z (f - C p_j)
-        if (j > 0) {
-            blk_mm(mo, n, mv_n(Z, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);  // Z F
-            for (int q = tid; q < n; q += BLK_THREADS) mo[nn + q] = phi[q];
+        Phi = j > 0 ? nullptr : B2;
+        if (!LU) {
+            blk_copy(B1, n, mv_n(vP, n), n, n);
+            ok = blk_chol(B1, n, n, n, sm.sinv) && ok;                                       // R
+            blk_mm(B2, n, mv_n(B0, n), mv_n(B1, n), n, n, n, 1.0, 0.0, mv_none(), false);   // C R
+            blk_mm(B3, n, mv_t(B1, n), mv_n(B2, n), n, n, n, 1.0, 1.0, mv_none(), true);    // I + R^T C R
+            ok = blk_chol(B3, n, n, n, sm.sinv) && ok;                                       // Q
+            blk_mm(B2, n, mv_t(B1, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);  // R^T F
+            blk_mv(phi, mv_t(B1, n), v, n, n, 1.0, nullptr);                                // R^T v
+            blk_trsm_l(B3, n, n, B2, n, n, phi);   // Q^{-1}
+            blk_trsm_lt(B3, n, n, B2, n, n, phi);  // Q^{-T}
+            blk_trsm_lt(B1, n, n, B2, n, n, phi);  // R^{-T}
+            if (j > 0) {
+                for (int q = tid; q < nn; q += BLK_THREADS) mo[q] = B2[q];
+                for (int q = tid; q < n; q += BLK_THREADS) mo[nn + q] = phi[q];
+            }
         } else {
-            blk_mm(Y, n, mv_n(Z, n), mv_n(e.F, n), n, n, n, 1.0, 0.0, mv_none(), false);
-            Phi = Y;
+            // W = [I + C P_j | F | v] in B1 | B2 | B3 (n x (2n + 1), ld n)
+            blk_mm(B1, n, mv_n(B0, n), mv_n(vP, n), n, n, n, 1.0, 1.0, mv_none(), false);
+            blk_copy(B2, n, mv_n(e.F, n), n, n);
+            blk_vcopy(B3, v, n);
+            ok = blk_gauss_jordan(B1, n, sm.piv, sm.prow, sm.mul, 2 * n + 1) && ok;
+            // row piv[i] of the right part is row i of the solution
+            for (int q = tid; q < nn + n; q += BLK_THREADS) {
+                const int i = q % n, jj = q / n;  // jj = n: the vector column
+                const double x = B2[sm.piv[i] + jj * n];
+                if (jj < n) {
+                    if (j > 0) mo[q] = x;
+                    else B0[q] = x;  // Phi of boundary 0 (C is no longer needed)
+                } else {
+                    phi[i] = x;
+                    if (j > 0) mo[nn + i] = x;
+                }
+            }
+            __syncthreads();
+            if (j == 0) Phi = B0;
         }
     } else if (src) {
         const ElemIn e = elem_in(src, n);

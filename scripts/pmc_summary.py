@@ -33,11 +33,19 @@ def main():
         if int(row.get("Grid_Size", 0)) == gmax[k]:
             per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {"workload": tag, "kernels": {}}
+    # PMC_SOLVES: the profiled run made that many solves of the workload and
+    # nothing else through these kernels -- bench.pmc_traffic then counts each
+    # kernel dispatches / solves times per solve (C4: the scan rounds)
+    if os.environ.get("PMC_SOLVES"):
+        out["solves"] = int(os.environ["PMC_SOLVES"])
     for k, d in per.items():
         short = k.split("(")[0].replace("void ", "")
         if "pdplqr" not in short:
             continue
         out["kernels"][short] = {c: sum(v) / len(v) for c, v in d.items()}
+        # dispatches of the kernel at that grid: each counter is collected by
+        # one pass of scripts/collect_pmc.sh, which sees every dispatch
+        out["kernels"][short]["dispatches"] = max(len(v) for v in d.values())
     # dominant kernel of the bench step: the value-form backward when present
     names = sorted(out["kernels"], key=lambda k: ("bwd_schur" not in k, dom not in k))
     bwd = [out["kernels"][k] for k in names if dom in k]

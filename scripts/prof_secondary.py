@@ -26,6 +26,9 @@ def main():
     elif which == "c4":
         r = bench.bench_horizon(0, dev, None, 1, 0, int(sys.argv[2]) if len(sys.argv) > 2 else 65536, steps=3,
                                 warmup=1)
+    elif which == "c4one":  # exactly one solve (PMC passes with PMC_SOLVES=1)
+        r = bench.bench_horizon(0, dev, None, 1, 0, int(sys.argv[2]) if len(sys.argv) > 2 else 65536, steps=1,
+                                warmup=0)
     elif which == "wide":
         r = bench.bench_batched_c3(0, dev, None, steps=3, warmup=1, N=256, batch=1024, n=24, m=16)
     else:
