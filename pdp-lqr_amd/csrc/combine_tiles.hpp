@@ -815,4 +815,140 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
                              elem_in(eb, n), n, need_FCf, need_Pp, sm, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Closed-loop boundary map of an element under a value function (one wave):
+//     [Phi | phi] = (I + C P)^{-1} [F | f - C p]
+// as a SOLVE, not as (I - C Y) times the right-hand side: when C P is large
+// (|C P| ~ 1e4) Z = (I + C P)^{-1} is small and I - C Y cancels, which costs
+// digits in every boundary state (tests/test_gpu_wide.py, 50/10 with
+// penalties: 1e-10 off instead of 1e-12).  The reference never forms Z either:
+// its Cholesky form goes through P^{-1} and (C + P^{-1})^{-1}
+// (condensed_system.hpp:252-289), its LU form solves with PartialPivLU of
+// I + C P (:117-137).
+//   CHOLESKY: R = chol(P), S = I + R^T C R = Q Q^T,
+//             [Phi | phi] = R^{-T} Q^{-T} Q^{-1} R^T [F | v]
+//             (both factors by chol_blk4, the three triangular solves in LDS,
+//             one lane per right-hand-side column);
+//   LU:       Gauss-Jordan with partial pivoting on [I + C P | F | v]
+//             (comb_core_lu's pivot rule).
+// The result lands in LDS: Phi at out (n x n, ld n), phi at out + n n.
+// Scratch: tmap_smem_doubles(n) doubles (16-byte aligned) at `scr`.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int tmap_smem_doubles(int n) {
+    const int P = n <= 16 ? 16 : 32, PL = P + 1;
+    const int chol = 2 * P * PL + (n + 1) * n;     // R^T, Q^T, [B | b] (ld n)
+    const int lu = n * (2 * n + 1) + (2 * n + 1) + n;  // W, pivot row, pivot rows (int)
+    return ((chol > lu ? chol : lu) + 1) & ~1;
+}
+
+template <int T, bool LU>
+__device__ __forceinline__ bool tmap_solve(const double *F, const double *C, const double *f, const double *Pj,
+                                           const double *pj, int n, double *scr, double *out, int lane) {
+    constexpr int P = 16 * T, PL = P + 1;
+    const int g = lane >> 4, c = lane & 15;
+    bool ok = true;
+    WM<T> Cs, Pm;
+    WV<T> pv, fv, v;
+    wm_load(Cs, C, n, n, false, 0.0, g, c);
+    wv_load(pv, pj, n, g, c);
+    wv_load(fv, f, n, g, c);
+    wv_tn(v, Cs, pv, n, -1.0, &fv);  // v = f - C p  (C symmetric)
+    if constexpr (!LU) {
+        double *Rt = scr, *Qt = scr + P * PL, *B = scr + 2 * P * PL;  // B: [R^T F | R^T v], ld n
+        WM<T> U, R;
+        wm_load(U, Pj, n, n, false, 1.0, g, c);
+        ok = chol_blk4<T, false, T>(U, U.t, n, g, c);  // U = R^T (upper)
+        wm_store(U, Rt, PL, n, g, c);
+        wave_sync();
+        wm_load(R, Rt, PL, n, true, 1.0, g, c);  // R
+        {
+            WM<T> T1, S;
+            wm_tn(T1, Cs, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C R
+            wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C R
+            ok = chol_blk4<T, false, T>(S, S.t, n, g, c) && ok;            // S = Q^T (upper)
+            wm_store(S, Qt, PL, n, g, c);
+        }
+        {
+            WM<T> Fs, X;
+            WV<T> y;
+            wm_load(Fs, F, n, n, false, 0.0, g, c);
+            wm_tn(X, R, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F
+            wm_store(X, B, n, n, g, c);
+            wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
+            wv_store(y, B + n * n, n, g, c);
+        }
+        wave_sync();
+        if (lane <= n) {  // lane l solves right-hand-side column l (l = n: the vector)
+            double *col = B + lane * n;
+            for (int i = 0; i < n; ++i) {  // Q z = col, Q(i, k) = Q^T(k, i)
+                double a = col[i];
+                for (int k = 0; k < i; ++k) a = __builtin_fma(-Qt[k + i * PL], col[k], a);
+                col[i] = a / Qt[i + i * PL];
+            }
+            for (int i = n - 1; i >= 0; --i) {  // Q^T y = z
+                double a = col[i];
+                for (int k = i + 1; k < n; ++k) a = __builtin_fma(-Qt[i + k * PL], col[k], a);
+                col[i] = a / Qt[i + i * PL];
+            }
+            for (int i = n - 1; i >= 0; --i) {  // R^T x = y
+                double a = col[i];
+                for (int k = i + 1; k < n; ++k) a = __builtin_fma(-Rt[i + k * PL], col[k], a);
+                col[i] = a / Rt[i + i * PL];
+            }
+        }
+        wave_sync();
+        for (int q = lane; q < n * n + n; q += 64) out[q] = B[q];
+    } else {
+        const int ncol = 2 * n + 1;
+        double *W = scr, *prow = scr + n * ncol;
+        int *piv = reinterpret_cast<int *>(prow + ncol);
+        {
+            WM<T> A, Fs;
+            wm_load(Pm, Pj, n, n, false, 0.0, g, c);
+            wm_tn(A, Cs, Pm, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);  // I + C P  (C symmetric)
+            wm_store(A, W, n, n, g, c);
+            wm_load(Fs, F, n, n, false, 0.0, g, c);
+            wm_store(Fs, W + n * n, n, n, g, c);
+            wv_store(v, W + 2 * n * n, n, g, c);
+        }
+        wave_sync();
+        const bool row = lane < n;
+        const int i = row ? lane : 0;
+        bool used = false;
+        for (int k = 0; k < n; ++k) {
+            double a = (row && !used) ? fabs(W[i + k * n]) : -1.0;
+            int arg = lane;
+#pragma unroll
+            for (int mk = 1; mk < 64; mk <<= 1) {
+                const double oa = shfl_xor_f64(a, mk);
+                const int ob = __shfl_xor(arg, mk, 64);
+                if (oa > a || (oa == a && ob < arg)) {
+                    a = oa;
+                    arg = ob;
+                }
+            }
+            const int p = __builtin_amdgcn_readfirstlane(arg);
+            const double pvv = W[p + k * n];
+            ok = ok && pvv != 0.0 && fabs(pvv) <= 1.7976931348623157e308;
+            const double inv = 1.0 / pvv;
+            const bool me = row && i == p;
+            used = used || me;
+            if (lane == 0) piv[k] = p;
+            for (int j = lane; j < ncol; j += 64) prow[j] = W[p + j * n];
+            const double mi = W[i + k * n] * inv;
+            wave_sync();
+            if (row)
+                for (int j = 0; j < ncol; ++j) W[i + j * n] = me ? prow[j] * inv : __builtin_fma(-mi, prow[j], W[i + j * n]);
+            wave_sync();
+        }
+        // row piv[i] of the right part is row i of the solution
+        for (int q = lane; q < n * n + n; q += 64) {
+            const int ii = q % n, jj = q / n;
+            out[q] = W[piv[ii] + (n + jj) * n];
+        }
+    }
+    wave_sync();
+    return ok;
+}
+
 }  // namespace pdplqr

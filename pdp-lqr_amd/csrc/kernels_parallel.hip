@@ -429,23 +429,15 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     WM<T> Phi, PhiT;
     WV<T> phi;
     if (src) {
-        WM<T> Fs;
-        WV<T> fs;
-        wm_load(Fs, src, n, n, false, 0.0, g, c);
-        wv_load(fs, src + 2 * nn, n, g, c);
-        if (vP) {
-            WM<T> Cs, Y, Z, Zt;
-            WV<T> pv, v1;
-            wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
-            ok = comb_core_t<T, LU>(Y, Z, Zt, Cs, vP, n, sm, lane) && ok;
-            wv_load(pv, vp, n, g, c);
-            wv_tn(v1, Cs, pv, n, -1.0, &fs);  // f - C p_j  (C symmetric)
-            wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p_j)
-            if (j > 0) wm_tn(Phi, Zt, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Z F
-            else wm_tn(PhiT, Fs, Zt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // F^T Z^T
+        if (vP) {  // [Phi | phi] = (I + C P_j)^{-1} [F | f - C p_j] (tmap_solve: a solve, no I - C Y)
+            double *mscr = dyn + (A.right ? 2 * op_stage_len(n) : 0), *mout = mscr + tmap_smem_doubles(n);
+            ok = tmap_solve<T, LU>(src, src + nn, src + 2 * nn, vP, vp, n, mscr, mout, lane) && ok;
+            wv_load(phi, mout + nn, n, g, c);
+            if (j > 0) wm_load(Phi, mout, n, n, false, 0.0, g, c);
+            else wm_load(PhiT, mout, n, n, true, 0.0, g, c);
         } else {
-            phi = fs;
-            if (j > 0) Phi = Fs;
+            wv_load(phi, src + 2 * nn, n, g, c);
+            if (j > 0) wm_load(Phi, src, n, n, false, 0.0, g, c);
             else wm_load(PhiT, src, n, n, true, 0.0, g, c);
         }
     }
@@ -529,17 +521,21 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     if (src && vP) {
         const ElemIn e = elem_in(src, n);
         WM<T> R;
-        // ---- phase A: R = chol(P_j) (w0..w2); v = f - C p_j (w3) ----
-        if (wv < 3) {
+        // ---- phase A: R = chol(P_j) (w0, w1); R^{-1} (w2: the same factorisation
+        //      carrying the identity) ----
+        if (wv < 2) {
             ok = mw_chol_R<T>(R, vP, sm.S + wv * (n * PL), PL, n, g, c) && ok;
-        } else {
-            WM<T> Cs;
-            WV<T> pv, fs, v;
-            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
-            wv_load(pv, vp, n, g, c);
-            wv_load(fs, e.f, n, g, c);
-            wv_tn(v, Cs, pv, n, -1.0, &fs);
-            wv_store(v, sm.fv, n, g, c);
+        } else if (wv == 2) {
+            WM<T> Pm, Ri;
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Ri.t[a][bt][r] = (16 * a + 4 * r + g == 16 * bt + c) ? 1.0 : 0.0;
+            wm_load(Pm, vP, n, n, false, 1.0, g, c);
+            ok = chol_blk4<T, true, T>(Pm, Ri.t, n, g, c) && ok;  // Ri = R^{-1}
+            wm_store(Ri, sm.B2, PL, n, g, c);
         }
         // ---- phase B ----
         if (wv == 0) {
@@ -559,23 +555,20 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
             wm_load(Cs, e.C, n, n, false, 0.0, g, c);
             wv_load(pv, vp, n, g, c);
             wv_load(fs, e.f, n, g, c);
-            wv_tn(v, Cs, pv, n, -1.0, &fs);
+            wv_tn(v, Cs, pv, n, -1.0, &fs);                  // v = f - C p_j
             wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
             wv_store(y, sm.bv, n, g, c);
-        } else if (wv == 2) {
-            WM<T> Cs, B;
-            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
-            wm_tn(B, R, Cs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T C
-            wm_store(B, sm.B2, PL, n, g, c);
         }
+        if (wv == 2 && lane == 0) sm.ok[2] = ok;
         __syncthreads();
-        ok = ok && sm.ok[0];
-        // ---- phase C: chol(S) carrying one column tile per wave ----
+        ok = ok && sm.ok[0] && sm.ok[2];
+        // ---- phase C: chol(S) carrying one column tile per wave: X1 = Q^{-1} R^T F,
+        //      V = Q^{-1} R^{-1}, x3 = Q^{-1} R^T v ----
         {
             WM<T> Sm;
             wm_load(Sm, sm.S, PL, n, false, 1.0, g, c);
             d4 B[T][1], V[T][1];
-            int kind, tile = 0;  // 0: X1, 1: X2, 2: x3
+            int kind, tile = 0;  // 0: X1, 1: V, 2: x3
             if (T == 2) {
                 kind = wv < 2 ? 0 : 1;
                 tile = wv & 1;
@@ -613,29 +606,25 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
         }
         __syncthreads();
         ok = ok && sm.ok[1];
-        // ---- phase D: phi = v - X2^T x3 (every wave: it is needed below); Phi ----
-        {
-            WM<T> X2;
-            WV<T> x3, v;
-            wm_load(X2, sm.B2, PL, n, false, 0.0, g, c);
+        // ---- phase D: [Phi | phi] = R^{-T} Q^{-T} [X1 | x3] = V^T [X1 | x3]: the
+        //      solve of (I + C P_j) [Phi | phi] = [F | v] (no I - C Y cancellation,
+        //      see tmap_solve in combine_tiles.hpp) ----
+        if (wv == 0) {
+            WM<T> Vm, X1;
+            WV<T> x3;
+            wm_load(Vm, sm.B2, PL, n, false, 0.0, g, c);
+            wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
             wv_load(x3, sm.bv, n, g, c);
-            wv_load(v, sm.fv, n, g, c);
-            wv_tn(phi, X2, x3, n, -1.0, &v);
+            wv_tn(phi, Vm, x3, n, 1.0, (const WV<T> *)nullptr);
             if (j > 0) {
-                if (wv == 0) {
-                    WM<T> X1, Fs, Phi;
-                    wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
-                    wm_load(Fs, e.F, n, n, false, 0.0, g, c);
-                    wm_tn(Phi, X2, X1, n, -1.0, 0.0, &Fs, g, c);  // F - X2^T X1
-                    wm_store(Phi, mo, n, n, g, c);
-                    wv_store(phi, mo + nn, n, g, c);
-                }
-            } else if (wv == 0) {
-                WM<T> X1, FsT, PhiT;
+                WM<T> Phi;
+                wm_tn(Phi, Vm, X1, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // V^T X1
+                wm_store(Phi, mo, n, n, g, c);
+                wv_store(phi, mo + nn, n, g, c);
+            } else {
+                WM<T> PhiT;
                 WV<T> x0v;
-                wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
-                wm_load(FsT, e.F, n, n, true, 0.0, g, c);
-                wm_tn(PhiT, X1, X2, n, -1.0, 0.0, &FsT, g, c);  // Phi^T = F^T - X1^T X2
+                wm_tn(PhiT, X1, Vm, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi^T = X1^T V
                 wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
                 wv_tn(x, PhiT, x0v, n, 1.0, &phi);
                 have_x = true;
@@ -854,7 +843,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    const size_t smem = a.right ? op_stage_bytes(a.n) : 0;
+    const size_t smem = (a.right ? op_stage_bytes(a.n) : 0) + (size_t)(tmap_smem_doubles(a.n) + a.n * a.n + a.n) * sizeof(double);
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_maps<1, true>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_maps<1, false>), grid, blk, smem, st, a);
     else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_maps<2, true>), grid, blk, smem, st, a);
@@ -957,26 +946,18 @@ __global__ __launch_bounds__(64) void k_fold_shards(const double *elems_all, int
 template <int T, bool LU>
 __global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const double *suf, int R, int r, int n,
                                                   int batch, double *maps, int *flag) {
-    __shared__ CombSmem<T> sm;
-    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    extern __shared__ __attribute__((aligned(16))) double dyn[];  // tmap_solve scratch
+    const int lane = wave_lane();
     const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / r;
     const int j = blockIdx.x % r;
     const double *src = elems_all + ((long long)j * batch + b) * es;  // e_j, rank-major all-gather
     const double *v = suf + (b * R + j + 1) * (long long)es;           // V_{j+1}
-    WM<T> Fs, Cs, Y, Z, Zt, Phi;
-    WV<T> fs, pv, v1, phi;
-    wm_load(Fs, src, n, n, false, 0.0, g, c);
-    wm_load(Cs, src + nn, n, n, false, 0.0, g, c);
-    wv_load(fs, src + 2 * nn, n, g, c);
-    const bool ok = comb_core_t<T, LU>(Y, Z, Zt, Cs, v + 2 * nn + n, n, sm, lane);
-    wv_load(pv, v + 3 * nn + n, n, g, c);
-    wv_tn(v1, Cs, pv, n, -1.0, &fs);                     // f - C p  (C symmetric)
-    wv_tn(phi, Zt, v1, n, 1.0, (const WV<T> *)nullptr);  // Z (f - C p)
-    wm_tn(Phi, Zt, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Z F
     double *mo = maps + (b * r + j) * (long long)mw;
-    wm_store(Phi, mo, n, n, g, c);
-    wv_store(phi, mo + nn, n, g, c);
+    double *mout = dyn + tmap_smem_doubles(n);
+    // [Phi | phi] = (I + C P)^{-1} [F | f - C p]
+    const bool ok = tmap_solve<T, LU>(src, src + nn, src + 2 * nn, v + 2 * nn + n, v + 3 * nn + n, n, dyn, mout, lane);
+    for (int q = lane; q < mw; q += 64) mo[q] = mout[q];
     if (!ok && lane == 0) atomicOr(flag + b, 4);
 }
 
@@ -1014,13 +995,14 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
     if (wide_state(n)) return launch_rank_fold_maps_wide(elems, suf, x0, R, r, n, batch, maps, out_pre, flag, lu, st);
     const int T = tile_order(n);
     const dim3 gm(batch * r), blk(64);
+    const size_t rsm = (size_t)(tmap_smem_doubles(n) + n * n + n) * sizeof(double);
     if (T == 1) {
-        if (lu) hipLaunchKernelGGL((k_rank_maps<1, true>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
-        else hipLaunchKernelGGL((k_rank_maps<1, false>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
+        if (lu) hipLaunchKernelGGL((k_rank_maps<1, true>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
+        else hipLaunchKernelGGL((k_rank_maps<1, false>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
         hipLaunchKernelGGL(k_rank_chain<1>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else if (T == 2) {
-        if (lu) hipLaunchKernelGGL((k_rank_maps<2, true>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
-        else hipLaunchKernelGGL((k_rank_maps<2, false>), gm, blk, 0, st, elems, suf, R, r, n, batch, maps, flag);
+        if (lu) hipLaunchKernelGGL((k_rank_maps<2, true>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
+        else hipLaunchKernelGGL((k_rank_maps<2, false>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
         hipLaunchKernelGGL(k_rank_chain<2>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else {
         return PDPLQR_ERR_UNSUPPORTED;

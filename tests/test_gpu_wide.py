@@ -175,3 +175,26 @@ def test_wide_horizon_shards_match_oracle(n, m, N, batch, R, seglen):
     got, ref = _run_virtual(n, m, N, batch, R, seglen)
     for b in range(batch):
         assert rel_err(got[b], ref[b]) < TOL, b
+
+
+@pytest.mark.parametrize("n,m", [(12, 4), (24, 8), (50, 10)])
+@pytest.mark.parametrize("condensed", ["CHOLESKY", "LU"])
+def test_boundary_maps_large_penalty(n, m, condensed):
+    """Large constraint penalties (rho = 10 / inv_rho ~ 10..200) make |C P| at
+    the segment boundaries ~1e4: Z = (I + C P)^{-1} is then small, and forming
+    it as I - C Y cancels ~4 digits per boundary map (numpy: boundary states
+    1e-10..1e-9 off at 24/8 and 50/10, against ~1e-11 for a solve).  The maps
+    solve (I + C P) [Phi | phi] = [F | f - C p] instead (tmap_solve, the 4-wave
+    V = Q^{-1} R^{-1} form, the wide kernels' triangular solves), so the
+    trajectory stays at the 1e-9 bar with many short segments (seglen 2)."""
+    from pdplqr import BatchedLQRSolver
+
+    N, batch, nc = 24, 2, 4
+    p = _problem(n, m, N, batch, nc, 7 * n + m)
+    p["irho"] = 0.1 * p["irho"]
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=3, keep_factors=True, condensed=condensed,
+                          segment_len=2, ncs=p["ncs"])
+    out = _solve(bs, p, nc)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        assert rel_err(out[b], _oracle_serial(p, b, n, m, N)) < TOL, b
