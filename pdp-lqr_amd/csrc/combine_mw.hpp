@@ -150,6 +150,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int PL = sm.ld;
     bool ok = true;
+    COMB_MARK(0);
     // ---------------- phase A ----------------
     // (matrices are loaded right before their last use: at most four 2 x 2
     // tile matrices live per wave)
@@ -194,6 +195,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wm_store(K, sm.K1, PL, n, g, c);
         }
     }
+    COMB_MARK(1);  // wave 0: R formed
     // ---------------- phase B ----------------
     if (wv == 0) {
         WM<T> Ca, T1, S;
@@ -245,7 +247,9 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         wm_tn(B, R, K0, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T C_a F_b^T
         wm_store(B, sm.B2, PL, n, g, c);
     }
+    COMB_MARK(2);  // wave 0: S stored
     __syncthreads();
+    COMB_MARK(3);  // every wave through phase B
     // ---------------- phase C: chol(S) carrying one column tile per wave ----------------
     // T = 2: w0 / w1 the two tiles of X1, w2 / w3 those of W (w3 also [x3 | x4]);
     // T = 1: w0 [x3 | x4], w1 X1, w2 W.  Without F, C, f: X1 and x4 only.
@@ -283,6 +287,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         } else if (kind >= 0) {
             okS = chol_blk4<T, true, 1>(S, B, n, g, c);
         }
+        COMB_MARK(4);  // wave 0: chol(S) done
         __syncthreads();  // every wave has read its right-hand sides
         if (kind == 0) mw_col_store<T>(B, sm.B1, PL, tile, n, g, c);
         else if (kind == 1) mw_col_store<T>(B, sm.B2, PL, tile, n, g, c);
@@ -291,6 +296,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         if (wv == (T == 2 ? 0 : 1) && lane == 0) sm.ok[1] = okS;
     }
     __syncthreads();
+    COMB_MARK(5);  // phase C complete
     ok = ok && sm.ok[1];
     // ---------------- phase D ----------------
     if (wv == 0) {  // P = P_a + X1^T X1
@@ -331,6 +337,13 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wv_store(fo, of, n, g, c);
         }
     }
+    COMB_MARK(6);  // wave 0: P stored
+#ifdef PDPLQR_COMB_PROFILE
+    __syncthreads();
+#endif
+    COMB_MARK(7);  // every wave through phase D
+    COMB_MARK(8);
+    COMB_MARK(9);
     return ok;
 }
 

@@ -36,8 +36,11 @@ ok = (t[:, 0] > 0) & (t[:, 9] > t[:, 0])
 for k in range(1, 10):
     ok &= t[:, k] >= t[:, k - 1]
 t = t[ok]
-names = ["load Ca", "load Pb+chol R", "T1,S products", "chol Q", "U solve (LDS)", "Y,Z,Zt products", "P path",
-         "F,C path", "vectors"]
+mw = os.environ.get("COMB_MW", "1") != "0"  # the 4-wave combine (combine_mw.hpp) marks
+names = (["A: chol R (w0)", "B: S products (w0)", "B: wait slowest wave", "C: chol S carrying (w0)",
+          "C: wait + store", "D: P (w0)", "D: wait slowest wave", "-", "-"] if mw else
+         ["load Ca", "load Pb+chol R", "T1,S products", "chol Q", "U solve (LDS)", "Y,Z,Zt products", "P path",
+          "F,C path", "vectors"])
 d = np.diff(t[:, :10], axis=1)
 print(f"blocks={len(t)}  wall_clock64 ticks (100 MHz): total median {np.median(t[:, 9] - t[:, 0]):.0f}")
 for k, nm in enumerate(names):
