@@ -29,6 +29,7 @@
 // lower n x n at stage offset k ps: it is all backward_without_factorization
 // needs besides the rollout record (k_seg_bwd_nofact).
 #include "device_common.hpp"
+#include <stdlib.h>
 #include "parallel.hpp"
 
 namespace pdplqr {
@@ -414,6 +415,366 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
     if (lane == 0) A.seg_status[bi * S + seg] = fail_stage < 0 ? 0 : fail_stage + 1;
 }
 
+// ---------------------------------------------------------------------------
+// The same segment backward on a 4-wave workgroup (horizon shards at 24/8:
+// one problem, a few hundred segments -- the stage chain of ONE wave is the
+// latency the whole C4 slice waits on).  Wave w owns column tile w of the
+// padded stage matrix (columns 16 w .. 16 w + 15, all 64 rows); column D =
+// s + n carries the aug vector (rows [u; x]: lp, rows y: F c + f), so the
+// elimination updates it with the matrix.  Per stage:
+//   * waves whose columns include [u; x]: G = P E~ (rows x; P symmetrised
+//     from the published x block), then rows [u; x] = H~ + E~^T G;
+//   * y (and aug) columns: rows [u; x] = E~^T Q[x, col] from the wave's own
+//     registers, rows y unchanged (-C, f);  the rows y of the [u; x] columns
+//     (F E~) are never formed: the elimination takes the pivot COLUMNS from the
+//     pivot rows by symmetry, so nothing reads them;
+//   * lp (column -> row via LDS) and F c complete the aug column;
+//   * the m u-pivots in blocks of 4: every wave publishes its part of the 4
+//     pivot rows, Muu^{-1} is formed wave-uniformly, and each row tile takes one
+//     rank-4 MFMA update  M -= M[:, J] (Muu^{-1} M[J, :])  (A operand = pivot
+//     rows by symmetry, B operand = X of the lane's own column).
+// Records as k_seg_bwd_aug: FR_k = [L(:, 0:m) | lu'] with L(:, J) = M[:, J]
+// Luu^{-T}, G_k = -L(y, u)^T, the factor cache P_k / lp_k, the element.
+// Conditions: s <= 32 (the x columns sit in tiles 0, 1), D = s + n < 64,
+// m % 4 == 0, m <= 16.
+// ---------------------------------------------------------------------------
+#ifdef PDPLQR_COMB_PROFILE
+__device__ unsigned long long g_aug_t[1024 * 8];
+#define AUG_MARK(q)                                                                             \
+    do {                                                                                        \
+        if (tid == 0 && k == N1 - 2) g_aug_t[(blockIdx.x % 1024) * 8 + (q)] = wall_clock64(); \
+    } while (0)
+#else
+#define AUG_MARK(q) \
+    do {            \
+    } while (0)
+#endif
+
+template <int NN, int MM>
+__global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
+    constexpr int n = NN, m = MM, s = NN + MM, D = s + NN, AUG = D;
+    constexpr int ps = s * (s + 1) / 2, PN = n * (n + 1) / 2;
+    constexpr int XLD = n + 1;                       // leading dimension of the published P block
+    constexpr int IN = n * s + ps + n + s;           // stage input doubles: E~ | H~ packed | c | h~
+    constexpr int INQ = (IN + 255) / 256;            // per thread
+    constexpr int K0 = m / 4, K1 = s / 4;            // K chunks of the x rows
+    static_assert(s <= 32 && D < 64 && m % 4 == 0 && m <= 16 && n % 4 == 0, "4-wave aug shape");
+    __shared__ double Xq[n * XLD];                   // P_{k+1} (x rows, x cols)
+    __shared__ double In[IN];                        // E~ (n x s) | H~ packed | c | h~ of this stage
+    __shared__ double Pr[2][4 * 64];                 // pivot rows of block 0 / 1 at every column
+    __shared__ double lpa[32], fcv[32];              // h~ + G^T c per [u; x] column, F c per y column
+    __shared__ int s_bad;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+    const int col = 16 * wv + c;
+    const bool cux = col < s, cy = col >= s && col < D, caug = col == AUG;
+    const Shape &sh = A.sh;
+    const int S = A.S;
+    const long long bi = blockIdx.x / S;
+    const int seg = blockIdx.x % S;
+    const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
+    const bool last = (seg == S - 1) && A.last_is_terminal;
+    const long long frs = (long long)s * m + m;
+    const double *Eb = A.E + bi * sh.perE;
+    const double *cb = A.c + bi * sh.perc;
+    const double *Hb = A.Hw + bi * sh.perHw;
+    const double *hb = A.hw + bi * sh.perh;
+    double *FRb = A.FR + bi * sh.perKD;
+    double *Gb = A.G + bi * (long long)sh.N * m * n;
+    double *Lcb = A.Lc ? A.Lc + bi * sh.perHw : nullptr;
+    double *lpb = A.lpc ? A.lpc + bi * sh.perh : nullptr;
+    const double *Es = In, *Hs = In + n * s, *cs = Hs + ps, *hs = cs + n;
+    int fail_stage = -1;
+    // stage inputs: HBM -> registers (issued a stage ahead) -> LDS
+    double pre[INQ];
+    auto in_load = [&](int k) {
+#pragma unroll
+        for (int q = 0; q < INQ; ++q) {
+            const int i = tid + 256 * q;
+            const double *src = i < n * s ? Eb + (long long)k * n * s + i
+                                : i < n * s + ps ? Hb + (long long)k * sh.ps + (i - n * s)
+                                : i < n * s + ps + n ? cb + (long long)k * n + (i - n * s - ps)
+                                                     : hb + (long long)k * s + (i - n * s - ps - n);
+            pre[q] = i < IN ? *src : 0.0;
+        }
+    };
+    auto in_store = [&]() {
+#pragma unroll
+        for (int q = 0; q < INQ; ++q) {
+            const int i = tid + 256 * q;
+            if (i < IN) In[i] = pre[q];
+        }
+    };
+    if (N1 > N0) in_load(N1 - 1);
+    // ---- segment terminal: Q over [x; y; aug] ----
+    d4 Q[4];
+    {
+        const double *HN = Hb + (long long)sh.N * sh.ps;
+        bool bad = false;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g;
+                const bool xi = i >= m && i < s, yi = i >= s && i < D;
+                const bool xj = col >= m && col < s;
+                double v = 0.0;
+                if (last) {
+                    if (xi && xj) v = HN[i >= col ? pidx(i - m, col - m, n) : pidx(col - m, i - m, n)];
+                    if (xi && caug) v = hb[(long long)sh.N * s + (i - m)];
+                    if (xi && i == col && psd_bad(v)) bad = true;
+                } else if (xi && cy && col - s == i - m) {
+                    v = 1.0;  // F^T = I (rows x of the y columns)
+                }
+                (void)yi;
+                Q[a][r] = v;
+            }
+        if (tid == 0) s_bad = 0;
+        __syncthreads();
+        if (bad) s_bad = 1;
+        if (last) {
+            if (Lcb)
+                for (int t = tid; t < PN; t += 256) Lcb[(long long)sh.N * sh.ps + t] = HN[t];
+            if (lpb)
+                for (int t = tid; t < n; t += 256) lpb[(long long)sh.N * s + t] = hb[(long long)sh.N * s + t];
+        }
+        in_store();
+        __syncthreads();
+        if (s_bad) fail_stage = sh.N;
+    }
+    for (int k = N1 - 1; k >= N0; --k) {
+        AUG_MARK(0);
+        // ---- publish P_{k+1} (rows x of the x columns); next stage's inputs in flight ----
+        if (col >= m && col < s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    if (i >= m && i < s) Xq[(i - m) + (col - m) * XLD] = Q[a][r];
+                }
+        if (k > N0) in_load(k - 1);
+        __syncthreads();  // B1
+        AUG_MARK(1);
+        if (tid == 0) s_bad = 0;  // every thread read the previous stage's flag before B1
+        // ---- G = P E~ (rows x, [u; x] columns: waves 0, 1) ----
+        d4 G[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
+        if (wv < 2) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int kk = K0; kk < K1; ++kk) {
+                    const int i = 16 * a + c, kx = 4 * kk + g;  // P row i, P column kx (padded index)
+                    const double av = (i >= m && i < s)
+                                          ? 0.5 * (Xq[(i - m) + (kx - m) * XLD] + Xq[(kx - m) + (i - m) * XLD])
+                                          : 0.0;
+                    const double bv = cux ? Es[(kx - m) + col * n] : 0.0;
+                    G[a] = mfma_f64(av, bv, G[a]);
+                }
+        }
+        AUG_MARK(2);
+        // ---- rows [u; x]: H~ + E~^T G ([u; x] columns), E~^T Q[x, col] (y / aug columns) ----
+        d4 Mu[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            d4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g;
+                acc[r] = (cux && i < s) ? Hs[i >= col ? pidx(i, col, s) : pidx(col, i, s)] : 0.0;
+            }
+#pragma unroll
+            for (int kk = K0; kk < K1; ++kk) {
+                const int i = 16 * a + c, kx = 4 * kk + g;
+                const double av = (i < s) ? Es[(kx - m) + i * n] : 0.0;
+                const double bv = cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3];
+                acc = mfma_f64(av, bv, acc);
+            }
+            Mu[a] = acc;
+        }
+        // ---- aug pieces: lpa[col] = h~ + G^T c ([u; x] columns), fcv = F c (y columns) ----
+        {
+            double part = 0.0;
+#pragma unroll
+            for (int kk = K0; kk < K1; ++kk) {
+                const double cx = cs[4 * kk + g - m];
+                part = __builtin_fma(cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3], cx, part);
+            }
+            part = sum_groups(part);
+            if (g == 0) {
+                if (cux) lpa[col] = hs[col] + part;
+                else if (cy) fcv[col - s] = part;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) Q[a] = Mu[a];
+        AUG_MARK(3);
+        __syncthreads();  // B2
+        AUG_MARK(4);
+        if (caug)  // aug column: rows [u; x] += h~ + G^T c (E~^T p is already in), rows y += F c
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    if (i < s) Q[a][r] += lpa[i];
+                    else if (i < D) Q[a][r] += fcv[i - s];
+                }
+        // ---- the m u-pivots, 4 per block ----
+        double *FRk = FRb + (long long)k * frs;
+        double *Gk = Gb + (long long)k * m * n;
+        bool ok = true;
+#pragma unroll
+        for (int blk = 0; blk < m / 4; ++blk) {
+            const int j0 = 4 * blk;
+            double *P4 = Pr[blk & 1];
+            P4[g * 64 + col] = Q[0][blk];  // row j0 + g at this column
+            __syncthreads();
+            double a4[4][4], L[4][4], T4[4][4], inv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) a4[i][j] = P4[i * 64 + j0 + j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                ok = ok && (a4[j][j] > 0.0);
+                inv[j] = rsqrt_f64(a4[j][j]);
+                L[j][j] = a4[j][j] * inv[j];
+#pragma unroll
+                for (int i = j + 1; i < 4; ++i) L[i][j] = a4[i][j] * inv[j];
+#pragma unroll
+                for (int i = j + 1; i < 4; ++i)
+#pragma unroll
+                    for (int kq = j + 1; kq <= i; ++kq) a4[i][kq] = __builtin_fma(-L[i][j], L[kq][j], a4[i][kq]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {  // T4 = Luu^{-1}
+                T4[i][i] = inv[i];
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int kq = j; kq < i; ++kq) v = __builtin_fma(L[i][kq], T4[kq][j], v);
+                    T4[i][j] = -v * inv[i];
+                }
+            }
+            // X[g][col] = (Muu^{-1} M[J, col])[g] = sum_l (T4^T T4)[g][l] pr[l]
+            double pr[4], y4[4];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) pr[l] = P4[l * 64 + col];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {  // y = T4 pr
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l <= i; ++l) v = __builtin_fma(T4[i][l], pr[l], v);
+                y4[i] = v;
+            }
+            double xg = 0.0;  // (T4^T y)[g]
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = i; l < 4; ++l) v = __builtin_fma(T4[l][i], y4[l], v);
+                xg = (g == i) ? v : xg;
+            }
+            // rank-4 update of every row tile: M[16 a + c'][col] -= M[16 a + c'][J] X[J][col]
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                if (wv < 2 && a >= 2) continue;  // rows y of the [u; x] columns are never read
+                // M[16 a + c][j0 + g] = M[j0 + g][16 a + c] (symmetry; the aug column and the
+                // padding are not rows: zero)
+                const double av = (16 * a + c < D) ? P4[g * 64 + 16 * a + c] : 0.0;
+                Q[a] = mfma_f64(-av, xg, Q[a]);
+            }
+            // records: L(i, j0 + l) = sum_l' M[i][j0 + l'] T4[l][l'],  i < s (FR),  i in y (G_k)
+            if (wv == 0 || wv == 1) {
+                const int i = (wv == 0) ? lane : s + lane;  // wave 0: FR rows, wave 1: coupling rows
+                if ((wv == 0 && i < s) || (wv == 1 && !last && lane < n)) {
+                    double mi[4];
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) mi[l] = P4[l * 64 + i];
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int l2 = 0; l2 <= l; ++l2) v = __builtin_fma(mi[l2], T4[l][l2], v);
+                        if (wv == 0) gstore(FRk + (long long)(j0 + l) * s + i, i >= j0 + l ? v : 0.0);
+                        else gstore(Gk + (j0 + l) + lane * m, -v);
+                    }
+                }
+            }
+            if (tid == 2 * 64) {  // lu' = T4 lu, lu = M[J][aug]
+                double lu[4];
+#pragma unroll
+                for (int l = 0; l < 4; ++l) lu[l] = P4[l * 64 + AUG];
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int l2 = 0; l2 <= l; ++l2) v = __builtin_fma(T4[l][l2], lu[l2], v);
+                    gstore(FRk + (long long)s * m + j0 + l, v);
+                    if (lpb) gstore(lpb + (long long)k * s + j0 + l, v);
+                }
+            }
+        }
+        AUG_MARK(5);
+        // ---- P_k diagonal check, factor cache (P_k packed lower, p_k) ----
+        {
+            bool bad = false;
+            if (col >= m && col < s)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g;
+                        if (i == col && psd_bad(Q[a][r])) bad = true;
+                        if (Lcb && i >= col && i < s) gstore(Lcb + (long long)k * sh.ps + pidx(i - m, col - m, n), Q[a][r]);
+                    }
+            if (caug && lpb)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * a + 4 * r + g;
+                        if (i >= m && i < s) gstore(lpb + (long long)k * s + i, Q[a][r]);
+                    }
+            if (bad) s_bad = 1;
+        }
+        AUG_MARK(6);
+        if (k > N0) in_store();  // this stage's inputs were last read before B2
+        __syncthreads();  // B_end: inputs, flags
+        AUG_MARK(7);
+        if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
+    }
+    // ---- export the element ----
+    double *eo = A.elem + (bi * S + seg) * (long long)(3 * n * n + 2 * n);
+    double *eF = eo, *eC = eo + n * n, *ef = eo + 2 * n * n, *eP = ef + n, *ep = eP + n * n;
+    if (col >= m && col < s)  // P (publish, then symmetrise)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * a + 4 * r + g;
+                if (i >= m && i < s) Xq[(i - m) + (col - m) * XLD] = Q[a][r];
+            }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * a + 4 * r + g;
+            const bool xi = i >= m && i < s, yi = i >= s && i < D;
+            if (xi && cy) eF[(col - s) + (i - m) * n] = last ? 0.0 : Q[a][r];  // F = (F^T)^T
+            if (yi && cy) eC[(i - s) + (col - s) * n] = last ? 0.0 : -Q[a][r];
+            if (xi && caug) ep[i - m] = Q[a][r];
+            if (yi && caug) ef[i - s] = last ? 0.0 : Q[a][r];
+        }
+    __syncthreads();
+    for (int q = tid; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        eP[q] = 0.5 * (Xq[i + j * XLD] + Xq[j + i * XLD]);
+    }
+    if (tid == 0) A.seg_status[bi * S + seg] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
 // Kernel for this shape: tile order T = ceil((2 n + m) / 16), compile-time
 // specialisations for the benchmark shapes.
 static const void *aug_kernel(const Shape &sh) {
@@ -427,10 +788,18 @@ static const void *aug_kernel(const Shape &sh) {
     return reinterpret_cast<const void *>(&k_seg_bwd_aug<4, 0, 0>);
 }
 
+// the 4-wave stage for 24/8 (PDPLQR_AUG_1WAVE: the one-wave k_seg_bwd_aug, A/B)
+static bool aug_mw(const Shape &sh) { return sh.n == 24 && sh.m == 8 && !getenv("PDPLQR_AUG_1WAVE"); }
+
 int seg_backward_slots(const Shape &sh, int device) {
     if (wide_stage(sh)) return wide_seg_backward_slots(sh, device);
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    if (aug_mw(sh)) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_bwd_aug_mw<24, 8>, 256, 0) != hipSuccess || per <= 0)
+            per = 1;
+        return cus * per;
+    }
     const void *k = aug_kernel(sh);
     if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 64, 0) != hipSuccess || per <= 0) per = 1;
     return cus * per;
@@ -438,6 +807,11 @@ int seg_backward_slots(const Shape &sh, int device) {
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st) {
     if (wide_stage(a.sh)) return launch_seg_backward_wide(a, st);
+    if (aug_mw(a.sh) && a.sh.N >= 1) {
+        hipLaunchKernelGGL((k_seg_bwd_aug_mw<24, 8>), dim3((unsigned)(a.sh.batch * a.S)), dim3(256), 0, st, a);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     const void *k = aug_kernel(a.sh);
     if (!k) {
         set_error("parallel solver: n + m > 32 is not supported by this build");
@@ -449,3 +823,9 @@ int launch_seg_backward(const SegArgs &a, hipStream_t st) {
 }
 
 }  // namespace pdplqr
+
+#ifdef PDPLQR_COMB_PROFILE
+extern "C" int pdplqr_debug_aug_times(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_aug_t), sizeof(unsigned long long) * 1024 * 8) == hipSuccess ? 0 : -2;
+}
+#endif

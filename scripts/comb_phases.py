@@ -27,6 +27,8 @@ sh.update_problem_data(torch.zeros(1, N * (n + m) + n, dtype=torch.float64, devi
 elem = torch.empty(1, sh.es, dtype=torch.float64, device=dev)
 sh.backward(elem, True)
 sh.synchronize()
+sh.backward(elem, True)
+sh.synchronize()
 L = _lib.lib()
 buf = np.zeros(1024 * 16, dtype=np.uint64)
 L.pdplqr_debug_comb_times.argtypes = [C.c_void_p]
@@ -51,3 +53,18 @@ if len(seg):
     st = seg[:, 12]
     print(f"segment backward ({len(seg)} waves, median {np.median(st):.0f} stages): ticks per stage "
           f"riccati {np.median(seg[:, 10] / st):.0f}  element {np.median(seg[:, 11] / st):.0f}")
+# stage phases of the 4-wave segment backward (k_seg_bwd_aug_mw, second stage of each segment)
+if hasattr(L, "pdplqr_debug_aug_times"):
+    ab = np.zeros(1024 * 8, dtype=np.uint64)
+    L.pdplqr_debug_aug_times.argtypes = [C.c_void_p]
+    if L.pdplqr_debug_aug_times(C.c_void_p(ab.ctypes.data)) == 0:
+        a = ab.reshape(1024, 8).astype(np.int64)
+        ok = (a[:, 0] > 0) & np.all(np.diff(a, axis=1) >= 0, axis=1)
+        a = a[ok]
+        if len(a):
+            an = ["B1 (publish, barrier)", "G = P E~", "rows [u;x] + aug", "B2", "u-pivot blocks", "checks, cache",
+                  "inputs, B_end"]
+            da = np.diff(a, axis=1)
+            print(f"aug stage ({len(a)} blocks): total median {np.median(a[:, 7] - a[:, 0]):.0f} ticks")
+            for k, nm in enumerate(an):
+                print(f"  {nm:24s} {np.median(da[:, k]):8.0f}")

@@ -164,12 +164,11 @@ def test_big_admm_serial_matches_oracle():
 
 
 def test_big_shape_limits():
-    """n + m > 64: every solver refuses; 32 < n + m <= 64: PARALLEL and KKT refuse."""
+    """n + m > 64: every solver refuses; 32 < n + m <= 64 runs on every solver
+    (kernels_big.hip, kernels_wide.hip; tests/test_gpu_wide.py)."""
     from pdplqr import BatchedLQRSolver, PdplqrError
 
-    with pytest.raises(PdplqrError):
-        BatchedLQRSolver(50, 15, 4, 1)
-    with pytest.raises(PdplqrError):
-        BatchedLQRSolver(30, 10, 8, 1, solver="parallel", num_segments=2)
-    with pytest.raises(PdplqrError):
-        BatchedLQRSolver(30, 10, 8, 1, solver="kkt")
+    for solver in ("serial", "parallel", "kkt"):
+        with pytest.raises(PdplqrError):
+            BatchedLQRSolver(50, 15, 4, 1, solver=solver, num_segments=2)
+        BatchedLQRSolver(30, 10, 8, 1, solver=solver, num_segments=2).close()
