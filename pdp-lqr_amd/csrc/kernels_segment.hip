@@ -557,39 +557,56 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
         AUG_MARK(1);
         if (tid == 0) s_bad = 0;  // every thread read the previous stage's flag before B1
         // ---- G = P E~ (rows x, [u; x] columns: waves 0, 1) ----
+        // Every operand is read from LDS before the first product, so the two
+        // accumulation chains run back to back (a wait on each product's LDS
+        // reads put the LDS latency on the chain: 1.2 us per stage, r3g).
+        constexpr int NK = K1 - K0;
+        double bvE[NK];  // E~[kx - m][col] (B operand of G)
+#pragma unroll
+        for (int q = 0; q < NK; ++q) bvE[q] = cux ? Es[(4 * (K0 + q) + g - m) + (cux ? col : 0) * n] : 0.0;
         d4 G[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
         if (wv < 2) {
+            double avP[2][NK];  // P_sym[16 a + c][kx]
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int kk = K0; kk < K1; ++kk) {
-                    const int i = 16 * a + c, kx = 4 * kk + g;  // P row i, P column kx (padded index)
-                    const double av = (i >= m && i < s)
-                                          ? 0.5 * (Xq[(i - m) + (kx - m) * XLD] + Xq[(kx - m) + (i - m) * XLD])
-                                          : 0.0;
-                    const double bv = cux ? Es[(kx - m) + col * n] : 0.0;
-                    G[a] = mfma_f64(av, bv, G[a]);
+                for (int q = 0; q < NK; ++q) {
+                    const int i = 16 * a + c, kx = 4 * (K0 + q) + g;
+                    const bool xi = i >= m && i < s;
+                    const int ii = xi ? i - m : 0;
+                    avP[a][q] = xi ? 0.5 * (Xq[ii + (kx - m) * XLD] + Xq[(kx - m) + ii * XLD]) : 0.0;
                 }
+#pragma unroll
+            for (int q = 0; q < NK; ++q)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
         }
         AUG_MARK(2);
         // ---- rows [u; x]: H~ + E~^T G ([u; x] columns), E~^T Q[x, col] (y / aug columns) ----
         d4 Mu[2];
+        {
+            double avE[2][NK];  // E~^T[16 a + c][kx] = E~[kx - m][16 a + c]
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            d4 acc;
+            for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * a + 4 * r + g;
-                acc[r] = (cux && i < s) ? Hs[i >= col ? pidx(i, col, s) : pidx(col, i, s)] : 0.0;
-            }
+                for (int q = 0; q < NK; ++q) {
+                    const int i = 16 * a + c, kx = 4 * (K0 + q) + g;
+                    avE[a][q] = (i < s) ? Es[(kx - m) + (i < s ? i : 0) * n] : 0.0;
+                }
 #pragma unroll
-            for (int kk = K0; kk < K1; ++kk) {
-                const int i = 16 * a + c, kx = 4 * kk + g;
-                const double av = (i < s) ? Es[(kx - m) + i * n] : 0.0;
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    Mu[a][r] = (cux && i < s) ? Hs[i >= col ? pidx(i, col, s) : pidx(col, i, s)] : 0.0;
+                }
+#pragma unroll
+            for (int q = 0; q < NK; ++q) {
+                const int kk = K0 + q;
                 const double bv = cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3];
-                acc = mfma_f64(av, bv, acc);
+#pragma unroll
+                for (int a = 0; a < 2; ++a) Mu[a] = mfma_f64(avE[a][q], bv, Mu[a]);
             }
-            Mu[a] = acc;
         }
         // ---- aug pieces: lpa[col] = h~ + G^T c ([u; x] columns), fcv = F c (y columns) ----
         {
@@ -629,11 +646,24 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
             double *P4 = Pr[blk & 1];
             P4[g * 64 + col] = Q[0][blk];  // row j0 + g at this column
             __syncthreads();
-            double a4[4][4], L[4][4], T4[4][4], inv[4];
+            // every LDS read of the block up front (one wait), then the arithmetic
+            double a4[4][4], L[4][4], T4[4][4], inv[4], pr[4], avv[4], mi[4], lu[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j <= i; ++j) a4[i][j] = P4[i * 64 + j0 + j];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) pr[l] = P4[l * 64 + col];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)  // M[16 a + c][j0 + g] = M[j0 + g][16 a + c] (symmetry;
+                avv[a] = (16 * a + c < D) ? P4[g * 64 + 16 * a + c] : 0.0;  // aug / padding: not rows)
+            // records: wave 0 the FR rows i < s, wave 1 the coupling rows s + lane
+            const int ir = (wv == 0) ? lane : s + lane;
+            const bool rec = (wv == 0 && ir < s) || (wv == 1 && !last && lane < n);
+#pragma unroll
+            for (int l = 0; l < 4; ++l) mi[l] = (wv < 2) ? P4[l * 64 + (ir < 64 ? ir : 0)] : 0.0;
+#pragma unroll
+            for (int l = 0; l < 4; ++l) lu[l] = P4[l * 64 + AUG];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 ok = ok && (a4[j][j] > 0.0);
@@ -657,18 +687,16 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
                     T4[i][j] = -v * inv[i];
                 }
             }
-            // X[g][col] = (Muu^{-1} M[J, col])[g] = sum_l (T4^T T4)[g][l] pr[l]
-            double pr[4], y4[4];
+            // X[g][col] = (Muu^{-1} M[J, col])[g] = (T4^T (T4 pr))[g]
+            double y4[4];
 #pragma unroll
-            for (int l = 0; l < 4; ++l) pr[l] = P4[l * 64 + col];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {  // y = T4 pr
+            for (int i = 0; i < 4; ++i) {
                 double v = 0.0;
 #pragma unroll
                 for (int l = 0; l <= i; ++l) v = __builtin_fma(T4[i][l], pr[l], v);
                 y4[i] = v;
             }
-            double xg = 0.0;  // (T4^T y)[g]
+            double xg = 0.0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 double v = 0.0;
@@ -680,32 +708,20 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 if (wv < 2 && a >= 2) continue;  // rows y of the [u; x] columns are never read
-                // M[16 a + c][j0 + g] = M[j0 + g][16 a + c] (symmetry; the aug column and the
-                // padding are not rows: zero)
-                const double av = (16 * a + c < D) ? P4[g * 64 + 16 * a + c] : 0.0;
-                Q[a] = mfma_f64(-av, xg, Q[a]);
+                Q[a] = mfma_f64(-avv[a], xg, Q[a]);
             }
-            // records: L(i, j0 + l) = sum_l' M[i][j0 + l'] T4[l][l'],  i < s (FR),  i in y (G_k)
-            if (wv == 0 || wv == 1) {
-                const int i = (wv == 0) ? lane : s + lane;  // wave 0: FR rows, wave 1: coupling rows
-                if ((wv == 0 && i < s) || (wv == 1 && !last && lane < n)) {
-                    double mi[4];
+            // records: L(i, j0 + l) = sum_l' M[i][j0 + l'] T4[l][l']
+            if (rec) {
 #pragma unroll
-                    for (int l = 0; l < 4; ++l) mi[l] = P4[l * 64 + i];
+                for (int l = 0; l < 4; ++l) {
+                    double v = 0.0;
 #pragma unroll
-                    for (int l = 0; l < 4; ++l) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int l2 = 0; l2 <= l; ++l2) v = __builtin_fma(mi[l2], T4[l][l2], v);
-                        if (wv == 0) gstore(FRk + (long long)(j0 + l) * s + i, i >= j0 + l ? v : 0.0);
-                        else gstore(Gk + (j0 + l) + lane * m, -v);
-                    }
+                    for (int l2 = 0; l2 <= l; ++l2) v = __builtin_fma(mi[l2], T4[l][l2], v);
+                    if (wv == 0) gstore(FRk + (long long)(j0 + l) * s + ir, ir >= j0 + l ? v : 0.0);
+                    else gstore(Gk + (j0 + l) + lane * m, -v);
                 }
             }
             if (tid == 2 * 64) {  // lu' = T4 lu, lu = M[J][aug]
-                double lu[4];
-#pragma unroll
-                for (int l = 0; l < 4; ++l) lu[l] = P4[l * 64 + AUG];
 #pragma unroll
                 for (int l = 0; l < 4; ++l) {
                     double v = 0.0;
