@@ -76,7 +76,13 @@ __device__ __forceinline__ void mw_col_load(d4 (&B)[T][1], const double *p, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g, jj = 16 * j + c;
+#if PDPLQR_BF_LOAD
+            const bool in = i < n && jj < n;
+            const double v = p[(in ? i : 0) + (in ? jj : 0) * PL];  // branch-free (see wm_load)
+            B[a][0][r] = in ? v : 0.0;
+#else
             B[a][0][r] = (i < n && jj < n) ? p[i + jj * PL] : 0.0;
+#endif
         }
 }
 
@@ -100,7 +106,13 @@ __device__ __forceinline__ void mw_vec2_load(d4 (&B)[T][1], const double *p, int
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g;
+#if PDPLQR_BF_LOAD
+            const bool in = i < n && c < 2;
+            const double v = p[(in ? i : 0) + (in ? c : 0) * P];  // branch-free (see wm_load)
+            B[a][0][r] = in ? v : 0.0;
+#else
             B[a][0][r] = (i < n && c < 2) ? p[i + c * P] : 0.0;
+#endif
         }
 }
 
@@ -122,7 +134,9 @@ template <int T>
 __device__ __forceinline__ bool mw_chol_R(WM<T> &R, const double *Pb, double *scr, int PL, int n, int g, int c) {
     WM<T> U;
     wm_load(U, Pb, n, n, false, 1.0, g, c);
+    COMB_MARK(19);  // P_b loaded
     const bool ok = chol_blk4<T, false, T>(U, U.t, n, g, c);  // U = R^T
+    COMB_MARK(20);  // factored
     wm_store(U, scr, PL, n, g, c);
     wave_sync();
     wm_load(R, scr, PL, n, true, 1.0, g, c);
@@ -160,6 +174,11 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         } else {
             // S, B1, B2 are consecutive blocks (a select of the three pointers
             // compiled to a table in scratch)
+#ifdef PDPLQR_EXP_SHARE_R  // timing experiment only (wrong results): waves 1, 2 skip their chol
+            if (wv > 0) {
+                wm_load(R, eb.P, n, n, false, 1.0, g, c);
+            } else
+#endif
             ok = mw_chol_R<T>(R, eb.P, sm.S + wv * (n * sm.ld), sm.ld, n, g, c);
         }
     } else {
@@ -285,6 +304,9 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
                 V[a][0] = BV[a][1];
             }
         } else if (kind >= 0) {
+#ifdef PDPLQR_EXP_SHARE_S  // timing experiment only (wrong results): one chol(S)
+            if (wv == 0)
+#endif
             okS = chol_blk4<T, true, 1>(S, B, n, g, c);
         }
         COMB_MARK(4);  // wave 0: chol(S) done

@@ -30,12 +30,12 @@ struct WM {
 
 // Phase timestamps of the combines (debug builds with -DPDPLQR_COMB_PROFILE:
 // lane 0 of every block records wall_clock64() at each mark into slot
-// blockIdx % 1024; read back with pdplqr_debug_comb_times).
+// blockIdx % 1024, 32 marks per block; read back with pdplqr_debug_comb_times).
 #if defined(PDPLQR_COMB_PROFILE) && defined(PDPLQR_COMB_PROFILE_TU)  // kernels_parallel.hip only
-extern __device__ unsigned long long g_comb_t[1024 * 16];
+extern __device__ unsigned long long g_comb_t[1024 * 32];
 #define COMB_MARK(k)                                                                     \
     do {                                                                                 \
-        if (threadIdx.x == 0) g_comb_t[(blockIdx.x % 1024) * 16 + (k)] = wall_clock64(); \
+        if (threadIdx.x == 0) g_comb_t[(blockIdx.x % 1024) * 32 + (k)] = wall_clock64(); \
     } while (0)
 #else
 #define COMB_MARK(k) \
@@ -59,6 +59,19 @@ struct CombSmem {
 
 // M <- n x n block at p (column-major, leading dimension ld, or its transpose);
 // outside the block: `pad` on the diagonal, 0 elsewhere
+// K-chunk-outer products (PDPLQR_TN_CHUNK_OUTER=1; =0 one chain per output
+// tile, every MFMA in its own basic block) and branch-free tile loads
+// (PDPLQR_BF_LOAD=1: clamped address + select).  Same-box A/B on the 24 x 24
+// combine (profiles/r03/comb_ab.log): chunk-outer 1824 -> 1676 ticks, the
+// branch-free loads 1728 -> 1824 (they also read the all-padding registers a
+// guard skips as a whole), so they stay off here.
+#ifndef PDPLQR_BF_LOAD
+#define PDPLQR_BF_LOAD 0
+#endif
+#ifndef PDPLQR_TN_CHUNK_OUTER
+#define PDPLQR_TN_CHUNK_OUTER 1
+#endif
+
 template <int T>
 __device__ __forceinline__ void wm_load(WM<T> &M, const double *p, int ld, int n, bool trans, double pad, int g,
                                         int c) {
@@ -68,10 +81,20 @@ __device__ __forceinline__ void wm_load(WM<T> &M, const double *p, int ld, int n
         for (int b = 0; b < T; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+                // branch-free: an unconditional read at a clamped address and a
+                // select (a guarded read compiles to an exec-mask region with its
+                // own wait per element)
                 const int i = 16 * a + 4 * r + g, j = 16 * b + c;
+#if PDPLQR_BF_LOAD
+                const bool in = i < n && j < n;
+                const int ic = in ? i : 0, jc = in ? j : 0;
+                const double x = trans ? p[jc + ic * ld] : p[ic + jc * ld];
+                M.t[a][b][r] = in ? x : ((i == j) ? pad : 0.0);
+#else
                 double v = (i == j) ? pad : 0.0;
                 if (i < n && j < n) v = trans ? p[j + i * ld] : p[i + j * ld];
                 M.t[a][b][r] = v;
+#endif
             }
 }
 
@@ -106,23 +129,46 @@ __device__ __forceinline__ void wm_store_t(const WM<T> &M, double *p, int n, int
 template <int T>
 __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, int n, double sgn, double diag,
                                       const WM<T> *add, int g, int c) {
+    // K chunk outermost: the T x T output tiles are independent accumulation
+    // chains, issued back to back inside one chunk (one uniform branch per
+    // chunk for a runtime n; a chain per tile would put every MFMA in its own
+    // basic block and wait for the previous one's result)
+    d4 acc[T][T];
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll
-        for (int b = 0; b < T; ++b) {
-            d4 acc;
+        for (int b = 0; b < T; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * a + 4 * r + g, j = 16 * b + c;
-                acc[r] = (add ? add->t[a][b][r] : 0.0) + (i == j ? diag : 0.0);
+                acc[a][b][r] = (add ? add->t[a][b][r] : 0.0) + (i == j ? diag : 0.0);
             }
+#if PDPLQR_TN_CHUNK_OUTER
+#pragma unroll
+    for (int kt = 0; kt < T; ++kt)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            if (16 * kt + 4 * kk < n) {
+#pragma unroll
+                for (int a = 0; a < T; ++a)
+#pragma unroll
+                    for (int b = 0; b < T; ++b) acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
+            }
+#else
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
 #pragma unroll
             for (int kt = 0; kt < T; ++kt)
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk)
-                    if (16 * kt + 4 * kk < n) acc = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc);
-            C.t[a][b] = acc;
-        }
+                    if (16 * kt + 4 * kk < n) acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
+#endif
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b) C.t[a][b] = acc[a][b];
 }
 
 // ---------------------------------------------------------------------------
@@ -262,6 +308,11 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, d4 (&B)[T][TB], int n_rt, 
 // PDPLQR_T4_MFMA=0 keeps the broadcast form (A/B diagnostics).
 #ifndef PDPLQR_T4_MFMA
 #define PDPLQR_T4_MFMA 1
+#endif
+// Blocked-Cholesky trailing update on the upper tiles only, the next block's
+// diagonal tile first (PDPLQR_CHOL_UPPER=0: every tile pair, row order; A/B)
+#ifndef PDPLQR_CHOL_UPPER
+#define PDPLQR_CHOL_UPPER 1
 #endif
 
 // The lane picks are products with 0/1 weights (loop-invariant per lane), not
@@ -463,11 +514,26 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
 #endif
             }
         }
+        // Trailing update, upper tiles only (the panels read M's row blocks
+        // M.t[tj][ta], ta >= tj, and the diagonal tiles; a lower tile is never
+        // read again).  The next block's diagonal tile goes first: its
+        // readlanes wait on that one product.
+#if PDPLQR_CHOL_UPPER
+        const int ntj = (blk + 1) >> 2;
+        if (ntj < T) M.t[ntj][ntj] = mfma_f64(-vt[ntj], vt[ntj], M.t[ntj][ntj]);
+#pragma unroll
+        for (int ta = 0; ta < T; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < T; ++tb)
+                if (ta >= tj && tb >= ta && !(ta == ntj && tb == ntj))
+                    M.t[ta][tb] = mfma_f64(-vt[ta], vt[tb], M.t[ta][tb]);
+#else
 #pragma unroll
         for (int ta = 0; ta < T; ++ta)
 #pragma unroll
             for (int tb = 0; tb < T; ++tb)
                 if (ta >= tj && tb >= tj) M.t[ta][tb] = mfma_f64(-vt[ta], vt[tb], M.t[ta][tb]);
+#endif
         if (AUG)
 #pragma unroll
             for (int ta = 0; ta < T; ++ta)
@@ -679,7 +745,12 @@ __device__ __forceinline__ void wv_load(WV<T> &x, const double *p, int n, int g,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g;
+#if PDPLQR_BF_LOAD
+            const double v = p[i < n ? i : 0];  // branch-free (see wm_load)
+            x.t[a][r] = (c == 0 && i < n) ? v : 0.0;
+#else
             x.t[a][r] = (c == 0 && i < n) ? p[i] : 0.0;
+#endif
         }
 }
 
@@ -699,16 +770,29 @@ __device__ __forceinline__ void wv_store(const WV<T> &x, double *p, int n, int g
 template <int T>
 __device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, int n, double sgn,
                                       const WV<T> *add) {
+    d4 acc[T];  // chunk outermost (see wm_tn)
 #pragma unroll
-    for (int a = 0; a < T; ++a) {
-        d4 acc = add ? add->t[a] : d4{0.0, 0.0, 0.0, 0.0};
+    for (int a = 0; a < T; ++a) acc[a] = add ? add->t[a] : d4{0.0, 0.0, 0.0, 0.0};
+#if PDPLQR_TN_CHUNK_OUTER
+#pragma unroll
+    for (int kt = 0; kt < T; ++kt)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            if (16 * kt + 4 * kk < n) {
+#pragma unroll
+                for (int a = 0; a < T; ++a) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
+            }
+#else
+#pragma unroll
+    for (int a = 0; a < T; ++a)
 #pragma unroll
         for (int kt = 0; kt < T; ++kt)
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk)
-                if (16 * kt + 4 * kk < n) acc = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc);
-        y.t[a] = acc;
-    }
+                if (16 * kt + 4 * kk < n) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
+#endif
+#pragma unroll
+    for (int a = 0; a < T; ++a) y.t[a] = acc[a];
 }
 
 // symmetric store: out = (M + M^T) / 2 (n x n, ld n) through the LDS staging buffer

@@ -33,7 +33,7 @@
 namespace pdplqr {
 
 #ifdef PDPLQR_COMB_PROFILE
-__device__ unsigned long long g_comb_t[1024 * 16];
+__device__ unsigned long long g_comb_t[1024 * 32];
 #endif
 
 // Element views: [F | C | f | P | p] packed contiguously (3 n^2 + 2 n doubles)
@@ -363,15 +363,27 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
         return;
     }
     const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    COMB_MARK(16);  // kernel entry
+#ifdef PDPLQR_COMB_PROFILE
+    if (threadIdx.x == 0) {
+        g_comb_t[(blockIdx.x % 1024) * 32 + 21] = d;  // the round
+        g_comb_t[(blockIdx.x % 1024) * 32 + 22] = fcf;
+    }
+#endif
     const MwSmem sm = mw_smem(mwbuf, n);
     double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
     stage_range_blk(ea, in + (long long)i * is, es);
     stage_range_blk(eb, in + (long long)(i + d) * is, es);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    COMB_MARK(17);  // operands staged
     double *o = out + (long long)i * es;
     const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
                                   elem_in(eb, n), n, fcf, sm);
+#ifdef PDPLQR_COMB_PROFILE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    COMB_MARK(18);  // wave 0's stores complete
+#endif
     if (!fcf && wv == 1)
         for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
     if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
@@ -464,13 +476,126 @@ __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     }
 }
 
+// The boundary map of element e under the value function (vP, vp) on a
+// 4-wave block (CHOLESKY form, every operand in LDS):
+//     R = chol(P), S = I + R^T C R = Q Q^T,  X1 = Q^{-1} R^T F,
+//     V = Q^{-1} R^{-1},  x3 = Q^{-1} R^T (f - C p)
+//     Phi = V^T X1,  phi = V^T x3
+// -- the solve of (I + C P) [Phi | phi] = [F | f - C p] (no I - C Y
+// cancellation, see tmap_solve in combine_tiles.hpp).  Wave 0 returns Phi (or
+// Phi^T when trans) and phi; every wave returns the block-uniform status.
+template <int T>
+__device__ __forceinline__ bool mw_map(const ElemIn &e, const double *vP, const double *vp, int n, const MwSmem &sm,
+                                       bool trans, WM<T> &Phi, WV<T> &phi) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int PL = sm.ld;
+    bool ok = true;
+    WM<T> R;
+    // ---- phase A: R = chol(P_j) (w0, w1); R^{-1} (w2: the same factorisation
+    //      carrying the identity) ----
+    if (wv < 2) {
+        ok = mw_chol_R<T>(R, vP, sm.S + wv * (n * PL), PL, n, g, c) && ok;
+    } else if (wv == 2) {
+        WM<T> Pm, Ri;
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Ri.t[a][bt][r] = (16 * a + 4 * r + g == 16 * bt + c) ? 1.0 : 0.0;
+        wm_load(Pm, vP, n, n, false, 1.0, g, c);
+        ok = chol_blk4<T, true, T>(Pm, Ri.t, n, g, c) && ok;  // Ri = R^{-1}
+        wm_store(Ri, sm.B2, PL, n, g, c);
+    }
+    // ---- phase B ----
+    if (wv == 0) {
+        WM<T> Cs, T1, Sm;
+        wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+        wm_tn(T1, Cs, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C R
+        wm_tn(Sm, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);  // I + R^T C R
+        wm_store(Sm, sm.S, PL, n, g, c);
+        if (lane == 0) sm.ok[0] = ok;
+    } else if (wv == 1) {
+        WM<T> Fs, B;
+        wm_load(Fs, e.F, n, n, false, 0.0, g, c);
+        wm_tn(B, R, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F
+        wm_store(B, sm.B1, PL, n, g, c);
+        WM<T> Cs;
+        WV<T> pv, fs, v, y;
+        wm_load(Cs, e.C, n, n, false, 0.0, g, c);
+        wv_load(pv, vp, n, g, c);
+        wv_load(fs, e.f, n, g, c);
+        wv_tn(v, Cs, pv, n, -1.0, &fs);                  // v = f - C p_j
+        wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
+        wv_store(y, sm.bv, n, g, c);
+    }
+    if (wv == 2 && lane == 0) sm.ok[2] = ok;
+    __syncthreads();
+    ok = ok && sm.ok[0] && sm.ok[2];
+    // ---- phase C: chol(S) carrying one column tile per wave: X1 = Q^{-1} R^T F,
+    //      V = Q^{-1} R^{-1}, x3 = Q^{-1} R^T v ----
+    {
+        WM<T> Sm;
+        wm_load(Sm, sm.S, PL, n, false, 1.0, g, c);
+        d4 B[T][1], V[T][1];
+        int kind, tile = 0;  // 0: X1, 1: V, 2: x3
+        if (T == 2) {
+            kind = wv < 2 ? 0 : 1;
+            tile = wv & 1;
+        } else {
+            kind = wv == 0 ? 2 : (wv == 1 ? 0 : (wv == 2 ? 1 : -1));
+        }
+        const bool vec3 = T == 2 && wv == 3;
+        if (kind == 0) mw_col_load<T>(B, sm.B1, PL, tile, n, g, c);
+        else if (kind == 1) mw_col_load<T>(B, sm.B2, PL, tile, n, g, c);
+        else if (kind == 2) mw_vec2_load<T>(B, sm.bv, n, g, c);
+        if (vec3) mw_vec2_load<T>(V, sm.bv, n, g, c);
+        bool okS = true;
+        if (vec3) {
+            d4 BV[T][2];
+#pragma unroll
+            for (int a = 0; a < T; ++a) {
+                BV[a][0] = B[a][0];
+                BV[a][1] = V[a][0];
+            }
+            okS = chol_blk4<T, true, 2>(Sm, BV, n, g, c);
+#pragma unroll
+            for (int a = 0; a < T; ++a) {
+                B[a][0] = BV[a][0];
+                V[a][0] = BV[a][1];
+            }
+        } else if (kind >= 0) {
+            okS = chol_blk4<T, true, 1>(Sm, B, n, g, c);
+        }
+        __syncthreads();
+        if (kind == 0) mw_col_store<T>(B, sm.B1, PL, tile, n, g, c);
+        else if (kind == 1) mw_col_store<T>(B, sm.B2, PL, tile, n, g, c);
+        else if (kind == 2) mw_vec2_store<T>(B, sm.bv, n, g, c);
+        if (vec3) mw_vec2_store<T>(V, sm.bv, n, g, c);
+        if (wv == 0 && lane == 0) sm.ok[1] = okS;
+    }
+    __syncthreads();
+    ok = ok && sm.ok[1];
+    // ---- phase D: [Phi | phi] = R^{-T} Q^{-T} [X1 | x3] = V^T [X1 | x3]: the
+    //      solve of (I + C P_j) [Phi | phi] = [F | v] (no I - C Y cancellation,
+    //      see tmap_solve in combine_tiles.hpp) ----
+    if (wv == 0) {
+        WM<T> Vm, X1;
+        WV<T> x3;
+        wm_load(Vm, sm.B2, PL, n, false, 0.0, g, c);
+        wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
+        wv_load(x3, sm.bv, n, g, c);
+        wv_tn(phi, Vm, x3, n, 1.0, (const WV<T> *)nullptr);
+        if (!trans) wm_tn(Phi, Vm, X1, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // V^T X1
+        else wm_tn(Phi, X1, Vm, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);        // Phi^T = X1^T V
+    }
+    return ok;
+}
+
 // k_seg_maps on a 4-wave block (CHOLESKY form, combine_mw.hpp): the same
 // outputs.  V_j = suf_j (x) right is the P-only 4-wave combine; the map is
-//     R = chol(P_j), S = I + R^T C R = Q Q^T,  X1 = Q^{-1} R^T F,
-//     X2 = Q^{-1} R^T C,  x3 = Q^{-1} R^T (f - C p_j)
-//     Phi = Z F = F - X2^T X1,   phi = Z (f - C p_j) = v - X2^T x3
-// (Z = (I + C P_j)^{-1} = I - C R S^{-1} R^T), with the products after the
-// factorisations one deep and split over the waves by output tile.
+// mw_map's solve, with the products after the factorisations one deep and
+// split over the waves by output tile.
 template <int T>
 __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
@@ -480,7 +605,6 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
     const MwSmem sm = mw_smem(mwbuf, n);
-    const int PL = sm.ld;
     const double *right = A.right ? A.right + b * (A.rstride ? A.rstride : (long long)es) : nullptr;
     double *vo = A.vfun + (b * J + j) * (long long)mw;
     double *mo = A.maps + (b * J + j) * (long long)mw;
@@ -519,114 +643,16 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     WV<T> phi, x;
     bool have_x = false;  // j = 0: x_0 formed (wave 0)
     if (src && vP) {
-        const ElemIn e = elem_in(src, n);
-        WM<T> R;
-        // ---- phase A: R = chol(P_j) (w0, w1); R^{-1} (w2: the same factorisation
-        //      carrying the identity) ----
-        if (wv < 2) {
-            ok = mw_chol_R<T>(R, vP, sm.S + wv * (n * PL), PL, n, g, c) && ok;
-        } else if (wv == 2) {
-            WM<T> Pm, Ri;
-#pragma unroll
-            for (int a = 0; a < T; ++a)
-#pragma unroll
-                for (int bt = 0; bt < T; ++bt)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) Ri.t[a][bt][r] = (16 * a + 4 * r + g == 16 * bt + c) ? 1.0 : 0.0;
-            wm_load(Pm, vP, n, n, false, 1.0, g, c);
-            ok = chol_blk4<T, true, T>(Pm, Ri.t, n, g, c) && ok;  // Ri = R^{-1}
-            wm_store(Ri, sm.B2, PL, n, g, c);
-        }
-        // ---- phase B ----
+        WM<T> Phi;
+        ok = mw_map<T>(elem_in(src, n), vP, vp, n, sm, j == 0, Phi, phi) && ok;
         if (wv == 0) {
-            WM<T> Cs, T1, Sm;
-            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
-            wm_tn(T1, Cs, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C R
-            wm_tn(Sm, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);  // I + R^T C R
-            wm_store(Sm, sm.S, PL, n, g, c);
-            if (lane == 0) sm.ok[0] = ok;
-        } else if (wv == 1) {
-            WM<T> Fs, B;
-            wm_load(Fs, e.F, n, n, false, 0.0, g, c);
-            wm_tn(B, R, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F
-            wm_store(B, sm.B1, PL, n, g, c);
-            WM<T> Cs;
-            WV<T> pv, fs, v, y;
-            wm_load(Cs, e.C, n, n, false, 0.0, g, c);
-            wv_load(pv, vp, n, g, c);
-            wv_load(fs, e.f, n, g, c);
-            wv_tn(v, Cs, pv, n, -1.0, &fs);                  // v = f - C p_j
-            wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
-            wv_store(y, sm.bv, n, g, c);
-        }
-        if (wv == 2 && lane == 0) sm.ok[2] = ok;
-        __syncthreads();
-        ok = ok && sm.ok[0] && sm.ok[2];
-        // ---- phase C: chol(S) carrying one column tile per wave: X1 = Q^{-1} R^T F,
-        //      V = Q^{-1} R^{-1}, x3 = Q^{-1} R^T v ----
-        {
-            WM<T> Sm;
-            wm_load(Sm, sm.S, PL, n, false, 1.0, g, c);
-            d4 B[T][1], V[T][1];
-            int kind, tile = 0;  // 0: X1, 1: V, 2: x3
-            if (T == 2) {
-                kind = wv < 2 ? 0 : 1;
-                tile = wv & 1;
-            } else {
-                kind = wv == 0 ? 2 : (wv == 1 ? 0 : (wv == 2 ? 1 : -1));
-            }
-            const bool vec3 = T == 2 && wv == 3;
-            if (kind == 0) mw_col_load<T>(B, sm.B1, PL, tile, n, g, c);
-            else if (kind == 1) mw_col_load<T>(B, sm.B2, PL, tile, n, g, c);
-            else if (kind == 2) mw_vec2_load<T>(B, sm.bv, n, g, c);
-            if (vec3) mw_vec2_load<T>(V, sm.bv, n, g, c);
-            bool okS = true;
-            if (vec3) {
-                d4 BV[T][2];
-#pragma unroll
-                for (int a = 0; a < T; ++a) {
-                    BV[a][0] = B[a][0];
-                    BV[a][1] = V[a][0];
-                }
-                okS = chol_blk4<T, true, 2>(Sm, BV, n, g, c);
-#pragma unroll
-                for (int a = 0; a < T; ++a) {
-                    B[a][0] = BV[a][0];
-                    V[a][0] = BV[a][1];
-                }
-            } else if (kind >= 0) {
-                okS = chol_blk4<T, true, 1>(Sm, B, n, g, c);
-            }
-            __syncthreads();
-            if (kind == 0) mw_col_store<T>(B, sm.B1, PL, tile, n, g, c);
-            else if (kind == 1) mw_col_store<T>(B, sm.B2, PL, tile, n, g, c);
-            else if (kind == 2) mw_vec2_store<T>(B, sm.bv, n, g, c);
-            if (vec3) mw_vec2_store<T>(V, sm.bv, n, g, c);
-            if (wv == 0 && lane == 0) sm.ok[1] = okS;
-        }
-        __syncthreads();
-        ok = ok && sm.ok[1];
-        // ---- phase D: [Phi | phi] = R^{-T} Q^{-T} [X1 | x3] = V^T [X1 | x3]: the
-        //      solve of (I + C P_j) [Phi | phi] = [F | v] (no I - C Y cancellation,
-        //      see tmap_solve in combine_tiles.hpp) ----
-        if (wv == 0) {
-            WM<T> Vm, X1;
-            WV<T> x3;
-            wm_load(Vm, sm.B2, PL, n, false, 0.0, g, c);
-            wm_load(X1, sm.B1, PL, n, false, 0.0, g, c);
-            wv_load(x3, sm.bv, n, g, c);
-            wv_tn(phi, Vm, x3, n, 1.0, (const WV<T> *)nullptr);
             if (j > 0) {
-                WM<T> Phi;
-                wm_tn(Phi, Vm, X1, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // V^T X1
                 wm_store(Phi, mo, n, n, g, c);
                 wv_store(phi, mo + nn, n, g, c);
             } else {
-                WM<T> PhiT;
                 WV<T> x0v;
-                wm_tn(PhiT, X1, Vm, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi^T = X1^T V
                 wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
-                wv_tn(x, PhiT, x0v, n, 1.0, &phi);
+                wv_tn(x, Phi, x0v, n, 1.0, &phi);
                 have_x = true;
             }
         }
@@ -961,6 +987,35 @@ __global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const
     if (!ok && lane == 0) atomicOr(flag + b, 4);
 }
 
+// k_rank_maps on a 4-wave block (CHOLESKY form): the map of e_j under
+// V_{j+1} by mw_map, both operands staged into LDS first.  A one-wave
+// tmap_solve chains three triangular solves after the factorisations
+// (43 us per launch at n = 24); mw_map spreads them over the waves.
+template <int T>
+__global__ __launch_bounds__(256) void k_rank_maps_mw(const double *elems_all, const double *suf, int R, int r, int n,
+                                                      int batch, double *maps, int *flag) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
+    const long long b = blockIdx.x / r;
+    const int j = blockIdx.x % r;
+    const MwSmem sm = mw_smem(mwbuf, n);
+    double *es0 = mwbuf + mw_smem_doubles(n), *es1 = es0 + elem_slot(n);
+    stage_range_blk(es0, elems_all + ((long long)j * batch + b) * es, es);           // e_j (rank-major all-gather)
+    stage_range_blk(es1, suf + (b * R + j + 1) * (long long)es + 2 * nn + n, mw);  // [P | p] of V_{j+1}
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    WM<T> Phi;
+    WV<T> phi;
+    const bool ok = mw_map<T>(elem_in(es0, n), es1, es1 + nn, n, sm, false, Phi, phi);
+    double *mo = maps + (b * r + j) * (long long)mw;
+    if (wv == 0) {
+        wm_store(Phi, mo, n, n, g, c);
+        wv_store(phi, mo + nn, n, g, c);
+    }
+    if (!ok && threadIdx.x == 0) atomicOr(flag + b, 4);
+}
+
 template <int T>
 __global__ __launch_bounds__(64) void k_rank_chain(const double *maps, const double *x0, int r, int n,
                                                    double *out_pre_all) {
@@ -1002,6 +1057,10 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
         hipLaunchKernelGGL(k_rank_chain<1>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else if (T == 2) {
         if (lu) hipLaunchKernelGGL((k_rank_maps<2, true>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
+        else if (seg_scan_mw(n, false))
+            hipLaunchKernelGGL(k_rank_maps_mw<2>, gm, dim3(256),
+                               (size_t)(mw_smem_doubles(n) + elem_slot(n) + ((n * n + n + 1) & ~1)) * sizeof(double),
+                               st, elems, suf, R, r, n, batch, maps, flag);
         else hipLaunchKernelGGL((k_rank_maps<2, false>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
         hipLaunchKernelGGL(k_rank_chain<2>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else {
@@ -1041,6 +1100,6 @@ int launch_fold_shards(const double *elems, int R, int r, int n, int batch, doub
 
 #ifdef PDPLQR_COMB_PROFILE
 extern "C" int pdplqr_debug_comb_times(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_comb_t), sizeof(unsigned long long) * 1024 * 16) == hipSuccess ? 0 : -2;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_comb_t), sizeof(unsigned long long) * 1024 * 32) == hipSuccess ? 0 : -2;
 }
 #endif

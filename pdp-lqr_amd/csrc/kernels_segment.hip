@@ -486,15 +486,20 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
     int fail_stage = -1;
     // stage inputs: HBM -> registers (issued a stage ahead) -> LDS
     double pre[INQ];
+    // branch-free: every thread issues INQ loads at clamped addresses (a guarded
+    // load compiles to an exec-mask region with its own wait)
     auto in_load = [&](int k) {
+        const long long oE = (long long)k * n * s, oH = (long long)k * sh.ps, oc = (long long)k * n,
+                        oh = (long long)k * s;
 #pragma unroll
         for (int q = 0; q < INQ; ++q) {
-            const int i = tid + 256 * q;
-            const double *src = i < n * s ? Eb + (long long)k * n * s + i
-                                : i < n * s + ps ? Hb + (long long)k * sh.ps + (i - n * s)
-                                : i < n * s + ps + n ? cb + (long long)k * n + (i - n * s - ps)
-                                                     : hb + (long long)k * s + (i - n * s - ps - n);
-            pre[q] = i < IN ? *src : 0.0;
+            const int i = min(tid + 256 * q, IN - 1);
+            const long long off = i < n * s ? oE + i
+                                  : i < n * s + ps ? oH + (i - n * s)
+                                  : i < n * s + ps + n ? oc + (i - n * s - ps)
+                                                       : oh + (i - n * s - ps - n);
+            const double *base = i < n * s ? Eb : i < n * s + ps ? Hb : i < n * s + ps + n ? cb : hb;
+            pre[q] = __builtin_nontemporal_load(base + off);
         }
     };
     auto in_store = [&]() {
@@ -561,21 +566,27 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
         // accumulation chains run back to back (a wait on each product's LDS
         // reads put the LDS latency on the chain: 1.2 us per stage, r3g).
         constexpr int NK = K1 - K0;
+        // (branch-free: clamped LDS addresses, values masked by a 0 / 1 factor)
+        const double fux = cux ? 1.0 : 0.0;
+        const int colc = cux ? col : 0;
         double bvE[NK];  // E~[kx - m][col] (B operand of G)
 #pragma unroll
-        for (int q = 0; q < NK; ++q) bvE[q] = cux ? Es[(4 * (K0 + q) + g - m) + (cux ? col : 0) * n] : 0.0;
+        for (int q = 0; q < NK; ++q) bvE[q] = fux * Es[(4 * (K0 + q) + g - m) + colc * n];
         d4 G[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
         if (wv < 2) {
             double avP[2][NK];  // P_sym[16 a + c][kx]
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < 2; ++a) {
+                const int i = 16 * a + c;
+                const bool xi = i >= m && i < s;
+                const int ii = xi ? i - m : 0;
+                const double hx = xi ? 0.5 : 0.0;
 #pragma unroll
                 for (int q = 0; q < NK; ++q) {
-                    const int i = 16 * a + c, kx = 4 * (K0 + q) + g;
-                    const bool xi = i >= m && i < s;
-                    const int ii = xi ? i - m : 0;
-                    avP[a][q] = xi ? 0.5 * (Xq[ii + (kx - m) * XLD] + Xq[(kx - m) + ii * XLD]) : 0.0;
+                    const int kx = 4 * (K0 + q) + g;
+                    avP[a][q] = hx * (Xq[ii + (kx - m) * XLD] + Xq[(kx - m) + ii * XLD]);
                 }
+            }
 #pragma unroll
             for (int q = 0; q < NK; ++q)
 #pragma unroll
@@ -587,18 +598,24 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
         {
             double avE[2][NK];  // E~^T[16 a + c][kx] = E~[kx - m][16 a + c]
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < 2; ++a) {
+                const int i = 16 * a + c;
+                const double fi = i < s ? 1.0 : 0.0;
+                const int ic = i < s ? i : 0;
 #pragma unroll
                 for (int q = 0; q < NK; ++q) {
-                    const int i = 16 * a + c, kx = 4 * (K0 + q) + g;
-                    avE[a][q] = (i < s) ? Es[(kx - m) + (i < s ? i : 0) * n] : 0.0;
+                    const int kx = 4 * (K0 + q) + g;
+                    avE[a][q] = fi * Es[(kx - m) + ic * n];
                 }
+            }
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int i = 16 * a + 4 * r + g;
-                    Mu[a][r] = (cux && i < s) ? Hs[i >= col ? pidx(i, col, s) : pidx(col, i, s)] : 0.0;
+                    const bool on = cux && i < s;
+                    const int ic = on ? i : 0, jc = on ? col : 0;
+                    Mu[a][r] = (on ? 1.0 : 0.0) * Hs[ic >= jc ? pidx(ic, jc, s) : pidx(jc, ic, s)];
                 }
 #pragma unroll
             for (int q = 0; q < NK; ++q) {
@@ -656,12 +673,13 @@ __global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
             for (int l = 0; l < 4; ++l) pr[l] = P4[l * 64 + col];
 #pragma unroll
             for (int a = 0; a < 4; ++a)  // M[16 a + c][j0 + g] = M[j0 + g][16 a + c] (symmetry;
-                avv[a] = (16 * a + c < D) ? P4[g * 64 + 16 * a + c] : 0.0;  // aug / padding: not rows)
+                avv[a] = (16 * a + c < D ? 1.0 : 0.0) * P4[g * 64 + 16 * a + c];  // aug / padding: not rows)
             // records: wave 0 the FR rows i < s, wave 1 the coupling rows s + lane
             const int ir = (wv == 0) ? lane : s + lane;
             const bool rec = (wv == 0 && ir < s) || (wv == 1 && !last && lane < n);
+            const int irc = ir < 64 ? ir : 0;
 #pragma unroll
-            for (int l = 0; l < 4; ++l) mi[l] = (wv < 2) ? P4[l * 64 + (ir < 64 ? ir : 0)] : 0.0;
+            for (int l = 0; l < 4; ++l) mi[l] = P4[l * 64 + irc];
 #pragma unroll
             for (int l = 0; l < 4; ++l) lu[l] = P4[l * 64 + AUG];
 #pragma unroll

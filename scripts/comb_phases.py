@@ -30,10 +30,11 @@ sh.synchronize()
 sh.backward(elem, True)
 sh.synchronize()
 L = _lib.lib()
-buf = np.zeros(1024 * 16, dtype=np.uint64)
+buf = np.zeros(1024 * 32, dtype=np.uint64)
 L.pdplqr_debug_comb_times.argtypes = [C.c_void_p]
 assert L.pdplqr_debug_comb_times(C.c_void_p(buf.ctypes.data)) == 0
-t = buf.reshape(1024, 16).astype(np.int64)
+tall = buf.reshape(1024, 32).astype(np.int64)
+t = tall
 ok = (t[:, 0] > 0) & (t[:, 9] > t[:, 0])
 for k in range(1, 10):
     ok &= t[:, k] >= t[:, k - 1]
@@ -47,7 +48,27 @@ d = np.diff(t[:, :10], axis=1)
 print(f"blocks={len(t)}  wall_clock64 ticks (100 MHz): total median {np.median(t[:, 9] - t[:, 0]):.0f}")
 for k, nm in enumerate(names):
     print(f"  {nm:18s} {np.median(d[:, k]):8.0f}")
-seg = buf.reshape(1024, 16).astype(np.int64)
+ka = tall[ok]
+if len(ka) and (ka[:, 16] > 0).all():  # kernel-level marks of k_seg_scan_mw
+    med = lambda v: float(np.median(v))
+    print(f"  scan kernel: entry -> staged {med(ka[:, 17] - ka[:, 16]):.0f}, staged -> combine "
+          f"{med(ka[:, 0] - ka[:, 17]):.0f}, combine end -> stores done {med(ka[:, 18] - ka[:, 9]):.0f}, "
+          f"entry -> stores done {med(ka[:, 18] - ka[:, 16]):.0f}")
+    print(f"  chol R: load P_b {med(ka[:, 19] - ka[:, 0]):.0f}, chol_blk4 {med(ka[:, 20] - ka[:, 19]):.0f}, "
+          f"transpose {med(ka[:, 1] - ka[:, 20]):.0f}")
+    for fl, nm in ((1, "full combines (F, C, f, P, p)"), (0, "P-only combines (right operand at the terminal)")):
+        sel = ka[:, 22] == fl
+        if sel.any():
+            dd = np.diff(ka[sel][:, :10], axis=1)
+            print(f"  {nm}: {sel.sum()} blocks, total {med(ka[sel][:, 9] - ka[sel][:, 0]):.0f}; " +
+                  ", ".join(f"{names[k].split(':')[-1].strip()} {np.median(dd[:, k]):.0f}" for k in range(6)))
+    # blocks of the last recorded round of each distance: entry spread and end spread
+    for dist in sorted(set(ka[:, 21].tolist()))[-3:]:
+        r = ka[ka[:, 21] == dist]
+        e0 = r[:, 16].min()
+        print(f"  round d={dist}: {len(r)} blocks, entry first -> median {med(r[:, 16] - e0):.0f} -> last "
+              f"{(r[:, 16] - e0).max()}, stores done median {med(r[:, 18] - e0):.0f} last {(r[:, 18] - e0).max()}")
+seg = buf.reshape(1024, 32).astype(np.int64)
 seg = seg[seg[:, 12] > 0]
 if len(seg):
     st = seg[:, 12]
