@@ -458,8 +458,13 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             h->updated = true;
         }
         // the Riccati-ordered KKT path folds the right-hand side into its
-        // elimination (kkt_riccati.hip): it re-runs the backward on every rhs
-        if (refactor || (kkt && kkt_ric_active(h))) {
+        // elimination (kkt_riccati.hip): with a factor cache (12/4) the later
+        // iterations run only its right-hand-side pass, else the whole backward
+        if (kkt && kkt_linear_supported(h)) {
+            if ((rc = refactor ? kkt_backward_cached(h, s->irho) : kkt_backward_linear(h, s->irho))) return rc;
+            h->factored = true;
+            refactor = false;
+        } else if (refactor || (kkt && kkt_ric_active(h))) {
             if ((rc = solver_backward(h, kkt ? s->irho : s->rho))) return rc;
             h->factored = true;
             refactor = false;

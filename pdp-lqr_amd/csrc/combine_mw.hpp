@@ -19,9 +19,10 @@
 //     f = F_b v1 + f_b - W^T x3              (v1 = f_a - C_a p_b)
 //     p = p_a + F_a^T u - X1^T x4            (u = p_b + P_b f_a)
 // Phases (barriers between them), waves w0..w3:
-//   A  w0-w2: R = chol(P_b) (redundantly, no exchange);  w3: K1 = F_b C_a F_b^T + C_b,
-//            F_b v1 + f_b, p_a + F_a^T u (inputs only)
-//   B  w0: S;  w1: R^T F_a, K2 = F_b F_a, R^T v1, R^T C_a u;  w2: R^T C_a F_b^T   -> LDS
+//   A  w0: R = chol(P_b) (U = R^T to LDS);  w1: K2 = F_b F_a, C_a u, v1;
+//      w2: K0 = C_a F_b^T;  w3: K1 = F_b C_a F_b^T + C_b, F_b v1 + f_b,
+//      p_a + F_a^T u (inputs only)
+//   B  w0: S;  w1: R^T F_a, R^T v1, R^T C_a u;  w2: R^T K0 (R read from LDS) -> LDS
 //   C  every wave: chol(S) carrying ONE column tile of the right-hand sides
 //   D  w0: P;  w1: F;  w2: C;  w3: f, p                                    -> HBM
 // When the right operand holds the real terminal (F = C = f = 0 there and in
@@ -168,18 +169,45 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
     // ---------------- phase A ----------------
     // (matrices are loaded right before their last use: at most four 2 x 2
     // tile matrices live per wave)
+    // R is factored ONCE (wave 0) and shared through LDS: waves 1 and 2 form
+    // the products that do not need R meanwhile (a redundant factorisation per
+    // wave costs issue slots the co-resident blocks of a scan round need).
+    // Wave 0's factor U = R^T lands in sm.S; S then goes to the staged P_b
+    // slot (P_b is dead after phase A), so the R reads and S cannot race.
     WM<T> R;
-    if (wv < 3) {
-        if (wv == 2 && !fcf) {
-        } else {
-            // S, B1, B2 are consecutive blocks (a select of the three pointers
-            // compiled to a table in scratch)
-#ifdef PDPLQR_EXP_SHARE_R  // timing experiment only (wrong results): waves 1, 2 skip their chol
-            if (wv > 0) {
-                wm_load(R, eb.P, n, n, false, 1.0, g, c);
-            } else
-#endif
-            ok = mw_chol_R<T>(R, eb.P, sm.S + wv * (n * sm.ld), sm.ld, n, g, c);
+    double *Sd = const_cast<double *>(eb.P);  // S, leading dimension n
+    if (wv == 0) {
+        ok = mw_chol_R<T>(R, eb.P, sm.S, sm.ld, n, g, c);
+    } else if (wv == 1) {
+        WV<T> fa, pb, u, cu;
+        wv_load(fa, ea.f, n, g, c);
+        wv_load(pb, eb.p, n, g, c);
+        {
+            WM<T> Pb;
+            wm_load(Pb, eb.P, n, n, false, 0.0, g, c);
+            wv_tn(u, Pb, fa, n, 1.0, &pb);  // u = p_b + P_b f_a
+        }
+        WM<T> Ca;
+        wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
+        wv_tn(cu, Ca, u, n, 1.0, (const WV<T> *)nullptr);  // C_a u
+        wv_store(cu, sm.bv + n, n, g, c);
+        if (fcf) {
+            WV<T> v1;
+            wv_tn(v1, Ca, pb, n, -1.0, &fa);  // v1 = f_a - C_a p_b
+            wv_store(v1, sm.bv, n, g, c);
+            WM<T> Fa, Fbt, B;
+            wm_load(Fa, ea.F, n, n, false, 0.0, g, c);
+            wm_load(Fbt, eb.F, n, n, true, 0.0, g, c);
+            wm_tn(B, Fbt, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // F_b F_a
+            wm_store(B, sm.K2, PL, n, g, c);
+        }
+    } else if (wv == 2) {
+        if (fcf) {
+            WM<T> Ca, Fbt, K0;
+            wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
+            wm_load(Fbt, eb.F, n, n, true, 0.0, g, c);
+            wm_tn(K0, Ca, Fbt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a F_b^T
+            wm_store(K0, sm.B2, PL, n, g, c);
         }
     } else {
         WV<T> fa, pb, u;
@@ -215,54 +243,36 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         }
     }
     COMB_MARK(1);  // wave 0: R formed
+    __syncthreads();  // U = R^T in sm.S; P_b's slot free
     // ---------------- phase B ----------------
     if (wv == 0) {
         WM<T> Ca, T1, S;
         wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
         wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
         wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
-        wm_store(S, sm.S, PL, n, g, c);
+        wm_store(S, Sd, n, n, g, c);
         if (lane == 0) sm.ok[0] = ok;
     } else if (wv == 1) {
+        wm_load(R, sm.S, PL, n, true, 1.0, g, c);
         {
             WM<T> Fa, B;
             wm_load(Fa, ea.F, n, n, false, 0.0, g, c);
             wm_tn(B, R, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F_a
             wm_store(B, sm.B1, PL, n, g, c);
-            if (fcf) {
-                WM<T> Fbt;
-                wm_load(Fbt, eb.F, n, n, true, 0.0, g, c);
-                wm_tn(B, Fbt, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // F_b F_a
-                wm_store(B, sm.K2, PL, n, g, c);
-            }
         }
-        WV<T> fa, pb, u, cu, y;
-        wv_load(fa, ea.f, n, g, c);
-        wv_load(pb, eb.p, n, g, c);
-        {
-            WM<T> Pb;
-            wm_load(Pb, eb.P, n, n, false, 0.0, g, c);
-            wv_tn(u, Pb, fa, n, 1.0, &pb);  // u = p_b + P_b f_a
-        }
-        WM<T> Ca;
-        wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
-        wv_tn(cu, Ca, u, n, 1.0, (const WV<T> *)nullptr);
+        WV<T> cu, v1, y;
+        wv_load(cu, sm.bv + n, n, g, c);
+        if (fcf) wv_load(v1, sm.bv, n, g, c);
         wv_tn(y, R, cu, n, 1.0, (const WV<T> *)nullptr);  // R^T C_a u
         wv_store(y, sm.bv + n, n, g, c);
         if (fcf) {
-            WV<T> v1;
-            wv_tn(v1, Ca, pb, n, -1.0, &fa);                  // v1 = f_a - C_a p_b
             wv_tn(y, R, v1, n, 1.0, (const WV<T> *)nullptr);  // R^T v1
             wv_store(y, sm.bv, n, g, c);
         }
     } else if (wv == 2 && fcf) {
         WM<T> K0, B;
-        {
-            WM<T> Ca, Fbt;
-            wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
-            wm_load(Fbt, eb.F, n, n, true, 0.0, g, c);
-            wm_tn(K0, Ca, Fbt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a F_b^T
-        }
+        wm_load(R, sm.S, PL, n, true, 1.0, g, c);
+        wm_load(K0, sm.B2, PL, n, false, 0.0, g, c);
         wm_tn(B, R, K0, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T C_a F_b^T
         wm_store(B, sm.B2, PL, n, g, c);
     }
@@ -275,7 +285,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
     ok = ok && sm.ok[0];
     {
         WM<T> S;
-        wm_load(S, sm.S, PL, n, false, 1.0, g, c);
+        wm_load(S, Sd, n, n, false, 1.0, g, c);
         d4 B[T][1], V[T][1];
         int kind = -1, tile = 0;  // 0: X1, 1: W, 2: vectors (block-uniform)
         if (T == 2) {
@@ -304,9 +314,6 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
                 V[a][0] = BV[a][1];
             }
         } else if (kind >= 0) {
-#ifdef PDPLQR_EXP_SHARE_S  // timing experiment only (wrong results): one chol(S)
-            if (wv == 0)
-#endif
             okS = chol_blk4<T, true, 1>(S, B, n, g, c);
         }
         COMB_MARK(4);  // wave 0: chol(S) done

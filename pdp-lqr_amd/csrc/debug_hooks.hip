@@ -48,9 +48,18 @@ __global__ __launch_bounds__(256) void k_debug_combine_mw(const double *a, const
                                                           int *ok) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const pdplqr::MwSmem sm = pdplqr::mw_smem(mwbuf, n);
-    const int nn = n * n;
+    const int nn = n * n, es = 3 * nn + 2 * n;
+    // operands staged into LDS as the scan kernel does (mw_combine writes S
+    // over the right operand's P block)
+    const int own = (int)((pdplqr::mw_smem_bytes(n) + 15) / 16 * 2), slot = (es + 1) & ~1;
+    double *la = mwbuf + own, *lb = la + slot;
+    for (int q = threadIdx.x; q < es; q += blockDim.x) {
+        la[q] = a[q];
+        lb[q] = b[q];
+    }
+    __syncthreads();
     const bool good = pdplqr::mw_combine<T>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n,
-                                            pdplqr::elem_in(a, n), pdplqr::elem_in(b, n), n, fcf != 0, sm);
+                                            pdplqr::elem_in(la, n), pdplqr::elem_in(lb, n), n, fcf != 0, sm);
     if (threadIdx.x == 0) *ok = good ? 1 : 0;
 }
 
@@ -68,7 +77,7 @@ extern "C" int pdplqr_debug_combine_mw(int n, const double *a, const double *b, 
     PDPLQR_HIP_TRY(hipMemcpy((char *)d + 2 * es, out, es, hipMemcpyHostToDevice));  // untouched blocks kept
     const double *da = d, *db = (const double *)((char *)d + es);
     double *dout = (double *)((char *)d + 2 * es);
-    const size_t sm = mw_smem_bytes(n);
+    const size_t sm = (size_t)((mw_smem_bytes(n) + 15) / 16 * 2 + 2 * ((3 * n * n + 2 * n + 1) & ~1)) * sizeof(double);
     if (T == 1) hipLaunchKernelGGL(k_debug_combine_mw<1>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
     else hipLaunchKernelGGL(k_debug_combine_mw<2>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
     PDPLQR_HIP_TRY(hipDeviceSynchronize());

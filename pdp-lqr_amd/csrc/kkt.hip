@@ -1319,6 +1319,7 @@ struct KKTState {
     double *rec = nullptr;    // rollout records [b][N][FS]
     double *x0acc = nullptr;  // sum of the x0s since update_problem_data [b][n]
     double *Ef = nullptr, *Df = nullptr;  // frozen E, D once set_model re-runs (else the model's)
+    double *ncache = nullptr;  // factor cache of the linear-only pass (ADMM), allocated on first use
 };
 
 template <typename X>
@@ -1538,6 +1539,33 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
     else hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
+}
+
+bool kkt_linear_supported(pdplqr_handle h) {
+    KKTState *ks = h->kkt;
+    return ks && (ks->ric == 0 || ks->ric == 4) && !getenv("PDPLQR_KKT_NO_LINEAR");
+}
+
+// The factorisation with the linear pass's cache (ADMM iteration 1, and after
+// a rho change: the KKT matrix depends on rho through the y diagonal)
+int kkt_backward_cached(pdplqr_handle h, const double *inv_rho) {
+    KKTState *ks = h->kkt;
+    const Shape &sh = h->sh;
+    int rc;
+    if (!ks->ncache && (rc = kalloc(h, &ks->ncache, sh.batch * kkt_ric_cache_doubles(sh, ks->ric)))) return rc;
+    rc = launch_kkt_ric_backward(sh, ks->ric, ks->Ef ? ks->Ef : h->E, h->c, ks->Df ? ks->Df : h->D, h->Hw, h->hw,
+                                 h->gw, inv_rho, h->d_off, h->y_off, h->ncs[sh.N], h->cfg.rho_dyn, ks->rec, h->status,
+                                 h->stream, ks->ncache);
+    if (rc == PDPLQR_ERR_UNSUPPORTED) set_error("KKT backward: unaligned buffers for the Riccati-ordered path");
+    return rc;
+}
+
+// Same rho, new right-hand side (h~, g of the last update_problem_data)
+int kkt_backward_linear(pdplqr_handle h, const double *inv_rho) {
+    KKTState *ks = h->kkt;
+    const Shape &sh = h->sh;
+    return launch_kkt_ric_nofact(sh, ks->ric, ks->Df ? ks->Df : h->D, h->hw, h->gw, inv_rho, h->d_off, h->y_off,
+                                 h->ncs[sh.N], ks->ncache, ks->rec, h->stream);
 }
 
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {

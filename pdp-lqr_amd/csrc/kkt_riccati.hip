@@ -60,6 +60,7 @@ struct KKTRicArgs {
     const double *irho;       // backward's inv_rho
     const int32_t *d_off, *y_off;
     double *rec;              // [b][N][KKT_FS] rollout records
+    double *cache = nullptr;  // linear-pass factor cache [b][N][KKT_CF] (ADMM), or null
     int32_t *status;
     double rho_dyn;
     int nc_last;              // constraint rows of the terminal stage
@@ -74,6 +75,16 @@ struct KRecShape {
     static constexpr int PTF = 3 * 4 * n;             // floats of P~ (48 lanes x 3)
     static constexpr int FS = OPT + (PTF + 1) / 2;    // doubles per stage
 };
+
+// Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
+// backward when KKTRicArgs::cache is set), per stage six 64-lane slots:
+//   0..2  E^ = E~ - rho_dyn G (x rows 4 r + g, r = 1..3; G = P~ E~)
+//   3     w = Lxu (lane (g, c): L(c, g))
+//   4     lanes 0..15: q = G^T c~ (per column), lanes 16..31: T = Luu^{-1} (16 + 4 i + j)
+//   5     rho D (lane (g, c): rho_g D[g][c], stage 0 without the x columns)
+// so that lp = h~ + q + E^^T p - (rho D)^T g, lu' = T lu, k~ = T^T lu',
+// p_k = lp_x - Lxu lu': the right-hand-side dependent part of the backward.
+constexpr int KKT_CF = 6 * 64;
 
 // Stage record streamed by the backward: E | c | h~ | packed H~ | D | inv_rho | g
 template <int NN, int MM, int NC>
@@ -111,6 +122,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     const double *ib = A.irho + b * (long long)sh.ny;
     double *RB = A.rec + b * (long long)N * RS::FS;
     const double rd = A.rho_dyn;
+    double *const cache = A.cache;  // (a member read inside the stage lambda would put A in scratch)
     int fail_stage = -1;
 
     // ---- terminal: P_N = H~_N + D_N^T rho D_N, p_N = h~_N - D_N^T rho g_N ----
@@ -198,7 +210,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         for (int q = 0; q < NI; ++q) *reinterpret_cast<d2v *>(&stg[slot][2 * (q * 64 + lane)]) = R[q];
     };
 
-    auto process = [&](int k, bool sym) {
+    auto process = [&](int k, bool sym) __attribute__((always_inline)) {
         const double *R = stg[k & 1];
         double *Rk = RB + (long long)k * RS::FS;
         SchurIn in;
@@ -250,15 +262,27 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         d4 Mn = in.H;
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk) Mn = mfma_f64(in.E[kk], G[kk], Mn);
-        double part = 0.0;
+        double part = 0.0, rhoD = 0.0;
         if constexpr (NC > 0) {
             // lane (g, c): D[g][c] (rows g < NC); stage 0 keeps only the u columns
             const bool dv = g < NC && (k > 0 || c < m);
             const double dgc = dv ? R[SH::OD + (g < NC ? g : 0) + c * NC] : 0.0;
             const double rq = (g < NC) ? rcp_f64(R[SH::OI + (g < NC ? g : 0)]) : 0.0;
             const double gq = (g < NC) ? R[SH::OG + (g < NC ? g : 0)] : 0.0;
-            Mn = mfma_f64(dgc, rq * dgc, Mn);      // D^T diag(rho) D
+            rhoD = rq * dgc;
+            Mn = mfma_f64(dgc, rhoD, Mn);          // D^T diag(rho) D
             part = -dgc * rq * gq;                 // -(D^T rho g)[c]
+        }
+        double *Ck = cache ? cache + ((long long)b * N + k) * KKT_CF : nullptr;
+        double qcol = 0.0;
+        if (Ck) {  // wave-uniform: the linear pass's copy of this stage's factor
+#pragma unroll
+            for (int kk = 1; kk < 4; ++kk) {
+                gstore(Ck + 64 * (kk - 1) + lane, __builtin_fma(-rd, G[kk], in.E[kk]));
+                qcol = __builtin_fma(G[kk], in.ct[kk], qcol);
+            }
+            qcol = sum_groups(qcol);
+            gstore(Ck + 5 * 64 + lane, rhoD);
         }
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk) {
@@ -299,6 +323,15 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         ok = (int)ok & (int)!__any(bad);
         fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
         schur_store_record_gain<MM, s>(Rk, go, g, c);  // [K~ | k~]
+        if (Ck) {
+            double tv = 0.0;
+#pragma unroll
+            for (int i = 0; i < MM; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) tv = (lane == 16 + 4 * i + j) ? go.T[i][j] : tv;
+            gstore(Ck + 3 * 64 + lane, w);
+            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : tv);
+        }
         wave_sync();  // stage k's LDS reads retire before slot reuse
     };
     auto step = [&](int k, d2v(&X)[NI], bool first, bool sym) {
@@ -326,6 +359,128 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     }
     if (k == 0) process(0, true);
     if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+// ---------------------------------------------------------------------------
+// The right-hand-side part of the backward on a cached factor (the KKT
+// matrix, i.e. rho, unchanged; h~ and g new): QDLDLSolver::solve after a
+// factorisation (qdldl_solver.hpp:88-151) in the Riccati order.  Per stage
+// (KKT_CF cache, written by k_kkt_ric_bwd):
+//     lp = h~ + q + E^^T p_{k+1} - (rho D)^T g,   lu' = T lu,   k~ = T^T lu',
+//     p_k = lp_x - Lxu lu'
+// and the rollout record's k~ and p_{k+1} are rewritten (K~, P~ stay).  One
+// wave per problem; the cache slots are read one stage ahead into registers
+// (two sets, the loop unrolled by two so no register set is copied).
+// ---------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
+    constexpr int n = 12, m = 4, s = 16;
+    using RS = KRecShape<n, m>;
+    __shared__ double pc[16];
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const Shape &sh = A.sh;
+    const int N = sh.N;
+    const double *hb = A.hw + b * sh.perh;
+    const double *gb = NC > 0 ? A.gw + b * (long long)sh.ny : nullptr;
+    const double *Cb = A.cache + b * (long long)N * KKT_CF;
+    double *RB = A.rec + b * (long long)N * RS::FS;
+    // terminal: p_N = h~_N - D_N^T rho g_N (x rows)
+    double prow[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        prow[r] = i >= m ? hb[(long long)N * s + (i - m)] : 0.0;
+    }
+    const int ncN = A.nc_last;
+    if (ncN > 0) {
+        const double *DN = A.D + b * (long long)sh.ndD + A.d_off[N];
+        const double *gN = A.gw + b * (long long)sh.ny + A.y_off[N];
+        const double *iN = A.irho + b * (long long)sh.ny + A.y_off[N];
+        for (int q = 0; q < ncN; ++q) {
+            const double rq = 1.0 / iN[q], gq = gN[q];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 4 * r + g;
+                const double di = i >= m ? DN[q + (i - m) * ncN] : 0.0;
+                prow[r] = __builtin_fma(-di * rq, gq, prow[r]);
+            }
+        }
+    }
+    double sel[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sel[j] = (g == j) ? 1.0 : 0.0;
+    struct Set {
+        double e[3], w, q, rd, h, gv;
+        double T[10];
+    };
+    auto load = [&](Set &X, int k) {
+        const double *Ck = Cb + (long long)k * KKT_CF;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) X.e[r] = Ck[64 * r + lane];
+        X.w = Ck[3 * 64 + lane];
+        X.q = Ck[4 * 64 + c];
+#pragma unroll
+        for (int t = 0; t < 10; ++t) X.T[t] = Ck[4 * 64 + 16 + (t < 1 ? 0 : t < 3 ? t + 3 : t < 6 ? t + 5 : t + 6)];
+        X.rd = NC > 0 ? Ck[5 * 64 + lane] : 0.0;
+        X.h = hb[(long long)k * s + c];
+        X.gv = NC > 0 ? gb[(long long)k * NC + (g < NC ? g : 0)] : 0.0;
+    };
+    auto stage = [&](const Set &X, int k) {
+        double *Rk = RB + (long long)k * RS::FS;
+        {  // record: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
+            const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
+            const double pv = __builtin_fma(prow[1], (double)(cp == 1), __builtin_fma(prow[2], (double)(cp == 2),
+                                                                                       prow[3] * (double)(cp == 3)));
+            gstore(Rk + RS::OPV + (4 * cp + g - m), pv);
+        }
+        double part = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) part = __builtin_fma(X.e[r], prow[r + 1], part);
+        if (NC > 0) part = __builtin_fma(-X.rd, X.gv, part);
+        const double lp = X.h + X.q + sum_groups(part);  // lp[c], every group
+        double lu[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lu[j] = readlane_f64(lp, j);
+        // T[i][j] at t = i (i + 1) / 2 + j
+        double luq[4], kq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int j = 0; j <= i; ++j) v = __builtin_fma(X.T[i * (i + 1) / 2 + j], lu[j], v);
+            luq[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int l = i; l < 4; ++l) v = __builtin_fma(X.T[l * (l + 1) / 2 + i], luq[l], v);
+            kq[i] = v;
+        }
+        const double kv = lane == 0 ? kq[0] : lane == 1 ? kq[1] : lane == 2 ? kq[2] : kq[3];
+        if (lane < m) gstore(Rk + RS::OKQ + lane, kv);
+        double lq = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lq = __builtin_fma(sel[j], luq[j], lq);
+        const double pcol = lp - sum_groups(X.w * lq);  // p_k[c - m] on c >= m
+        if (g == 0) pc[c] = pcol;
+        wave_sync();
+#pragma unroll
+        for (int r = 1; r < 4; ++r) prow[r] = pc[4 * r + g];
+        wave_sync();
+    };
+    Set X0, X1;
+    load(X0, N - 1);
+    if (N >= 2) load(X1, N - 2);
+    int k = N - 1;
+    for (; k >= 1; k -= 2) {
+        stage(X0, k);
+        if (k >= 2) load(X0, k - 2);
+        stage(X1, k - 1);
+        if (k >= 3) load(X1, k - 3);
+    }
+    if (k == 0) stage(X0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -689,7 +844,7 @@ size_t kkt_ric_rec_doubles(const Shape &sh, int ric) {
 int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
-                            int32_t *status, hipStream_t st) {
+                            int32_t *status, hipStream_t st, double *cache) {
     if (nc == KKT_RIC_WIDE) {
         KKTRicArgs a;
         a.sh = sh;
@@ -733,8 +888,37 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     a.status = status;
     a.rho_dyn = rho_dyn;
     a.nc_last = nc_last;
+    a.cache = cache;
     if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_bwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
     else hipLaunchKernelGGL(k_kkt_ric_bwd<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+size_t kkt_ric_cache_doubles(const Shape &sh, int ric) {
+    return ric == 0 || ric == 4 ? (size_t)sh.N * KKT_CF : 0;
+}
+
+int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double *hw, const double *gw,
+                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last,
+                          const double *cache, double *rec, hipStream_t st) {
+    if (nc != 0 && nc != 4) return PDPLQR_ERR_UNSUPPORTED;
+    KKTRicArgs a;
+    a.sh = sh;
+    a.E = a.c = a.Hw = nullptr;
+    a.D = D;
+    a.hw = hw;
+    a.gw = gw;
+    a.irho = irho;
+    a.d_off = d_off;
+    a.y_off = y_off;
+    a.rec = rec;
+    a.cache = const_cast<double *>(cache);
+    a.status = nullptr;
+    a.rho_dyn = 0.0;
+    a.nc_last = nc_last;
+    if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_nofact<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_kkt_ric_nofact<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

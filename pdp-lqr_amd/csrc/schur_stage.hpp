@@ -106,6 +106,7 @@ struct SchurSmem {
 struct GainOut {
     double kt;  // lane (g, c): K~[g][c - m] on x rows c >= m
     double kq;  // k~[g] (every lane of group g)
+    double T[4][4];  // Luu^{-1} (wave-uniform; read by the KKT factor cache only)
 };
 
 // PDPLQR_SCHUR_LDSU = 1: the u rows reach the lanes through LDS instead of
@@ -232,6 +233,10 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         }
         go->kt = kt;
         go->kq = kq;
+#pragma unroll
+        for (int i = 0; i < MM; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) go->T[i][j] = T[i][j];
     }
 #endif
 #if PDPLQR_LP_IN_P

@@ -29,6 +29,11 @@ int kkt_on_model(pdplqr_handle h);
 int kkt_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
                double sigma);
 int kkt_backward(pdplqr_handle h, const double *inv_rho);
+// ADMM: the backward also writes the factor cache (false: no cached path for this shape);
+// kkt_backward_cached / kkt_backward_linear run the factor and the rhs-only pass
+bool kkt_linear_supported(pdplqr_handle h);
+int kkt_backward_cached(pdplqr_handle h, const double *inv_rho);
+int kkt_backward_linear(pdplqr_handle h, const double *inv_rho);
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws);
 int kkt_dim(pdplqr_handle h);
 int kkt_before_model(pdplqr_handle h);  // set_model on a formed KKT handle: keep the frozen matrix
@@ -41,7 +46,12 @@ size_t kkt_ric_rec_doubles(const Shape &sh, int ric);  // rollout record doubles
 int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
-                            int32_t *status, hipStream_t st);
+                            int32_t *status, hipStream_t st, double *cache = nullptr);
+// linear-only pass on the factor cache the backward wrote (ric 0 / 4 only)
+size_t kkt_ric_cache_doubles(const Shape &sh, int ric);  // per problem; 0 where unsupported
+int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double *hw, const double *gw,
+                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last,
+                          const double *cache, double *rec, hipStream_t st);
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
                            double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric);
 }  // namespace pdplqr

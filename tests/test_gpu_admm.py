@@ -111,6 +111,26 @@ def test_kkt_solver_fixed_iterations():
         assert rel_err(w[b], ow) < TOL_KKT and rel_err(y[b], oy) < TOL_KKT and rel_err(z[b], oz) < TOL_KKT, b
 
 
+def test_kkt_linear_pass_equals_refactor(monkeypatch):
+    """12/4 KKT x-updates after the first: the right-hand-side pass on the
+    factor cache (k_kkt_ric_nofact) against re-running the whole Riccati-
+    ordered backward every iteration (PDPLQR_KKT_NO_LINEAR=1) -- the same
+    matrix, so the same iterates to rounding -- and both against the oracle
+    (a box on u at every stage, nc = 4)."""
+    models, x0s = _ubox_models(3, n=12, m=4, N=37, nc=4, bound=0.4, seed0=310)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s, seed=3)
+    rho = np.full(lb.shape, 5.0)
+    st = dict(max_iter=25, eps_abs=0.0, eps_rel=0.0)
+    w1, y1, z1, _ = _run_gpu("kkt", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, False, **st)
+    monkeypatch.setenv("PDPLQR_KKT_NO_LINEAR", "1")
+    w2, y2, z2, _ = _run_gpu("kkt", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, False, **st)
+    monkeypatch.delenv("PDPLQR_KKT_NO_LINEAR")
+    assert rel_err(w1, w2) < 1e-11 and rel_err(y1, y2) < 1e-11 and rel_err(z1, z2) < 1e-11
+    for b in range(len(pms)):
+        ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="kkt", **st)
+        assert rel_err(w1[b], ow) < TOL_KKT and rel_err(y1[b], oy) < TOL_KKT and rel_err(z1[b], oz) < TOL_KKT, b
+
+
 @pytest.mark.parametrize("check_every", [1, 25])
 def test_converged_runs_freeze_per_problem(check_every):
     """Quadrotor with 4 start heights: each problem converges at its own
