@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
             if (FUSE) {
                 // k_update_problem_data then k_penalty: (h - sigma w) - sum
                 double hj = a.hv[wo] - a.sigma * wn;
-                if (nc > 0) hj -= ag;
+                if (nc > 0 && !a.no_penalty) hj -= ag;
                 a.hw[wo] = hj;
             }
         }
@@ -443,6 +443,10 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     a.eps_rel = st->eps_rel;
     a.max_nc = h->max_nc;
     a.it = 0;
+    // KKT with the factor cache: the update pass also forms the next h~ = h - sigma w
+    // and g (the KKT path takes rho through g in its backward, no penalty in h~)
+    const bool kkt_lin = kkt && kkt_linear_supported(h);
+    a.no_penalty = kkt ? 1 : 0;
     const dim3 ugrid((unsigned)B), ublk(256);
     const double *irho_or_null = Y > 0 ? s->irho : nullptr;
     int it = 1;
@@ -453,14 +457,18 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     for (;; ++it) {
         // x-update: the reference protocol (iteration 1 and after a rho
         // change: H~ depends on rho), then vectors only
-        if (refactor || kkt) {
+        if (refactor || (kkt && !kkt_lin)) {
             if ((rc = solver_update(h, s->w, s->y, s->z, irho_or_null, st->sigma))) return rc;
             h->updated = true;
+        } else if (kkt_lin) {
+            // h~, g came from the previous update pass; the x0 sum of the KKT
+            // right-hand side restarts as update_problem_data would restart it
+            if ((rc = kkt_rhs_restart(h))) return rc;
         }
         // the Riccati-ordered KKT path folds the right-hand side into its
         // elimination (kkt_riccati.hip): with a factor cache (12/4) the later
         // iterations run only its right-hand-side pass, else the whole backward
-        if (kkt && kkt_linear_supported(h)) {
+        if (kkt_lin) {
             if ((rc = refactor ? kkt_backward_cached(h, s->irho) : kkt_backward_linear(h, s->irho))) return rc;
             h->factored = true;
             refactor = false;
@@ -483,7 +491,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         }
         const bool last = it >= st->max_iter;
         const bool check = last || it % st->check_every == 0;
-        const bool fuse = !kkt && !last;
+        const bool fuse = (!kkt || kkt_lin) && !last;
         a.it = it;
         if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
         if (fuse && can_fuse) {

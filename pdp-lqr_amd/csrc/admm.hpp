@@ -15,6 +15,7 @@ struct AdmmArgs {
     double *prim, *dual, *rscale;
     double alpha, sigma, eps_abs, eps_rel, rho_tol;
     int max_nc, it, adaptive;
+    int no_penalty = 0;  // fused next-update h~ without the penalty term (KKT: rho enters through g)
 };
 
 // Termination test of iteration a.it for problem b from the five maxima

@@ -39,6 +39,7 @@ struct Shape {
     int ny;             // sum_k nc_k
     int ndD;            // sum_k nc_k * dim_k
     long long perE, perc, perH, perh, perHw, perKD;
+    int mw = 1;  // PARALLEL: the 4-wave horizon kernels may run (parallel_init's family choice)
 };
 
 // Riccati (serial, batched) kernels: kernels_riccati.hip

@@ -794,8 +794,8 @@ static size_t mw_maps_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 3 * el
 
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
-bool seg_scan_mw(int n, bool lu) {
-    if (lu || getenv("PDPLQR_SCAN_1WAVE")) return false;
+bool seg_scan_mw(int n, bool lu, int mw) {
+    if (!mw || lu || getenv("PDPLQR_SCAN_1WAVE")) return false;
     return tile_order(n) == 2 || (tile_order(n) == 1 && getenv("PDPLQR_SCAN_MW"));
 }
 
@@ -806,7 +806,7 @@ int seg_scan_slots(const Shape &sh, int device) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const size_t smem = op_stage_bytes(sh.n);
     hipError_t e;
-    if (seg_scan_mw(sh.n, false))
+    if (seg_scan_mw(sh.n, false, sh.mw))
         e = sh.n <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<1>, 256, mw_scan_bytes(sh.n))
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_seg_scan_mw<2>, 256, mw_scan_bytes(sh.n));
     else
@@ -842,7 +842,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
-    if (seg_scan_mw(a.n, a.lu)) {
+    if (seg_scan_mw(a.n, a.lu, a.mw)) {
         const size_t sm = mw_scan_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_scan_mw<1>, grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_scan_mw<2>, grid, dim3(256), sm, st, a);
@@ -862,7 +862,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     if (wide_state(a.n)) return launch_seg_maps_wide(a, batch, st);
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
-    if (seg_scan_mw(a.n, a.lu) && !getenv("PDPLQR_MAPS_1WAVE")) {
+    if (seg_scan_mw(a.n, a.lu, a.mw) && !getenv("PDPLQR_MAPS_1WAVE")) {
         const size_t sm = mw_maps_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_maps_mw<1>, grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_maps_mw<2>, grid, dim3(256), sm, st, a);

@@ -823,7 +823,7 @@ static const void *aug_kernel(const Shape &sh) {
 }
 
 // the 4-wave stage for 24/8 (PDPLQR_AUG_1WAVE: the one-wave k_seg_bwd_aug, A/B)
-static bool aug_mw(const Shape &sh) { return sh.n == 24 && sh.m == 8 && !getenv("PDPLQR_AUG_1WAVE"); }
+static bool aug_mw(const Shape &sh) { return sh.mw && sh.n == 24 && sh.m == 8 && !getenv("PDPLQR_AUG_1WAVE"); }
 
 int seg_backward_slots(const Shape &sh, int device) {
     if (wide_stage(sh)) return wide_seg_backward_slots(sh, device);

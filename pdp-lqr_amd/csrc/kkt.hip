@@ -1560,6 +1560,12 @@ int kkt_backward_cached(pdplqr_handle h, const double *inv_rho) {
     return rc;
 }
 
+int kkt_rhs_restart(pdplqr_handle h) {
+    KKTState *ks = h->kkt;
+    PDPLQR_HIP_TRY(hipMemsetAsync(ks->x0acc, 0, h->sh.batch * h->sh.n * sizeof(double), h->stream));
+    return PDPLQR_OK;
+}
+
 // Same rho, new right-hand side (h~, g of the last update_problem_data)
 int kkt_backward_linear(pdplqr_handle h, const double *inv_rho) {
     KKTState *ks = h->kkt;

@@ -369,8 +369,8 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 //     lp = h~ + q + E^^T p_{k+1} - (rho D)^T g,   lu' = T lu,   k~ = T^T lu',
 //     p_k = lp_x - Lxu lu'
 // and the rollout record's k~ and p_{k+1} are rewritten (K~, P~ stay).  One
-// wave per problem; the cache slots are read one stage ahead into registers
-// (two sets, the loop unrolled by two so no register set is copied).
+// wave per problem; the cache slots are read three stages ahead into registers
+// (three sets, the loop unrolled by three so no register set is copied).
 // ---------------------------------------------------------------------------
 template <int NC>
 __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
@@ -414,19 +414,53 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         double e[3], w, q, rd, h, gv;
         double T[10];
     };
+    // The three register sets are loaded by asm (global_load_dwordx2) and
+    // waited for by an explicit vmcnt with the set's registers as operands:
+    // compiler-placed waits drained every set at the top of the loop (it
+    // rotates the sets through register copies).  LV loads per set; each
+    // stage issues 2 stores; a set is waited for with at most 2 LV younger ops
+    // outstanding (conservative in steady state, where 2 LV + 4 are).
+    constexpr int LV = 18;
+    auto gl = [](double &x, const double *p) {
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
+    };
     auto load = [&](Set &X, int k) {
         const double *Ck = Cb + (long long)k * KKT_CF;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) X.e[r] = Ck[64 * r + lane];
-        X.w = Ck[3 * 64 + lane];
-        X.q = Ck[4 * 64 + c];
+        for (int r = 0; r < 3; ++r) gl(X.e[r], Ck + 64 * r + lane);
+        gl(X.w, Ck + 3 * 64 + lane);
+        gl(X.q, Ck + 4 * 64 + c);
 #pragma unroll
-        for (int t = 0; t < 10; ++t) X.T[t] = Ck[4 * 64 + 16 + (t < 1 ? 0 : t < 3 ? t + 3 : t < 6 ? t + 5 : t + 6)];
-        X.rd = NC > 0 ? Ck[5 * 64 + lane] : 0.0;
-        X.h = hb[(long long)k * s + c];
-        X.gv = NC > 0 ? gb[(long long)k * NC + (g < NC ? g : 0)] : 0.0;
+        for (int t = 0; t < 10; ++t) gl(X.T[t], Ck + 4 * 64 + 16 + (t < 1 ? 0 : t < 3 ? t + 3 : t < 6 ? t + 5 : t + 6));
+        gl(X.rd, Ck + 5 * 64 + lane);  // (zeros when NC = 0)
+        gl(X.h, hb + (long long)k * s + c);
+        gl(X.gv, NC > 0 ? gb + (long long)k * NC + (g < NC ? g : 0) : hb);
     };
-    auto stage = [&](const Set &X, int k) {
+    auto wait = [&](Set &X) {
+        asm volatile("s_waitcnt vmcnt(%18)"
+                     : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
+                       "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
+                       "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
+                     : "n"(2 * LV)
+                     : "memory");
+    };
+    // every set landed (the sets the tail does not read are dead to the
+    // compiler, which would reuse their registers under the loads in flight)
+    auto wait_all = [&](Set &X, Set &Y, Set &Z) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q),
+                     "+v"(X.rd), "+v"(X.h), "+v"(X.gv), "+v"(Y.e[0]), "+v"(Y.e[1]), "+v"(Y.e[2]), "+v"(Y.w),
+                     "+v"(Y.q), "+v"(Y.rd), "+v"(Y.h), "+v"(Y.gv), "+v"(Z.e[0]), "+v"(Z.e[1]), "+v"(Z.e[2]),
+                     "+v"(Z.w), "+v"(Z.q), "+v"(Z.rd), "+v"(Z.h), "+v"(Z.gv)::"memory");
+        asm volatile("" : "+v"(X.T[0]), "+v"(X.T[1]), "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]),
+                     "+v"(X.T[6]), "+v"(X.T[7]), "+v"(X.T[8]), "+v"(X.T[9]), "+v"(Y.T[0]), "+v"(Y.T[1]),
+                     "+v"(Y.T[2]), "+v"(Y.T[3]), "+v"(Y.T[4]), "+v"(Y.T[5]), "+v"(Y.T[6]), "+v"(Y.T[7]),
+                     "+v"(Y.T[8]), "+v"(Y.T[9]));
+        asm volatile("" : "+v"(Z.T[0]), "+v"(Z.T[1]), "+v"(Z.T[2]), "+v"(Z.T[3]), "+v"(Z.T[4]), "+v"(Z.T[5]),
+                     "+v"(Z.T[6]), "+v"(Z.T[7]), "+v"(Z.T[8]), "+v"(Z.T[9]));
+    };
+    auto stage = [&](Set &X, int k) {
+        wait(X);
+        if (NC == 0) X.rd = X.gv = 0.0;
         double *Rk = RB + (long long)k * RS::FS;
         {  // record: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
@@ -470,17 +504,26 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         for (int r = 1; r < 4; ++r) prow[r] = pc[4 * r + g];
         wave_sync();
     };
-    Set X0, X1;
+    // three register sets in flight: a stage's chain is ~0.3 us, HBM latency
+    // ~1 us (one set ahead: 0.91 us per stage, latency-bound)
+    // (loads unconditional, at clamped stages: a load inside a branch made the
+    // wait-count pass drain every set in flight at the top of the loop)
+    Set X0, X1, X2;
     load(X0, N - 1);
-    if (N >= 2) load(X1, N - 2);
+    load(X1, N >= 2 ? N - 2 : 0);
+    load(X2, N >= 3 ? N - 3 : 0);
     int k = N - 1;
-    for (; k >= 1; k -= 2) {
+    for (; k >= 2; k -= 3) {
         stage(X0, k);
-        if (k >= 2) load(X0, k - 2);
+        load(X0, k >= 3 ? k - 3 : 0);
         stage(X1, k - 1);
-        if (k >= 3) load(X1, k - 3);
+        load(X1, k >= 4 ? k - 4 : 0);
+        stage(X2, k - 2);
+        load(X2, k >= 5 ? k - 5 : 0);
     }
-    if (k == 0) stage(X0, 0);
+    wait_all(X0, X1, X2);
+    if (k >= 0) stage(X0, k);
+    if (k >= 1) stage(X1, k - 1);
 }
 
 // ---------------------------------------------------------------------------

@@ -28,6 +28,7 @@ struct ScanArgs {
     int *flag;                 // [b]: a combine was not positive definite
     int lu = 0;                // LU form of the combine (CondensedSystemSolverType::LU)
     double *scratch = nullptr; // radix-4 rounds: two private element slots per block [b][S][2][es]
+    int mw = 1;                // the 4-wave combine may run (Shape::mw)
 };
 
 struct MapArgs {
@@ -43,6 +44,7 @@ struct MapArgs {
     double *xhat, *lam;        // [b][S+1][n]
     int *flag;
     int lu = 0;                // LU form of the combine
+    int mw = 1;                // the 4-wave kernels may run (Shape::mw)
 };
 
 struct MapScanArgs {
@@ -69,7 +71,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
 // one launch = the two Hillis-Steele rounds at distances dist and 2 dist (two
 // waves per block); false when this shape keeps the radix-2 rounds
 bool seg_scan4_supported(int n);
-bool seg_scan_mw(int n, bool lu);  // the 4-wave combine runs the scan rounds
+bool seg_scan_mw(int n, bool lu, int mw = 1);  // the 4-wave combine runs the scan rounds
 int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st);
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 // Composition radix of the boundary-map prefix scan (2 or 4).

@@ -81,6 +81,7 @@ static RiccatiArgs riccati_args(pdplqr_handle h) {
 }
 
 static int parallel_init(pdplqr_handle h) {
+    h->sh.mw = 1;
     const Shape &sh = h->sh;
     if (sh.s > 64) return unsupported("PARALLEL solver with n + m > 64");
     ParallelState *ps = new ParallelState();
@@ -108,7 +109,24 @@ static int parallel_init(pdplqr_handle h) {
     // b ~45 us, c ~5.5 us at 24/8; a ~10 us, b ~15 us for s <= 16).
     int Lsub = h->cfg.segment_len;
     if (Lsub <= 0 && getenv("PDPLQR_SEGMENT_LEN")) Lsub = atoi(getenv("PDPLQR_SEGMENT_LEN"));  // diagnostics
-    if (Lsub <= 0) {
+    const bool auto_len = Lsub <= 0;
+    for (int family = 0; family < 2 && auto_len; ++family) {
+        // family 0: the 4-wave kernels where they apply (Shape::mw); family 1
+        // (only when family 0 ended with long segments): the one-wave kernels.
+        // The 4-wave combine and stage need 256 threads and ~53 KB of LDS per
+        // segment, so their resident slots run out first: at 24/8 the slice of
+        // an 8-rank split (N = 8192) runs 0.48 ms on them against 0.59 one-wave,
+        // but a whole N = 65536 horizon is cut into 505 segments of 130 stages
+        // and runs 1.29 ms against 1.15 with the one-wave kernels' 1009 segments
+        // of 65 (scripts/c4_variants.py, profiles/r03/c4_family.log).
+        if (family == 1) {
+            int longest = 0;
+            for (int i = 0; i < ns; ++i)
+                longest = std::max(longest, (ps->ref_len[i] + ((ps->ref_len[i] + Lsub - 1) / Lsub) - 1) /
+                                                ((ps->ref_len[i] + Lsub - 1) / Lsub));
+            if (longest <= 64 || getenv("PDPLQR_MW_ALWAYS")) break;
+            h->sh.mw = 0;
+        }
         const double a = 10.0, b = sh.s <= 16 ? 15.0 : 45.0, cm = sh.s <= 16 ? 4.0 : 5.5;
         const long long sb = seg_backward_slots(sh, h->cfg.device), ss = seg_scan_slots(sh, h->cfg.device);
         const long long B = sh.batch;
@@ -242,6 +260,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
         s.flag = ps->flag;
         s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
         s.scratch = ps->scan4;
+        s.mw = sh.mw;
         int rc = r4 ? launch_seg_scan4(s, sh.batch, h->stream) : launch_seg_scan(s, sh.batch, h->stream);
         if (rc) return rc;
         sin = s.out;
@@ -271,6 +290,7 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     ma.lam = ps->lam;
     ma.flag = ps->flag;
     ma.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
+    ma.mw = sh.mw;
     int rc = launch_seg_maps(ma, sh.batch, h->stream);
     if (rc) return rc;
     double *mb[2] = {ps->mapA, ps->mapB};

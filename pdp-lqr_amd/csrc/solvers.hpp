@@ -34,6 +34,7 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho);
 bool kkt_linear_supported(pdplqr_handle h);
 int kkt_backward_cached(pdplqr_handle h, const double *inv_rho);
 int kkt_backward_linear(pdplqr_handle h, const double *inv_rho);
+int kkt_rhs_restart(pdplqr_handle h);  // x0 sum of the rhs restarts (ADMM: h~, g formed by the update pass)
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws);
 int kkt_dim(pdplqr_handle h);
 int kkt_before_model(pdplqr_handle h);  // set_model on a formed KKT handle: keep the frozen matrix
