@@ -430,7 +430,9 @@ __device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) 
 // AUG: carries TB column tiles, B <- C^{-1} B (final); M is left stale.
 // !AUG: M <- C^T, the transposed factor (upper triangle, zeros below,
 // identity padding kept): each block's ROW of C^T is exactly its panel V.
-template <int T, bool AUG, int TB>
+// KEEP (default !AUG): M <- C^T as well -- with AUG, the factor and the
+// carried solve C^{-1} B in one pass.
+template <int T, bool AUG, int TB, bool KEEP = !AUG>
 __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g, int c) {
     bool ok = true;
     const int nb = (n + 3) >> 2;
@@ -491,7 +493,7 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
 #endif
             const int col = 16 * ta + c;
             vt[ta] = (col >= j0 + 4) ? v : 0.0;  // trailing rows of the panel
-            if (!AUG) M.t[tj][ta][rj] = (col >= j0) ? v : 0.0;  // row block of C^T, final
+            if (KEEP) M.t[tj][ta][rj] = (col >= j0) ? v : 0.0;  // row block of C^T, final
         }
         if (AUG) {
 #pragma unroll
@@ -541,7 +543,7 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
                 for (int tb = 0; tb < TB; ++tb)
                     if (ta >= tj) B[ta][tb] = mfma_f64(-vt[ta], B[tj][tb][rj], B[ta][tb]);
     }
-    if (!AUG)
+    if (KEEP)
 #pragma unroll
         for (int ta = 0; ta < T; ++ta)
 #pragma unroll
@@ -910,9 +912,11 @@ __device__ __forceinline__ bool tcombine(double *out, const double *ea, const do
 // (condensed_system.hpp:252-289), its LU form solves with PartialPivLU of
 // I + C P (:117-137).
 //   CHOLESKY: R = chol(P), S = I + R^T C R = Q Q^T,
-//             [Phi | phi] = R^{-T} Q^{-T} Q^{-1} R^T [F | v]
-//             (both factors by chol_blk4, the three triangular solves in LDS,
-//             one lane per right-hand-side column);
+//             [Phi | phi] = R^{-T} Q^{-T} Q^{-1} R^T [F | v] = V^T Q^{-1} R^T [F | v],
+//             V = Q^{-1} R^{-1}: chol(P) carries the identity (R^{-1}), chol(S)
+//             carries [R^T F | R^T v | R^{-1}], one product V^T [X1 | x3] after it
+//             (round 2 ran three triangular solves in LDS, one lane per column:
+//             a dependent LDS read per FMA);
 //   LU:       Gauss-Jordan with partial pivoting on [I + C P | F | v]
 //             (comb_core_lu's pivot rule).
 // The result lands in LDS: Phi at out (n x n, ld n), phi at out + n n.
@@ -938,50 +942,72 @@ __device__ __forceinline__ bool tmap_solve(const double *F, const double *C, con
     wv_load(fv, f, n, g, c);
     wv_tn(v, Cs, pv, n, -1.0, &fv);  // v = f - C p  (C symmetric)
     if constexpr (!LU) {
-        double *Rt = scr, *Qt = scr + P * PL, *B = scr + 2 * P * PL;  // B: [R^T F | R^T v], ld n
+        // R = chol(P) carrying the identity (U = R^T and R^{-1} in one pass),
+        // S = I + R^T C R = Q Q^T carrying [R^T F | R^T v | R^{-1}]:
+        // [X1 | x3 | V] = Q^{-1} [...], and [Phi | phi] = V^T [X1 | x3]
+        // (= R^{-T} Q^{-T} Q^{-1} R^T [F | v]; no triangular solve left)
+        double *Rt = scr;
         WM<T> U, R;
-        wm_load(U, Pj, n, n, false, 1.0, g, c);
-        ok = chol_blk4<T, false, T>(U, U.t, n, g, c);  // U = R^T (upper)
+        d4 BB[T][2 * T + 1];
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) BB[a][T + 1 + bt][r] = (16 * a + 4 * r + g == 16 * bt + c) ? 1.0 : 0.0;
+        {
+            d4 Ri[T][T];
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt) Ri[a][bt] = BB[a][T + 1 + bt];
+            wm_load(U, Pj, n, n, false, 1.0, g, c);
+            ok = chol_blk4<T, true, T, true>(U, Ri, n, g, c);  // U = R^T (upper), Ri = R^{-1}
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt) BB[a][T + 1 + bt] = Ri[a][bt];
+        }
         wm_store(U, Rt, PL, n, g, c);
         wave_sync();
         wm_load(R, Rt, PL, n, true, 1.0, g, c);  // R
+        WM<T> S;
         {
-            WM<T> T1, S;
+            WM<T> T1;
             wm_tn(T1, Cs, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C R
             wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C R
-            ok = chol_blk4<T, false, T>(S, S.t, n, g, c) && ok;            // S = Q^T (upper)
-            wm_store(S, Qt, PL, n, g, c);
         }
         {
             WM<T> Fs, X;
             WV<T> y;
             wm_load(Fs, F, n, n, false, 0.0, g, c);
             wm_tn(X, R, Fs, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F
-            wm_store(X, B, n, n, g, c);
-            wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);  // R^T v
-            wv_store(y, B + n * n, n, g, c);
-        }
-        wave_sync();
-        if (lane <= n) {  // lane l solves right-hand-side column l (l = n: the vector)
-            double *col = B + lane * n;
-            for (int i = 0; i < n; ++i) {  // Q z = col, Q(i, k) = Q^T(k, i)
-                double a = col[i];
-                for (int k = 0; k < i; ++k) a = __builtin_fma(-Qt[k + i * PL], col[k], a);
-                col[i] = a / Qt[i + i * PL];
-            }
-            for (int i = n - 1; i >= 0; --i) {  // Q^T y = z
-                double a = col[i];
-                for (int k = i + 1; k < n; ++k) a = __builtin_fma(-Qt[i + k * PL], col[k], a);
-                col[i] = a / Qt[i + i * PL];
-            }
-            for (int i = n - 1; i >= 0; --i) {  // R^T x = y
-                double a = col[i];
-                for (int k = i + 1; k < n; ++k) a = __builtin_fma(-Rt[i + k * PL], col[k], a);
-                col[i] = a / Rt[i + i * PL];
+            wv_tn(y, R, v, n, 1.0, (const WV<T> *)nullptr);              // R^T v
+#pragma unroll
+            for (int a = 0; a < T; ++a) {
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt) BB[a][bt] = X.t[a][bt];
+                BB[a][T] = y.t[a];
             }
         }
+        ok = chol_blk4<T, true, 2 * T + 1>(S, BB, n, g, c) && ok;
+        WM<T> X1, V, Phi;
+        WV<T> x3, ph;
+#pragma unroll
+        for (int a = 0; a < T; ++a) {
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                X1.t[a][bt] = BB[a][bt];
+                V.t[a][bt] = BB[a][T + 1 + bt];
+            }
+            x3.t[a] = BB[a][T];
+        }
+        wm_tn(Phi, V, X1, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // V^T X1
+        wv_tn(ph, V, x3, n, 1.0, (const WV<T> *)nullptr);             // V^T x3
+        wave_sync();  // every lane's reads of Rt done before out (may alias scr) is written
+        wm_store(Phi, out, n, n, g, c);
+        wv_store(ph, out + n * n, n, g, c);
         wave_sync();
-        for (int q = lane; q < n * n + n; q += 64) out[q] = B[q];
     } else {
         const int ncol = 2 * n + 1;
         double *W = scr, *prow = scr + n * ncol;
