@@ -43,6 +43,40 @@ __device__ __forceinline__ Mv mv_none() { return Mv{nullptr, 0, 0}; }
 // lower: only tiles on or below the diagonal are formed (C symmetric by
 // construction) and mirrored on store.  C may alias A, B (not add when
 // lower).  M, N <= 64.
+// element offset of a view: strides for dense / transposed, the packed lower
+// index of (max, min) for packed symmetric views (PK)
+template <bool PK>
+__device__ __forceinline__ int mv_off(int i, int j, int si, int sj, int ld) {
+    if constexpr (PK) return i >= j ? pidx(i, j, ld) : pidx(j, i, ld);
+    else return i * si + j * sj;
+}
+
+// The product loop, specialised on whether A / B are packed views: the view
+// kind is hoisted out of the loop (a runtime switch per element cost a scalar
+// branch per load) and the loads are branch-free (clamped indices and a
+// select: a guarded load compiles to an exec-mask region with its own wait).
+template <bool PA, bool PB>
+__device__ __forceinline__ void blk_mm_loop(d4 (&acc)[4], const int (&ti)[4], const int (&tj)[4], const bool (&on)[4],
+                                            const Mv &A, const Mv &B, int M, int N, int K, int g, int c) {
+    const int sai = A.kind == 1 ? A.ld : 1, saj = A.kind == 1 ? 1 : A.ld;
+    const int sbi = B.kind == 1 ? B.ld : 1, sbj = B.kind == 1 ? 1 : B.ld;
+    for (int k0 = 0; k0 < K; k0 += 4) {
+        const int k = k0 + g;
+        const int kc = k < K ? k : K - 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!on[t]) continue;  // wave-uniform
+            const int i = 16 * ti[t] + c, j = 16 * tj[t] + c;
+            const int ic = i < M ? i : M - 1, jc = j < N ? j : N - 1;
+            const double av = A.p[mv_off<PA>(ic, kc, sai, saj, A.ld)];
+            const double bv = B.p[mv_off<PB>(kc, jc, sbi, sbj, B.ld)];
+            const double a = (k < K && i < M) ? av : 0.0;
+            const double b = (k < K && j < N) ? bv : 0.0;
+            acc[t] = mfma_f64(a, b, acc[t]);
+        }
+    }
+}
+
 __device__ __noinline__ void blk_mm(double *C, int ldc, Mv A, Mv B, int M, int N, int K, double alpha, double diag,
                                     Mv add, bool lower) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -59,17 +93,10 @@ __device__ __noinline__ void blk_mm(double *C, int ldc, Mv A, Mv B, int M, int N
         acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     }
     __syncthreads();  // the operands are complete
-    for (int k0 = 0; k0 < K; k0 += 4) {
-        const int k = k0 + g;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (!on[t]) continue;  // wave-uniform
-            const int i = 16 * ti[t] + c, j = 16 * tj[t] + c;
-            const double a = (k < K && i < M) ? A.at(i, k) : 0.0;
-            const double b = (k < K && j < N) ? B.at(k, j) : 0.0;
-            acc[t] = mfma_f64(a, b, acc[t]);
-        }
-    }
+    if (A.kind != 2 && B.kind != 2) blk_mm_loop<false, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    else if (A.kind == 2 && B.kind != 2) blk_mm_loop<true, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    else if (A.kind != 2) blk_mm_loop<false, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    else blk_mm_loop<true, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
     __syncthreads();  // every read of the operands is done: C may overwrite them
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

@@ -451,7 +451,13 @@ __device__ unsigned long long g_aug_t[1024 * 8];
 #endif
 
 template <int NN, int MM>
-__global__ __launch_bounds__(256) void k_seg_bwd_aug_mw(SegArgs A) {
+// PDPLQR_AUG_MW_OCC: resident blocks per CU the register allocation targets
+// (2: 215 VGPRs, no spill; 3: 168 VGPRs with 19 spill ops per stage -- the
+// N = 8192 slice 0.49 -> 0.62 ms, forced 4-wave N = 65536 1.32 -> 1.54 ms)
+#ifndef PDPLQR_AUG_MW_OCC
+#define PDPLQR_AUG_MW_OCC 2
+#endif
+__global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegArgs A) {
     constexpr int n = NN, m = MM, s = NN + MM, D = s + NN, AUG = D;
     constexpr int ps = s * (s + 1) / 2, PN = n * (n + 1) / 2;
     constexpr int XLD = n + 1;                       // leading dimension of the published P block
