@@ -261,21 +261,25 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     const int lane = wave_lane();
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
-    const long long b = blockIdx.x / S;
-    const int i = blockIdx.x % S;
+    const int per = scan_round_blocks(S, d, A.sk);
+    const long long b = blockIdx.x / per;
+    int i, j;
+    if (!scan_round_operands(S, d, A.sk, blockIdx.x % per, i, j)) return;
     const long long is = A.istride ? A.istride : es;
     const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
-    if (i + d >= S) {  // suf_i already reaches the last segment
-        elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
+    if (j < 0) {  // suf_i already reaches the end of its block / the last segment
+        if (in != out) elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
         return;
     }
-    // The right operand covers segments [i + d, min(i + 2d - 1, S - 1)].  When
+    // The right operand covers segments [j, min(j + d - 1, S - 1)].  When
     // that range holds the real terminal its F = C = f = 0, and so are the
-    // result's: only the value function (P, p) is combined.
-    const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    // result's: only the value function (P, p) is combined.  In place (sk = 2)
+    // is safe: every operand block but P_a is staged in LDS first, and P_a is
+    // read into registers that the symmetrised P store depends on.
+    const bool fcf = !(A.terminal && j + d - 1 >= S - 1);
     const ElemIn ea = stage_left(ebuf, in + (long long)i * is, n, lane);
-    const ElemIn eb = stage_right(ebuf + op_stage_len(n), in + (long long)(i + d) * is, n, lane);
+    const ElemIn eb = stage_right(ebuf + op_stage_len(n), in + (long long)j * is, n, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     double *o = out + (long long)i * es;
@@ -353,16 +357,19 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n;
-    const long long b = blockIdx.x / S;
-    const int i = blockIdx.x % S;
+    const int per = scan_round_blocks(S, d, A.sk);
+    const long long b = blockIdx.x / per;
+    int i, j;
+    if (!scan_round_operands(S, d, A.sk, blockIdx.x % per, i, j)) return;  // block-uniform
     const long long is = A.istride ? A.istride : es;
     const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
-    if (i + d >= S) {  // block-uniform
-        if (wv == 0) elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
+    if (j < 0) {  // block-uniform
+        if (wv == 0 && in != out) elem_copy(out + (long long)i * es, in + (long long)i * is, n, lane);
         return;
     }
-    const bool fcf = !(A.terminal && i + 2 * d - 1 >= S - 1);
+    // both operands are staged in LDS before any store: in place (sk = 2) is safe
+    const bool fcf = !(A.terminal && j + d - 1 >= S - 1);
     COMB_MARK(16);  // kernel entry
 #ifdef PDPLQR_COMB_PROFILE
     if (threadIdx.x == 0) {
@@ -373,7 +380,7 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     const MwSmem sm = mw_smem(mwbuf, n);
     double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
     stage_range_blk(ea, in + (long long)i * is, es);
-    stage_range_blk(eb, in + (long long)(i + d) * is, es);
+    stage_range_blk(eb, in + (long long)j * is, es);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     COMB_MARK(17);  // operands staged
@@ -838,8 +845,11 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
-    if (wide_state(a.n)) return launch_seg_scan_wide(a, batch, st);
-    const dim3 grid((unsigned)(batch * a.S)), blk(64);
+    if (wide_state(a.n)) {
+        if (a.sk) return PDPLQR_ERR_UNSUPPORTED;  // the wide combine reads its operands from HBM
+        return launch_seg_scan_wide(a, batch, st);
+    }
+    const dim3 grid((unsigned)(batch * scan_round_blocks(a.S, a.dist, a.sk))), blk(64);
     const int T = tile_order(a.n);
     const size_t smem = op_stage_bytes(a.n);
     if (seg_scan_mw(a.n, a.lu, a.mw)) {

@@ -29,7 +29,36 @@ struct ScanArgs {
     int lu = 0;                // LU form of the combine (CondensedSystemSolverType::LU)
     double *scratch = nullptr; // radix-4 rounds: two private element slots per block [b][S][2][es]
     int mw = 1;                // the 4-wave combine may run (Shape::mw)
+    // Round form.  0: Hillis-Steele (every entry i < S - dist combines with
+    // i + dist; in -> out ping-pong).  Sklansky (the same ceil(log2 S) rounds,
+    // half the combines per round): 1 = the first round (dist 1; in -> out,
+    // entries without a partner copied), 2 = a later round, in place (in == out):
+    // entry i in the lower half of its 2 dist block combines with the first
+    // entry j of the upper half, which already holds [j, j + dist - 1].
+    int sk = 0;
 };
+
+// Blocks per problem of one scan round.
+__host__ __device__ inline int scan_round_blocks(int S, int dist, int sk) {
+    return sk == 2 ? dist * ((S - dist + 2 * dist - 1) / (2 * dist)) : S;
+}
+
+// Operands of block q of a round: the result goes to entry i, the right
+// operand is entry j (j < 0: entry i is copied / kept, no combine); false when
+// the block has nothing to do.  The right operand covers [j, min(j + dist - 1,
+// S - 1)] in every form.
+__host__ __device__ inline bool scan_round_operands(int S, int dist, int sk, int q, int &i, int &j) {
+    if (sk == 2) {
+        const int blk = q / dist, pos = q % dist;
+        i = blk * 2 * dist + pos;
+        j = blk * 2 * dist + dist;
+        return j < S;
+    }
+    i = q;
+    if (sk == 1) j = ((i & 1) || i + 1 >= S) ? -1 : i + 1;
+    else j = i + dist < S ? i + dist : -1;
+    return true;
+}
 
 struct MapArgs {
     int n, S;

@@ -80,6 +80,8 @@ static RiccatiArgs riccati_args(pdplqr_handle h) {
     return a;
 }
 
+static bool scan_sklansky(const Shape &sh);
+
 static int parallel_init(pdplqr_handle h) {
     h->sh.mw = 1;
     const Shape &sh = h->sh;
@@ -142,8 +144,10 @@ static int parallel_init(pdplqr_handle h) {
             }
             return S;
         };
+        const bool sk = scan_sklansky(h->sh);  // (Sklansky rounds: S / 2 combines each)
         auto cost = [&](long long S, long long per) {
-            const long long rb = (B * S + sb - 1) / sb, rs = (B * S + ss - 1) / ss;
+            const long long sc = sk ? (S + 1) / 2 : S;
+            const long long rb = (B * S + sb - 1) / sb, rs = (B * sc + ss - 1) / ss;
             int lg = 0, lg1 = 0;
             while ((1LL << lg) < S) ++lg;
             while ((1LL << lg1) < S + 1) ++lg1;
@@ -213,6 +217,14 @@ static int parallel_init(pdplqr_handle h) {
 // segment backward + suffix scan; `last_is_terminal` = 0 for a non-final
 // horizon shard.
 static int parallel_scans(pdplqr_handle h, int last_is_terminal);
+
+// The suffix scan runs Sklansky rounds (half the combines of a Hillis-Steele
+// round, same depth; PDPLQR_SCAN_HS=1: Hillis-Steele, A/B) on the shapes whose
+// combine kernels stage their operands before storing (n <= 32) and that do
+// not take the two-round k_seg_scan4 launches.
+static bool scan_sklansky(const Shape &sh) {
+    return !wide_state(sh.n) && !seg_scan4_supported(sh.n) && !getenv("PDPLQR_SCAN_HS");
+}
 void graph_release(pdplqr_handle h);
 
 static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
@@ -249,6 +261,26 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
     double *bufs[2] = {ps->bufA, ps->bufB};
     int round = 0;
     const bool r4 = ps->scan4 != nullptr;  // two rounds per launch (k_seg_scan4)
+    if (scan_sklansky(sh) && ps->S > 1) {
+        // Sklansky rounds: the first into bufA, the later ones in place there
+        for (int d = 1; d < ps->S; d <<= 1) {
+            ScanArgs s;
+            s.n = sh.n;
+            s.S = ps->S;
+            s.dist = d;
+            s.terminal = last_is_terminal;
+            s.in = d == 1 ? sin : ps->bufA;
+            s.out = ps->bufA;
+            s.flag = ps->flag;
+            s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
+            s.mw = sh.mw;
+            s.sk = d == 1 ? 1 : 2;
+            int rc = launch_seg_scan(s, sh.batch, h->stream);
+            if (rc) return rc;
+        }
+        ps->suf_final = ps->bufA;
+        return PDPLQR_OK;
+    }
     for (int d = 1; d < ps->S; d <<= (r4 ? 2 : 1), ++round) {
         ScanArgs s;
         s.n = sh.n;

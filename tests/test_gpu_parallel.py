@@ -193,6 +193,50 @@ def test_radix4_scan_equals_radix2(N, batch, seglen, condensed, monkeypatch):
     assert np.array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("n,m,N,batch,seglen,condensed,one_wave",
+                         [(24, 8, 96, 2, 5, "CHOLESKY", False), (24, 8, 40, 1, 3, "CHOLESKY", False),
+                          (24, 8, 7, 2, 3, "CHOLESKY", False), (24, 8, 512, 1, 0, "CHOLESKY", False),
+                          (24, 8, 96, 2, 5, "CHOLESKY", True), (20, 6, 130, 2, 4, "LU", False),
+                          (24, 8, 12, 1, 4, "CHOLESKY", False), (18, 4, 33, 3, 2, "CHOLESKY", True)])
+def test_sklansky_scan_matches_hillis_steele(n, m, N, batch, seglen, condensed, one_wave, monkeypatch):
+    """The suffix scan's Sklansky rounds (n <= 32: the first round into a
+    buffer, the later ones in place, half the combines per round) give the
+    Hillis-Steele rounds' solution (PDPLQR_SCAN_HS=1) to rounding -- the same
+    elements associated differently -- and both match the serial oracle.
+    Segment counts 3..~130 cover partial upper halves and the terminal
+    element's (P, p)-only combines; one_wave forces the one-wave combine."""
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    if one_wave:
+        monkeypatch.setenv("PDPLQR_SCAN_1WAVE", "1")
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 2000 + N)
+    ws0 = np.zeros((batch, N * (n + m) + n))
+    outs = []
+    for hs in (False, True):
+        if hs:
+            monkeypatch.setenv("PDPLQR_SCAN_HS", "1")
+        bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=False,
+                              segment_len=seglen if seglen else 16, condensed=condensed)
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+        bs.backward()
+        out = np.zeros_like(ws0)
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0)
+        outs.append(out)
+        bs.close()
+    assert rel_err(outs[0], outs[1]) < 1e-11
+    ser = BatchedLQRSolver(n, m, N, batch, solver="serial")
+    ser.set_model(E, c, H, h)
+    ser.update_problem_data(ws0, sigma=1e-6)
+    ser.backward()
+    ref = np.zeros_like(ws0)
+    ser.forward(x0, ref)
+    ser.close()
+    assert rel_err(outs[0], ref) < TOL
+
+
 def test_graph_replay_matches_direct():
     """Protocol calls replayed from a captured hipGraph (PDPLQR_GRAPH=1, read at
     library load: run in a child process) give the same trajectory as direct
