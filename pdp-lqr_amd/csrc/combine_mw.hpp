@@ -37,6 +37,13 @@ namespace pdplqr {
 // LDS of one combine, in a dynamic buffer sized by mw_smem_bytes(n): five
 // n x n blocks at leading dimension ld = n + 1 (odd for even n: column reads
 // hit distinct banks) and four n-vectors.  At n = 24: 24.6 KB, 6 blocks per CU.
+// Phase B: R^T C_a u and R^T v1 on wave 3 (idle there otherwise) instead of
+// after R^T F_a on wave 1, the slowest wave of the phase (comb_ab.log: the
+// block waited 2.5 us for it).  0: on wave 1 (A/B).
+#ifndef PDPLQR_MW_VEC_W3
+#define PDPLQR_MW_VEC_W3 1
+#endif
+
 struct MwSmem {
     int ld;
     double *S;   // w0: R transpose scratch, then S; phase D: w0's staging
@@ -260,6 +267,10 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wm_tn(B, R, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F_a
             wm_store(B, sm.B1, PL, n, g, c);
         }
+#if PDPLQR_MW_VEC_W3
+    } else if (wv == 3) {  // the two vector products on the wave phase B leaves idle
+        wm_load(R, sm.S, PL, n, true, 1.0, g, c);
+#endif
         WV<T> cu, v1, y;
         wv_load(cu, sm.bv + n, n, g, c);
         if (fcf) wv_load(v1, sm.bv, n, g, c);

@@ -254,12 +254,12 @@ __device__ __forceinline__ void stage_range_blk(double *dst, const double *src, 
 __host__ __device__ inline int mw_smem_doubles(int n) { return (int)((mw_smem_bytes(n) + 15) / 16 * 2); }
 __host__ __device__ inline int elem_slot(int n) { return (3 * n * n + 2 * n + 1) & ~1; }
 
-template <int T, bool LU>
+template <int T, bool LU, int NC = 0>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
     extern __shared__ __attribute__((aligned(16))) double ebuf[];  // 2 operand images (op_stage_bytes)
     const int lane = wave_lane();
-    const int n = A.n, S = A.S, d = A.dist;
+    const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n;
     const int per = scan_round_blocks(S, d, A.sk);
     const long long b = blockIdx.x / per;
@@ -351,11 +351,11 @@ __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
 
 // One Hillis-Steele round with the 4-wave combine (combine_mw.hpp; CHOLESKY
 // form): the same operands, output and terminal rule as k_seg_scan.
-template <int T>
+template <int T, int NC = 0>
 __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = A.n, S = A.S, d = A.dist;
+    const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n;
     const int per = scan_round_blocks(S, d, A.sk);
     const long long b = blockIdx.x / per;
@@ -408,12 +408,12 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
 // maps x0 through the global prefix of earlier shards (or the identity) and
 // writes x_0 directly.  maps: [b][S+1][Phi | phi], vfun: [b][S+1][P | p].
 // ---------------------------------------------------------------------------
-template <int T, bool LU>
+template <int T, bool LU, int NC = 0>
 __global__ __launch_bounds__(64) void k_seg_maps(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];  // 2 operand images when A.right
     __shared__ CombSmem<T> sm;
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
-    const int n = A.n, S = A.S, J = S + 1, nn = n * n;
+    const int n = NC ? NC : A.n, S = A.S, J = S + 1, nn = n * n;
     const int es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
@@ -603,11 +603,11 @@ __device__ __forceinline__ bool mw_map(const ElemIn &e, const double *vP, const 
 // outputs.  V_j = suf_j (x) right is the P-only 4-wave combine; the map is
 // mw_map's solve, with the products after the factorisations one deep and
 // split over the waves by output tile.
-template <int T>
+template <int T, int NC = 0>
 __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const int n = A.n, S = A.S, J = S + 1, nn = n * n;
+    const int n = NC ? NC : A.n, S = A.S, J = S + 1, nn = n * n;
     const int es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
@@ -748,10 +748,10 @@ __global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
 // j < 4 d are anchored: ceil(log4 (S + 1)) launches instead of
 // ceil(log2 (S + 1)), each at most three products in sequence.  The running
 // map is kept transposed (Phi^T), the form the matrix-vector product reads.
-template <int T>
+template <int T, int NC = 0>
 __global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
-    const int n = A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
+    const int n = NC ? NC : A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
     const long long b = blockIdx.x / J;
     const int j = blockIdx.x % J;
     const double *in = A.in + b * (long long)J * mw;
@@ -798,6 +798,16 @@ static int tile_order(int n);
 // dynamic LDS of the 4-wave kernels: the combine's own + staged operand elements
 static size_t mw_scan_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 2 * elem_slot(n)) * sizeof(double); }
 static size_t mw_maps_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 3 * elem_slot(n)) * sizeof(double); }
+
+// n = 24 (the C4 horizon shape) runs kernel instances with n a compile-time
+// constant: every bounds guard of the tile loads / stores folds away (the
+// runtime-n scan kernel is ~14 k instructions, past the instruction cache a
+// 4-wave block with four different phase paths cycles through).
+// PDPLQR_CT_N24=0: runtime n everywhere (A/B).
+#ifndef PDPLQR_CT_N24
+#define PDPLQR_CT_N24 1
+#endif
+static inline bool ct_n24(int n) { return PDPLQR_CT_N24 && n == 24; }
 
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
@@ -855,6 +865,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     if (seg_scan_mw(a.n, a.lu, a.mw)) {
         const size_t sm = mw_scan_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_scan_mw<1>, grid, dim3(256), sm, st, a);
+        else if (ct_n24(a.n)) hipLaunchKernelGGL((k_seg_scan_mw<2, 24>), grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_scan_mw<2>, grid, dim3(256), sm, st, a);
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
@@ -862,6 +873,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_scan<1, true>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_scan<1, false>), grid, blk, smem, st, a);
     else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_scan<2, true>), grid, blk, smem, st, a);
+    else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_seg_scan<2, false, 24>), grid, blk, smem, st, a);
     else if (T == 2) hipLaunchKernelGGL((k_seg_scan<2, false>), grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -875,6 +887,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     if (seg_scan_mw(a.n, a.lu, a.mw) && !getenv("PDPLQR_MAPS_1WAVE")) {
         const size_t sm = mw_maps_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_maps_mw<1>, grid, dim3(256), sm, st, a);
+        else if (ct_n24(a.n)) hipLaunchKernelGGL((k_seg_maps_mw<2, 24>), grid, dim3(256), sm, st, a);
         else hipLaunchKernelGGL(k_seg_maps_mw<2>, grid, dim3(256), sm, st, a);
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
@@ -883,6 +896,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_maps<1, true>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_maps<1, false>), grid, blk, smem, st, a);
     else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_maps<2, true>), grid, blk, smem, st, a);
+    else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_seg_maps<2, false, 24>), grid, blk, smem, st, a);
     else if (T == 2) hipLaunchKernelGGL((k_seg_maps<2, false>), grid, blk, smem, st, a);
     else return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -898,6 +912,7 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
     const int T = tile_order(a.n);
     if (PDPLQR_MAP_RADIX == 4) {
         if (T == 1) hipLaunchKernelGGL(k_map_scan4<1>, grid, blk, 0, st, a);
+        else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_map_scan4<2, 24>), grid, blk, 0, st, a);
         else if (T == 2) hipLaunchKernelGGL(k_map_scan4<2>, grid, blk, 0, st, a);
         else return PDPLQR_ERR_UNSUPPORTED;
     } else if (T == 1) hipLaunchKernelGGL(k_map_scan<1>, grid, blk, 0, st, a);
@@ -1001,11 +1016,12 @@ __global__ __launch_bounds__(64) void k_rank_maps(const double *elems_all, const
 // V_{j+1} by mw_map, both operands staged into LDS first.  A one-wave
 // tmap_solve chains three triangular solves after the factorisations
 // (43 us per launch at n = 24); mw_map spreads them over the waves.
-template <int T>
-__global__ __launch_bounds__(256) void k_rank_maps_mw(const double *elems_all, const double *suf, int R, int r, int n,
+template <int T, int NC = 0>
+__global__ __launch_bounds__(256) void k_rank_maps_mw(const double *elems_all, const double *suf, int R, int r, int n_,
                                                       int batch, double *maps, int *flag) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int n = NC ? NC : n_;
     const int nn = n * n, es = 3 * nn + 2 * n, mw = nn + n;
     const long long b = blockIdx.x / r;
     const int j = blockIdx.x % r;
@@ -1067,6 +1083,10 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
         hipLaunchKernelGGL(k_rank_chain<1>, dim3(batch), dim3(64), 0, st, maps, x0, r, n, out_pre);
     } else if (T == 2) {
         if (lu) hipLaunchKernelGGL((k_rank_maps<2, true>), gm, blk, rsm, st, elems, suf, R, r, n, batch, maps, flag);
+        else if (seg_scan_mw(n, false) && ct_n24(n))
+            hipLaunchKernelGGL((k_rank_maps_mw<2, 24>), gm, dim3(256),
+                               (size_t)(mw_smem_doubles(n) + elem_slot(n) + ((n * n + n + 1) & ~1)) * sizeof(double),
+                               st, elems, suf, R, r, n, batch, maps, flag);
         else if (seg_scan_mw(n, false))
             hipLaunchKernelGGL(k_rank_maps_mw<2>, gm, dim3(256),
                                (size_t)(mw_smem_doubles(n) + elem_slot(n) + ((n * n + n + 1) & ~1)) * sizeof(double),
