@@ -446,6 +446,10 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         launch_fast<1, 12, 4>(a, st);
     } else if (fast_ok && a.sh.n == 24 && a.sh.m == 8) {
         launch_fast<2, 24, 8>(a, st);
+    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16 && !getenv("PDPLQR_NO_T3")) {
+        // s = 40 on 3 x 3 register tiles (one wave per problem) instead of the
+        // block-wide LDS kernels of kernels_big.hip / kernels_wide.hip
+        launch_fast<3, 24, 16>(a, st);
     } else if (a.sh.s <= 16) {
         hipLaunchKernelGGL(k_riccati_bwd<1>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (a.sh.s <= 32) {
@@ -916,6 +920,12 @@ template <bool SEG>
 static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                       double *ws, const SegFwd &sf, hipStream_t st) {
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
+    if (!SEG && sh.s > 32 && sh.s <= 48 && sh.m <= 16 && !getenv("PDPLQR_NO_T3")) {
+        // 32 < s <= 48: the register rollout on 3 row tiles (one wave per problem)
+        hipLaunchKernelGGL((k_riccati_fwd<3, 16, false>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     if (sh.s > 32) {
         if (!SEG && big_shape(sh)) return launch_riccati_forward_big(sh, E, c, FR, x0, ws, st);
         if (SEG && big_shape(sh)) return launch_riccati_forward_seg_big(sh, E, c, FR, sf, ws, st);

@@ -23,7 +23,9 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-9
 
-SHAPES = [(30, 10, 12, 3), (40, 24, 6, 2), (33, 1, 9, 2), (1, 40, 5, 2), (20, 13, 15, 3), (48, 16, 4, 2)]
+# (24, 16): the one-wave 3 x 3 register-tile backward (k_riccati_bwd_fast<3, 24, 16>)
+SHAPES = [(30, 10, 12, 3), (40, 24, 6, 2), (33, 1, 9, 2), (1, 40, 5, 2), (20, 13, 15, 3), (48, 16, 4, 2),
+          (24, 16, 21, 3), (24, 16, 2, 2)]
 
 
 @pytest.fixture(scope="module", autouse=True)
