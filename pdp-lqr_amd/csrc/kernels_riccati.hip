@@ -428,6 +428,204 @@ static void launch_fast(const RiccatiArgs &a, hipStream_t st) {
     else hipLaunchKernelGGL((k_riccati_bwd_fast<T, NN, MM, false>), dim3(a.sh.batch), dim3(64), 0, st, a);
 }
 
+// ---------------------------------------------------------------------------
+// Value-form backward on 3 x 3 register tiles (32 < s <= 48, n % 4 == 0,
+// m % 4 == 0, m <= 16; keep_factors = 0): the 12/4 kernels_schur.hip scheme
+// at T = 3.  The stage matrix M_k = H~_k + E^T P_{k+1} E and lp = h~ + E^T
+// (P_{k+1} c + p_{k+1}) (lqr_kernel.hpp:121-143 with P = Lxx Lxx^T) are formed
+// from P_{k+1} itself (LDS, symmetrised on read), and only the m u-pivots are
+// eliminated (chol_tiles over [0, m), lp carried): the trailing block left is
+// P_k, the carried lp rows are p_k (lqr_kernel.hpp:145-146).  16 pivots a
+// stage instead of the full factor's 40 at 24/16, and no L round trip.  The
+// stage records arrive by LDS-DMA as in k_riccati_bwd_fast; the rollout
+// record is the same [L(:, 0:m) | lu'].  Status as the value-form 12/4 path:
+// a u-pivot that is not positive, or a P_k diagonal that is psd_bad.
+// PDPLQR_NO_VF3=1: the full-factor k_riccati_bwd_fast<3> (A/B).
+// ---------------------------------------------------------------------------
+template <int NN, int MM>
+__global__ __launch_bounds__(64, 1) void k_riccati_bwd_vf3(RiccatiArgs A) {
+    constexpr int T = 3;
+    using SH = FastShape<NN, MM>;
+    constexpr int n = SH::n, m = SH::m, s = SH::s, ps = SH::ps, NI = SH::NI, CH = SH::CH;
+    constexpr int PL = n + 1;          // leading dimension of P in LDS
+    constexpr int NC = n / 4;          // K chunks over the state index
+    constexpr int TG = (n + 15) / 16;  // row tiles of G = P E
+    static_assert(SH::ok && s > 32 && s <= 16 * T && n % 4 == 0 && m % 4 == 0 && m <= 16, "value-form T = 3 shape");
+    __shared__ BwdSmem<T> sm;  // pivot broadcast, 1/sqrt(pivot), lu', lp redistribution
+    __shared__ double Ps[n * PL];
+    __shared__ double pvs[n];
+    __shared__ __attribute__((aligned(16))) double stg[2][NI * 128];
+    const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
+    const long long b = blockIdx.x;
+    const Shape &sh = A.sh;
+    const int N = sh.N;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.KD + b * sh.perKD;
+    int fail_stage = -1;
+
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            int ch = q * 64 + lane;
+            ch = ch < CH ? ch : CH - 1;
+            const int d = 2 * ch;
+            const double *src = d < SH::OC   ? Eb + (long long)k * n * s + d
+                                : d < SH::OH ? cb + (long long)k * n + (d - SH::OC)
+                                : d < SH::OP ? hb + (long long)k * s + (d - SH::OH)
+                                             : Hb + (long long)k * ps + (d - SH::OP);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(&stg[slot][q * 128]), 16, 0,
+                                             0);
+        }
+    };
+
+    // ---- terminal (lqr_kernel.hpp:80-91): P_N = H~_N (packed, order n), p_N = h~_N ----
+    {
+        const double *HN = Hb + (long long)N * ps;
+        bool bad = false;
+        for (int q = lane; q < n * n; q += 64) {
+            const int i = q % n, j = q / n;
+            const double v = HN[i >= j ? pidx(i, j, n) : pidx(j, i, n)];
+            Ps[i + j * PL] = v;
+            if (i == j && psd_bad(v)) bad = true;
+        }
+        if (lane < n) pvs[lane] = hb[(long long)N * s + lane];
+        if (__any(bad)) fail_stage = N;
+        wave_sync();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma(N - 1, (N - 1) & 1);
+    for (int k = N - 1; k >= 0; --k) {
+        if (k > 0) {
+            dma(k - 1, (k - 1) & 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // stage k's record has landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        wave_sync();
+        const double *R = stg[k & 1];
+        // E[t][j] (t = 4 cc + g, j = 16 bt + c): the B operand of G = P E and,
+        // by symmetry of the layouts, the A operand of E^T G
+        double Ev[NC][T], cv[NC], pv[NC], ap[NC][TG];
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) {
+            const int t = 4 * cc + g;
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                const int j = 16 * bt + c;
+                Ev[cc][bt] = (j < s) ? R[SH::OE + j * n + t] : 0.0;
+            }
+            cv[cc] = R[SH::OC + t];
+            pv[cc] = pvs[t];
+#pragma unroll
+            for (int a = 0; a < TG; ++a) {  // P[16 a + c][t], symmetrised
+                const int i = 16 * a + c;
+                const int ic = i < n ? i : 0;
+                ap[cc][a] = (i < n) ? 0.5 * (Ps[ic + t * PL] + Ps[t + ic * PL]) : 0.0;
+            }
+        }
+        d4 M[T][T];
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                    M[a][bt][r] = (i < s && j < s) ? R[SH::OP + (i >= j ? pidx(i, j, s) : pidx(j, i, s))]
+                                                   : (i == j ? 1.0 : 0.0);
+                }
+        double hv[T];
+#pragma unroll
+        for (int bt = 0; bt < T; ++bt) hv[bt] = (16 * bt + c < s) ? R[SH::OH + 16 * bt + c] : 0.0;
+        // ---- G = P E (rows: state index, TG tiles) ----
+        d4 G[TG][T];
+#pragma unroll
+        for (int a = 0; a < TG; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) G[a][bt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
+#pragma unroll
+            for (int a = 0; a < TG; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt) G[a][bt] = mfma_f64(ap[cc][a], Ev[cc][bt], G[a][bt]);
+        // ---- M = H~ + E^T G ----
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int bt = 0; bt < T; ++bt) M[a][bt] = mfma_f64(Ev[cc][a], G[cc >> 2][bt][cc & 3], M[a][bt]);
+        // ---- lp = h~ + G^T c + E^T p_{k+1} (column j = 16 bt + c), to rows ----
+        double lpr[T][4];
+        {
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt) {
+                double part = 0.0;
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) {
+                    part = __builtin_fma(G[cc >> 2][bt][cc & 3], cv[cc], part);
+                    part = __builtin_fma(Ev[cc][bt], pv[cc], part);
+                }
+                part += shfl_xor_f64(part, 16);
+                part += shfl_xor_f64(part, 32);
+                if (g == 0) sm.lp[16 * bt + c] = hv[bt] + part;
+            }
+            wave_sync();
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    lpr[a][r] = (i < s) ? sm.lp[i] : 0.0;
+                }
+        }
+        // ---- the m u-pivots (lp carried): trailing block = P_k, lp rows x = p_k ----
+        const bool okk = chol_tiles<T>(M, lpr, sm.col, sm.inv, sm.luq, 0, m, m, true, g, c);
+        bool bad = false;
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int bt = 0; bt < T; ++bt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g, j = 16 * bt + c;
+                    if (i >= m && i < s && j >= m && j < s) {
+                        Ps[(i - m) + (j - m) * PL] = M[a][bt][r];
+                        if (i == j && psd_bad(M[a][bt][r])) bad = true;
+                    }
+                }
+        if (c == 0)
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    if (i >= m && i < s) pvs[i - m] = lpr[a][r];
+                }
+        if ((!okk || __any(bad)) && fail_stage < 0) fail_stage = k;
+        // ---- rollout record FR_k = [L(:, 0:m) | lu'], L(i, j) = M[i][j] / sqrt(M[j][j]) ----
+        double *FRk = FRb + (long long)k * (s * m + m);
+        if (c < m) {
+            const double iv = sm.inv[c];
+#pragma unroll
+            for (int a = 0; a < T; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * a + 4 * r + g;
+                    if (i < s) FRk[c * s + i] = (i >= c) ? M[a][0][r] * iv : 0.0;
+                }
+        }
+        if (lane < m) FRk[s * m + lane] = sm.luq[lane];
+        wave_sync();
+    }
+    if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
 // 16-byte alignment of every per-problem / per-stage block (fast path).
 static bool fast_aligned(const RiccatiArgs &a) {
     const Shape &sh = a.sh;
@@ -449,7 +647,9 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
     } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16 && !getenv("PDPLQR_NO_T3")) {
         // s = 40 on 3 x 3 register tiles (one wave per problem) instead of the
         // block-wide LDS kernels of kernels_big.hip / kernels_wide.hip
-        launch_fast<3, 24, 16>(a, st);
+        if (!a.Lc && !getenv("PDPLQR_NO_VF3"))
+            hipLaunchKernelGGL((k_riccati_bwd_vf3<24, 16>), dim3(a.sh.batch), dim3(64), 0, st, a);
+        else launch_fast<3, 24, 16>(a, st);
     } else if (a.sh.s <= 16) {
         hipLaunchKernelGGL(k_riccati_bwd<1>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (a.sh.s <= 32) {

@@ -103,11 +103,13 @@ def test_big_constrained_model_matches_oracle():
     assert rel_err(np.concatenate(out), o.forward(x0)) < TOL
 
 
+@pytest.mark.parametrize("n,m", [(30, 6), (24, 16)])
 @pytest.mark.parametrize("keep", [True, False])
-def test_big_non_spd_sets_status_flag(keep):
+def test_big_non_spd_sets_status_flag(keep, n, m):
+    """(24, 16): k_riccati_bwd_fast<3> (keep) and the value-form k_riccati_bwd_vf3."""
     from pdplqr import BatchedLQRSolver
 
-    n, m, N, batch = 30, 6, 10, 3
+    N, batch = 10, 3
     E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 3)
     s = n + m
     H = H.copy()
