@@ -114,9 +114,12 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
         const int dim = kk < sh.N ? sh.s : sh.n;
         const bool col = stg && j < dim;
         const long long wo = (long long)b * sh.perh + (long long)kk * sh.s + (j < dim ? j : 0);
-        const int yo0 = a.y_off[kk], nc = stg ? a.y_off[kk + 1] - yo0 : 0;
+        // uniform row layout (a.uni): the offsets are arithmetic, so the trip's
+        // loads do not wait on an offset load first
+        const int yo0 = a.uni ? kk * a.uni : a.y_off[kk];
+        const int nc = !stg ? 0 : (a.uni ? (kk < sh.N ? a.uni : 0) : a.y_off[kk + 1] - yo0);
         const long long yo = (long long)b * sh.ny + yo0;
-        const double *Dk = a.D + (long long)b * sh.ndD + a.d_off[kk];
+        const double *Dk = a.D + (long long)b * sh.ndD + (a.uni ? (long long)kk * a.uni * sh.s : a.d_off[kk]);
         const double wtj = col ? a.wt[wo] : 0.0, wj = col ? a.w[wo] : 0.0;
         const double wn = al * wtj + bl * wj;
         double ag = 0.0, ad = 0.0, ay = 0.0;
@@ -447,6 +450,12 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     // and g (the KKT path takes rho through g in its backward, no penalty in h~)
     const bool kkt_lin = kkt && kkt_linear_supported(h);
     a.no_penalty = kkt ? 1 : 0;
+    {
+        const int c0 = sh.N > 0 ? h->ncs[0] : 0;
+        bool uni = c0 > 0 && h->ncs[sh.N] == 0 && !getenv("PDPLQR_ADMM_NO_UNI");
+        for (int k = 0; k < sh.N && uni; ++k) uni = h->ncs[k] == c0;
+        a.uni = uni ? c0 : 0;
+    }
     const dim3 ugrid((unsigned)B), ublk(256);
     const double *irho_or_null = Y > 0 ? s->irho : nullptr;
     int it = 1;

@@ -16,6 +16,7 @@ struct AdmmArgs {
     double alpha, sigma, eps_abs, eps_rel, rho_tol;
     int max_nc, it, adaptive;
     int no_penalty = 0;  // fused next-update h~ without the penalty term (KKT: rho enters through g)
+    int uni = 0;         // > 0: every stage k < N has exactly uni rows, the terminal none (offsets by arithmetic)
 };
 
 // Termination test of iteration a.it for problem b from the five maxima
