@@ -378,7 +378,7 @@ def bench_batched_c3(local, dev, dist, steps=10, warmup=3, N=256, batch=4096, n=
     bst = 8 * (n * (n + m) + n + (n + m) ** 2 + (n + m)) + 8 * (n + m)  # 3,936 B at 12/4
     wide = n + m > 32
     if (n, m) == (24, 16):  # the 3 x 3 register-tile backward and rollout (kernels_riccati.hip)
-        kern = ("k_riccati_bwd_vf3", "k_riccati_fwd<3")
+        kern = ("k_riccati_bwd_vf3", "k_rollout_dma3")
     else:
         kern = ("k_seg_bwd_wide", "k_riccati_fwd_big") if wide else ("k_riccati_bwd_schur", "k_rollout_dma")
     tag = f"C3_N{N}_b{batch}" if (n, m) == (12, 4) else f"W_n{n}_m{m}_N{N}_b{batch}"

@@ -451,7 +451,13 @@ __global__ __launch_bounds__(64, 1) void k_riccati_bwd_vf3(RiccatiArgs A) {
     constexpr int NC = n / 4;          // K chunks over the state index
     constexpr int TG = (n + 15) / 16;  // row tiles of G = P E
     static_assert(SH::ok && s > 32 && s <= 16 * T && n % 4 == 0 && m % 4 == 0 && m <= 16, "value-form T = 3 shape");
-    __shared__ BwdSmem<T> sm;  // pivot broadcast, 1/sqrt(pivot), lu', lp redistribution
+    // pivot broadcast, 1/sqrt(pivot), lu', lp redistribution: BwdSmem without
+    // its factor block (37.5 KB a block in all: 4 blocks, one per SIMD, per CU)
+    struct VfSmem {
+        alignas(16) double col[4 * 16 * T];
+        double inv[16 * T], luq[16 * T], lp[16 * T];
+    };
+    __shared__ VfSmem sm;
     __shared__ double Ps[n * PL];
     __shared__ double pvs[n];
     __shared__ __attribute__((aligned(16))) double stg[2][NI * 128];
@@ -1110,6 +1116,140 @@ __global__ __launch_bounds__(64) void k_seg_fwd_dma(Shape sh, const double *__re
     }
 }
 
+// ---------------------------------------------------------------------------
+// The serial rollout for 32 < s <= 48 (R = 3 row tiles) with the stage
+// records streamed through an LDS-DMA ring, as k_seg_fwd_dma does for the
+// segments: E_k, c_k and the rollout record land in slot k % D by
+// global_load_lds_dwordx4, D - 1 stages ahead.  The register-prefetch
+// k_riccati_fwd<3> keeps only one stage in flight at one wave per SIMD.
+// vm ops per iteration: NI DMA + 1 u store + RX x stores (RX = ceil(n / 16)
+// row tiles that hold state rows), so "stage k has landed" is a fixed vmcnt.
+// ---------------------------------------------------------------------------
+template <int NN, int MM>
+struct SerRec3 {
+    static constexpr int n = NN, m = MM, s = NN + MM, FRS = s * m + m;
+    static constexpr int OE = 0, OC = n * s, OF = OC + n, REC = OF + FRS;
+    static constexpr int CH = REC / 2, NI = (CH + 63) / 64, TAIL = CH - (NI - 1) * 64;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FRS % 2 == 0 && s > 32 && s <= 48 && m <= 16;
+};
+
+template <int NN, int MM, int D>
+__global__ __launch_bounds__(64) void k_rollout_dma3(Shape sh, const double *__restrict__ E,
+                                                     const double *__restrict__ c, const double *__restrict__ FR,
+                                                     const double *__restrict__ x0, double *__restrict__ ws) {
+    using SR = SerRec3<NN, MM>;
+    static_assert(SR::ok, "serial rollout record layout");
+    constexpr int R = 3, NJ = 4 * R, n = NN, m = MM, s = NN + MM, NI = SR::NI, RX = (NN + 15) / 16;
+    constexpr int VM = (1 + RX) + (D - 2) * (NI + 1 + RX) + NI;  // vm ops younger than stage k's DMA
+    static_assert(VM <= 63 && D >= 2, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) double ring[D][SR::REC];
+    __shared__ double sw[64];  // w_k = [u; x]
+    const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
+    const long long b = blockIdx.x;
+    const int N = sh.N;
+    const double *Eb = E + b * sh.perE;
+    const double *cb = c + b * sh.perc;
+    const double *Fb = FR + b * sh.perKD;
+    double *wb = ws + b * sh.perh;
+    if (lane < n) sw[m + lane] = x0[b * n + lane];
+    auto dma = [&](int k, int slot) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+            if (q < NI - 1 || lane < SR::TAIL) {
+                const int d = 2 * (q * 64 + lane);
+                const double *src = d < SR::OC   ? Eb + (long long)k * (n * s) + d
+                                    : d < SR::OF ? cb + (long long)k * n + (d - SR::OC)
+                                                 : Fb + (long long)k * SR::FRS + (d - SR::OF);
+                dma16(src, &ring[slot][q * 128]);
+            }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) dma(j < N ? j : N - 1, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    if (lane < n) wb[m + lane] = sw[m + lane];  // ws[0].tail(n) = x0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    for (int k = 0; k < N; ++k) {
+        const int kp = k + D - 1;
+        dma(kp < N ? kp : N - 1, kp % D);  // past the end: re-load into a consumed slot
+        if (k < D - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+        wave_sync();
+        const double *Rk = ring[k % D];
+        FwdIn<R, MM> cur;
+        fwd_load<R, MM>(cur, Rk + SR::OE, Rk + SR::OC, Rk + SR::OF, n, m, s, g, cl);
+        // v = lu' + Lxu^T x  (lqr_kernel.hpp:197)
+        double v = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < NJ; ++qq) {
+            const int t = 4 * qq + g;
+            const double xt = (t < n) ? sw[m + t] : 0.0;
+            v = __builtin_fma(cur.lxu[qq], xt, v);
+        }
+        v += shfl_xor_f64(v, 16);
+        v += shfl_xor_f64(v, 32);
+        v += cur.lu;
+        double ax[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            double a = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = 4 * jj + g;
+                if (j >= m && j < s) a = __builtin_fma(cur.E[q][jj], sw[j], a);
+            }
+            ax[q] = a;
+        }
+        // u = -Luu^{-T} v: back substitution, u_i broadcast from lane i
+        double rdg[MM];
+#pragma unroll
+        for (int i = 0; i < MM; ++i) rdg[i] = rcp_f64(cur.luu[i]);
+        double acc = 0.0, myu = 0.0;
+#pragma unroll
+        for (int i = MM - 1; i >= 0; --i) {
+            const double cand = -(v + acc) * rdg[i];  // valid on lane cl == i
+            const double ui = readlane_f64(cand, i);
+            if (cl == i) myu = ui;
+            acc = __builtin_fma(cur.luu[i], ui, acc);
+            if (lane == 0) sw[i] = ui;
+        }
+        wave_sync();
+        double xn[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            double a = ax[q];
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = 4 * jj + g;
+                if (j < m) a = __builtin_fma(cur.E[q][jj], sw[j], a);
+            }
+            a += shfl_xor_f64(a, 16);
+            a += shfl_xor_f64(a, 32);
+            xn[q] = a + cur.c[q];
+        }
+        wave_sync();
+        if (g == 0 && cl < m) gstore(wb + (long long)k * s + cl, myu);
+        if (g == 0) {
+#pragma unroll
+            for (int q = 0; q < RX; ++q) {
+                const int t = cl + 16 * q;
+                if (t < n) {
+                    sw[m + t] = xn[q];
+                    gstore(wb + (long long)(k + 1) * s + ((k + 1 < N) ? m : 0) + t, xn[q]);
+                }
+            }
+        }
+        wave_sync();
+    }
+}
+
+static bool ser3_aligned(const Shape &sh, const double *E, const double *c, const double *FR) {
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return al(E) && al(c) && al(FR) && sh.perE % 2 == 0 && sh.perc % 2 == 0 && sh.perKD % 2 == 0;
+}
+
 static bool segfwd_aligned(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf) {
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     return al(E) && al(c) && al(FR) && al(sf.G) && sh.perE % 2 == 0 && sh.perc % 2 == 0 && sh.perKD % 2 == 0 &&
@@ -1120,6 +1260,12 @@ template <bool SEG>
 static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                       double *ws, const SegFwd &sf, hipStream_t st) {
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
+    if (!SEG && sh.n == 24 && sh.m == 16 && ser3_aligned(sh, E, c, FR) && !getenv("PDPLQR_NO_T3") &&
+        !getenv("PDPLQR_NO_DMA")) {
+        hipLaunchKernelGGL((k_rollout_dma3<24, 16, 3>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
     if (!SEG && sh.s > 32 && sh.s <= 48 && sh.m <= 16 && !getenv("PDPLQR_NO_T3")) {
         // 32 < s <= 48: the register rollout on 3 row tiles (one wave per problem)
         hipLaunchKernelGGL((k_riccati_fwd<3, 16, false>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
