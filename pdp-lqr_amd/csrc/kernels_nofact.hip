@@ -78,8 +78,18 @@ __device__ __forceinline__ double nofact_q(const double *R, int oe, int oc, cons
     return sum_groups(qv) + ht;
 }
 
+// Ring depth 3 (8.9 KB of LDS): 16 blocks per CU, so batch 4096 is one
+// residency round; depth 4 (11.8 KB) fit 13 and left a second, mostly idle
+// round: backward_without_factorization 2.83 -> 2.64 ms at the headline
+// config (profiles/r03/nofact_depth_ab.log).
 #ifndef PDPLQR_NOFACT_DEPTH
-#define PDPLQR_NOFACT_DEPTH 4
+#define PDPLQR_NOFACT_DEPTH 3
+#endif
+// The fused ADMM pass (k_nofact_admm_dma, 15.6 KB at depth 4) runs C5's batch
+// of 1024 at 4 blocks per CU, where LDS does not bound the residency: it keeps
+// depth 4.
+#ifndef PDPLQR_NOFACT_ADMM_DEPTH
+#define PDPLQR_NOFACT_ADMM_DEPTH 4
 #endif
 
 template <int NN, int MM, int D>
@@ -391,10 +401,10 @@ int launch_nofact_admm(const RiccatiArgs &a, const AdmmArgs &q, bool check, hipS
         sh.perh % 2 || sh.perHw % 2 || sh.ndD % 2 || sh.ny % 2)
         return PDPLQR_ERR_UNSUPPORTED;
     if (check)
-        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st,
+        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st,
                            a, q);
     else
-        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_DEPTH, false>), dim3(sh.batch), dim3(64), 0,
+        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, false>), dim3(sh.batch), dim3(64), 0,
                            st, a, q);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
