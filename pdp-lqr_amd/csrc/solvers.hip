@@ -223,7 +223,9 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal);
 // combine kernels stage their operands before storing (n <= 32) and that do
 // not take the two-round k_seg_scan4 launches.
 static bool scan_sklansky(const Shape &sh) {
-    return !wide_state(sh.n) && (!seg_scan4_supported(sh.n) || getenv("PDPLQR_NO_SCAN4")) && !getenv("PDPLQR_SCAN_HS");
+    // (n <= 16 with PDPLQR_NO_SCAN4: radix-2 Hillis-Steele, the bit-exact
+    // reference of k_seg_scan4; PDPLQR_SCAN_SK=1 takes Sklansky there, A/B only)
+    return !wide_state(sh.n) && (!seg_scan4_supported(sh.n) || getenv("PDPLQR_SCAN_SK")) && !getenv("PDPLQR_SCAN_HS");
 }
 void graph_release(pdplqr_handle h);
 
