@@ -300,12 +300,12 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
 // latencies but one dispatch, operand fetch and write-back less.  Each
 // combine's right operand covers [first, min(first + span - 1, S - 1)]; when
 // that range holds the real terminal, F = C = f = 0 (see k_seg_scan).
-template <int T, bool LU>
+template <int T, bool LU, int NC = 0>
 __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
     __shared__ CombSmem<T> smv[2];
     extern __shared__ __attribute__((aligned(16))) double ebuf[];  // per wave: 2 operand images
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = A.n, S = A.S, d = A.dist;
+    const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n, ol = op_stage_len(n);
     const long long b = blockIdx.x / S;
     const int i = blockIdx.x % S;
@@ -808,6 +808,8 @@ static size_t mw_maps_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 3 * el
 #define PDPLQR_CT_N24 1
 #endif
 static inline bool ct_n24(int n) { return PDPLQR_CT_N24 && n == 24; }
+// n = 12 (the C2 / headline state size) likewise for the n <= 16 kernels
+static inline bool ct_n12(int n) { return PDPLQR_CT_N24 && n == 12; }
 
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
@@ -849,6 +851,7 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
     const size_t smem = 2 * op_stage_bytes(a.n);
     if (!seg_scan4_supported(a.n) || !a.scratch) return PDPLQR_ERR_UNSUPPORTED;
     if (a.lu) hipLaunchKernelGGL((k_seg_scan4<1, true>), grid, blk, smem, st, a);
+    else if (ct_n12(a.n)) hipLaunchKernelGGL((k_seg_scan4<1, false, 12>), grid, blk, smem, st, a);
     else hipLaunchKernelGGL((k_seg_scan4<1, false>), grid, blk, smem, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -894,6 +897,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     }
     const size_t smem = (a.right ? op_stage_bytes(a.n) : 0) + (size_t)(tmap_smem_doubles(a.n) + a.n * a.n + a.n) * sizeof(double);
     if (T == 1 && a.lu) hipLaunchKernelGGL((k_seg_maps<1, true>), grid, blk, smem, st, a);
+    else if (T == 1 && ct_n12(a.n)) hipLaunchKernelGGL((k_seg_maps<1, false, 12>), grid, blk, smem, st, a);
     else if (T == 1) hipLaunchKernelGGL((k_seg_maps<1, false>), grid, blk, smem, st, a);
     else if (T == 2 && a.lu) hipLaunchKernelGGL((k_seg_maps<2, true>), grid, blk, smem, st, a);
     else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_seg_maps<2, false, 24>), grid, blk, smem, st, a);
@@ -911,7 +915,8 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     if (PDPLQR_MAP_RADIX == 4) {
-        if (T == 1) hipLaunchKernelGGL(k_map_scan4<1>, grid, blk, 0, st, a);
+        if (T == 1 && ct_n12(a.n)) hipLaunchKernelGGL((k_map_scan4<1, 12>), grid, blk, 0, st, a);
+        else if (T == 1) hipLaunchKernelGGL(k_map_scan4<1>, grid, blk, 0, st, a);
         else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_map_scan4<2, 24>), grid, blk, 0, st, a);
         else if (T == 2) hipLaunchKernelGGL(k_map_scan4<2>, grid, blk, 0, st, a);
         else return PDPLQR_ERR_UNSUPPORTED;
