@@ -641,17 +641,20 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     sh.close()
     oerr = None
     if world == 1:  # the whole horizon is this rank's: check it against the serial oracle
-        from oracle.oracle import OracleSerial
-        from pdplqr.model import PackedModel
-
-        pm = PackedModel(n, m, Ntot, np.zeros(Ntot + 1, dtype=np.int32), E0[0].cpu().numpy(), c[0].cpu().numpy(),
-                         H0[0].cpu().numpy(), h[0].cpu().numpy(), np.zeros(0))
-        o = OracleSerial(pm)
-        o.update_problem_data(np.zeros(Ntot * s + n), None, None, None, 1e-6)
-        o.backward(None)
-        ref = o.forward(x0[0].cpu().numpy())
-        oerr = float(np.linalg.norm(out[0].cpu().numpy() - ref) / np.linalg.norm(ref))
-        del pm, o, ref
+        oerr = _horizon_oracle_err([(E0[0], c[0], H0[0], h[0])], [out[0].cpu().numpy()], x0[0], n, m, Ntot)
+    else:
+        # every rank's slice of the trajectory to rank 0, which regenerates the
+        # other ranks' model slices (same device generator and seeds) and checks
+        # the assembled horizon against the serial oracle
+        outs = [None] * world
+        dist.all_gather_object(outs, out[0].cpu().numpy())
+        if rank == 0:
+            parts = []
+            for r, (a0, a1) in enumerate(split_horizon(Ntot, world)):
+                Er, cr, Hr, hr, _ = gen_batch_device(n, m, a1 - a0, 1, seed=4242 + r, device=dev)
+                parts.append((Er[0], cr[0], Hr[0], hr[0]))
+                del Er, Hr
+            oerr = _horizon_oracle_err(parts, outs, x0[0], n, m, Ntot)
     del E0, H0
     bst = 8 * (n * s + n + s * s + s) + 8 * s  # 15,040 B per stage at 24/8
     # SURVEY 8(d) flop model: 103,235 per stage (backward + forward) + 59,968 for the segment element
@@ -662,6 +665,32 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
                                        ("k_seg_bwd_aug", "k_seg_scan", "k_seg_maps", "k_map_scan", "k_seg_fwd_dma"),
                                        flops_stage=103235 + 59968,
                                        kernel_desc="whole horizon solve (latency-bound: see DESIGN.md section 6)")}
+
+
+def _horizon_oracle_err(parts, outs, x0, n, m, Ntot):
+    """Relative error of a horizon-sharded trajectory against the serial oracle
+    over the whole horizon (test infrastructure, outside the timed region).
+    parts: per rank (E, c, H, h) of its slice (the last carries the terminal);
+    outs: per rank its w slice (stages, then the slice's end state)."""
+    from oracle.oracle import OracleSerial
+    from pdplqr.model import PackedModel
+
+    s = n + m
+    R = len(parts)
+    Ls = [p[1].numel() // n for p in parts]
+    E = np.concatenate([p[0].cpu().numpy()[:L * n * s] for p, L in zip(parts, Ls)])
+    c = np.concatenate([p[1].cpu().numpy() for p in parts])
+    H = np.concatenate([p[2].cpu().numpy()[:L * s * s] for p, L in zip(parts, Ls)] +
+                       [parts[-1][2].cpu().numpy()[Ls[-1] * s * s:]])
+    h = np.concatenate([p[3].cpu().numpy()[:L * s] for p, L in zip(parts, Ls)] +
+                       [parts[-1][3].cpu().numpy()[Ls[-1] * s:]])
+    w = np.concatenate([o[:L * s] for o, L in zip(outs, Ls)] + [outs[R - 1][Ls[-1] * s:]])
+    pm = PackedModel(n, m, Ntot, np.zeros(Ntot + 1, dtype=np.int32), E, c, H, h, np.zeros(0))
+    o = OracleSerial(pm)
+    o.update_problem_data(np.zeros(Ntot * s + n), None, None, None, 1e-6)
+    o.backward(None)
+    ref = o.forward(x0.cpu().numpy())
+    return float(np.linalg.norm(w - ref) / np.linalg.norm(ref))
 
 
 def headline_oracle_err(E, c, Hs, h, x0, out, n, m, N, probs):
@@ -734,6 +763,38 @@ def bwd_kernel_name(n, m, keep):
     return "k_riccati_bwd<1>" if s <= 16 else "k_riccati_bwd<2>"
 
 
+def _spawn_ranks(n):
+    """One child process per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in
+    its environment, rendezvous on 127.0.0.1), as torch.distributed.run would
+    start them; returns the first non-zero exit status.  A rank that fails ends
+    the others (they would wait in a collective): the exact PIDs started here."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r and not rc:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -748,9 +809,18 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 secondary lines")
     ap.add_argument("--c4-N", type=int, default=65536)
+    ap.add_argument("--secondary", default="all",
+                    help="comma list of secondary lines (C2,C3,wide,reuse,C5,C4) or 'all'")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here
+        # (this process has not touched the GPU: nothing before this line does)
+        sys.exit(_spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if BACKEND != "nccl":  # rehearsal: more ranks than GPUs share the devices
@@ -889,17 +959,21 @@ def main():
     del E, c, h, x0, ws0, out, Hk
     torch.cuda.empty_cache()
     if not args.no_secondary:
-        res["secondary"] = {"C2_single_N1024_parallel": bench_single(local, dev, dist),
-                            "C3_batched_N256": bench_batched_c3(local, dev, dist),
-                            "wide_24x16_N256_b1024": bench_batched_c3(local, dev, dist, steps=5, warmup=2, N=256,
-                                                                      batch=1024, n=24, m=16),
-                            "factor_reuse": bench_factor_reuse(local, dev, dist, N=N, batch=B),
-                            "C5_conic_kkt": bench_conic(local, dev, dist),
-                            "C4_horizon_sharded": bench_horizon(local, dev, dist, world, rank, args.c4_N)}
-    if rank == 0 and world == 1 and not args.no_cpu:
+        lines = [("C2", "C2_single_N1024_parallel", lambda: bench_single(local, dev, dist)),
+                 ("C3", "C3_batched_N256", lambda: bench_batched_c3(local, dev, dist)),
+                 ("wide", "wide_24x16_N256_b1024", lambda: bench_batched_c3(local, dev, dist, steps=5, warmup=2,
+                                                                             N=256, batch=1024, n=24, m=16)),
+                 ("reuse", "factor_reuse", lambda: bench_factor_reuse(local, dev, dist, N=N, batch=B)),
+                 ("C5", "C5_conic_kkt", lambda: bench_conic(local, dev, dist)),
+                 ("C4", "C4_horizon_sharded", lambda: bench_horizon(local, dev, dist, world, rank, args.c4_N))]
+        pick = None if args.secondary == "all" else set(args.secondary.split(","))
+        res["secondary"] = {key: fn() for tag, key, fn in lines if pick is None or tag in pick}
+    if rank == 0 and not args.no_cpu:
+        # rank 0 only, after every timed region (the other ranks are done)
         res["cpu_baseline"] = cpu_baseline(n, m, N, seconds=args.cpu_seconds)
     elif rank == 0:
         res["cpu_baseline"] = None
+    assert res["n_gpus"] == args.gpus
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:

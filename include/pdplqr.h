@@ -87,6 +87,21 @@ typedef struct {
     int32_t segment_len;     /* PARALLEL: device sub-segment length (0 = auto).  Every
                                 reference segment is refined into pieces of at most this
                                 many stages; results are identical up to rounding. */
+    int32_t num_devices;     /* PARALLEL: > 1 splits the horizon into num_devices
+                                contiguous slices, one per GPU, driven by this one
+                                handle (replaces the OpenMP team of
+                                LQRParallelSolver, lqr_solver_parallel.hpp:22-25,102-113):
+                                slice backward on every device, one RCCL all-gather of
+                                the slice elements (3 nx^2 + 2 nx doubles per problem),
+                                slice forward.  0 or 1: one device (`device`).  With
+                                num_devices > 1 backward_without_factorization, admm_solve,
+                                the shard_* calls and set_stream are unsupported, and
+                                `device` is ignored.  num_devices = 1 with a non-NULL
+                                `devices` runs the same split with one slice (RCCL
+                                communicator of one rank). */
+    const int32_t *devices;  /* num_devices HIP ordinals, or NULL = 0 .. num_devices - 1.
+                                A device may repeat (same-device rehearsal: the exchange
+                                then uses device copies, as with PDPLQR_MD_P2P=1). */
 } pdplqr_config;
 
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,
@@ -194,6 +209,14 @@ int pdplqr_shard_element_size(pdplqr_handle h);
 int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem);
 int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_all, int32_t num_shards,
                          int32_t shard_id, double *ws, int mem);
+
+/* The slicing of a num_devices = R split (pdplqr_config.num_devices), host
+ * arithmetic only (no device call): per slice r, 8 int64 at out[8 r]:
+ * N0, N1 (stages [N0, N1)), last (holds the real terminal), y0 / ny_stages (its
+ * stages' constraint rows in the full y vector), nc_terminal (its terminal's
+ * rows: nc_N for the last slice, 0 otherwise), d0 / nd_stages (its stages'
+ * entries in the full D array).  ncs: N+1 entries or NULL. */
+int pdplqr_multidev_plan(int32_t N, int32_t R, const int32_t *ncs, int32_t nx, int32_t nu, int64_t *out);
 
 /* ---------------------------------------------------------------------- */
 /* ADMM outer loop for conic LQ (new).  The         */

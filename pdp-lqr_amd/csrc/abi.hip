@@ -146,6 +146,21 @@ int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out) {
     sh.perHw = ((long long)sh.N * sh.ps + sh.pn + 1) / 2 * 2;  // 16-byte aligned per problem
     sh.perKD = (long long)sh.N * (sh.s * sh.m + sh.m);  // rollout record [L(:,0:m) | lu']
 
+    if (C.num_devices > 1 || (C.num_devices == 1 && C.devices)) {  // the horizon split over devices (multidev.hip)
+        if (C.num_devices > 1024) {
+            delete h;
+            return invalid("num_devices out of range");
+        }
+        h->cfg.devices = nullptr;
+        const int mrc = md_create(h, C);
+        if (mrc) {
+            md_release(h);
+            delete h;
+            return mrc;
+        }
+        *out = h;
+        return PDPLQR_OK;
+    }
     int rc = PDPLQR_OK;
     hipError_t e = hipSetDevice(C.device);
     if (e != hipSuccess) {
@@ -226,6 +241,11 @@ fail:
 
 int pdplqr_destroy(pdplqr_handle h) {
     if (!h) return PDPLQR_OK;
+    if (h->md) {
+        md_release(h);
+        delete h;
+        return PDPLQR_OK;
+    }
     (void)hipSetDevice(h->cfg.device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     solver_release(h);
@@ -236,14 +256,22 @@ int pdplqr_destroy(pdplqr_handle h) {
 
 int pdplqr_set_stream(pdplqr_handle h, void *stream) {
     if (!h) return invalid("null handle");
+    if (h->md) {
+        set_error("set_stream: a num_devices > 1 handle runs one stream per device");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
     h->stream = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
     return PDPLQR_OK;
 }
 
-void *pdplqr_get_stream(pdplqr_handle h) { return h ? reinterpret_cast<void *>(h->stream) : nullptr; }
+void *pdplqr_get_stream(pdplqr_handle h) {
+    if (h && h->md) return md_stream(h);  // the first slice's device stream
+    return h ? reinterpret_cast<void *>(h->stream) : nullptr;
+}
 
 int pdplqr_synchronize(pdplqr_handle h) {
     if (!h) return invalid("null handle");
+    if (h->md) return md_synchronize(h);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
     return PDPLQR_OK;
@@ -258,6 +286,7 @@ int pdplqr_set_model_arrays(pdplqr_handle h, int mask, const double *E, const do
         ((mask & PDPLQR_MODEL_HV) && !hv))
         return invalid("set_model: null E/c/H/h");
     if ((mask & PDPLQR_MODEL_D) && h->sh.ndD > 0 && !D) return invalid("set_model: constraints declared but D is null");
+    if (h->md) return md_set_model(h, mask, E, c, H, hv, D, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
     const long long B = sh.batch;
@@ -284,10 +313,15 @@ int pdplqr_set_model_arrays(pdplqr_handle h, int mask, const double *E, const do
     }
     const bool first = !h->model_set;
     h->model_set = true;
-    if (mask & (PDPLQR_MODEL_H | PDPLQR_MODEL_HV)) {
+    if ((mask & (PDPLQR_MODEL_H | PDPLQR_MODEL_HV)) && h->cfg.solver != PDPLQR_SOLVER_KKT) {
         h->hw_cached = false;  // H~ is re-formed from the new model
         h->updated = false;
     }
+    // KKT: the matrix (H + sigma_f I) is frozen at the first upload and the
+    // right-hand side was formed by update_problem_data (form_rhs,
+    // kkt.hpp:224-300), so a later H / h upload leaves the protocol state as
+    // it is: backward without a new update_problem_data stays valid, as in the
+    // reference's QDLDLSolver.
     // The factor cache survives a model upload: the reference re-reads model_
     // lazily and never invalidates its workspace factors (lqr_solver.hpp:25,65-70).
     return first || h->cfg.solver == PDPLQR_SOLVER_KKT ? solver_on_model(h) : PDPLQR_OK;
@@ -313,6 +347,7 @@ int pdplqr_update_problem_data(pdplqr_handle h, const double *ws, const double *
         set_error("update_problem_data before set_model");
         return PDPLQR_ERR_STATE;
     }
+    if (h->md) return md_update(h, ws, ys, zs, inv_rho, sigma, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
     const long long B = sh.batch;
@@ -341,6 +376,13 @@ static int backward_common(pdplqr_handle h, const double *rho, int mem, bool fac
     if (!fact && !h->factored) {
         set_error("backward_without_factorization needs a preceding backward");
         return PDPLQR_ERR_STATE;
+    }
+    if (h->md) {
+        if (!fact) {
+            set_error("backward_without_factorization: not supported with num_devices > 1");
+            return PDPLQR_ERR_UNSUPPORTED;
+        }
+        return md_backward(h, rho, mem);
     }
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     h->host_staged = false;
@@ -377,6 +419,7 @@ int pdplqr_forward(pdplqr_handle h, const double *x0, double *ws, int mem) {
         return PDPLQR_ERR_STATE;
     }
     if (!x0 || !ws) return invalid("forward: null x0/ws");
+    if (h->md) return md_forward(h, x0, ws, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
     const double *dx0;
@@ -396,6 +439,7 @@ int pdplqr_forward(pdplqr_handle h, const double *x0, double *ws, int mem) {
 
 int pdplqr_clear_workspace(pdplqr_handle h) {
     if (!h) return invalid("null handle");
+    if (h->md) return md_clear(h);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
     const long long B = sh.batch;
@@ -450,6 +494,7 @@ int pdplqr_get_value_function(pdplqr_handle h, int32_t b, int32_t k, double *P, 
 
 int pdplqr_get_status(pdplqr_handle h, int32_t *flags) {
     if (!h || !flags) return invalid("null argument");
+    if (h->md) return md_status(h, flags);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
     return solver_status(h, flags);

@@ -361,6 +361,10 @@ void pdplqr_admm_settings_init(pdplqr_admm_settings *s) {
 int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const double *x0, const double *lb,
                       const double *ub, const double *rho, double *ws, double *ys, double *zs, int mem) {
     if (!h || !st) return PDPLQR_ERR_INVALID;
+    if (h->md) {
+        set_error("admm_solve: not supported with num_devices > 1");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
     if (!h->model_set) {
         set_error("admm_solve before set_model");
         return PDPLQR_ERR_STATE;

@@ -52,6 +52,11 @@ struct RiccatiArgs {
     int32_t *status;       // per-problem factorization status
     const short2 *tab_s;   // packed-lower index tables (i, j)
     const short2 *tab_n;
+    // rho penalty fused into the streamed backward (launch_riccati_backward_pen):
+    // D, rho, g of a uniform nc rows per stage (k < N), nc_last at the terminal
+    const double *D = nullptr, *rho = nullptr, *gw = nullptr;
+    const int32_t *d_off = nullptr, *y_off = nullptr;
+    int nc_last = 0;
 };
 
 int launch_update_problem_data(const Shape &sh, const double *H, const double *hv, const double *ws,
@@ -63,6 +68,10 @@ int launch_penalty(const Shape &sh, const double *D, const double *rho, const do
                    const short2 *tab_n, int with_H, int max_nc, hipStream_t st);
 int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st);  // ERR_UNSUPPORTED: not applicable
+// the rho penalty (lqr_kernel.hpp:82-88,106-112) fused into the 12/4 value-form
+// backward, H~ / h~ penalised in place as the reference does; ERR_UNSUPPORTED
+// when the shape / row layout needs k_penalty + the plain backward
+int launch_riccati_backward_pen(const RiccatiArgs &a, int nc, hipStream_t st);
 bool schur_gain_record(const RiccatiArgs &a);  // the backward leaves the gain-form record [K~ | k~]
 int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                        double *ws, hipStream_t st, bool gain = false);  // ERR_UNSUPPORTED: not applicable
@@ -80,7 +89,19 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 namespace pdplqr { struct ParallelState;
 struct KKTState;
-struct AdmmState; }
+struct AdmmState;
+struct MultiDev;
+// one slice of a num_devices split (multidev.hip)
+struct MdSlice {
+    int N0 = 0, N1 = 0;          // stages [N0, N1)
+    bool last = false;           // holds the real terminal
+    long long y0 = 0, ny_st = 0; // constraint rows of the slice's stages in the full y vector
+    int nc_term = 0;             // rows of the slice's terminal (the last slice: nc_N)
+    long long d0 = 0, nd_st = 0; // D entries of the slice's stages in the full D array
+    std::vector<int32_t> ncs;    // the slice handle's ncs (N1 - N0 + 1)
+};
+void md_plan(int N, int R, const std::vector<int32_t> &ncs, int n, int m, std::vector<MdSlice> &out);
+}
 
 struct pdplqr_handle_s {
     pdplqr_config cfg;
@@ -120,6 +141,7 @@ struct pdplqr_handle_s {
     int admm_iters = 0;                    // iterations of the last admm_solve
     int admm_rho_updates = 0;              // adaptive-rho refactorizations of the last admm_solve
     int shard_last = 1;  // last shard_backward's is_last_shard
+    pdplqr::MultiDev *md = nullptr;  // num_devices > 1 (multidev.hip): the slices' handles
     // replayable launch sequences of backward / backward_without_factorization /
     // forward (solvers.hip: hipGraph captured on first use per argument set)
     struct Graph {

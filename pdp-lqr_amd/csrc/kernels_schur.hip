@@ -39,17 +39,20 @@ namespace pdplqr {
 // hits 32 distinct banks.  A 16-byte chunk (2 rows of one column, n even)
 // moves as a unit, so the copy stays one ds_write_b128 per chunk with a fixed
 // per-lane destination (LO* = LDS offsets).
-template <int NN, int MM>
+// NC > 0 (fused rho penalty): D (NC x s), rho (NC), g (NC) follow H~.
+template <int NN, int MM, int NC = 0>
 struct SchurShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
     static constexpr int ps = s * (s + 1) / 2;
-    static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, Q = OP + ps;
+    static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, OD = OP + ps, OR = OD + NC * s, OG = OR + NC,
+                         Q = OG + NC;
     static constexpr int CH = Q / 2, NI = (CH + 63) / 64;
     static constexpr int LDE = PDPLQR_LDS_PAD ? ((n / 2) % 2 == 1 ? n : n + 2) : n;
     static constexpr int LSH = (LDE - n) * s;  // shift of everything after E in the LDS copy
-    static constexpr int LOC = OC + LSH, LOH = OH + LSH, LOP = OP + LSH;
+    static constexpr int LOC = OC + LSH, LOH = OH + LSH, LOP = OP + LSH, LOD = OD + LSH, LOR = OR + LSH,
+                         LOG = OG + LSH;
     static constexpr int SLOT = NI * 128 + LSH;  // every lane's chunk of the last load lands inside
-    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && s % 2 == 0 && ps % 2 == 0 && s <= 16;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && s % 2 == 0 && ps % 2 == 0 && s <= 16 && NC % 2 == 0;
 };
 
 // Symmetrise P every PDPLQR_SYM_EVERY stages (1, 2 or 4) on the compile-time
@@ -67,15 +70,29 @@ using SymOff = std::integral_constant<bool, false>;
 #ifndef PDPLQR_SCHUR_WAVES
 #define PDPLQR_SCHUR_WAVES 4
 #endif
+// waves per SIMD of the fused-penalty instance (NC > 0): its fourth staging
+// chunk and the write-back addresses do not fit 128 VGPRs (at 4 waves the
+// compiler spilled inside the stage loop, and every scratch reload drains the
+// staging loads); C5 runs one wave per SIMD (batch 1024) anyway
+#ifndef PDPLQR_PEN_WAVES
+#define PDPLQR_PEN_WAVES 2
+#endif
 
 // NN = MM = 0: runtime shape, register prefetch of the next stage.
 // NN, MM > 0 : compile-time shape, stage records streamed by LDS-DMA
 //              (global_load_lds_dwordx4) into a double buffer.
-template <int NN, int MM, bool GAIN = false>
-__global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_riccati_bwd_schur(RiccatiArgs A) {
+// NC > 0: the rho penalty of every stage (lqr_kernel.hpp:82-88,106-112) fused
+// into the stream: the stage record carries D_k (NC rows), rho_k, g_k; the
+// penalised H~_k + D^T rho D and h~_k - D^T rho g feed the stage and are written
+// back in place (the reference's data.H += / data.h -= semantics, so a second
+// backward without update_problem_data penalises again, as there).
+template <int NN, int MM, bool GAIN = false, int NC = 0>
+__global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_SCHUR_WAVES) : 3)) void k_riccati_bwd_schur(
+    RiccatiArgs A) {
     static_assert(!GAIN || (NN == 12 && MM == 4 && PDPLQR_SCHUR_BLOCK), "gain-form record: 12/4 block path");
+    static_assert(NC == 0 || (GAIN && NC == 4), "fused penalty: 12/4 gain-form path, 4 rows per stage");
     constexpr bool CT = NN > 0;
-    using SH = SchurShape<(CT ? NN : 2), (CT ? MM : 2)>;
+    using SH = SchurShape<(CT ? NN : 2), (CT ? MM : 2), NC>;
     constexpr int NI = CT ? SH::NI : 1;
     __shared__ SchurSmem sm;
     __shared__ __attribute__((aligned(16))) double stg[CT ? 2 : 1][CT ? SH::SLOT : 2];
@@ -92,6 +109,9 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
     double *FRb = A.KD + b * sh.perKD;
     const int frs = GAIN ? n * m + m : s * m + m;  // doubles per stage of the record
     int fail_stage = -1;
+    const double *Db = NC > 0 ? A.D + b * (long long)sh.ndD : nullptr;
+    const double *rb = NC > 0 ? A.rho + b * (long long)sh.ny : nullptr;
+    const double *gb = NC > 0 ? A.gw + b * (long long)sh.ny : nullptr;
 
     // ---- terminal (lqr_kernel.hpp:80-91): P_N = H~_N, p_N = h~_N ----
     d4 Pm;
@@ -100,13 +120,40 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         d4 Mt[1][1];
         load_M<1>(Mt, Hb + (long long)N * ps, n, m, m, s, g, c);
         Pm = Mt[0][0];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * r + g;
+            prow[r] = (i >= m && i < s) ? hb[(long long)N * s + (i - m)] : 0.0;
+        }
+        if constexpr (NC > 0) {
+            const int ncN = A.nc_last;
+            if (ncN > 0) {  // rare: plain loops (D_N is ncN x n), written back in place as the stages
+                const double *DN = Db + A.d_off[N], *rN = rb + A.y_off[N], *gN = gb + A.y_off[N];
+                for (int q = 0; q < ncN; ++q) {
+                    const double rq = rN[q], gq = gN[q];
+                    const double dc = c >= m ? DN[q + (c - m) * ncN] : 0.0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 4 * r + g;
+                        const double di = i >= m ? DN[q + (i - m) * ncN] : 0.0;
+                        Pm[r] = __builtin_fma(di, rq * dc, Pm[r]);
+                        prow[r] = __builtin_fma(-di, rq * gq, prow[r]);
+                    }
+                }
+                double *HN = A.Hw + b * sh.perHw + (long long)N * ps;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 4 * r + g;
+                    if (i >= m && c >= m && i >= c) HN[pidx(i - m, c - m, n)] = Pm[r];
+                    if (c == 0 && i >= m) A.hw[b * sh.perh + (long long)N * s + (i - m)] = prow[r];
+                }
+            }
+        }
         bool bad = false;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 4 * r + g;
-            const bool xr = i >= m && i < s;
-            prow[r] = xr ? hb[(long long)N * s + (i - m)] : 0.0;
-            if (i == c && xr && psd_bad(Pm[r])) bad = true;  // P_N = H~_N semidefinite is valid
+            if (i == c && i >= m && i < s && psd_bad(Pm[r])) bad = true;  // P_N = H~_N semidefinite is valid
         }
         if (__any(bad)) fail_stage = N;
     }
@@ -132,8 +179,16 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             gbase[q] = d < SH::OC   ? Eb + d
                        : d < SH::OH ? cb + (d - SH::OC)
                        : d < SH::OP ? hb + (d - SH::OH)
-                                    : Hb + (d - SH::OP);
-            gstride[q] = d < SH::OC ? SH::n * SH::s : d < SH::OH ? SH::n : d < SH::OP ? SH::s : SH::ps;
+                       : d < SH::OD ? Hb + (d - SH::OP)
+                       : d < SH::OR ? Db + (d - SH::OD)
+                       : d < SH::OG ? rb + (d - SH::OR)
+                                    : gb + (d - SH::OG);
+            gstride[q] = d < SH::OC   ? SH::n * SH::s
+                         : d < SH::OH ? SH::n
+                         : d < SH::OP ? SH::s
+                         : d < SH::OD ? SH::ps
+                         : d < SH::OR ? NC * SH::s
+                                      : NC;
         }
         auto gload = [&](d2v(&R)[NI], int k) {
 #pragma unroll
@@ -148,19 +203,28 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
         // R's loads have landed once at most `after` younger vm ops are
         // outstanding.  One immediate per call site: a branchy wait made the
         // compiler copy R (still in flight) into other registers.
+        // store instructions per stage (all unconditional): the record (1, or 2
+        // with PDPLQR_REC_DIRECT's L form), plus with NC > 0 the in-place
+        // write-back of h~ (1) and of the packed H~ (4)
+        constexpr int ST = ((PDPLQR_REC_DIRECT && !GAIN) ? 2 : 1) + (NC > 0 ? 5 : 0);
+        static_assert(NI == 3 || NI == 4, "register staging");
         auto vwait5 = [&](d2v(&R)[NI]) {  // steady state
-            static_assert(NI == 3, "register staging");
-            if (PDPLQR_REC_DIRECT && !GAIN)
-                asm volatile("s_waitcnt vmcnt(7)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
-            else asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if constexpr (NI == 3)
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]) : "n"(NI + 2 * ST) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) : "n"(NI + 2 * ST)
+                             : "memory");
         };
         auto vwait4 = [&](d2v(&R)[NI]) {  // first step
-            if (PDPLQR_REC_DIRECT && !GAIN)
-                asm volatile("s_waitcnt vmcnt(5)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
-            else asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if constexpr (NI == 3)
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]) : "n"(NI + ST) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) : "n"(NI + ST)
+                             : "memory");
         };
         auto vwait0 = [&](d2v(&R)[NI]) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            if constexpr (NI == 3) asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2])::"memory");
+            else asm volatile("s_waitcnt vmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3])::"memory");
         };
         auto lput = [&](const d2v(&R)[NI], int slot) {
 #pragma unroll
@@ -192,6 +256,23 @@ __global__ __launch_bounds__(64, (NN > 0 ? PDPLQR_SCHUR_WAVES : 3)) void k_ricca
             const double *R = stg[k & 1];
             SchurIn in;
             schur_load(in, R + SH::OE, R + SH::LOC, R + SH::LOP, R + SH::LOH, n, m, s, g, c, SH::LDE);
+            if constexpr (NC > 0) {
+                // H~ += D^T diag(rho) D as (a^T)(sgn a) with a = sqrt|rho| D (lane (g, c): row g,
+                // column c): entry (i, j) and (j, i) multiply the same two factors in the same
+                // order, so the penalised tile stays bitwise symmetric and the duplicate
+                // write-back stores below (each entry from both of its lanes) carry equal bits
+                const double dgc = R[SH::LOD + g + c * NC], rq = R[SH::LOR + g], gq = R[SH::LOG + g];
+                const double a = sqrt(fabs(rq)) * dgc;
+                in.H = mfma_f64(a, rq < 0.0 ? -a : a, in.H);
+                in.h -= sum_groups(dgc * (rq * gq));  // h~ -= D^T (rho o g)
+                double *Hk = A.Hw + b * sh.perHw + (long long)k * SH::ps;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 4 * r + g;
+                    gstore(Hk + (i >= c ? pidx(i, c, SH::s) : pidx(c, i, SH::s)), in.H[r]);
+                }
+                gstore(A.hw + b * sh.perh + (long long)k * SH::s + c, in.h);
+            }
             double w, luq[4];
             GainOut go;
             const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN>(
@@ -279,6 +360,20 @@ static bool schur_ct(const RiccatiArgs &a) {  // the compile-time 12/4 kernel ap
 // PDPLQR_REC_L: keep the [L(:, 0:m) | lu'] record (A/B).
 bool schur_gain_record(const RiccatiArgs &a) {
     return PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4 && schur_ct(a) && !getenv("PDPLQR_REC_L");
+}
+
+// The fused-penalty backward applies: the 12/4 gain-form kernel, nc = 4 rows on
+// every stage k < N (the C5 layout), nc_N <= 4, 16-byte aligned per-problem
+// blocks of D, rho and g.
+int launch_riccati_backward_pen(const RiccatiArgs &a, int nc, hipStream_t st) {
+    const Shape &sh = a.sh;
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (nc != 4 || a.nc_last > 4 || !schur_gain_record(a) || getenv("PDPLQR_NO_PEN_FUSE") || !a.D || !a.rho ||
+        !a.gw || !al(a.D) || !al(a.rho) || !al(a.gw) || sh.ny % 2 || sh.ndD % 2)
+        return PDPLQR_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, true, 4>), dim3(sh.batch), dim3(64), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
 }
 
 // Returns PDPLQR_ERR_UNSUPPORTED when the shape / options need the full-factor kernels.

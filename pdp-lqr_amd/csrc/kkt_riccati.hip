@@ -24,20 +24,22 @@
 //       lambda_{k+1} = P~ v + p~);
 //   * (u_k, x_k): the value-form stage of kernels_schur.hip on
 //       M_k = H~_k + E~^T P~ E~ (+ D^T rho D),  lp = h~ + E^T (P~ c + p~).
-// P~ is formed by the Neumann series P~ = sum_j (-rho_dyn P)^j P, one MFMA
-// product per term (A operand = P's own registers, B = the previous term), with
-// as many terms as the trace bound e = rho_dyn tr(P) >= rho_dyn ||P|| asks:
-// terms until e^{J+1} <= 1e-16 (rho_dyn = 1e-6 and ||P|| ~ 10..100: 2 or 3).
+// P~ is formed by the Neumann series P~ = sum_j (-rho_dyn P)^j P (one MFMA
+// product per term) while e = rho_dyn ||P||_F is small enough for eight terms
+// to reach rounding (e <= 0.015: rho_dyn = 1e-6 and ||P|| up to 1.5e4), and
+// EXACTLY otherwise: Gauss-Jordan inversion of the SPD S = I + rho_dyn P and
+// P~ = P S^{-1} (ptilde_exact; the wide kernel: Cholesky of S and two
+// triangular solves).  A non-SPD S is flagged in the status, as a bad pivot.
 // p~ never appears alone: lp = h~ + G^T (c - rho_dyn p) + E~^T p with
 // G = P~ E~, and the forward uses x+ = v - rho_dyn (P~ (v - rho_dyn p) + p).
 //
 // Per stage this reads E, c, h~, packed H~ = H + sigma_f I, D, inv_rho, g
 // (428 doubles at 12/4 with 4 rows) once and writes the rollout record
-// [K~ | k~ | p_{k+1} | P~_{k+1} (fp32)] -- against the natural-order path's
-// once-per-model H^{-1} / G tiles and its three solve phases over explicit
-// fp64 tiles (kkt.hip).  P~ is stored in fp32: it only enters
-// rho_dyn P~ v, a 1e-6-relative correction of the state, so its 6e-8 rounding
-// is ~1e-13 of x.
+// [K~ | k~ | p_{k+1} | P~_{k+1} (fp64, packed lower)] -- against the
+// natural-order path's once-per-model H^{-1} / G tiles and its three solve
+// phases over explicit fp64 tiles (kkt.hip).  P~ stays fp64: rho_dyn P~ has
+// norm rho_dyn lambda / (1 + rho_dyn lambda), up to 1 when rho_dyn ||P|| is large,
+// so a rounded P~ would move x by its own relative rounding.
 //
 // update_rhs_initial_stage ACCUMULATES -S0 x0 and -A0 x0 into the right-hand
 // side on every forward (kkt.hpp:207-222): the solve then uses the sum of every
@@ -66,14 +68,17 @@ struct KKTRicArgs {
     int nc_last;              // constraint rows of the terminal stage
 };
 
-// record per stage: K~ (m x n row-major) | k~ (m) | p_{k+1} (n) | P~_{k+1} fp32
-// (float3 per lane (g, c >= m): P~[4 + g][c], P~[8 + g][c], P~[12 + g][c])
+// record per stage: K~ (m x n row-major) | k~ (m) | p_{k+1} (n) | P~_{k+1}
+// (fp64; packed lower, pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full
+// matrix row-major: three unmasked stores a lane, no index arithmetic)
+#ifndef PDPLQR_KKT_PT_FULL
+#define PDPLQR_KKT_PT_FULL 0
+#endif
 template <int NN, int MM>
 struct KRecShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
     static constexpr int OK = 0, OKQ = n * m, OPV = OKQ + m, OPT = OPV + n;
-    static constexpr int PTF = 3 * 4 * n;             // floats of P~ (48 lanes x 3)
-    static constexpr int FS = OPT + (PTF + 1) / 2;    // doubles per stage
+    static constexpr int FS = OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);  // doubles per stage
 };
 
 // Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
@@ -99,6 +104,82 @@ struct KBwdShape {
 
 // sum of a value over the whole wave (every lane gets it)
 __device__ __forceinline__ double wave_sum(double v) { return sum_groups(sum_row16(v)); }
+
+// Bound below which the Neumann series P~ = sum_{j<8} (-rho_dyn P)^j P is used:
+// with e = rho_dyn ||P||_F (>= the spectral radius of rho_dyn P for ANY
+// symmetric P) the truncation after J terms is <= e^(J+1) / (1 - e) of ||P~||,
+// so at e <= 0.015 eight terms leave < 4e-17.  Above it P~ is formed exactly.
+#ifndef PDPLQR_KKT_NEUMANN_MAX
+#define PDPLQR_KKT_NEUMANN_MAX 0.015
+#endif
+
+// Exact P~ = (I + rho_dyn P)^{-1} P of the x block (tile indices 4..15) of a
+// 16 x 16 C/D-layout tile: in-place Gauss-Jordan inversion of S = I + rho_dyn P
+// (12 pivots, no pivoting: S is SPD with eigenvalues >= 1 whenever P is PSD,
+// so every pivot is >= 1), then one product P S^{-1}.  Rows / columns < 4 of the
+// result are not meaningful (the callers read the x block only).  False if a
+// pivot is not positive (P not PSD enough for S to be SPD).
+// (inlined: a call inside the stage loop would save / restore registers whose
+// staging loads are still in flight, the hazard tests/test_kernel_static.py guards)
+__device__ __forceinline__ bool ptilde_exact(const d4 &P, double rd, int g, int c, d4 &Pt) {
+    d4 S;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 4 * r + g;
+        S[r] = (i >= 4 && c >= 4) ? rd * P[r] : 0.0;
+        if (i == c) S[r] += 1.0;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 4; j < 16; ++j) {
+        const int rj = j >> 2, gj = j & 3;
+        double colj[4];  // S[4 r + g][j] of the lane's rows (u rows: 0)
+        colj[0] = 0.0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) colj[r] = __shfl(S[r], 16 * g + j, 64);
+        const double rowj = __shfl(S[rj], 16 * gj + c, 64);  // S[j][c]
+        const double piv = readlane_f64(S[rj], 16 * gj + j);
+        ok = ok && piv > 0.0;
+        const double ip = rcp_f64(piv);
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+            const int i = 4 * r + g;
+            const double a = colj[r] * ip;
+            S[r] = (i == j) ? ((c == j) ? ip : rowj * ip) : ((c == j) ? -a : __builtin_fma(-a, rowj, S[r]));
+        }
+    }
+    d4 Y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 1; kk < 4; ++kk) Y = mfma_f64(P[kk], S[kk], Y);  // P^T S^{-1} = P S^{-1}
+    Pt = Y;
+    return ok;
+}
+
+// P~ of the x block for the 12/4 kernels: the Neumann series while it has
+// converged to rounding (e <= PDPLQR_KKT_NEUMANN_MAX, wave-uniform), the exact
+// inversion above otherwise.  False: S = I + rho_dyn P was not SPD.
+__device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c, d4 &Pt) {
+    double f = 0.0;
+#pragma unroll
+    for (int r = 1; r < 4; ++r) f = (c >= 4) ? __builtin_fma(Pm[r], Pm[r], f) : f;
+    const double e = rd * sqrt(wave_sum(f));
+    if (__builtin_amdgcn_readfirstlane((int)(e > PDPLQR_KKT_NEUMANN_MAX))) return ptilde_exact(Pm, rd, g, c, Pt);
+    Pt = Pm;
+    d4 T = Pm, Pneg;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
+    double ej = e;
+    for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // wave-uniform
+        d4 Tn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 1; kk < 4; ++kk) Tn = mfma_f64(Pneg[kk], T[kk], Tn);  // (-rho_dyn P) T (x rows)
+        T = Tn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Pt[r] += T[r];
+        ej *= e;
+    }
+    return true;
+}
 
 template <int NC>
 __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
@@ -215,30 +296,9 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         double *Rk = RB + (long long)k * RS::FS;
         SchurIn in;
         schur_load(in, R + SH::OE, R + SH::OC, R + SH::OP, R + SH::OH, n, m, s, g, c, n);
-        // ---- the lambda_{k+1} elimination: P~ = sum_j (-rho_dyn P)^j P ----
-        const double diag = [&] {
-            double d = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) d = (4 * r + g == c && c >= m) ? Pm[r] : d;
-            return wave_sum(d);
-        }();
-        const double e = rd * fabs(diag);
-        d4 Pt = Pm, T = Pm;
-        {
-            d4 Pneg;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
-            double ej = e;
-            for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // wave-uniform
-                d4 Tn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int kk = 1; kk < 4; ++kk) Tn = mfma_f64(Pneg[kk], T[kk], Tn);  // (-rho_dyn P) T (x rows)
-                T = Tn;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Pt[r] += T[r];
-                ej *= e;
-            }
-        }
+        // ---- the lambda_{k+1} elimination: P~ = (I + rho_dyn P)^{-1} P ----
+        d4 Pt;
+        const bool pt_ok = ptilde_12(Pm, rd, g, c, Pt);
         // ---- record part 1: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]) and P~_{k+1} ----
         {
             // every lane stores (duplicates carry the same value): one store
@@ -248,11 +308,15 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             const double pv = __builtin_fma(prow[1], (double)(cp == 1), __builtin_fma(prow[2], (double)(cp == 2),
                                                                                        prow[3] * (double)(cp == 3)));
             gstore(Rk + RS::OPV + (4 * cp + g - m), pv);
-            // P~ (fp32): lanes c >= m only -- lanes c < m hold u-column values
+            // P~ (fp64, packed lower of the x block): lane (g, c >= m) holds
+            // x rows g, 4 + g, 8 + g of x column c - m
             if (c >= m) {
-                float *dst = reinterpret_cast<float *>(Rk + RS::OPT) + 3 * (12 * g + (c - m));
-                typedef float f3v __attribute__((ext_vector_type(3)));
-                *(__attribute__((address_space(1))) f3v *)dst = f3v{(float)Pt[1], (float)Pt[2], (float)Pt[3]};
+#pragma unroll
+                for (int r = 1; r < 4; ++r) {
+                    const int i = 4 * (r - 1) + g, j = c - m;
+                    if (PDPLQR_KKT_PT_FULL) gstore(Rk + RS::OPT + i * n + j, Pt[r]);
+                    else if (i >= j) gstore(Rk + RS::OPT + pidx(i, j, n), Pt[r]);
+                }
             }
         }
         // ---- G = P~ E~, M = H~ + E~^T G + D^T rho D ----
@@ -320,7 +384,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             const int i = 4 * r + g;
             if (i == c && i >= m && psd_bad(Pm[r])) bad = true;
         }
-        ok = (int)ok & (int)!__any(bad);
+        ok = (int)ok & (int)!__any(bad) & (int)pt_ok;
         fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
         schur_store_record_gain<MM, s>(Rk, go, g, c);  // [K~ | k~]
         if (Ck) {
@@ -541,7 +605,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
     constexpr int OE = 0, OC = n * s, OF = OC + n, REC = OF + FS, CH = REC / 2, NI = (CH + 63) / 64;
     constexpr int TAIL = CH - (NI - 1) * 64;
     constexpr int NQ = 3;
-    static_assert(REC % 2 == 0 && NI == 3, "record layout");
+    static_assert(REC % 2 == 0 && (NI == 3 || NI == 4), "record layout");
     __shared__ __attribute__((aligned(16))) double ring[D][REC];
     __shared__ double sx[16], sz[16], sx0[16];
     const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
@@ -589,16 +653,13 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         const int cm = cl < m ? cl : m - 1, cn = cl < n ? cl : n - 1;
         const double g0 = (g == 0) ? 1.0 : 0.0;
         double kx[NQ], ex[NQ], eu[m], xt[NQ];
-        float pt[NQ];
-        {
-            const float *P3 = reinterpret_cast<const float *>(F + RS::OPT) + 3 * (12 * g + cn);
+        double pt[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int t = 4 * q + g;
-                kx[q] = F[RS::OK + cm * n + t];
-                ex[q] = R[OE + (m + t) * n + cn];
-                pt[q] = P3[q];  // P~[4 q + g][cl] (= P~[cl][4 q + g])
-            }
+        for (int q = 0; q < NQ; ++q) {
+            const int t = 4 * q + g;
+            kx[q] = F[RS::OK + cm * n + t];
+            ex[q] = R[OE + (m + t) * n + cn];
+            pt[q] = F[RS::OPT + (PDPLQR_KKT_PT_FULL ? t * n + cn : t >= cn ? pidx(t, cn, n) : pidx(cn, t, n))];  // P~[4 q + g][cl]
         }
 #pragma unroll
         for (int i = 0; i < m; ++i) eu[i] = g0 * R[OE + i * n + cn];
@@ -631,7 +692,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         wave_sync();
         double y = 0.0;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) y = __builtin_fma((double)pt[q], sz[4 * q + g], y);
+        for (int q = 0; q < NQ; ++q) y = __builtin_fma(pt[q], sz[4 * q + g], y);
         y = sum_groups(y);
         const double xn = __builtin_fma(-rho_dyn, y + pv, a);
         wave_sync();  // all reads of x_k done before it is overwritten
@@ -646,12 +707,12 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
 // Wide shapes (n + m <= 64, any per-stage constraint counts): the same
 // elimination on one 256-thread block per problem with the matrices in LDS
 // (blk_la.hpp).  Per stage k (value function (P, p) of stage k + 1):
-//     P~ = sum_j (-rho_dyn P)^j P   (the same trace-bounded Neumann series),
+//     P~ = (I + rho_dyn P)^{-1} P   (Neumann series / exact, as the 12/4 kernel),
 //     G = P~ E~,  M = H~ + E~^T G + D^T rho D,
 //     lp = h~ + G^T (c - rho_dyn p) + E~^T p - D^T rho g   (stage 0: D's u columns),
 // then the m u-pivots of M (L-form record, as the serial solver's FR_k) leave
 // P_k, p_k.  Record per stage: [L(:, 0:m) | lu' | p_{k+1} | P~_{k+1}] (fp64).
-// LDS: XA (n x s: P, then G), XB (n x s: the Neumann term), Mb (s x s: E~,
+// LDS: XA (n x s: P, then G), XB (n x s: the Neumann term or chol(S)), Mb (s x s: E~,
 // then M), Pt (n x n: P~), vectors.
 // ---------------------------------------------------------------------------
 namespace {
@@ -665,6 +726,7 @@ static size_t kw_smem_bytes(int n, int s) { return (size_t)(2 * n * s + s * s + 
 __global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
     extern __shared__ __attribute__((aligned(16))) double wbuf[];
     __shared__ int s_bad;
+    __shared__ double s_red[4];
     const int tid = threadIdx.x;
     const long long b = blockIdx.x;
     const Shape &sh = A.sh;
@@ -713,17 +775,43 @@ __global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
         double *Rk = RB + (long long)k * FS;
         const int nck = A.y_off[k + 1] - A.y_off[k];
         const double *Dk = Db ? Db + A.d_off[k] : nullptr;
-        // ---- P~ = sum_j (-rho_dyn P)^j P, terms while (rho_dyn |tr P|)^(j+1) > 1e-16 ----
-        double tr = 0.0;
-        for (int i = 0; i < n; ++i) tr += XA[i + i * n];  // every thread (LDS broadcast)
-        const double e = rd * fabs(tr);
-        blk_copy(Pt, n, mv_n(XA, n), n, n);
-        blk_copy(XB, n, mv_n(XA, n), n, n);
-        double ej = e;
-        for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // block-uniform
-            blk_mm(XB, n, mv_n(XA, n), mv_n(XB, n), n, n, n, -rd, 0.0, mv_none(), false);
-            for (int q = tid; q < n * n; q += BLK_THREADS) Pt[q] += XB[q];
-            ej *= e;
+        // ---- P~ = (I + rho_dyn P)^{-1} P: the Neumann series while e = rho_dyn ||P||_F
+        // <= PDPLQR_KKT_NEUMANN_MAX (terms while e^(j+1) > 1e-16), exact otherwise ----
+        double f = 0.0;
+        for (int q = tid; q < n * n; q += BLK_THREADS) f = __builtin_fma(XA[q], XA[q], f);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o, 64);
+        if ((tid & 63) == 0) s_red[tid >> 6] = f;
+        __syncthreads();
+        const double e = rd * sqrt((s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));  // block-uniform
+        bool pt_ok = true;
+        if (e > PDPLQR_KKT_NEUMANN_MAX) {
+            // S = I + rho_dyn P (XB), Cholesky carrying P (Pt): Pt = L^{-1} P, then L^T X = Pt
+            for (int q = tid; q < n * n; q += BLK_THREADS) {
+                const int i = q % n, j = q / n;
+                Pt[q] = XA[q];
+                XB[q] = __builtin_fma(rd, XA[q], i == j ? 1.0 : 0.0);
+            }
+            pt_ok = blk_chol(XB, n, n, n, t1, Pt, n, n);
+            blk_trsm_lt(XB, n, n, Pt, n, n, nullptr);
+            for (int q = tid; q < n * n; q += BLK_THREADS) {  // symmetrise (pairs i > j)
+                const int i = q % n, j = q / n;
+                if (i > j) {
+                    const double v = 0.5 * (Pt[i + j * n] + Pt[j + i * n]);
+                    Pt[i + j * n] = v;
+                    Pt[j + i * n] = v;
+                }
+            }
+            __syncthreads();
+        } else {
+            blk_copy(Pt, n, mv_n(XA, n), n, n);
+            blk_copy(XB, n, mv_n(XA, n), n, n);
+            double ej = e;
+            for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // block-uniform
+                blk_mm(XB, n, mv_n(XA, n), mv_n(XB, n), n, n, n, -rd, 0.0, mv_none(), false);
+                for (int q = tid; q < n * n; q += BLK_THREADS) Pt[q] += XB[q];
+                ej *= e;
+            }
         }
         // ---- record: p_{k+1}, P~_{k+1}; stage inputs ----
         for (int q = tid; q < n; q += BLK_THREADS) Rk[s * m + m + q] = pv[q];
@@ -790,7 +878,7 @@ __global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
         }
         for (int q = tid; q < n; q += BLK_THREADS) pv[q] = lp[m + q];
         __syncthreads();
-        if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
+        if ((!ok || !pt_ok || s_bad) && fail_stage < 0) fail_stage = k;
     }
     if (tid == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
 }

@@ -448,6 +448,16 @@ static int run_graphed(pdplqr_handle h, int slot, const void *k1, const void *k2
     return PDPLQR_OK;
 }
 
+// the constraint row count shared by every stage k < N, or 0
+static int uniform_nc(pdplqr_handle h) {
+    const int N = h->sh.N;
+    if (N < 1) return 0;
+    const int nc = h->ncs[0];
+    for (int k = 1; k < N; ++k)
+        if (h->ncs[k] != nc) return 0;
+    return nc;
+}
+
 int solver_backward(pdplqr_handle h, const double *rho) {
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) h->shard_last = 1;
     // the record form is host state: set outside the (replayable) launch sequence
@@ -457,6 +467,21 @@ int solver_backward(pdplqr_handle h, const double *rho) {
     // layout the forward does not read)
     return run_graphed(h, 0, rho, reinterpret_cast<const void *>((intptr_t)(h->rec_gain ? 2 : 1)), [&]() -> int {
         if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_backward(h, rho);  // rho = inv_rho (qdldl_solver.hpp:88)
+        if (h->cfg.solver == PDPLQR_SOLVER_SERIAL && h->max_nc > 0) {
+            // the penalty inside the streamed backward (one pass, H~ / h~ penalised in place)
+            const int nc = uniform_nc(h);
+            if (nc > 0 && h->rec_gain) {
+                RiccatiArgs a = riccati_args(h);
+                a.D = h->D;
+                a.rho = rho;
+                a.gw = h->gw;
+                a.d_off = h->d_off;
+                a.y_off = h->y_off;
+                a.nc_last = h->ncs[h->sh.N];
+                const int rc = launch_riccati_backward_pen(a, nc, h->stream);
+                if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
+            }
+        }
         int rc = launch_penalty(h->sh, h->D, rho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
                                 h->max_nc, h->stream);
         if (rc) return rc;
@@ -547,6 +572,18 @@ extern "C" {
 
 int pdplqr_get_segments(pdplqr_handle h, int32_t *idx_start, int32_t *Nseg) {
     if (!h || !idx_start || !Nseg) return PDPLQR_ERR_INVALID;
+    if (h->md) {  // the reference segmentation of the whole horizon (host arithmetic)
+        std::vector<int32_t> st, len;
+        if (!ref_segmentation(h->sh.N, h->cfg.num_segments, h->cfg.load_balancing != 0, st, len)) {
+            set_error("segmentation yields an empty segment");
+            return PDPLQR_ERR_INVALID;
+        }
+        for (size_t i = 0; i < st.size(); ++i) {
+            idx_start[i] = st[i];
+            Nseg[i] = len[i];
+        }
+        return PDPLQR_OK;
+    }
     if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL || !h->par) {
         set_error("get_segments needs a PARALLEL handle");
         return PDPLQR_ERR_INVALID;

@@ -55,4 +55,17 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
                           const double *cache, double *rec, hipStream_t st);
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
                            double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric);
+// num_devices > 1 (multidev.hip): the horizon split over the devices of one process
+int md_create(pdplqr_handle h, const pdplqr_config &C);
+void md_release(pdplqr_handle h);
+int md_set_model(pdplqr_handle h, int mask, const double *E, const double *c, const double *H, const double *hv,
+                 const double *D, int mem);
+int md_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho, double sigma,
+              int mem);
+int md_backward(pdplqr_handle h, const double *rho, int mem);
+int md_forward(pdplqr_handle h, const double *x0, double *ws, int mem);
+int md_status(pdplqr_handle h, int32_t *flags);
+int md_synchronize(pdplqr_handle h);
+int md_clear(pdplqr_handle h);
+void *md_stream(pdplqr_handle h);
 }  // namespace pdplqr

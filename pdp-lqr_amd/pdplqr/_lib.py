@@ -31,7 +31,7 @@ EXPORTS = [
     "pdplqr_backward", "pdplqr_backward_without_factorization", "pdplqr_forward", "pdplqr_clear_workspace",
     "pdplqr_get_value_function", "pdplqr_get_status", "pdplqr_get_segments", "pdplqr_shard_element_size",
     "pdplqr_shard_backward", "pdplqr_shard_forward", "pdplqr_device_count",
-    "pdplqr_admm_settings_init", "pdplqr_admm_solve", "pdplqr_admm_info",
+    "pdplqr_admm_settings_init", "pdplqr_admm_solve", "pdplqr_admm_info", "pdplqr_multidev_plan",
 ]
 
 
@@ -47,7 +47,7 @@ class Config(C.Structure):
         ("solver", C.c_int32), ("num_segments", C.c_int32), ("load_balancing", C.c_int32),
         ("condensed_type", C.c_int32), ("device", C.c_int32), ("keep_factors", C.c_int32),
         ("ncs", C.POINTER(C.c_int32)), ("rho_dyn", C.c_double), ("kkt_sigma", C.c_double),
-        ("segment_len", C.c_int32),
+        ("segment_len", C.c_int32), ("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)),
     ]
 
 
@@ -108,6 +108,7 @@ def lib() -> C.CDLL:
     L.pdplqr_admm_settings_init.restype = None
     L.pdplqr_admm_solve.argtypes = [vp, C.POINTER(AdmmSettings), dp, dp, dp, dp, dp, dp, dp, C.c_int]
     L.pdplqr_admm_info.argtypes = [vp, ip, ip, dp, dp, dp]
+    L.pdplqr_multidev_plan.argtypes = [i32, i32, ip, i32, i32, C.POINTER(C.c_int64)]
     for nm in EXPORTS:
         f = getattr(L, nm)
         if nm not in ("pdplqr_config_init", "pdplqr_last_error", "pdplqr_get_stream", "pdplqr_admm_settings_init"):

@@ -70,7 +70,7 @@ class _Handle:
 
     def __init__(self, nx, nu, N, batch=1, solver=_lib.PDPLQR_SOLVER_SERIAL, num_segments=1, load_balancing=True,
                  condensed_type=_lib.PDPLQR_CONDENSED_CHOLESKY, device=0, keep_factors=True, ncs=None,
-                 rho_dyn=1e-6, kkt_sigma=1e-6, segment_len=0):
+                 rho_dyn=1e-6, kkt_sigma=1e-6, segment_len=0, devices=None):
         L = lib()
         cfg = Config()
         L.pdplqr_config_init(C.byref(cfg))
@@ -84,6 +84,13 @@ class _Handle:
         cfg.rho_dyn = float(rho_dyn)
         cfg.kkt_sigma = float(kkt_sigma)
         cfg.segment_len = int(segment_len)
+        self._devs = None
+        if devices is not None and len(devices) > 0:
+            # the horizon split over the listed GPUs by this one handle
+            # (multidev.hip; one entry: the same split with one slice)
+            self._devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
+            cfg.num_devices = int(self._devs.size)
+            cfg.devices = self._devs.ctypes.data_as(C.POINTER(C.c_int32))
         self._ncs = None
         if ncs is not None:
             self._ncs = np.ascontiguousarray(np.asarray(ncs, dtype=np.int32))
@@ -347,10 +354,15 @@ class LQRParallelSolver(_ModelSolver):
 
     def __init__(self, model: LQRModel, num_segments: int, load_balancing: bool = True,
                  solver_type: CondensedSystemSolverType = CondensedSystemSolverType.CHOLESKY, device: int = 0,
-                 segment_len: int = 0):
+                 segment_len: int = 0, devices=None):
+        """``devices``: a list of HIP ordinals; more than one splits the horizon
+        across them (one slice per device, one RCCL all-gather of the slice
+        elements per backward; include/pdplqr.h num_devices) -- the multi-GPU
+        form of the reference's OpenMP team (lqr_solver_parallel.hpp:102-113)."""
         self.num_segments = int(num_segments)
         self._init_handle(model, device=device, keep_factors=True, num_segments=num_segments,
-                          load_balancing=load_balancing, condensed_type=int(solver_type), segment_len=segment_len)
+                          load_balancing=load_balancing, condensed_type=int(solver_type), segment_len=segment_len,
+                          devices=devices)
 
     def backward_without_factorization(self, rho_vecs):
         self._hd.backward_without_factorization(self._y(rho_vecs))
@@ -383,13 +395,15 @@ class BatchedLQRSolver:
 
     def __init__(self, n: int, m: int, N: int, batch: int, solver: str = "serial", num_segments: int = 1,
                  load_balancing: bool = True, condensed: str = "CHOLESKY", keep_factors: bool = False,
-                 ncs=None, device: int = 0, segment_len: int = 0):
+                 ncs=None, device: int = 0, segment_len: int = 0, rho_dyn: float = 1e-6, kkt_sigma: float = 1e-6,
+                 devices=None):
         kind = {"serial": _lib.PDPLQR_SOLVER_SERIAL, "parallel": _lib.PDPLQR_SOLVER_PARALLEL,
                 "kkt": _lib.PDPLQR_SOLVER_KKT}[solver]
         self.n, self.m, self.N, self.batch = n, m, N, batch
         self._hd = _Handle(n, m, N, batch, kind, num_segments=num_segments, load_balancing=load_balancing,
                            condensed_type=int(CondensedSystemSolverType[condensed]), device=device,
-                           keep_factors=keep_factors, ncs=ncs, segment_len=segment_len)
+                           keep_factors=keep_factors, ncs=ncs, segment_len=segment_len, rho_dyn=rho_dyn,
+                           kkt_sigma=kkt_sigma, devices=devices)
 
     @property
     def handle(self) -> _Handle:

@@ -15,29 +15,52 @@ def regs(op):
     m = re.match(r"v(\d+)$", op)
     return {int(m.group(1))} if m else set()
 
+# register-staged kernels per source file (kernel name patterns)
+KERNELS = {"kernels_schur.hip": r"k_riccati_bwd_schurILi12ELi4E", "kkt_riccati.hip": r"k_kkt_ric_bwdILi"}
+
+
 def main(src, asm="/tmp/_schur_check.s"):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Iinclude",
-                           "--cuda-device-only", "-S", src, "-o", asm], stderr=subprocess.DEVNULL)
+                           "-mllvm", "-amdgpu-mfma-vgpr-form", "--cuda-device-only", "-S", src, "-o", asm],
+                          stderr=subprocess.DEVNULL)
     text = open(asm).read().split("\n")
-    # every compile-time 12/4 instantiation (L-form and gain-form record)
-    starts = [i for i, l in enumerate(text) if re.match(r"_Z\w*k_riccati_bwd_schurILi12ELi4E\w*:", l)]
+    pat = KERNELS.get(src.split("/")[-1], KERNELS["kernels_schur.hip"])
+    # every compile-time instantiation (L-form and gain-form record, fused penalty; KKT row counts)
+    starts = [i for i, l in enumerate(text) if re.match(r"_Z\w*" + pat + r"\w*:", l)]
     if not starts:
-        print("no k_riccati_bwd_schur<12, 4> instantiation found")
+        print("no register-staged kernel instantiation found")
         return 1
     rc = 0
     for st in starts:
         end = next(i for i in range(st, len(text)) if text[i].startswith(".Lfunc_end"))
         print(text[st].rstrip(":"))
-        rc |= check(text[st:end])
+        body = text[st:end]
+        calls = [l.strip() for l in body if l.strip().startswith("s_swappc") or l.strip().startswith("s_setpc")]
+        spill = [l for l in stage_loop(body) if l.startswith("scratch_")]
+        if calls or spill:  # a call or a spill in the stage loop may move registers with loads in flight
+            print("HAZARD: calls / stage-loop scratch traffic in a register-staged kernel:", (calls + spill)[:4])
+            rc = 1
+        rc |= check(body)
     return rc
 
 
+def stage_loop(lines):
+    """The loop that carries the staging loads (other loops of the kernel, e.g.
+    the terminal's penalty rows, are skipped): its instructions."""
+    for hdr in (i for i, l in enumerate(lines) if "Loop Header" in l):
+        lab = lines[hdr].split(":")[0]
+        backs = [i for i, l in enumerate(lines) if re.search(r"s_(c)?branch\w*\s+" + re.escape(lab) + r"\b", l)]
+        if not backs:
+            continue
+        body = lines[hdr:max(backs) + 1]
+        ins = [l.strip() for l in body if l.strip() and not l.strip().startswith((";", "."))]
+        if any(l.startswith("global_load_dwordx4") for l in ins):
+            return ins
+    raise SystemExit("no stage loop with staging loads found")
+
+
 def check(lines):
-    hdr = next(i for i, l in enumerate(lines) if "Inner Loop Header" in l)
-    lab = lines[hdr].split(":")[0]
-    back = max(i for i, l in enumerate(lines) if re.search(r"s_branch\s+" + re.escape(lab) + r"\b", l))
-    body = lines[hdr:back + 1]
-    ins = [l.strip() for l in body if l.strip() and not l.strip().startswith((";", "."))]
+    ins = stage_loop(lines)
     # in-flight sets: destinations of global_load_dwordx4 in the body
     loads = [(i, regs(l.split()[1].rstrip(","))) for i, l in enumerate(ins) if l.startswith("global_load_dwordx4")]
     bad = []

@@ -43,3 +43,35 @@ def test_bench_json_line():
     assert d["cpu_baseline"] is None  # --no-cpu
     # value = stages per second over the timed steps
     assert abs(d["value"] - 128 * 256 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
+
+
+def test_world_size_mismatch_fails_before_gpu():
+    """--gpus N under a launcher that started a different number of ranks is an
+    error (exit 2), decided before any GPU call (runs on CPU)."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], capture_output=True,
+                         text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode == 2 and "WORLD_SIZE=2" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [2])
+def test_bench_spawns_ranks(gpus):
+    """`bench.py --gpus N` without a launcher starts N ranks itself (gloo
+    rehearsal on one GPU): the line says n_gpus = N, value counts every rank's
+    batch, the C4 horizon is split over the N ranks and checked against the
+    serial oracle across ranks, and the CPU baseline is on the line."""
+    env = dict(os.environ, PDPLQR_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--N", "128", "--batch",
+                          "256", "--steps", "2", "--warmup", "1", "--cpu-seconds", "1", "--secondary", "C4",
+                          "--c4-N", "2048"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == gpus and d["status_ok"] is True
+    assert abs(d["value"] - gpus * 128 * 256 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
+    c4 = d["secondary"]["C4_horizon_sharded"]
+    assert c4["n_gpus"] == gpus and c4["oracle_rel_err"] < 1e-9
+    assert d["cpu_baseline"] is not None and d["cpu_baseline"]["value"] > 0

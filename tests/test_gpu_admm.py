@@ -369,3 +369,63 @@ def test_adaptive_rho_no_active_row_keeps_rho():
         assert oi["rho_updates"] == 0
         assert np.all(info["rho"][b] == 0.1), info["rho"][b]
         assert rel_err(w[b], ow) < 1e-9
+
+
+def _xbox_models(B, N=32, xb=0.1, ub_=0.5, seed0=900):
+    """12/4, four rows per stage: a box on u_0, u_1 and on the states x_0, x_1
+    (stage 0's state rows unbounded: x_0 is fixed); terminal rows box x_0..x_3.
+    Active state rows at a large rho put ~rho straight into P, which drives
+    rho_dyn ||P|| of the KKT path's lambda elimination out of the Neumann range."""
+    n, m = 12, 4
+    models, x0s = [], []
+    for b in range(B):
+        mod, x0 = random_model(n, m, N, seed=seed0 + b, nc=4, D_kind="ubox")
+        for k, nd in enumerate(mod.nodes):
+            nd.D_con[:] = 0.0
+            if k < N:
+                nd.D_con[0, 0] = nd.D_con[1, 1] = 1.0
+                nd.D_con[2, m] = nd.D_con[3, m + 1] = 1.0
+                nd.e_lb[:2], nd.e_ub[:2] = -ub_, ub_
+                xr = 1e6 if k == 0 else xb
+                nd.e_lb[2:], nd.e_ub[2:] = -xr, xr
+            else:
+                for r in range(4):
+                    nd.D_con[r, r] = 1.0
+                nd.e_lb[:], nd.e_ub[:] = -xb, xb
+        models.append(mod)
+        x0s.append(x0)
+    return models, x0s
+
+
+def test_kkt_state_box_large_rho_fixed_iterations():
+    """ADMM-KKT with active state boxes at rho = 3e5 (rho_dyn ||P|| ~ 0.4: the
+    exact Moreau envelope on every stage), fixed iterations, iterates vs the
+    oracle's QDLDL at 1e-8."""
+    models, x0s = _xbox_models(3)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s, seed=4)
+    rho = np.full(lb.shape, 3e5)
+    st = dict(max_iter=60, eps_abs=0.0, eps_rel=0.0, adaptive_rho=False)
+    w, y, z, info = _run_gpu("kkt", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, False, **st)
+    for b in range(len(pms)):
+        ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="kkt", **st)
+        assert rel_err(w[b], ow) < TOL_KKT and rel_err(y[b], oy) < TOL_KKT and rel_err(z[b], oz) < TOL_KKT, b
+
+
+def test_kkt_state_box_adaptive_rho_reaches_large_rho():
+    """Adaptive rho from 1e4 on state-boxed problems: problem 0 rescales up to
+    rho ~ 3e5 before it converges (oracle: 6 rescales, 1000 iterations).  Same
+    iteration counts, convergence and final rho as the oracle, iterates at 1e-8."""
+    models, x0s = _xbox_models(2)
+    pms, ncs, A, lb, ub, x0, ws, ys, zs = _batch(models, x0s, warm=False)
+    rho = np.full(lb.shape, 1e4)
+    st = dict(max_iter=3000, check_every=5, eps_abs=1e-6, eps_rel=1e-6)
+    w, y, z, info = _run_gpu("kkt", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, **st)
+    reached = 0.0
+    for b in range(len(pms)):
+        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], solver="kkt", **st)
+        assert oi["converged"] and bool(info["converged"][b])
+        assert info["iters"][b] == oi["iters"], (b, info["iters"][b], oi["iters"])
+        assert rel_err(info["rho"][b], oi["rho"]) < 1e-5, b
+        assert rel_err(w[b], ow) < TOL_KKT and rel_err(y[b], oy) < TOL_KKT, b
+        reached = max(reached, float(np.max(oi["rho"])))
+    assert reached >= 1e5, reached

@@ -294,3 +294,97 @@ def test_register_tile_stage_equals_generic():
             os.environ.pop("PDPLQR_KKT_STAGE_GENERIC", None)
     d = np.linalg.norm(outs["tiles"] - outs["generic"], axis=1) / np.linalg.norm(outs["generic"], axis=1)
     assert float(d.max()) < 1e-12, float(d.max())
+
+
+@pytest.mark.parametrize("name", ["e0.05_state_cost", "e0.5_state_box", "e3_rho_dyn", "wide_e0.5", "wide_e3"])
+def test_kkt_exact_moreau_envelope(name):
+    """P~ = (I + rho_dyn P)^{-1} P past the Neumann range:
+    rho_dyn ||P||_F of 0.05 (large state cost), 0.5 (state-box rows at
+    rho = 3e5) and 3 (rho = 1e5 with rho_dyn = 2e-5), on the 12/4 register
+    kernel and the wide LDS kernel (28/8).  QDLDL factors any quasi-definite
+    KKT (qdldl_solver.hpp:88-109), so the bar is the same 1e-8 against the
+    oracle's QDLDL and against the dense QDLDL-equivalent solve."""
+    from dense_ref import qdldl_equivalent
+    from kkt_cases import TARGET, e_max, kkt_case, packed
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch, rd, E, c, H, h, x0, ncs, D, ws, ys, zs, irho = kkt_case(name)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs, rho_dyn=rd)
+    bs.set_model(E, c, H, h, D)
+    bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+    bs.backward(irho)
+    out = np.zeros((batch, N * (n + m) + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = packed(n, m, N, ncs, E, c, H, h, D, b)
+        e = e_max(pm, ws[b], ys[b], zs[b], irho[b], 1e-6, rd)
+        assert TARGET[name] / 2 < e < 2 * TARGET[name], e
+        o = OracleKKT(pm, rho_dyn=rd)
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        o.backward(irho[b])
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+        wd = qdldl_equivalent(pm, x0[b], ws[b], ys[b], zs[b], irho[b], 1e-6, rho_dyn=rd)
+        assert rel_err(out[b], wd) < TOL, b
+        assert rel_err(u_parts(out[b], n, m, N), u_parts(wd, n, m, N)) < 1e-6
+
+
+def test_kkt_moreau_envelope_across_threshold():
+    """The same problems on either side of the Neumann / exact switch
+    (e = 0.015): a sweep of rho_dyn from 1e-6 to 1e-3 on one model, each solve
+    against the oracle at 1e-8 -- no seam at the switch."""
+    from kkt_cases import kkt_case, packed
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch, _, E, c, H, h, x0, ncs, D, ws, ys, zs, irho = kkt_case("e0.5_state_box")
+    irho = np.where(irho < 1e-3, 1e-2, irho)  # box rows at rho = 100: ||P|| ~ 1e2..1e3
+    for rd in (1e-6, 1e-5, 3e-5, 1e-4, 3e-4, 1e-3):
+        bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs, rho_dyn=rd)
+        bs.set_model(E, c, H, h, D)
+        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+        bs.backward(irho)
+        out = np.zeros((batch, N * (n + m) + n))
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0)
+        for b in range(batch):
+            o = OracleKKT(packed(n, m, N, ncs, E, c, H, h, D, b), rho_dyn=rd)
+            o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+            o.backward(irho[b])
+            assert rel_err(out[b], o.forward(x0[b])) < TOL, (rd, b)
+
+
+def test_kkt_h_upload_keeps_protocol_state():
+    """QDLDLSolver freezes its matrix at construction (qdldl_solver.hpp:36-45)
+    and forms the right-hand side in update_problem_data: a later H upload
+    (the facade's forward syncs H for update_rhs_initial_stage) must not
+    invalidate the protocol -- backward without a new update_problem_data is
+    valid, and the frozen matrix gives the same answer as an untouched solver."""
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch, nc = 12, 4, 20, 2, 4
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 77)
+    g = np.random.default_rng(78)
+    ncs = np.full(N + 1, nc, dtype=np.int32)
+    D = np.concatenate([g.standard_normal((batch, nc * dk)) for dk in [n + m] * N + [n]], axis=1)
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * (n + m) + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    outs = []
+    for touch in (False, True):
+        bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+        bs.set_model(E, c, H, h, D)
+        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+        bs.backward(irho)
+        out = np.zeros((batch, N * (n + m) + n))
+        bs.forward(x0, out)
+        if touch:
+            bs.set_model(E, c, 2.0 * H, h, D)
+        bs.backward(irho)
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0)
+        outs.append(out)
+    assert rel_err(outs[1], outs[0]) < 1e-13

@@ -1,0 +1,169 @@
+"""GPU parity of the num_devices split (pdp-lqr_amd/csrc/multidev.hip): one
+LQRParallelSolver / BatchedLQRSolver handle over a list of devices, the
+horizon cut into one slice per device, one all-gather of the slice elements
+per backward.  On a one-GPU box:
+
+* devices = [0]: the split with one slice, the exchange through a one-rank
+  RCCL communicator (ncclCommInitAll / ncclAllGather, dlopen'ed librccl);
+* devices = [0, 0, ...]: R slices on the same GPU, the exchange by device
+  copies (RCCL needs distinct devices) -- the slicing, the row / D offsets,
+  the per-slice terminals, the rank fold and the assembly of ws are the ones an
+  R-GPU run takes.
+
+Every answer is checked against the serial oracle (1e-9 relative, as
+tests/test_gpu_parallel.py).  Distinct GPUs with RCCL are not reachable here
+(unmeasured until an 8-GPU node runs it)."""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0, "no HIP device visible"
+
+
+def _lists(pm, d):
+    from pdplqr.model import unpack_model, unpack_ws
+
+    model = unpack_model(pm)
+    N = pm.N
+    off = np.concatenate([[0], np.cumsum(pm.ncs)])
+    sl = lambda v: [v[off[k]:off[k + 1]] for k in range(N + 1)]
+    return model, unpack_ws(d["ws"], pm.n, pm.m, N), sl(d["ys"]), sl(d["zs"]), sl(d["rho"]), sl(d["inv_rho"])
+
+
+def _oracle_serial(pm, d):
+    from oracle.oracle import OracleSerial
+
+    o = OracleSerial(pm)
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    return o.forward(d["x0"])
+
+
+@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("devices,condensed", [([0], "CHOLESKY"), ([0, 0], "CHOLESKY"), ([0, 0, 0], "LU"),
+                                               ([0, 0, 0, 0, 0], "CHOLESKY")])
+def test_multidev_solver_matches_oracle(name, devices, condensed):
+    from pdplqr import CondensedSystemSolverType, LQRParallelSolver
+
+    pm, d = load_golden(name)
+    if len(devices) > pm.N:
+        pytest.skip("more slices than stages")
+    model, ws, ys, zs, rho, irho = _lists(pm, d)
+    sol = LQRParallelSolver(model, 4, True, CondensedSystemSolverType[condensed], devices=devices)
+    sol.update_problem_data(ws, ys, zs, irho, float(d["sigma"]))
+    sol.backward(rho)
+    out = [w.copy() for w in ws]
+    sol.forward(d["x0"], out)
+    assert sol.status() == 0
+    assert rel_err(np.concatenate(out), _oracle_serial(pm, d)) < TOL
+
+
+@pytest.mark.parametrize("R", [1, 3, 8])
+def test_multidev_batched_constraints_device_buffers(R):
+    """batch 3, 12/4, per-stage constraint counts 0..4 (the row / D offsets of
+    every slice differ), torch device buffers and host buffers give the same
+    bits, every problem against the serial oracle; twice in a row (the handle
+    re-solves after a new update_problem_data)."""
+    import torch
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 61, 3
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 515)
+    g = np.random.default_rng(516)
+    ncs = g.integers(0, 5, size=N + 1).astype(np.int32)
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
+    ny = int(ncs.sum())
+    outs = []
+    for mode in ("host", "device"):
+        bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, ncs=ncs, devices=[0] * R)
+        cv = (lambda a: a) if mode == "host" else (lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda())
+        bs.set_model(cv(E), cv(c), cv(H), cv(h), cv(D))
+        res = []
+        for it in range(2):
+            ws = g.standard_normal((batch, N * s + n)) if mode == "host" or it else None
+            if mode == "host":
+                ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+                rho = 0.1 + g.random((batch, ny))
+                outs.append((ws, ys, zs, rho))
+            else:
+                ws, ys, zs, rho = outs[it]
+            irho = 1.0 / rho
+            bs.update_problem_data(cv(ws), cv(ys), cv(zs), cv(irho), sigma=1e-6)
+            bs.backward(cv(rho))
+            out = np.zeros((batch, N * s + n)) if mode == "host" else torch.zeros(batch, N * s + n,
+                                                                                   dtype=torch.float64).cuda()
+            bs.forward(cv(x0), out)
+            bs.synchronize()
+            assert np.all(bs.status() == 0)
+            res.append(out if mode == "host" else out.cpu().numpy())
+        bs.close()
+        if mode == "host":
+            host_res = res
+        else:
+            for a, b in zip(host_res, res):
+                assert np.array_equal(a, b)
+    for it, (ws, ys, zs, rho) in enumerate(outs):
+        for b in range(batch):
+            o = OracleSerial(PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b]))
+            o.update_problem_data(ws[b], ys[b], zs[b], 1.0 / rho[b], 1e-6)
+            o.backward(rho[b])
+            assert rel_err(host_res[it][b], o.forward(x0[b])) < TOL, (it, b)
+
+
+def test_multidev_c4_shape():
+    """24/8 over 8 slices of a 4096-stage horizon (C4's shape, 1/16 of its
+    length): the 8-device layout of config C4 against the serial oracle."""
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N = 24, 8, 4096
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, 1, 4242)
+    bs = BatchedLQRSolver(n, m, N, 1, solver="parallel", num_segments=8, devices=[0] * 8)
+    bs.set_model(E, c, H, h)
+    ws = np.zeros((1, N * s + n))
+    bs.update_problem_data(ws, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    o = OracleSerial(PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[0], c[0], H[0], h[0], np.zeros(0)))
+    o.update_problem_data(ws[0], None, None, None, 1e-6)
+    o.backward(None)
+    assert rel_err(out[0], o.forward(x0[0])) < TOL
+
+
+def test_multidev_unsupported_calls():
+    from pdplqr import BatchedLQRSolver, PdplqrError
+
+    n, m, N = 4, 2, 20
+    bs = BatchedLQRSolver(n, m, N, 1, solver="parallel", num_segments=2, devices=[0, 0])
+    with pytest.raises(PdplqrError):
+        bs.handle.set_stream(0)
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, 1, 1)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(np.zeros((1, N * (n + m) + n)), sigma=1e-6)
+    bs.backward()
+    with pytest.raises(PdplqrError):
+        bs.backward_without_factorization()
+    with pytest.raises(PdplqrError):  # the split needs the PARALLEL solver
+        BatchedLQRSolver(n, m, N, 1, solver="serial", devices=[0, 0])

@@ -532,3 +532,57 @@ def test_nofact_streamed_kernel_batched(N, batch):
         o.update_problem_data(ws2[b], None, None, None, 0.5)
         o.backward_without_factorization(None)
         assert rel_err(outs["dma"][b], o.forward(x0[b])) < TOL, b
+
+
+@pytest.mark.parametrize("N,ncN,backwards", [(64, 0, 1), (64, 4, 1), (37, 4, 2), (1, 0, 1), (2, 4, 2), (3, 0, 2),
+                                             (8, 2, 1)])
+def test_fused_penalty_backward(N, ncN, backwards):
+    """12/4 with four rows on every stage (C5's layout), keep_factors = 0: the
+    rho penalty runs inside the streamed value-form backward
+    (k_riccati_bwd_schur<12, 4, true, 4>) instead of the k_penalty pass.  Same
+    answer as the separate pass (PDPLQR_NO_PEN_FUSE) and as the oracle; a second
+    backward without update_problem_data penalises H~, h~ again in place, as
+    the reference's data.H += / data.h -= (lqr_kernel.hpp:106-112)."""
+    import os
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, nc, batch = 12, 4, 4, 3
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 91 + N)
+    g = np.random.default_rng(92 + N)
+    ncs = np.array([nc] * N + [ncN], dtype=np.int32)
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
+    ny = int(ncs.sum())
+    ws = g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    rho = 0.1 + g.random((batch, ny))
+    irho = 1.0 / rho
+    outs = {}
+    for mode in ("fused", "separate"):
+        if mode == "separate":
+            os.environ["PDPLQR_NO_PEN_FUSE"] = "1"
+        try:
+            bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=False, ncs=ncs)
+            bs.set_model(E, c, H, h, D)
+            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+            for _ in range(backwards):
+                bs.backward(rho)
+            out = np.zeros((batch, N * s + n))
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            outs[mode] = out
+            bs.close()
+        finally:
+            os.environ.pop("PDPLQR_NO_PEN_FUSE", None)
+    assert rel_err(outs["fused"], outs["separate"]) < 1e-11
+    for b in range(batch):
+        o = OracleSerial(PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b]))
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        for _ in range(backwards):
+            o.backward(rho[b])
+        assert rel_err(outs["fused"][b], o.forward(x0[b])) < TOL, b

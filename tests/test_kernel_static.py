@@ -15,9 +15,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="hipcc not installed")
-def test_schur_staging_has_no_inflight_hazard(tmp_path):
+@pytest.mark.parametrize("src", ["kernels_schur.hip", "kkt_riccati.hip"])
+def test_schur_staging_has_no_inflight_hazard(tmp_path, src):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "asm_inflight_check.py"),
-                        os.path.join(ROOT, "pdp-lqr_amd", "csrc", "kernels_schur.hip"), str(tmp_path / "k.s")],
+                        os.path.join(ROOT, "pdp-lqr_amd", "csrc", src), str(tmp_path / "k.s")],
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 hazards" in r.stdout
