@@ -35,24 +35,25 @@ inline void append(std::vector<double> &dst, const Dense &a) {
 struct PackedModel {
     std::vector<double> E, c, H, h, D;
 
-    void pack(const LQRModel &model) {
+    // packs the arrays in `mask` (PDPLQR_MODEL_*) only; the others keep their contents
+    void pack(const LQRModel &model, int mask = PDPLQR_MODEL_ALL) {
         const int N = model.N;
         if (static_cast<int>(model.nodes.size()) != N + 1)
             throw std::runtime_error("LQRModel: expected N + 1 nodes, got " + std::to_string(model.nodes.size()));
-        E.clear();
-        c.clear();
-        H.clear();
-        h.clear();
-        D.clear();
+        if (mask & PDPLQR_MODEL_E) E.clear();
+        if (mask & PDPLQR_MODEL_C) c.clear();
+        if (mask & PDPLQR_MODEL_H) H.clear();
+        if (mask & PDPLQR_MODEL_HV) h.clear();
+        if (mask & PDPLQR_MODEL_D) D.clear();
         for (int k = 0; k <= N; ++k) {
             const Node &nd = model.nodes[static_cast<size_t>(k)];
             if (k < N) {
-                append(E, nd.E);
-                append(c, nd.c);
+                if (mask & PDPLQR_MODEL_E) append(E, nd.E);
+                if (mask & PDPLQR_MODEL_C) append(c, nd.c);
             }
-            append(H, nd.H);
-            append(h, nd.h);
-            if (nd.n_con > 0) append(D, nd.D_con);
+            if (mask & PDPLQR_MODEL_H) append(H, nd.H);
+            if (mask & PDPLQR_MODEL_HV) append(h, nd.h);
+            if ((mask & PDPLQR_MODEL_D) && nd.n_con > 0) append(D, nd.D_con);
         }
     }
 };
@@ -78,7 +79,7 @@ inline void unflatten_ws(const std::vector<double> &flat, std::vector<VectorXs> 
 class Handle {
 public:
     Handle(const LQRModel &model, int solver, int num_segments = 1, bool load_balancing = true, int condensed = 1,
-           bool keep_factors = true) {
+           bool keep_factors = true, const std::vector<int> &devices = {}) {
         pdplqr_config cfg;
         pdplqr_config_init(&cfg);
         cfg.nx = model.n;
@@ -91,6 +92,11 @@ public:
         cfg.keep_factors = keep_factors ? 1 : 0;
         ncs_.assign(model.ncs.begin(), model.ncs.end());
         cfg.ncs = ncs_.data();
+        devs_.assign(devices.begin(), devices.end());
+        if (!devs_.empty()) {  // the horizon split over these GPUs (pdplqr_config.num_devices)
+            cfg.num_devices = static_cast<int32_t>(devs_.size());
+            cfg.devices = devs_.data();
+        }
         check(pdplqr_create(&cfg, &h_), "pdplqr_create");
         n_ = model.n;
         m_ = model.m;
@@ -104,9 +110,11 @@ public:
     // what the device holds: the reference reads its model lazily (H, h at
     // update_problem_data, E, c, D_con at backward / forward), so each facade
     // call syncs exactly what that call reads.  An unchanged model costs a host
-    // packing pass and a compare, no host -> device copy.
+    // packing pass and a compare of the arrays in `mask` only, no host ->
+    // device copy.
     void sync(const LQRModel &model, int mask) {
-        fresh_.pack(model);
+        if (!synced_) mask = PDPLQR_MODEL_ALL;
+        fresh_.pack(model, mask);
         int need = synced_ ? 0 : PDPLQR_MODEL_ALL;
         if (synced_) {
             if ((mask & PDPLQR_MODEL_E) && fresh_.E != packed_.E) need |= PDPLQR_MODEL_E;
@@ -172,7 +180,7 @@ private:
     static const double *nz(const std::vector<double> &v) { return v.empty() ? nullptr : v.data(); }
     pdplqr_handle h_ = nullptr;
     int n_ = 0, m_ = 0, N_ = 0;
-    std::vector<int32_t> ncs_;
+    std::vector<int32_t> ncs_, devs_;
     PackedModel packed_, fresh_;  // what the device holds / the model as packed now
     bool synced_ = false;
     std::vector<double> w_, y_, z_, r_;

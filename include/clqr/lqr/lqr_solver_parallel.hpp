@@ -7,7 +7,8 @@
 // condensed system.  On the GPU every reference segment is further split into
 // sub-segments and the condensed system becomes an associative prefix/suffix
 // scan; CondensedSystemSolverType is accepted and validated as in the
-// reference.  The OpenMP team / core pinning of the reference has no analogue.
+// reference.  The OpenMP team / core pinning of the reference has no analogue;
+// its multi-core split becomes the optional multi-GPU split (`devices`).
 #pragma once
 
 #include <stdexcept>
@@ -23,8 +24,17 @@ class LQRParallelSolver {
 public:
     LQRParallelSolver(const LQRModel &model, int num_segments, bool load_balancing = true,
                       CondensedSystemSolverType solver_type = CondensedSystemSolverType::CHOLESKY)
+        : LQRParallelSolver(model, num_segments, load_balancing, solver_type, std::vector<int>{}) {}
+
+    // MI355X extension: `devices` (HIP ordinals) splits the horizon into one
+    // slice per GPU, driven by this one object -- slice backward on every device,
+    // one RCCL all-gather of the slice elements, slice forward (pdplqr.h
+    // num_devices; backward_without_factorization is unsupported there).
+    LQRParallelSolver(const LQRModel &model, int num_segments, bool load_balancing,
+                      CondensedSystemSolverType solver_type, const std::vector<int> &devices)
         : model_(model),
-          hd_(model, PDPLQR_SOLVER_PARALLEL, num_segments, load_balancing, static_cast<int>(solver_type), true),
+          hd_(model, PDPLQR_SOLVER_PARALLEL, num_segments, load_balancing, static_cast<int>(solver_type), true,
+              devices),
           num_segments_(num_segments) {
         hd_.upload(model_);
     }

@@ -351,16 +351,17 @@ __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
 
 // One Hillis-Steele round with the 4-wave combine (combine_mw.hpp; CHOLESKY
 // form): the same operands, output and terminal rule as k_seg_scan.
+// the combine of block `blk` of one round (the body of k_seg_scan_mw, shared
+// with the all-rounds kernel below)
 template <int T, int NC = 0>
-__global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
-    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+__device__ __forceinline__ void mw_scan_block(const ScanArgs &A, long long blk, double *mwbuf) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n;
     const int per = scan_round_blocks(S, d, A.sk);
-    const long long b = blockIdx.x / per;
+    const long long b = blk / per;
     int i, j;
-    if (!scan_round_operands(S, d, A.sk, blockIdx.x % per, i, j)) return;  // block-uniform
+    if (!scan_round_operands(S, d, A.sk, (int)(blk % per), i, j)) return;  // block-uniform
     const long long is = A.istride ? A.istride : es;
     const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
@@ -394,6 +395,73 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     if (!fcf && wv == 1)
         for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
     if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
+}
+
+template <int T, int NC = 0>
+__global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    mw_scan_block<T, NC>(A, blockIdx.x, mwbuf);
+}
+
+// ---------------------------------------------------------------------------
+// Every Sklansky round of the suffix scan in ONE cooperative launch: the
+// resident grid walks the rounds' combine blocks and meets at a grid barrier
+// between rounds, instead of one launch (dispatch, ramp, drain) per round.
+// Same blocks, operands and results as the per-round k_seg_scan_mw launches.
+// The barrier (a counter and a generation word in device memory) makes each
+// round's stores visible to the next round's readers on every XCD (agent-scope
+// release / acquire fences); a wait that does not end within ~seconds gives up
+// and flags every problem (status N + 2) rather than hang.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned nblk) {
+    __syncthreads();
+    __shared__ int s_ok;
+    if (threadIdx.x == 0) {
+        s_ok = 1;
+        __threadfence();
+        unsigned *cnt = bar, *gen = bar + 1;
+        const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (atomicAdd(cnt, 1u) == nblk - 1) {
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            long long spins = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1LL << 26)) {
+                    s_ok = 0;
+                    break;
+                }
+            }
+        }
+        __threadfence();
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+template <int T, int NC = 0>
+__global__ __launch_bounds__(256) void k_seg_scan_mw_all(ScanArgs A0, const double *elem, double *buf, int batch,
+                                                         unsigned *bar) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const int S = A0.S;
+    for (int d = 1; d < S; d <<= 1) {
+        ScanArgs A = A0;
+        A.dist = d;
+        A.sk = d == 1 ? 1 : 2;
+        A.in = d == 1 ? elem : buf;
+        A.out = buf;
+        const long long total = (long long)batch * scan_round_blocks(S, d, A.sk);
+        for (long long q = blockIdx.x; q < total; q += gridDim.x) {
+            mw_scan_block<T, NC>(A, q, mwbuf);
+            __syncthreads();  // LDS reuse by the block's next combine
+        }
+        if (d * 2 < S && !grid_barrier(bar, gridDim.x)) {
+            if (threadIdx.x == 0)
+                for (int b = 0; b < batch; ++b) atomicOr(A0.flag + b, 1);
+            return;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -854,6 +922,35 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
     else if (ct_n12(a.n)) hipLaunchKernelGGL((k_seg_scan4<1, false, 12>), grid, blk, smem, st, a);
     else hipLaunchKernelGGL((k_seg_scan4<1, false>), grid, blk, smem, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// All Sklansky rounds of the suffix scan in one cooperative launch (4-wave
+// CHOLESKY combine shapes); ERR_UNSUPPORTED when it does not apply (the caller
+// then issues the per-round launches).  bar: two zeroed words of device memory.
+int launch_seg_scan_all(const ScanArgs &a, const double *elem, double *buf, int batch, unsigned *bar,
+                        hipStream_t st) {
+    if (wide_state(a.n) || !seg_scan_mw(a.n, a.lu, a.mw) || tile_order(a.n) != 2 || getenv("PDPLQR_SCAN_ROUNDS") ||
+        a.S < 2)
+        return PDPLQR_ERR_UNSUPPORTED;
+    const size_t sm = mw_scan_bytes(a.n);
+    const void *fn = ct_n24(a.n) ? reinterpret_cast<const void *>(&k_seg_scan_mw_all<2, 24>)
+                                 : reinterpret_cast<const void *>(&k_seg_scan_mw_all<2>);
+    int dev = 0, cus = 0, per = 0;
+    PDPLQR_HIP_TRY(hipGetDevice(&dev));
+    PDPLQR_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    PDPLQR_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, sm));
+    if (per <= 0) return PDPLQR_ERR_UNSUPPORTED;
+    const long long need = (long long)batch * a.S;  // the first round's blocks (the widest)
+    const unsigned grid = (unsigned)std::min<long long>(need, (long long)cus * per);
+    ScanArgs A0 = a;
+    int bt = batch;
+    void *args[] = {&A0, const_cast<double **>(&elem), &buf, &bt, &bar};
+    const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(grid), dim3(256), args, (unsigned)sm, st);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
     return PDPLQR_OK;
 }
 

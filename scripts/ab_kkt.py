@@ -68,7 +68,7 @@ def main():
         args = args[2:]
     solvers = ["kkt"]
     if args and args[0] == "--solvers":
-        solvers = args[1].split(",")
+        solvers = args[1].split("+")  # (scripts/gpu_run.sh splits its step arguments at commas)
         args = args[2:]
     res = {a: [] for a in args}
     for _ in range(rounds):

@@ -147,7 +147,19 @@ int main(int argc, char **argv) {
             const int ns = argc > 4 ? std::atoi(argv[4]) : 4;
             const auto ty = (argc > 5 && std::string(argv[5]) == "LU") ? lqr::CondensedSystemSolverType::LU
                                                                         : lqr::CondensedSystemSolverType::CHOLESKY;
-            lqr::LQRParallelSolver sol(model, ns, true, ty);
+            // devices=0,0,... : the multi-GPU split of the horizon (pdplqr.h num_devices)
+            std::vector<int> devs;
+            for (int a = 4; a < argc; ++a) {
+                const std::string arg = argv[a];
+                if (arg.rfind("devices=", 0) != 0) continue;
+                size_t p = 8;
+                while (p < arg.size()) {
+                    const size_t q = arg.find(',', p);
+                    devs.push_back(std::atoi(arg.substr(p, q == std::string::npos ? std::string::npos : q - p).c_str()));
+                    p = q == std::string::npos ? arg.size() : q + 1;
+                }
+            }
+            lqr::LQRParallelSolver sol(model, ns, true, ty, devs);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
             if (mutate) edit();
             sol.backward(rhov);

@@ -62,8 +62,12 @@ def _run(exe, tmp, name, args):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["quadrotor_N100", "random_n12_m4_N64_nc4", "random_n24_m8_N40",
                                   "quadrotor_N30_constrained"])
-@pytest.mark.parametrize("args", [["serial"], ["parallel", "4", "CHOLESKY"], ["parallel", "2", "LU"], ["qdldl"]])
+@pytest.mark.parametrize("args", [["serial"], ["parallel", "4", "CHOLESKY"], ["parallel", "2", "LU"], ["qdldl"],
+                                  ["parallel", "4", "CHOLESKY", "devices=0,0,0"], ["parallel", "2", "LU", "devices=0"]])
 def test_cpp_facade_matches_oracle(facade_bin, tmp_path, name, args):
+    """devices=...: LQRParallelSolver's multi-GPU split (one slice per listed
+    device; here all on GPU 0, and one slice through a one-rank RCCL
+    communicator) -- the answer is the serial one, so the oracle is OracleSerial."""
     from oracle.oracle import OracleKKT, OracleParallel, OracleSerial, segmentation
 
     pm, d = load_golden(name)
@@ -76,7 +80,8 @@ def test_cpp_facade_matches_oracle(facade_bin, tmp_path, name, args):
         o.backward(d["inv_rho"])
         tol = 1e-8
     else:
-        o = OracleSerial(pm) if args[0] == "serial" else OracleParallel(pm, int(args[1]), True, args[2])
+        split = any(a.startswith("devices=") for a in args)
+        o = OracleSerial(pm) if args[0] == "serial" or split else OracleParallel(pm, int(args[1]), True, args[2])
         o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
         o.backward(d["rho"])
         tol = 1e-9
