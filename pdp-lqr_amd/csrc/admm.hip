@@ -466,6 +466,8 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     bool refactor = true;  // iteration 1, and after an adaptive rho change
     bool fused = false;    // this iteration's backward already ran inside the fused update
     bool can_fuse = !kkt && Y > 0 && h->Lc != nullptr;  // cleared when the fused kernel does not apply
+    // KKT (Riccati-ordered 12/4, C5 rows): rollout + update fused (cleared when it does not apply)
+    bool can_fuse_kkt = kkt && kkt_ric_active(h) && a.uni == 4;
     int rho_updates = 0;
     for (;; ++it) {
         // x-update: the reference protocol (iteration 1 and after a rho
@@ -493,6 +495,33 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             if ((rc = solver_backward_prepared(h))) return rc;
         }
         fused = false;
+        const bool last = it >= st->max_iter;
+        const bool check = last || it % st->check_every == 0;
+        const bool fuse = (!kkt || kkt_lin) && !last;
+        a.it = it;
+        if (kkt && Y > 0 && can_fuse_kkt) {
+            // the KKT rollout and this iteration's update in one pass (kkt_riccati.hip)
+            if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
+            rc = kkt_forward_admm(h, s->x0, a, fuse, check);
+            if (rc == PDPLQR_OK) {
+                if (check) {
+                    PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
+                    PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+                    if (s->active_h[0] == 0) break;
+                    if (s->active_h[1] && !last) {
+                        hipLaunchKernelGGL(k_admm_rescale, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, sh.ny,
+                                           s->rscale, s->rho, s->irho);
+                        PDPLQR_HIP_TRY(hipGetLastError());
+                        refactor = true;
+                        ++rho_updates;
+                    }
+                }
+                if (last) break;
+                continue;
+            }
+            if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
+            can_fuse_kkt = false;
+        }
         if ((rc = solver_forward(h, s->x0, s->wt))) return rc;
         if (Y == 0) {  // nothing to split: one LQ solve is the answer
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->w, s->wt, W * sizeof(double), hipMemcpyDeviceToDevice, S));
@@ -502,10 +531,6 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));
             break;
         }
-        const bool last = it >= st->max_iter;
-        const bool check = last || it % st->check_every == 0;
-        const bool fuse = (!kkt || kkt_lin) && !last;
-        a.it = it;
         if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
         if (fuse && can_fuse) {
             // the update of this iteration and the backward_without_factorization

@@ -54,4 +54,11 @@ __device__ __forceinline__ void admm_decide(const AdmmArgs &a, int b, double rp,
 // PDPLQR_ERR_UNSUPPORTED when the shape / constraint layout is not covered.
 int launch_nofact_admm(const RiccatiArgs &r, const AdmmArgs &a, bool check, hipStream_t st);
 
+// KKT (Riccati-ordered, C5 row layout): the rollout with the ADMM update of the
+// iteration in the same pass (kkt_riccati.hip); ERR_UNSUPPORTED otherwise
+int launch_kkt_ric_forward_admm(const Shape &sh, const double *E, const double *c, const double *rec,
+                                const double *x0, double *x0acc, double rho_dyn, const AdmmArgs &q, bool fuse,
+                                bool check, hipStream_t st);
+int kkt_forward_admm(pdplqr_handle h, const double *x0, const AdmmArgs &q, bool fuse, bool check);
+
 }  // namespace pdplqr

@@ -301,14 +301,12 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
 // combine's right operand covers [first, min(first + span - 1, S - 1)]; when
 // that range holds the real terminal, F = C = f = 0 (see k_seg_scan).
 template <int T, bool LU, int NC = 0>
-__global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
-    __shared__ CombSmem<T> smv[2];
-    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // per wave: 2 operand images
+__device__ __forceinline__ void seg_scan4_block(const ScanArgs &A, long long blk, CombSmem<T> (&smv)[2], double *ebuf) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n, ol = op_stage_len(n);
-    const long long b = blockIdx.x / S;
-    const int i = blockIdx.x % S;
+    const long long b = blk / S;
+    const int i = (int)(blk % S);
     const long long is = A.istride ? A.istride : es;
     const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
@@ -348,6 +346,14 @@ __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
     }
     if (!ok && lane == 0) atomicOr(A.flag + b, 1);  // per problem
 }
+
+template <int T, bool LU, int NC = 0>
+__global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
+    __shared__ CombSmem<T> smv[2];
+    extern __shared__ __attribute__((aligned(16))) double ebuf[];  // per wave: 2 operand images
+    seg_scan4_block<T, LU, NC>(A, blockIdx.x, smv, ebuf);
+}
+
 
 // One Hillis-Steele round with the 4-wave combine (combine_mw.hpp; CHOLESKY
 // form): the same operands, output and terminal rule as k_seg_scan.
@@ -403,66 +409,6 @@ __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
     mw_scan_block<T, NC>(A, blockIdx.x, mwbuf);
 }
 
-// ---------------------------------------------------------------------------
-// Every Sklansky round of the suffix scan in ONE cooperative launch: the
-// resident grid walks the rounds' combine blocks and meets at a grid barrier
-// between rounds, instead of one launch (dispatch, ramp, drain) per round.
-// Same blocks, operands and results as the per-round k_seg_scan_mw launches.
-// The barrier (a counter and a generation word in device memory) makes each
-// round's stores visible to the next round's readers on every XCD (agent-scope
-// release / acquire fences); a wait that does not end within ~seconds gives up
-// and flags every problem (status N + 2) rather than hang.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned nblk) {
-    __syncthreads();
-    __shared__ int s_ok;
-    if (threadIdx.x == 0) {
-        s_ok = 1;
-        __threadfence();
-        unsigned *cnt = bar, *gen = bar + 1;
-        const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (atomicAdd(cnt, 1u) == nblk - 1) {
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            long long spins = 0;
-            while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1LL << 26)) {
-                    s_ok = 0;
-                    break;
-                }
-            }
-        }
-        __threadfence();
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-template <int T, int NC = 0>
-__global__ __launch_bounds__(256) void k_seg_scan_mw_all(ScanArgs A0, const double *elem, double *buf, int batch,
-                                                         unsigned *bar) {
-    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
-    const int S = A0.S;
-    for (int d = 1; d < S; d <<= 1) {
-        ScanArgs A = A0;
-        A.dist = d;
-        A.sk = d == 1 ? 1 : 2;
-        A.in = d == 1 ? elem : buf;
-        A.out = buf;
-        const long long total = (long long)batch * scan_round_blocks(S, d, A.sk);
-        for (long long q = blockIdx.x; q < total; q += gridDim.x) {
-            mw_scan_block<T, NC>(A, q, mwbuf);
-            __syncthreads();  // LDS reuse by the block's next combine
-        }
-        if (d * 2 < S && !grid_barrier(bar, gridDim.x)) {
-            if (threadIdx.x == 0)
-                for (int b = 0; b < batch; ++b) atomicOr(A0.flag + b, 1);
-            return;
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Boundary maps.  With the value function V_j = (P_j, p_j) at boundary j (the
@@ -817,11 +763,11 @@ __global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
 // ceil(log2 (S + 1)), each at most three products in sequence.  The running
 // map is kept transposed (Phi^T), the form the matrix-vector product reads.
 template <int T, int NC = 0>
-__global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
+__device__ __forceinline__ void map_scan4_block(const MapScanArgs &A, long long blk) {
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const int n = NC ? NC : A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
-    const long long b = blockIdx.x / J;
-    const int j = blockIdx.x % J;
+    const long long b = blk / J;
+    const int j = (int)(blk % J);
     const double *in = A.in + b * (long long)J * mw;
     double *out = A.out + b * (long long)J * mw;
     if (j < d) {  // anchored earlier: keep x_j for this round's partners
@@ -860,6 +806,12 @@ __global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
     wm_store_t(PaccT, out + (long long)j * mw, n, g, c);  // Phi_acc (natural) from its transpose
     wv_store(pacc, out + (long long)j * mw + nn, n, g, c);
 }
+
+template <int T, int NC = 0>
+__global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
+    map_scan4_block<T, NC>(A, blockIdx.x);
+}
+
 
 static int tile_order(int n);
 
@@ -922,35 +874,6 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
     else if (ct_n12(a.n)) hipLaunchKernelGGL((k_seg_scan4<1, false, 12>), grid, blk, smem, st, a);
     else hipLaunchKernelGGL((k_seg_scan4<1, false>), grid, blk, smem, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
-    return PDPLQR_OK;
-}
-
-// All Sklansky rounds of the suffix scan in one cooperative launch (4-wave
-// CHOLESKY combine shapes); ERR_UNSUPPORTED when it does not apply (the caller
-// then issues the per-round launches).  bar: two zeroed words of device memory.
-int launch_seg_scan_all(const ScanArgs &a, const double *elem, double *buf, int batch, unsigned *bar,
-                        hipStream_t st) {
-    if (wide_state(a.n) || !seg_scan_mw(a.n, a.lu, a.mw) || tile_order(a.n) != 2 || getenv("PDPLQR_SCAN_ROUNDS") ||
-        a.S < 2)
-        return PDPLQR_ERR_UNSUPPORTED;
-    const size_t sm = mw_scan_bytes(a.n);
-    const void *fn = ct_n24(a.n) ? reinterpret_cast<const void *>(&k_seg_scan_mw_all<2, 24>)
-                                 : reinterpret_cast<const void *>(&k_seg_scan_mw_all<2>);
-    int dev = 0, cus = 0, per = 0;
-    PDPLQR_HIP_TRY(hipGetDevice(&dev));
-    PDPLQR_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    PDPLQR_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, sm));
-    if (per <= 0) return PDPLQR_ERR_UNSUPPORTED;
-    const long long need = (long long)batch * a.S;  // the first round's blocks (the widest)
-    const unsigned grid = (unsigned)std::min<long long>(need, (long long)cus * per);
-    ScanArgs A0 = a;
-    int bt = batch;
-    void *args[] = {&A0, const_cast<double **>(&elem), &buf, &bt, &bar};
-    const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(grid), dim3(256), args, (unsigned)sm, st);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return PDPLQR_ERR_UNSUPPORTED;
-    }
     return PDPLQR_OK;
 }
 

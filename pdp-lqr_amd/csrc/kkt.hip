@@ -24,6 +24,7 @@
 // only the u columns of D_0 and x0 enters only through S0 x0 and A0 x0.
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
+#include "admm.hpp"
 #include "solvers.hpp"
 
 #include <algorithm>
@@ -1600,6 +1601,13 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     else hipLaunchKernelGGL(k_kkt_solve3, stages, wave, (PP + P) * sizeof(double), h->stream, a, x0, ws);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
+}
+
+int kkt_forward_admm(pdplqr_handle h, const double *x0, const AdmmArgs &q, bool fuse, bool check) {
+    KKTState *ks = h->kkt;
+    if (!ks || ks->ric != 4) return PDPLQR_ERR_UNSUPPORTED;
+    return launch_kkt_ric_forward_admm(h->sh, ks->Ef ? ks->Ef : h->E, h->c, ks->rec, x0, ks->x0acc, h->cfg.rho_dyn,
+                                       q, fuse, check, h->stream);
 }
 
 int kkt_dim(pdplqr_handle h) { return h->kkt ? h->kkt->dim : 0; }

@@ -45,6 +45,7 @@
 // side on every forward (kkt.hpp:207-222): the solve then uses the sum of every
 // x0 passed since the last update_problem_data (x0acc here), while ws[0]'s x
 // part is the x0 of the call (qdldl_solver.hpp:129-131).
+#include "admm.hpp"
 #include "blk_la.hpp"
 #include "schur_stage.hpp"
 #include "solvers.hpp"
@@ -593,28 +594,47 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
 // ---------------------------------------------------------------------------
 // forward: the gain-form rollout of kernels_rollout.hip plus the lambda
 // correction x+ = v - rho_dyn (P~ (v - rho_dyn p) + p), v = A x + B u + c.
+//
+// UPD (ADMM iterations on the C5 row layout, admm.hip): the z / y / w step of
+// the iteration runs in the same pass, stage by stage right after w~_k leaves
+// the chain -- w~ never goes to HBM and the separate update pass
+// (k_admm_update) disappears.  The ring record grows by the stage's w, D, z,
+// y, bounds, rho, 1 / rho and the model's h (120 doubles); the operations are
+// k_admm_update's (KKT form: h~ = h - sigma w, rho enters through g), the
+// stage's row sums by the same DPP butterfly; FUSE: also the next
+// update_problem_data's h~ and g; CHECK: the termination test (wave-wide
+// maxima, then admm_decide).  Rows: exactly Q.uni = 4 per stage k < N, none
+// at the terminal.
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
                                                     const double *__restrict__ x0, double *__restrict__ x0acc,
-                                                    double *__restrict__ ws, double rho_dyn) {
-    constexpr int n = 12, m = 4, s = 16;
+                                                    double *__restrict__ ws, double rho_dyn, AdmmArgs Q) {
+    constexpr int n = 12, m = 4, s = 16, NC = 4;
     using RS = KRecShape<n, m>;
     constexpr int FS = RS::FS;
-    constexpr int OE = 0, OC = n * s, OF = OC + n, REC = OF + FS, CH = REC / 2, NI = (CH + 63) / 64;
+    constexpr int OE = 0, OC = n * s, OF = OC + n, OW = OF + FS, OD = OW + s, OZ = OD + NC * s, OY = OZ + NC,
+                  OLB = OY + NC, OUB = OLB + NC, ORH = OUB + NC, OIR = ORH + NC, OH = OIR + NC;
+    constexpr int REC = UPD ? OH + s : OW, CH = REC / 2, NI = (CH + 63) / 64;
     constexpr int TAIL = CH - (NI - 1) * 64;
     constexpr int NQ = 3;
-    static_assert(REC % 2 == 0 && (NI == 3 || NI == 4), "record layout");
+    static_assert(REC % 2 == 0 && OW % 2 == 0 && (NI == 3 || NI == 4 || NI == 5), "record layout");
+    // vm ops per stage: NI DMA + the stores (plain: the w~ store; UPD: z, y, w
+    // [+ g, h~ with FUSE], each an instruction with live lanes)
+    constexpr int ST = UPD ? (FUSE ? 5 : 3) : 1;
     __shared__ __attribute__((aligned(16))) double ring[D][REC];
     __shared__ double sx[16], sz[16], sx0[16];
     const int lane = wave_lane(), g = lane >> 4, cl = lane & 15;
     const long long b = blockIdx.x;
+    if (UPD && Q.done[b]) return;  // frozen problem: no solve, no update (wave-uniform)
     const int N = sh.N;
     const double *Eb = E + b * sh.perE;
     const double *cb = c + b * sh.perc;
     const double *Fb = FR + b * (long long)N * FS;
     double *wb = ws + b * sh.perh;
+    const double al = UPD ? Q.alpha : 0.0, bl = 1.0 - al;
+    const long long pb = b * sh.perh, yb0 = b * (long long)sh.ny;
 
     auto dma = [&](int k, int slot) {
 #pragma unroll
@@ -623,9 +643,44 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
                 const int d = 2 * (q * 64 + lane);
                 const double *src = d < OC   ? Eb + (long long)k * (n * s) + d
                                     : d < OF ? cb + (long long)k * n + (d - OC)
-                                             : Fb + (long long)k * FS + (d - OF);
+                                    : d < OW ? Fb + (long long)k * FS + (d - OF)
+                                    : d < OD ? Q.w + pb + (long long)k * s + (d - OW)
+                                    : d < OZ ? Q.D + b * sh.ndD + (long long)k * NC * s + (d - OD)
+                                    : d < OY ? Q.z + yb0 + (long long)k * NC + (d - OZ)
+                                    : d < OLB ? Q.y + yb0 + (long long)k * NC + (d - OY)
+                                    : d < OUB ? Q.lb + yb0 + (long long)k * NC + (d - OLB)
+                                    : d < ORH ? Q.ub + yb0 + (long long)k * NC + (d - OUB)
+                                    : d < OIR ? Q.rho + yb0 + (long long)k * NC + (d - ORH)
+                                    : d < OH ? Q.irho + yb0 + (long long)k * NC + (d - OIR)
+                                             : Q.hv + pb + (long long)k * s + (d - OH);
                 dma16(src, &ring[slot][q * 128]);
             }
+        }
+    };
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
+    // the ADMM step of stage k from its ring record and this lane's w~_k[cl]
+    auto upd = [&](const double *R, int k, double wt) {
+        const double wo = R[OW + cl];
+        const double wn = al * wt + bl * wo;
+        const double d = R[OD + g + cl * NC];  // D_k[g][cl]
+        const double v = sum_row16(d * wt), vw = sum_row16(d * wo);
+        const double zr = R[OZ + g], yr = R[OY + g], rr = R[ORH + g], ir = R[OIR + g];
+        const double vrel = al * v + bl * zr;
+        const double zn = fmin(fmax(vrel + ir * yr, R[OLB + g]), R[OUB + g]);
+        const double yn = yr + rr * (vrel - zn);
+        const long long yo = yb0 + (long long)k * NC + g;
+        if (cl == 0) gstore(Q.z + yo, zn);
+        if (cl == 0) gstore(Q.y + yo, yn);
+        if (FUSE && cl == 0) gstore(Q.gw + yo, zn - ir * yn);
+        if (g == 0) gstore(Q.w + pb + (long long)k * s + cl, wn);
+        if (FUSE && g == 0) gstore(Q.hw + pb + (long long)k * s + cl, R[OH + cl] - Q.sigma * wn);
+        if (CHECK) {
+            const double dwn = al * v + bl * vw;  // D w^{k+1}
+            rp = fmax(rp, fabs(dwn - zn));
+            dwm = fmax(dwm, fabs(dwn));
+            zm = fmax(zm, fabs(zn));
+            rd = fmax(rd, fabs(sum_groups(d * (rr * (zn - zr)))));
+            dty = fmax(dty, fabs(sum_groups(d * yn)));
         }
     };
 
@@ -647,7 +702,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         const int kp = k + D - 1;
         dma(kp < N ? kp : N - 1, kp % D);
         if (k < D - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NI + 1) * (D - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NI + ST) * (D - 1)) : "memory");
         const double *R = ring[k % D];
         const double *F = R + OF;
         const int cm = cl < m ? cl : m - 1, cn = cl < n ? cl : n - 1;
@@ -667,7 +722,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         const double cc = R[OC + cn];
         const double pv = F[RS::OPV + cn];
         // ---- chain ----
-        const int lx = (lane >= m && lane < s) ? lane - m : 0;
+        const int lx = UPD ? (cl >= m ? cl - m : 0) : ((lane >= m && lane < s) ? lane - m : 0);
         const double xk = k == 0 ? sx0[lx] : sx[lx];  // ws[0]'s x part is the call's x0
 #pragma unroll
         for (int q = 0; q < NQ; ++q) xt[q] = sx[4 * q + g];
@@ -686,7 +741,8 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
             a = __builtin_fma(eu[i], ui, a);
         }
         a = sum_groups(a) + cc;  // v = A x + B u + c (every group)
-        if (lane < s) gstore(wb + (long long)k * s + lane, (lane < m) ? myu : xk);
+        if constexpr (UPD) upd(R, k, (cl < m) ? myu : xk);  // every group holds w~_k[cl]
+        else if (lane < s) gstore(wb + (long long)k * s + lane, (lane < m) ? myu : xk);
         // ---- lambda correction: x+ = v - rho_dyn (P~ (v - rho_dyn p) + p) ----
         if (g == 0 && cl < n) sz[cl] = __builtin_fma(-rho_dyn, pv, a);
         wave_sync();
@@ -698,6 +754,28 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         wave_sync();  // all reads of x_k done before it is overwritten
         if (g == 0 && cl < n) sx[cl] = xn;
         wave_sync();
+    }
+    if constexpr (UPD) {
+        // terminal (no rows): w_N relaxed, h~_N = h_N - sigma w_N
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane < n) {
+            const long long o = pb + (long long)N * s + lane;
+            const double wn = al * sx[lane] + bl * Q.w[o];
+            Q.w[o] = wn;
+            if (FUSE) Q.hw[o] = Q.hv[o] - Q.sigma * wn;
+        }
+        if (CHECK) {
+#pragma unroll
+            for (int msk = 32; msk >= 1; msk >>= 1) {
+                rp = fmax(rp, __shfl_xor(rp, msk, 64));
+                dwm = fmax(dwm, __shfl_xor(dwm, msk, 64));
+                zm = fmax(zm, __shfl_xor(zm, msk, 64));
+                rd = fmax(rd, __shfl_xor(rd, msk, 64));
+                dty = fmax(dty, __shfl_xor(dty, msk, 64));
+            }
+            if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty);
+        }
+        return;
     }
     if (lane < n) wb[(long long)N * s + lane] = sx[lane];
 }
@@ -1063,7 +1141,35 @@ int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, co
         return PDPLQR_OK;
     }
     hipLaunchKernelGGL(k_kkt_ric_fwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
-                       rho_dyn);
+                       rho_dyn, AdmmArgs{});
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// The KKT rollout with the ADMM update of the iteration in the same pass
+// (admm.hip; C5 layout: 12/4, 4 rows on every stage k < N, none at N).
+int launch_kkt_ric_forward_admm(const Shape &sh, const double *E, const double *c, const double *rec,
+                                const double *x0, double *x0acc, double rho_dyn, const AdmmArgs &q, bool fuse,
+                                bool check, hipStream_t st) {
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (getenv("PDPLQR_NO_ADMM_FUSE") || sh.n != 12 || sh.m != 4 || q.uni != 4 || !q.no_penalty ||
+        sh.ny != 4 * sh.N || !al(E) || !al(c) || !al(rec) || !al(q.w) || !al(q.D) || !al(q.z) || !al(q.y) ||
+        !al(q.lb) || !al(q.ub) || !al(q.rho) || !al(q.irho) || !al(q.hv) || sh.perE % 2 || sh.perc % 2 ||
+        sh.perh % 2 || sh.ndD % 2 || sh.ny % 2)
+        return PDPLQR_ERR_UNSUPPORTED;
+    const dim3 grid((unsigned)sh.batch), blk(64);
+    if (fuse && check)
+        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, true, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+                           (double *)nullptr, rho_dyn, q);
+    else if (fuse)
+        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, true, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+                           (double *)nullptr, rho_dyn, q);
+    else if (check)
+        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, false, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+                           (double *)nullptr, rho_dyn, q);
+    else
+        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, false, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+                           (double *)nullptr, rho_dyn, q);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

@@ -422,14 +422,6 @@ int md_backward(pdplqr_handle h, const double *rho, int mem) {
                              md->st[r])))
                 return rc;
         }
-        // slices sharing a device run one after the other (the all-rounds scan is
-        // a cooperative launch: two of them side by side on one device could
-        // not both keep their whole grids resident)
-        for (int q = 0; q < r; ++q)
-            if (md->dev[q] == md->dev[r]) {
-                PDPLQR_HIP_TRY(hipStreamWaitEvent(md->st[r], md->ev[r - 1], 0));
-                break;
-            }
         if ((rc = pdplqr_shard_backward(md->sh[r], ny ? md->rho[r] : nullptr, p.last ? 1 : 0, md->elem[r],
                                         PDPLQR_MEM_DEVICE)))
             return rc;

@@ -97,9 +97,6 @@ int seg_backward_slots(const Shape &sh, int device);
 int seg_scan_slots(const Shape &sh, int device);
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st);
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st);
-// every Sklansky round in one cooperative launch (ERR_UNSUPPORTED: use launch_seg_scan per round)
-int launch_seg_scan_all(const ScanArgs &a, const double *elem, double *buf, int batch, unsigned *bar,
-                        hipStream_t st);
 // one launch = the two Hillis-Steele rounds at distances dist and 2 dist (two
 // waves per block); false when this shape keeps the radix-2 rounds
 bool seg_scan4_supported(int n);

@@ -33,7 +33,6 @@ struct ParallelState {
     double *rscan[2] = {nullptr, nullptr}, *rmaps = nullptr;  // rank suffix scan, rank maps
     int rcap = 0;
     int *has_suf = nullptr;
-    unsigned *gbar = nullptr;  // grid barrier words of the all-rounds scan (zeroed once)
 };
 
 template <typename X>
@@ -206,9 +205,8 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->mapB, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->vfun, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->left, B * es)) || (rc = palloc(h, &ps->right, B * es)) ||
-        (rc = palloc(h, &ps->has_suf, 1)) || (rc = palloc(h, &ps->gbar, 4)))
+        (rc = palloc(h, &ps->has_suf, 1)))
         return rc;
-    PDPLQR_HIP_TRY(hipMemset(ps->gbar, 0, 4 * sizeof(unsigned)));
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_start, ps->seg_start_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_len, ps->seg_len_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemset(ps->flag, 0, B * sizeof(int)));
@@ -266,23 +264,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
     int round = 0;
     const bool r4 = ps->scan4 != nullptr;  // two rounds per launch (k_seg_scan4)
     if (scan_sklansky(sh) && ps->S > 1) {
-        // Sklansky rounds: the first into bufA, the later ones in place there;
-        // all of them in one cooperative launch where it applies
-        {
-            ScanArgs s;
-            s.n = sh.n;
-            s.S = ps->S;
-            s.terminal = last_is_terminal;
-            s.flag = ps->flag;
-            s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
-            s.mw = sh.mw;
-            const int rc = launch_seg_scan_all(s, sin, ps->bufA, sh.batch, ps->gbar, h->stream);
-            if (rc == PDPLQR_OK) {
-                ps->suf_final = ps->bufA;
-                return PDPLQR_OK;
-            }
-            if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
-        }
+        // Sklansky rounds: the first into bufA, the later ones in place there
         for (int d = 1; d < ps->S; d <<= 1) {
             ScanArgs s;
             s.n = sh.n;

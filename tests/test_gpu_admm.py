@@ -274,12 +274,14 @@ def test_adaptive_rho_matches_oracle(solver):
         assert rel_err(w[b], ow) < tol and rel_err(y[b], oy) < tol, b
 
 
+@pytest.mark.parametrize("solver", ["serial", "kkt"])
 @pytest.mark.parametrize("check_every,adaptive", [(1, False), (5, True), (25, True)])
-def test_fused_update_equals_unfused(check_every, adaptive):
+def test_fused_update_equals_unfused(check_every, adaptive, solver):
     """At 12/4 with 4 rows per stage (C5's layout) the serial solver runs the
-    ADMM update inside the streamed backward (k_nofact_admm_dma).  Same
-    per-problem iteration counts, convergence flags and rho as the separate
-    update pass (PDPLQR_NO_ADMM_FUSE), iterates to 1e-8, and the oracle."""
+    ADMM update inside the streamed backward (k_nofact_admm_dma), the KKT
+    solver inside its rollout (k_kkt_ric_fwd<3, true, ...>).  Same per-problem
+    iteration counts, convergence flags and rho as the separate update pass
+    (PDPLQR_NO_ADMM_FUSE), iterates to 1e-8, and the oracle."""
     import os
 
     n, m, nc, N, B = 12, 4, 4, 60, 6
@@ -318,7 +320,7 @@ def test_fused_update_equals_unfused(check_every, adaptive):
         if mode == "separate":
             os.environ["PDPLQR_NO_ADMM_FUSE"] = "1"
         try:
-            res[mode] = _run_gpu("serial", pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, True, **st)
+            res[mode] = _run_gpu(solver, pms, ncs, A, lb, ub, x0, ws, ys, zs, rho, solver == "serial", **st)
         finally:
             os.environ.pop("PDPLQR_NO_ADMM_FUSE", None)
     (wf, yf, zf, fi), (wsep, ysep, zsep, si) = res["fused"], res["separate"]
@@ -329,10 +331,11 @@ def test_fused_update_equals_unfused(check_every, adaptive):
         # rounding of the fused h~ sum (permlane tree vs k_penalty's sequential
         # sum) carried through up to 400 contractive iterations and rho changes
         assert float(d.max()) < 1e-8, float(d.max())
+    tol = 1e-9 if solver == "serial" else TOL_KKT
     for b in (0, B - 1):
-        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial", **st)
+        ow, oy, oz, oi = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver=solver, **st)
         assert oi["iters"] == fi["iters"][b]
-        assert rel_err(wf[b], ow) < 1e-9 and rel_err(yf[b], oy) < 1e-9, b
+        assert rel_err(wf[b], ow) < tol and rel_err(yf[b], oy) < tol, b
 
 
 def test_invalid_bounds_and_rho_are_rejected():
