@@ -679,8 +679,19 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
             rp = fmax(rp, fabs(dwn - zn));
             dwm = fmax(dwm, fabs(dwn));
             zm = fmax(zm, fabs(zn));
-            rd = fmax(rd, fabs(sum_groups(d * (rr * (zn - zr)))));
-            dty = fmax(dty, fabs(sum_groups(d * yn)));
+            // D^T rho (z+ - z) and D^T y+ of column cl, summed over the rows in
+            // k_admm_update's order (row 0 first, one fma per row): the row
+            // values come from their groups by readlane, D[r][cl] from the ring
+            const double tz = rr * (zn - zr);
+            double ad = 0.0, ay = 0.0;
+#pragma unroll
+            for (int r = 0; r < NC; ++r) {
+                const double dr = R[OD + r + cl * NC];
+                ad = __builtin_fma(dr, readlane_f64(tz, 16 * r), ad);
+                ay = __builtin_fma(dr, readlane_f64(yn, 16 * r), ay);
+            }
+            rd = fmax(rd, fabs(ad));
+            dty = fmax(dty, fabs(ay));
         }
     };
 

@@ -108,8 +108,11 @@ def lib() -> C.CDLL:
     L.pdplqr_admm_settings_init.restype = None
     L.pdplqr_admm_solve.argtypes = [vp, C.POINTER(AdmmSettings), dp, dp, dp, dp, dp, dp, dp, C.c_int]
     L.pdplqr_admm_info.argtypes = [vp, ip, ip, dp, dp, dp]
-    L.pdplqr_multidev_plan.argtypes = [i32, i32, ip, i32, i32, C.POINTER(C.c_int64)]
+    if hasattr(L, "pdplqr_multidev_plan"):  # (absent from pre-round-4 A/B variants)
+        L.pdplqr_multidev_plan.argtypes = [i32, i32, ip, i32, i32, C.POINTER(C.c_int64)]
     for nm in EXPORTS:
+        if LIB_PATH != os.path.join(_HERE, "libpdplqr.so") and not hasattr(L, nm):
+            continue  # an older A/B variant (PDPLQR_LIB) may predate a symbol
         f = getattr(L, nm)
         if nm not in ("pdplqr_config_init", "pdplqr_last_error", "pdplqr_get_stream", "pdplqr_admm_settings_init"):
             f.restype = C.c_int
