@@ -318,8 +318,8 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
     at a test that does not terminate, rho scales by
     e = sqrt((r_prim / max(|Dw|, |z|)) / (r_dual / |D^T y|)) (guards 1e-30, rows
     clamped to [1e-6, 1e6]) when e leaves [1/tol, tol], and the next x-update
-    re-forms and refactors; no rescale while |D^T y| <= eps_abs (no active row:
-    the dual normalisation is undefined).  One problem (PackedModel arrays of one batch
+    re-forms and refactors; no rescale while no row is active (no z at a bound:
+    y is rounding noise and the dual normalisation undefined) or |D^T y| <= 1e-30.  One problem (PackedModel arrays of one batch
     entry).  Returns (ws, ys, zs, info)."""
     n, m, N = pm.n, pm.m, pm.N
     s = n + m
@@ -365,6 +365,7 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
         zn = np.empty(ny)
         yn = np.empty(ny)
         rp = dwm = zm = rd = dty = 0.0
+        act = False  # some row's z at one of its bounds (OSQP: an active constraint)
         for (wo, dim, yo, nc, Dk) in blocks:
             if nc == 0:
                 continue
@@ -380,11 +381,12 @@ def admm_solve(pm, x0, lb, ub, rho, ws=None, ys=None, zs=None, solver="serial", 
                 zm = max(zm, float(np.max(np.abs(zn[sl]))))
                 rd = max(rd, float(np.max(np.abs(Dk.T @ (rho[sl] * (zn[sl] - z[sl]))))))
                 dty = max(dty, float(np.max(np.abs(Dk.T @ yn[sl]))))
+                act = act or bool(np.any((zn[sl] <= lb[sl]) | (zn[sl] >= ub[sl])))
         w, y, z = wn, yn, zn
         if check and rp <= eps_abs + eps_rel * max(dwm, zm) and rd <= eps_abs + eps_rel * dty:
             conv = True
             break
-        if check and adaptive_rho and it < max_iter and dty > eps_abs:
+        if check and adaptive_rho and it < max_iter and act and dty > 1e-30:
             e = np.sqrt((rp / (max(dwm, zm) + 1e-30)) / (rd / (dty + 1e-30) + 1e-30))
             if e > adaptive_rho_tolerance or e < 1.0 / adaptive_rho_tolerance:
                 rho = np.minimum(np.maximum(rho * e, 1e-6), 1e6)

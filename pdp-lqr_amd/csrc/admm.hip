@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
     constexpr int SPW = 64 / LPS;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane / LPS, j = lane % LPS;
     const double al = a.alpha, bl = 1.0 - a.alpha;
-    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0, act = 0.0;
     for (int kb = wv * SPW; kb <= sh.N; kb += 4 * SPW) {
         // wave-uniform trip count: lanes past the horizon idle in the loop
         const int k = kb + sub;
@@ -160,6 +160,7 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
                         zm = fmax(zm, fabs(zn));
                         ad += d * (rr[r] * (zn - zr[r]));
                         ay += d * yn;
+                        if (zn <= lo[r] || zn >= hi[r]) act = 1.0;
                     }
                 }
             }
@@ -195,6 +196,7 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
                     zm = fmax(zm, fabs(zn));
                     ad += d * (rr * (zn - zr));
                     ay += d * yn;
+                    if (zn <= a.lb[yo + r] || zn >= a.ub[yo + r]) act = 1.0;
                 }
             }
         }
@@ -213,18 +215,20 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
         }
     }
     if (CHECK) {
-        __shared__ double red[4][5];
+        __shared__ double red[4][6];
         rp = wave_max(rp);
         dwm = wave_max(dwm);
         zm = wave_max(zm);
         rd = wave_max(rd);
         dty = wave_max(dty);
+        act = wave_max(act);
         if (lane == 0) {
             red[wv][0] = rp;
             red[wv][1] = dwm;
             red[wv][2] = zm;
             red[wv][3] = rd;
             red[wv][4] = dty;
+            red[wv][5] = act;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -235,8 +239,9 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
                 zm = fmax(zm, red[q][2]);
                 rd = fmax(rd, red[q][3]);
                 dty = fmax(dty, red[q][4]);
+                act = fmax(act, red[q][5]);
             }
-            admm_decide(a, b, rp, dwm, zm, rd, dty);
+            admm_decide(a, b, rp, dwm, zm, rd, dty, act);
         }
     }
 }

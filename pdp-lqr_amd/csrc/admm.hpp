@@ -22,8 +22,9 @@ struct AdmmArgs {
 // Termination test of iteration a.it for problem b from the five maxima
 // (r_prim, |Dw|, |z|, r_dual, |D^T y|), then OSQP's rho estimate when the
 // test fails (admm.hip header).  One thread per problem.
+// act > 0: some row's z sits at one of its bounds (an active constraint).
 __device__ __forceinline__ void admm_decide(const AdmmArgs &a, int b, double rp, double dwm, double zm, double rd,
-                                            double dty) {
+                                            double dty, double act) {
     a.iters[b] = a.it;
     a.prim[b] = rp;
     a.dual[b] = rd;
@@ -33,10 +34,10 @@ __device__ __forceinline__ void admm_decide(const AdmmArgs &a, int b, double rp,
         a.conv[b] = 1;
     } else {
         atomicAdd(a.active, 1);
-        // no rescale while |D^T y| is below eps_abs (every row inactive: y = 0
-        // and the dual normalisation is undefined -- the estimate would
-        // collapse to ~1e-14 and pin rho at its lower clamp)
-        if (a.adaptive && dty > a.eps_abs) {
+        // no rescale while no row is active (y is rounding noise there and the
+        // dual normalisation undefined -- the estimate would collapse to ~1e-14
+        // and pin rho at its lower clamp) or |D^T y| vanishes (OSQP's 1e-30 guard)
+        if (a.adaptive && act > 0.0 && dty > 1e-30) {
             // OSQP's compute_rho_estimate: the ratio of the normalised
             // residuals, with its division guard 1e-30
             const double pn = rp / (fmax(dwm, zm) + 1e-30), dn = rd / (dty + 1e-30);

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
         for (int q = 0; q < NI; ++q)
             if (q < NI - 1 || lane < SH::TAIL) dma16(gbase[q] + (long long)k * gstride[q], &ring[slot][q * 128]);
     };
-    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0, act = 0.0;
     // The ADMM step of stage kk from its ring record; returns h~_kk[cl].
     // Exactly 5 stores (z, y, g: lanes c == 0; w, h~: row group 0).
     auto upd = [&](const double *R, int kk) -> double {
@@ -304,6 +304,7 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
             rp = fmax(rp, fabs(dwn - zn));
             dwm = fmax(dwm, fabs(dwn));
             zm = fmax(zm, fabs(zn));
+            if (zn <= R[SH::OLB + g] || zn >= R[SH::OUB + g]) act = 1.0;
             rd = fmax(rd, fabs(sum_groups(d * (rr * (zn - zr)))));
             dty = fmax(dty, fabs(sum_groups(d * yn)));
         }
@@ -386,8 +387,9 @@ __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs 
             zm = fmax(zm, __shfl_xor(zm, msk, 64));
             rd = fmax(rd, __shfl_xor(rd, msk, 64));
             dty = fmax(dty, __shfl_xor(dty, msk, 64));
+                act = fmax(act, __shfl_xor(act, msk, 64));
         }
-        if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty);
+        if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty, act);
     }
 }
 

@@ -657,7 +657,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
             }
         }
     };
-    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0;
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0, act = 0.0;
     // the ADMM step of stage k from its ring record and this lane's w~_k[cl]
     auto upd = [&](const double *R, int k, double wt) {
         const double wo = R[OW + cl];
@@ -679,6 +679,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
             rp = fmax(rp, fabs(dwn - zn));
             dwm = fmax(dwm, fabs(dwn));
             zm = fmax(zm, fabs(zn));
+            if (zn <= R[OLB + g] || zn >= R[OUB + g]) act = 1.0;
             // D^T rho (z+ - z) and D^T y+ of column cl, summed over the rows in
             // k_admm_update's order (row 0 first, one fma per row): the row
             // values come from their groups by readlane, D[r][cl] from the ring
@@ -783,8 +784,9 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
                 zm = fmax(zm, __shfl_xor(zm, msk, 64));
                 rd = fmax(rd, __shfl_xor(rd, msk, 64));
                 dty = fmax(dty, __shfl_xor(dty, msk, 64));
+                act = fmax(act, __shfl_xor(act, msk, 64));
             }
-            if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty);
+            if (lane == 0) admm_decide(Q, (int)b, rp, dwm, zm, rd, dty, act);
         }
         return;
     }
