@@ -824,9 +824,19 @@ __device__ __forceinline__ ElemIn elem_in(const double *e, int n) {
 
 // out = a (x) b  (a earlier, b later).  The output blocks are addressed
 // separately (oF, oC, of are not touched when need_FCf is false, oP, op not
-// when need_Pp is false) and must not alias the inputs.  P_a and C_b are read
-// once, as addends of the last products: they are loaded up front so a
-// global-memory source costs no exposed latency.
+// when need_Pp is false).  P_a and C_b are read once, as addends of the last
+// products: they are loaded up front so a global-memory source costs no
+// exposed latency.
+//
+// Aliasing contract (the in-place Sklansky rounds of k_seg_scan rely on it,
+// tests/test_gpu_parallel.py::test_sklansky_scan_matches_hillis_steele):
+// an output block may alias an input block only when
+//   * that input is P_a, which is loaded into registers (Pa) before the first
+//     store, and the first store (oP) depends on Pa; or
+//   * that input lives in a buffer the caller staged elsewhere (LDS) first.
+// Every other input block is read from its source after the first store, so
+// it must not overlap any output.  An edit that moves a store ahead of a read,
+// or reads P_a from memory again, breaks the in-place rounds.
 template <int T, bool LU = false>
 __device__ __forceinline__ bool tcombine_parts(double *oF, double *oC, double *of, double *oP, double *op,
                                                const ElemIn &ea, const ElemIn &eb, int n, bool need_FCf,

@@ -193,23 +193,31 @@ def test_radix4_scan_equals_radix2(N, batch, seglen, condensed, monkeypatch):
     assert np.array_equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("n,m,N,batch,seglen,condensed,one_wave",
-                         [(24, 8, 96, 2, 5, "CHOLESKY", False), (24, 8, 40, 1, 3, "CHOLESKY", False),
-                          (24, 8, 7, 2, 3, "CHOLESKY", False), (24, 8, 512, 1, 0, "CHOLESKY", False),
-                          (24, 8, 96, 2, 5, "CHOLESKY", True), (20, 6, 130, 2, 4, "LU", False),
-                          (24, 8, 12, 1, 4, "CHOLESKY", False), (18, 4, 33, 3, 2, "CHOLESKY", True)])
-def test_sklansky_scan_matches_hillis_steele(n, m, N, batch, seglen, condensed, one_wave, monkeypatch):
+@pytest.mark.parametrize("n,m,N,batch,seglen,condensed,one_wave,force_sk",
+                         [(24, 8, 96, 2, 5, "CHOLESKY", False, False), (24, 8, 40, 1, 3, "CHOLESKY", False, False),
+                          (24, 8, 7, 2, 3, "CHOLESKY", False, False), (24, 8, 512, 1, 0, "CHOLESKY", False, False),
+                          (24, 8, 96, 2, 5, "CHOLESKY", True, False), (20, 6, 130, 2, 4, "LU", False, False),
+                          (24, 8, 12, 1, 4, "CHOLESKY", False, False), (18, 4, 33, 3, 2, "CHOLESKY", True, False),
+                          # in-place rounds through the one-wave combine (tcombine_parts'
+                          # aliasing contract, combine_tiles.hpp) in LU form at T = 2 and
+                          # T = 1, the latter forced off the 4-way scan by PDPLQR_SCAN_SK
+                          (20, 6, 130, 2, 4, "LU", True, False), (24, 8, 96, 1, 5, "LU", True, False),
+                          (12, 4, 96, 2, 5, "LU", True, True), (12, 4, 40, 1, 2, "CHOLESKY", True, True)])
+def test_sklansky_scan_matches_hillis_steele(n, m, N, batch, seglen, condensed, one_wave, force_sk, monkeypatch):
     """The suffix scan's Sklansky rounds (n <= 32: the first round into a
     buffer, the later ones in place, half the combines per round) give the
     Hillis-Steele rounds' solution (PDPLQR_SCAN_HS=1) to rounding -- the same
     elements associated differently -- and both match the serial oracle.
     Segment counts 3..~130 cover partial upper halves and the terminal
-    element's (P, p)-only combines; one_wave forces the one-wave combine."""
+    element's (P, p)-only combines; one_wave forces the one-wave combine,
+    force_sk the Sklansky rounds where the 4-way scan would run (n <= 16)."""
     from pdplqr import BatchedLQRSolver
     from pdplqr.problems import random_batch_arrays
 
     if one_wave:
         monkeypatch.setenv("PDPLQR_SCAN_1WAVE", "1")
+    if force_sk:
+        monkeypatch.setenv("PDPLQR_SCAN_SK", "1")
     E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 2000 + N)
     ws0 = np.zeros((batch, N * (n + m) + n))
     outs = []
