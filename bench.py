@@ -66,49 +66,54 @@ def gen_batch_device(n, m, N, batch, seed, device):
     return E.reshape(batch, -1).contiguous(), c.reshape(batch, -1).contiguous(), H, h, x0
 
 
-def load_pmc_traffic(workload_tag, kernel=None):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/*_pmc.json), or None.  Only a summary collected on the
-    same workload AND the same backward kernel counts."""
+def _pmc_summaries():
+    """Every committed rocprofv3 PMC summary (profiles/**/*_pmc.json), oldest
+    first: top-level files (rounds 1-2), then profiles/rNN/ in round order, so
+    the last match for a workload is the newest."""
     pdir = os.path.join(ROOT, "profiles")
+    out = []
+    for dp, dns, fs in os.walk(pdir):
+        dns.sort()
+        for f in sorted(fs):
+            if f.endswith("_pmc.json"):
+                try:
+                    out.append(json.load(open(os.path.join(dp, f))))
+                except Exception:
+                    continue
+    return out
+
+
+def load_pmc_traffic(workload_tag, kernel=None):
+    """Per-launch HBM bytes of the dominant kernel from the newest committed
+    rocprofv3 PMC summary, or None.  Only a summary collected on the same
+    workload AND the same backward kernel counts."""
     best = None
-    if not os.path.isdir(pdir):
-        return None
-    for f in sorted(os.listdir(pdir)):
-        if f.endswith("_pmc.json"):
-            try:
-                d = json.load(open(os.path.join(pdir, f)))
-            except Exception:
-                continue
-            if (d.get("workload") == workload_tag and "bytes_per_launch" in d
-                    and (kernel is None or d.get("dominant_kernel", "").endswith(kernel))):
-                best = d
+    for d in _pmc_summaries():
+        if (d.get("workload") == workload_tag and "bytes_per_launch" in d
+                and (kernel is None or d.get("dominant_kernel", "").endswith(kernel))):
+            best = d
     return best
 
 
 def pmc_traffic(workload_tag, kernels):
-    """HBM bytes per solve of a secondary workload from a committed PMC summary
-    (profiles/**/*_pmc.json with this workload tag): the sum over the solve's
-    kernels (name substrings) of FETCH_SIZE x 2 + WRITE_SIZE (KB; gfx950
-    correction of MI355X_MICROARCH.md), or None."""
-    pdir = os.path.join(ROOT, "profiles")
+    """HBM bytes per solve of a secondary workload from the newest committed PMC
+    summary with this workload tag: the sum over the solve's kernels (name
+    substrings) of FETCH_SIZE x 2 + WRITE_SIZE (KB; gfx950 correction of
+    MI355X_MICROARCH.md), or None."""
     found = None
-    for dp, _, fs in os.walk(pdir):
-        for f in sorted(fs):
-            if not f.endswith("_pmc.json"):
-                continue
-            try:
-                d = json.load(open(os.path.join(dp, f)))
-            except Exception:
-                continue
-            if d.get("workload") == workload_tag:
-                found = d
+    for d in _pmc_summaries():
+        if d.get("workload") == workload_tag:
+            found = d
     if not found:
         return None
     tot, seen = 0.0, []
     for sub in kernels:
+        opt = sub.startswith("?")  # "?name": counted when that kernel ran in the profile
+        sub = sub.lstrip("?")
         ks = [k for k in found.get("kernels", {}) if sub in k]
         if not ks:
+            if opt:
+                continue
             return None
         c = found["kernels"][ks[0]]
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
@@ -537,7 +542,9 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
         ok = bool(np.all(bs.status() == 0)) and bool(torch.isfinite(out).all().item())
         # C5 = 4,704 B per stage (E, c, H, h, w + D, y, z, inv_rho, rho, w-bar)
         bst = 8 * (n * s + n + s * s + s) + 8 * s + 8 * (nc * s + 4 * nc + s)
-        kern = ("k_kkt_ric_bwd", "k_kkt_ric_fwd") if solver == "kkt" else ("k_penalty", "k_riccati_bwd_schur",
+        # the serial path's rho penalty is fused into the streamed backward
+        # (k_riccati_bwd_schur<12, 4, true, 4>); k_penalty runs where it is not
+        kern = ("k_kkt_ric_bwd", "k_kkt_ric_fwd") if solver == "kkt" else ("?k_penalty", "k_riccati_bwd_schur",
                                                                               "k_rollout_dma")
         res["kkt" if solver == "kkt" else "riccati"] = {
             "ms_per_solve": t * 1e3, "stages_per_s": N * batch / t, "status_ok": ok,
