@@ -78,6 +78,12 @@ struct SchurSmem {
 #define PDPLQR_LP_IN_P 1
 #endif
 
+// G = P E~ and M = H~ + E~^T G as independent per-chunk MFMAs summed by VALU
+// (compile-time m = 4) instead of one accumulation chain (A/B: schur_stage)
+#ifndef PDPLQR_SCHUR_SPLIT
+#define PDPLQR_SCHUR_SPLIT 0
+#endif
+
 // Compile-time m <= 4: the m u-pivots as ONE block step.  Every u row sits in
 // register 0 (row j = row group j), so
 //   * Muu (m x m) and lu come to every lane by v_readlane; Luu = chol(Muu),
@@ -272,13 +278,37 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
                                             GainOut *go = nullptr) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks that hold x rows
     d4 G = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-        if (kk >= k0 && kk <= k1) G = mfma_f64(Pm[kk], in.E[kk], G);
     d4 Mn = in.H;
+    if constexpr (PDPLQR_SCHUR_SPLIT && MM == 4) {
+        // the three x chunks (kk = 1..3 at m = 4, s = 16) on independent
+        // accumulators, summed by VALU: a dependent f64 MFMA waits ~186 cycles
+        // for its predecessor, three independent ones issue back to back
+        // (scripts/ubench/lat_bench.hip), so each product leaves the stage
+        // chain ~250 cycles earlier for 8 v_add_f64
+        // (PDPLQR_SCHUR_SPLIT = 2: two accumulators, chunks 1 | 2, 3 -- fewer
+        // live registers than three)
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        if constexpr (PDPLQR_SCHUR_SPLIT == 2) {
+            const d4 g2 = mfma_f64(Pm[2], in.E[2], z), g1 = mfma_f64(Pm[1], in.E[1], z);
+            G = g1 + mfma_f64(Pm[3], in.E[3], g2);
+            const d4 m2 = mfma_f64(in.E[2], G[2], z), m1 = mfma_f64(in.E[1], G[1], in.H);
+            Mn = m1 + mfma_f64(in.E[3], G[3], m2);
+        } else {
+            const d4 g1 = mfma_f64(Pm[1], in.E[1], z), g2 = mfma_f64(Pm[2], in.E[2], z),
+                     g3 = mfma_f64(Pm[3], in.E[3], z);
+            G = (g1 + g2) + g3;
+            const d4 m1 = mfma_f64(in.E[1], G[1], in.H), m2 = mfma_f64(in.E[2], G[2], z),
+                     m3 = mfma_f64(in.E[3], G[3], z);
+            Mn = (m1 + m2) + m3;
+        }
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-        if (kk >= k0 && kk <= k1) Mn = mfma_f64(in.E[kk], G[kk], Mn);
+        for (int kk = 0; kk < 4; ++kk)
+            if (kk >= k0 && kk <= k1) G = mfma_f64(Pm[kk], in.E[kk], G);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            if (kk >= k0 && kk <= k1) Mn = mfma_f64(in.E[kk], G[kk], Mn);
+    }
     double part = 0.0;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)

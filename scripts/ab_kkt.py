@@ -1,7 +1,9 @@
-"""Same-box A/B of the C5 KKT solve (backward + forward, N = 512, 12/4, nc = 4,
-batch 1024) across library variants.
+"""Same-box A/B of the C5 solve (backward + forward, N = 512, 12/4, nc = 4,
+batch 1024; solvers kkt / serial) and of the headline batch (solver "head":
+N = 1024, 12/4, batch 4096, backward and forward timed apart) across library
+variants.
 
-usage: python scripts/ab_kkt.py [--rounds R] LIB [LIB ...]
+usage: python scripts/ab_kkt.py [--rounds R] [--solvers kkt+serial+head] LIB [LIB ...]
   LIB: a path to a libpdplqr variant, or "default" (the in-tree library).
 Each (round, LIB) runs in a child process (the library is loaded once per
 process); prints one line per run and a median summary per LIB.
@@ -41,6 +43,25 @@ def child(solvers, N=512, batch=1024, steps=20, warmup=3):
     irho = 1.0 / rho
     out = torch.empty(batch, N * s + n, dtype=torch.float64, device=dev)
     res = {}
+    if "head" in solvers:
+        del E, c, H, h, D
+        torch.cuda.empty_cache()
+        Nh, bh = 1024, 4096
+        Eh, ch, Hh, hh, xh = bench.gen_batch_device(n, m, Nh, bh, seed=1234, device=dev)
+        bs = BatchedLQRSolver(n, m, Nh, bh, solver="serial")
+        bs.set_model(Eh, ch, Hh, hh)
+        bs.update_problem_data(torch.zeros(bh, Nh * s + n, dtype=torch.float64, device=dev), sigma=1e-6)
+        oh = torch.empty(bh, Nh * s + n, dtype=torch.float64, device=dev)
+        bs.backward()
+        tb = bench._timed(lambda: bs.backward(), 2 * steps, warmup, dev, None)
+        tf = bench._timed(lambda: bs.forward(xh, oh), 2 * steps, warmup, dev, None)
+        ok = bool(np.all(bs.status() == 0))
+        res["head_bwd"] = {"ms_per_solve": tb * 1e3, "status_ok": ok}
+        res["head_fwd"] = {"ms_per_solve": tf * 1e3, "status_ok": ok}
+        bs.close()
+        solvers = [x for x in solvers if x != "head"]
+        if solvers:
+            raise SystemExit("head runs alone")
     for solver in solvers:
         bs = BatchedLQRSolver(n, m, N, batch, solver=solver, ncs=ncs)
         bs.set_model(E, c, H, h, D)
@@ -86,7 +107,7 @@ def main():
             res[lib].append(d)
             print(os.path.basename(lib), json.dumps(d), flush=True)
     for lib, rs in res.items():
-        for s in solvers:
+        for s in (rs[0].keys() if rs else ()):
             v = sorted(r[s]["ms_per_solve"] for r in rs)
             print(f"SUMMARY {os.path.basename(lib)} {s} median {v[len(v) // 2]:.4f} ms  all {v}", flush=True)
 

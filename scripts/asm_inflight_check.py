@@ -4,6 +4,7 @@ LDS writes (lput) may write or read a register of a load set while that set's
 loads are in flight.  Reads the assembly of kernels_schur.hip (hipcc -S).
 Conservative linear scan over the loop body, wrapping the back edge; prints
 the offending lines and exits 1 on a hazard."""
+import os
 import re
 import subprocess
 import sys
@@ -21,7 +22,8 @@ KERNELS = {"kernels_schur.hip": r"k_riccati_bwd_schurILi12ELi4E", "kkt_riccati.h
 
 def main(src, asm="/tmp/_schur_check.s"):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Iinclude",
-                           "-mllvm", "-amdgpu-mfma-vgpr-form", "--cuda-device-only", "-S", src, "-o", asm],
+                           "-mllvm", "-amdgpu-mfma-vgpr-form", "--cuda-device-only", "-S", src, "-o", asm]
+                          + os.environ.get("ASM_CHECK_DEFS", "").split(),  # e.g. -DPDPLQR_SCHUR_SPLIT=1 (variants)
                           stderr=subprocess.DEVNULL)
     text = open(asm).read().split("\n")
     pat = KERNELS.get(src.split("/")[-1], KERNELS["kernels_schur.hip"])
