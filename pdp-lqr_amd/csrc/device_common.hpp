@@ -93,6 +93,26 @@ __device__ __forceinline__ double dpp_f64(double v) {
     return __hiloint2double(hi, lo);
 }
 
+// Masked move: lanes of the DPP rows in ROWS (row = 16-lane group g) and
+// banks in BANKS (bank = 4 consecutive lanes of a row) take v, the others keep
+// old (quad_perm identity: no data crosses lanes).
+template <int ROWS, int BANKS>
+__device__ __forceinline__ double dpp_keep(double old, double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0xE4, ROWS, BANKS, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0xE4, ROWS, BANKS, false);
+    return __hiloint2double(hi, lo);
+}
+
+// v[g] on the lanes of row group g (three masked moves instead of three
+// selects of two v_cndmask each)
+__device__ __forceinline__ double pick_group(const double (&v)[4]) {
+    double r = v[0];
+    r = dpp_keep<0x2, 0xF>(r, v[1]);
+    r = dpp_keep<0x4, 0xF>(r, v[2]);
+    r = dpp_keep<0x8, 0xF>(r, v[3]);
+    return r;
+}
+
 __device__ __forceinline__ double sum_row16(double v) {
     v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]

@@ -275,8 +275,9 @@ __global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_S
             }
             double w, luq[4];
             GainOut go;
-            const bool ok = schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN>(
-                Pm, prow, in, sm, m, s, g, c, w, luq, sym_rt, &go);
+            const bool ok =
+                schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN, GAIN && PDPLQR_SCHUR_LPW>(
+                    Pm, prow, in, sm, m, s, g, c, w, luq, sym_rt, &go);
             fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
             if constexpr (GAIN)
                 schur_store_record_gain<SH::m, SH::s>(FRb + (long long)k * frs, go, g, c);

@@ -78,6 +78,20 @@ struct SchurSmem {
 #define PDPLQR_LP_IN_P 1
 #endif
 
+// PDPLQR_SCHUR_SUBST: W, lu' and the gain record by forward / back
+// substitution with Luu (no explicit T = Luu^{-1}, 16 fewer uniform VALU a
+// stage); PDPLQR_SCHUR_DPP: per-row-group picks and the column-0 merge as
+// masked DPP moves (row_mask / bank_mask) instead of v_cndmask pairs (m = 4)
+#ifndef PDPLQR_SCHUR_SUBST
+#define PDPLQR_SCHUR_SUBST 0
+#endif
+#ifndef PDPLQR_SCHUR_DPP
+#define PDPLQR_SCHUR_DPP 0
+#endif
+#ifndef PDPLQR_SCHUR_LPW
+#define PDPLQR_SCHUR_LPW 0
+#endif
+
 // G = P E~ and M = H~ + E~^T G as independent per-chunk MFMAs summed by VALU
 // (compile-time m = 4) instead of one accumulation chain (A/B: schur_stage)
 #ifndef PDPLQR_SCHUR_SPLIT
@@ -122,12 +136,19 @@ struct GainOut {
 #define PDPLQR_SCHUR_LDSU 0
 #endif
 
-template <int MM, bool GAIN = false>
+// LPW (the batched backward's gain path; PDPLQR_SCHUR_LPW): lu rides in W.
+// Column 0 of the u rows is replaced by lu before the u-row columns are
+// gathered, so lane (g, 0) forms W_0 = Luu^{-1} lu = lu' and its gain column
+// Luu^{-T} lu' = k~: the MFMA's B operand is w on every lane (its column 0 is
+// lu', as LP_IN_P wants), k~ needs no uniform pass and no lane pick, and lu is
+// never read to the scalar side.  Row 0 of the product (u row) is dead.
+template <int MM, bool GAIN = false, bool LPW = false>
 __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], double &w, double (&luq)[4], int g,
                                                    int c, GainOut *go = nullptr, double *ldsu = nullptr,
                                                    double *ldsl = nullptr) {
     static_assert(MM >= 1 && MM <= 4, "u block");
     static_assert(!GAIN || !PDPLQR_SCHUR_T4, "gain record needs the VALU W");
+    static_assert(!LPW || (GAIN && MM == 4 && PDPLQR_LP_IN_P && !PDPLQR_SCHUR_LDSU), "lu in W: 12/4 gain path");
     double a[4][4], lu[4], L[4][4], T[4][4], inv[4];
     bool ok = true;
 #if PDPLQR_SCHUR_LDSU
@@ -189,6 +210,15 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
             T[i][j] = -v * inv[i];
         }
     }
+#if PDPLQR_SCHUR_SUBST
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {  // lu' = Luu^{-1} lu (forward substitution)
+        double v = lu[i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) v = __builtin_fma(-L[i][j], luq[j], v);
+        luq[i] = v * inv[i];
+    }
+#else
 #pragma unroll
     for (int i = 0; i < MM; ++i) {  // lu' = T lu
         double v = 0.0;
@@ -196,6 +226,7 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         for (int j = 0; j <= i; ++j) v = __builtin_fma(T[i][j], lu[j], v);
         luq[i] = v;
     }
+#endif
 #if PDPLQR_SCHUR_T4
     // W = T times the u rows (register 0 of every lane: the B operand) as one
     // MFMA (combine_tiles.hpp t4_apply); T zero-padded past m
@@ -207,6 +238,7 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
     w = t4_apply(t4_operand(Tz, g, c), M[0]);
 #else
     // column c of the u rows: m_l = M[l][c] (group l, register 0)
+    if constexpr (LPW) M[0] = (c == 0) ? lpr[0] : M[0];  // the readlanes above took Muu first
 #if PDPLQR_SCHUR_LDSU
     if constexpr (MM != 4)
 #else
@@ -216,26 +248,72 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
         for (int l = 0; l < MM; ++l) ml[l] = bcast_group(M[0], l);
     w = 0.0;
     double Wc[4];  // W[c][j], j < m: this lane's row of the u columns
+#if PDPLQR_SCHUR_SUBST
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {  // W_c = Luu^{-1} m_c (forward substitution, no T)
+        double v = ml[j];
+#pragma unroll
+        for (int l = 0; l < j; ++l) v = __builtin_fma(-L[j][l], Wc[l], v);
+        Wc[j] = v * inv[j];
+    }
+#else
 #pragma unroll
     for (int j = 0; j < MM; ++j) {
         double v = 0.0;
 #pragma unroll
         for (int l = 0; l <= j; ++l) v = __builtin_fma(T[j][l], ml[l], v);
         Wc[j] = v;
-        w = (g == j) ? v : w;  // W[c][g]; groups g >= m keep 0
+    }
+#endif
+    if constexpr (PDPLQR_SCHUR_DPP && MM == 4) {
+        w = pick_group(Wc);  // W[c][g]
+    } else {
+#pragma unroll
+        for (int j = 0; j < MM; ++j) w = (g == j) ? Wc[j] : w;  // W[c][g]; groups g >= m keep 0
     }
     if constexpr (GAIN) {  // K~[i][c] = sum_{l >= i} T[l][i] W[c][l], k~[i] = sum_{l >= i} T[l][i] lu'[l]
-        double kt = 0.0, kq = 0.0;
+        double ka[4] = {0.0, 0.0, 0.0, 0.0}, kb[4] = {0.0, 0.0, 0.0, 0.0};
+#if PDPLQR_SCHUR_SUBST
+#pragma unroll
+        for (int i = MM - 1; i >= 0; --i) {  // Luu^{-T} W_c, Luu^{-T} lu' (back substitution)
+            double a = Wc[i], q = luq[i];
+#pragma unroll
+            for (int l = i + 1; l < MM; ++l) {
+                a = __builtin_fma(-L[l][i], ka[l], a);
+                q = __builtin_fma(-L[l][i], kb[l], q);
+            }
+            ka[i] = a * inv[i];
+            kb[i] = q * inv[i];
+        }
+#else
 #pragma unroll
         for (int i = 0; i < MM; ++i) {
-            double a = 0.0, q = 0.0;
 #pragma unroll
             for (int l = i; l < MM; ++l) {
-                a = __builtin_fma(T[l][i], Wc[l], a);
-                q = __builtin_fma(T[l][i], luq[l], q);
+                ka[i] = __builtin_fma(T[l][i], Wc[l], ka[i]);
+                kb[i] = __builtin_fma(T[l][i], luq[l], kb[i]);
             }
-            kt = (g == i) ? a : kt;
-            kq = (g == i) ? q : kq;
+        }
+#endif
+        double kt = 0.0, kq = 0.0;
+        if constexpr (LPW) {
+            // lane (g, 0) holds k~[g]; lanes (g, 1..3) take it (DPP quad_perm
+            // [0,0,0,0] on bank 0 of every row) so the record store's four
+            // k~ writers carry equal values
+            kt = pick_group(ka);
+            const int lo = __builtin_amdgcn_update_dpp(__double2loint(kt), __double2loint(kt), 0x00, 0xF, 0x1, false);
+            const int hi = __builtin_amdgcn_update_dpp(__double2hiint(kt), __double2hiint(kt), 0x00, 0xF, 0x1, false);
+            kt = __hiloint2double(hi, lo);
+            kq = kt;
+        } else if constexpr (PDPLQR_SCHUR_DPP && MM == 4) {
+            kt = pick_group(ka);
+            kq = pick_group(kb);
+        } else {
+#pragma unroll
+            for (int i = 0; i < MM; ++i) {
+                kt = (g == i) ? ka[i] : kt;
+                kq = (g == i) ? kb[i] : kq;
+            }
         }
         go->kt = kt;
         go->kq = kq;
@@ -251,10 +329,25 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
     // K-chunks only, and G's u rows are never used) carries lp in, the B
     // operand's column 0 carries lu', so D[:, 0] = lp - W lu'; then the
     // column-0 result to every lane of its row (DPP row_newbcast:0)
-    const double lq = (g < MM) ? luq[g < MM ? g : 0] : 0.0;
+    if constexpr (LPW) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) M[r] = (c == 0) ? lpr[r] : M[r];
-    M = mfma_f64(-w, (c == 0) ? lq : w, M);  // M - W W^T; column 0: lp - W lu'
+        for (int r = 1; r < 4; ++r) M[r] = (c == 0) ? lpr[r] : M[r];
+        M = mfma_f64(-w, w, M);  // M - W W^T; column 0: lp - W lu' (lane (g, 0): w = lu'[g])
+    } else if constexpr (PDPLQR_SCHUR_DPP && MM == 4) {
+        // masked DPP moves instead of lane selects: lanes c < 4 (DPP bank 0 of
+        // every row) take lp and lu' -- columns 1..3 are dead u columns as
+        // well (they feed only G's u rows next stage), so they may carry the
+        // same lp - W lu' as column 0
+        const double lq = pick_group(luq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) M[r] = dpp_keep<0xF, 0x1>(M[r], lpr[r]);
+        M = mfma_f64(-w, dpp_keep<0xF, 0x1>(w, lq), M);  // M - W W^T; columns 0..3: lp - W lu'
+    } else {
+        const double lq = (g < MM) ? luq[g < MM ? g : 0] : 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) M[r] = (c == 0) ? lpr[r] : M[r];
+        M = mfma_f64(-w, (c == 0) ? lq : w, M);  // M - W W^T; column 0: lp - W lu'
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) lpr[r] = bcast_lane16(M[r], 0);
 #else
@@ -272,7 +365,7 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
 // after the m u-pivots (trailing block P_k, u columns unscaled L).  prow:
 // p~ in row layout (prow[r] = p[4 r + g - m] on x rows).
-template <int MM, bool SYM = true, bool GAIN = false>
+template <int MM, bool SYM = true, bool GAIN = false, bool LPW = false>
 __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const SchurIn &in, SchurSmem &sm, int m,
                                             int s, int g, int c, double &w, double (&luq)[4], bool sym_rt = true,
                                             GainOut *go = nullptr) {
@@ -330,7 +423,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
     }
     bool ok;
     if constexpr (MM > 0) {
-        ok = schur_block_pivots<MM, GAIN>(Mn, lpr[0], w, luq, g, c, go, sm.col, sm.lu4);
+        ok = schur_block_pivots<MM, GAIN, LPW>(Mn, lpr[0], w, luq, g, c, go, sm.col, sm.lu4);
         Pm = Mn;
     } else {
         d4 Mt[1][1];
