@@ -15,6 +15,26 @@ __device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// acc + sum of three MFMA products on independent accumulators, summed by
+// VALU: a dependent f64 MFMA waits ~186 cycles for its predecessor's result,
+// independent ones issue every 64 (scripts/ubench/lat_bench.hip), so a
+// three-deep accumulation chain becomes one product deep plus two v_add_f64
+// (different rounding order from the chain)
+// (PDPLQR_MFMA_SPLIT = 0: the plain accumulation chain, A/B)
+#ifndef PDPLQR_MFMA_SPLIT
+#define PDPLQR_MFMA_SPLIT 1
+#endif
+__device__ __forceinline__ d4 mfma_f64_x3(double a1, double b1, double a2, double b2, double a3, double b3,
+                                          const d4 &acc) {
+#if PDPLQR_MFMA_SPLIT
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    const d4 p1 = mfma_f64(a1, b1, acc), p2 = mfma_f64(a2, b2, z), p3 = mfma_f64(a3, b3, z);
+    return (p1 + p2) + p3;
+#else
+    return mfma_f64(a3, b3, mfma_f64(a2, b2, mfma_f64(a1, b1, acc)));
+#endif
+}
+
 // packed lower (column-major) index of (i, j), i >= j, dimension d
 __device__ __forceinline__ int pidx(int i, int j, int d) { return j * d - ((j * (j - 1)) >> 1) + (i - j); }
 

@@ -149,10 +149,8 @@ __device__ __forceinline__ bool ptilde_exact(const d4 &P, double rd, int g, int 
             S[r] = (i == j) ? ((c == j) ? ip : rowj * ip) : ((c == j) ? -a : __builtin_fma(-a, rowj, S[r]));
         }
     }
-    d4 Y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 1; kk < 4; ++kk) Y = mfma_f64(P[kk], S[kk], Y);  // P^T S^{-1} = P S^{-1}
-    Pt = Y;
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    Pt = mfma_f64_x3(P[1], S[1], P[2], S[2], P[3], S[3], z);  // P^T S^{-1} = P S^{-1}
     return ok;
 }
 
@@ -171,10 +169,8 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
     for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
     double ej = e;
     for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // wave-uniform
-        d4 Tn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 1; kk < 4; ++kk) Tn = mfma_f64(Pneg[kk], T[kk], Tn);  // (-rho_dyn P) T (x rows)
-        T = Tn;
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        T = mfma_f64_x3(Pneg[1], T[1], Pneg[2], T[2], Pneg[3], T[3], z);  // (-rho_dyn P) T (x rows)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pt[r] += T[r];
         ej *= e;
@@ -321,12 +317,11 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             }
         }
         // ---- G = P~ E~, M = H~ + E~^T G + D^T rho D ----
-        d4 G = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 1; kk < 4; ++kk) G = mfma_f64(Pt[kk], in.E[kk], G);
-        d4 Mn = in.H;
-#pragma unroll
-        for (int kk = 1; kk < 4; ++kk) Mn = mfma_f64(in.E[kk], G[kk], Mn);
+        // (one wave per SIMD at C5: the stage is chain-bound, and the split
+        // accumulators of mfma_f64_x3 take two MFMA latencies off each product)
+        const d4 z4 = {0.0, 0.0, 0.0, 0.0};
+        const d4 G = mfma_f64_x3(Pt[1], in.E[1], Pt[2], in.E[2], Pt[3], in.E[3], z4);
+        d4 Mn = mfma_f64_x3(in.E[1], G[1], in.E[2], G[2], in.E[3], G[3], in.H);
         double part = 0.0, rhoD = 0.0;
         if constexpr (NC > 0) {
             // lane (g, c): D[g][c] (rows g < NC); stage 0 keeps only the u columns
@@ -335,7 +330,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             const double rq = (g < NC) ? rcp_f64(R[SH::OI + (g < NC ? g : 0)]) : 0.0;
             const double gq = (g < NC) ? R[SH::OG + (g < NC ? g : 0)] : 0.0;
             rhoD = rq * dgc;
-            Mn = mfma_f64(dgc, rhoD, Mn);          // D^T diag(rho) D
+            Mn += mfma_f64(dgc, rhoD, z4);         // D^T diag(rho) D (off the G -> M chain)
             part = -dgc * rq * gq;                 // -(D^T rho g)[c]
         }
         double *Ck = cache ? cache + ((long long)b * N + k) * KKT_CF : nullptr;
