@@ -157,24 +157,69 @@ __device__ __forceinline__ bool ptilde_exact(const d4 &P, double rd, int g, int 
 // P~ of the x block for the 12/4 kernels: the Neumann series while it has
 // converged to rounding (e <= PDPLQR_KKT_NEUMANN_MAX, wave-uniform), the exact
 // inversion above otherwise.  False: S = I + rho_dyn P was not SPD.
+#ifndef PDPLQR_KKT_POW_TREE
+#define PDPLQR_KKT_POW_TREE 1
+#endif
 __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c, d4 &Pt) {
     double f = 0.0;
 #pragma unroll
     for (int r = 1; r < 4; ++r) f = (c >= 4) ? __builtin_fma(Pm[r], Pm[r], f) : f;
     const double e = rd * sqrt(wave_sum(f));
     if (__builtin_amdgcn_readfirstlane((int)(e > PDPLQR_KKT_NEUMANN_MAX))) return ptilde_exact(Pm, rd, g, c, Pt);
+    // J terms (-rho_dyn)^j P^{j+1}, j = 1..J, while e^j > 1e-16 (wave-uniform)
+    int J = 0;
+    for (double ej = e; J < 8 && ej > 1e-16; ej *= e) ++J;
+#if PDPLQR_KKT_POW_TREE
+    // the powers by a product tree instead of a chain of J products:
+    // P^2 | P^3 = P^2 P, P^4 = P^2 P^2 | P^5..P^8 = P^4 P^{1..4} | P^9 = P^8 P,
+    // so J = 3 (rho_dyn ||P|| ~ 1e-4) is two dependent products, not three
+    // (every power of the symmetric P is symmetric: its registers serve as the
+    // A operand, read as the transpose, like P's own)
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    auto mul = [&](const d4 &X, const d4 &Y) { return mfma_f64_x3(X[1], Y[1], X[2], Y[2], X[3], Y[3], z); };
+    auto acc = [&](const d4 &Q, double f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Pt[r] = __builtin_fma(f, Q[r], Pt[r]);
+    };
+    const double r1 = -rd, r2 = rd * rd, r3 = -r2 * rd, r4 = r2 * r2;
+    Pt = Pm;
+    if (J >= 1) {
+        const d4 Q2 = mul(Pm, Pm);
+        if (J >= 2) {
+            const d4 Q3 = mul(Q2, Pm);
+            d4 Q4 = z;
+            if (J >= 3) Q4 = mul(Q2, Q2);
+            if (J >= 4) {
+                const d4 Q5 = mul(Q4, Pm);
+                d4 Q6 = z, Q7 = z, Q8 = z, Q9 = z;
+                if (J >= 5) Q6 = mul(Q4, Q2);
+                if (J >= 6) Q7 = mul(Q4, Q3);
+                if (J >= 7) Q8 = mul(Q4, Q4);
+                if (J >= 8) Q9 = mul(Q8, Pm);
+                // smallest terms first
+                if (J >= 8) acc(Q9, r4 * r4);
+                if (J >= 7) acc(Q8, r4 * r3);
+                if (J >= 6) acc(Q7, r4 * r2);
+                if (J >= 5) acc(Q6, r4 * r1);
+                acc(Q5, r4);
+            }
+            if (J >= 3) acc(Q4, r3);
+            acc(Q3, r2);
+        }
+        acc(Q2, r1);
+    }
+#else
     Pt = Pm;
     d4 T = Pm, Pneg;
 #pragma unroll
     for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
-    double ej = e;
-    for (int j = 0; j < 8 && ej > 1e-16; ++j) {  // wave-uniform
+    for (int j = 0; j < J; ++j) {  // wave-uniform
         const d4 z = {0.0, 0.0, 0.0, 0.0};
         T = mfma_f64_x3(Pneg[1], T[1], Pneg[2], T[2], Pneg[3], T[3], z);  // (-rho_dyn P) T (x rows)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pt[r] += T[r];
-        ej *= e;
     }
+#endif
     return true;
 }
 
