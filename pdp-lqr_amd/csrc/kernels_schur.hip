@@ -77,6 +77,12 @@ using SymOff = std::integral_constant<bool, false>;
 #ifndef PDPLQR_PEN_WAVES
 #define PDPLQR_PEN_WAVES 2
 #endif
+// the fused-penalty instance has the registers (2 waves per SIMD) for G and M
+// on three independent MFMA accumulators each (schur_stage SPLIT = 1); C5 runs
+// it at one wave per SIMD, where the stage chain is what bounds it
+#ifndef PDPLQR_PEN_SPLIT
+#define PDPLQR_PEN_SPLIT 1
+#endif
 
 // NN = MM = 0: runtime shape, register prefetch of the next stage.
 // NN, MM > 0 : compile-time shape, stage records streamed by LDS-DMA
@@ -276,8 +282,9 @@ __global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_S
             double w, luq[4];
             GainOut go;
             const bool ok =
-                schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN, GAIN && PDPLQR_SCHUR_LPW>(
-                    Pm, prow, in, sm, m, s, g, c, w, luq, sym_rt, &go);
+                schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN, GAIN && PDPLQR_SCHUR_LPW,
+                            (NC > 0 ? PDPLQR_PEN_SPLIT : PDPLQR_SCHUR_SPLIT)>(Pm, prow, in, sm, m, s, g, c, w, luq,
+                                                                             sym_rt, &go);
             fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
             if constexpr (GAIN)
                 schur_store_record_gain<SH::m, SH::s>(FRb + (long long)k * frs, go, g, c);

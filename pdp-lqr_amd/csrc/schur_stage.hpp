@@ -365,14 +365,14 @@ __device__ __forceinline__ bool schur_block_pivots(d4 &M, double (&lpr)[4], doub
 // One stage.  Pm: in = tile whose trailing (x) block is P_{k+1}; out = M_k
 // after the m u-pivots (trailing block P_k, u columns unscaled L).  prow:
 // p~ in row layout (prow[r] = p[4 r + g - m] on x rows).
-template <int MM, bool SYM = true, bool GAIN = false, bool LPW = false>
+template <int MM, bool SYM = true, bool GAIN = false, bool LPW = false, int SPLIT = PDPLQR_SCHUR_SPLIT>
 __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const SchurIn &in, SchurSmem &sm, int m,
                                             int s, int g, int c, double &w, double (&luq)[4], bool sym_rt = true,
                                             GainOut *go = nullptr) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks that hold x rows
     d4 G = {0.0, 0.0, 0.0, 0.0};
     d4 Mn = in.H;
-    if constexpr (PDPLQR_SCHUR_SPLIT && MM == 4) {
+    if constexpr (SPLIT && MM == 4) {
         // the three x chunks (kk = 1..3 at m = 4, s = 16) on independent
         // accumulators, summed by VALU: a dependent f64 MFMA waits ~186 cycles
         // for its predecessor, three independent ones issue back to back
@@ -381,7 +381,7 @@ __device__ __forceinline__ bool schur_stage(d4 &Pm, double (&prow)[4], const Sch
         // (PDPLQR_SCHUR_SPLIT = 2: two accumulators, chunks 1 | 2, 3 -- fewer
         // live registers than three)
         const d4 z = {0.0, 0.0, 0.0, 0.0};
-        if constexpr (PDPLQR_SCHUR_SPLIT == 2) {
+        if constexpr (SPLIT == 2) {
             const d4 g2 = mfma_f64(Pm[2], in.E[2], z), g1 = mfma_f64(Pm[1], in.E[1], z);
             G = g1 + mfma_f64(Pm[3], in.E[3], g2);
             const d4 m2 = mfma_f64(in.E[2], G[2], z), m1 = mfma_f64(in.E[1], G[1], in.H);
