@@ -144,16 +144,29 @@ __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, 
                 acc[a][b][r] = (add ? add->t[a][b][r] : 0.0) + (i == j ? diag : 0.0);
             }
 #if PDPLQR_TN_CHUNK_OUTER
+    if constexpr (T == 1 && PDPLQR_MFMA_SPLIT) {
+        // one output tile: its K chunks would be ONE dependent chain (~186
+        // cycles a link); on separate accumulators they issue back to back
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        d4 p1 = z, p2 = z, p3 = z;
+        acc[0][0] = mfma_f64(sgn * X.t[0][0][0], Y.t[0][0][0], acc[0][0]);
+        if (4 < n) p1 = mfma_f64(sgn * X.t[0][0][1], Y.t[0][0][1], z);
+        if (8 < n) p2 = mfma_f64(sgn * X.t[0][0][2], Y.t[0][0][2], z);
+        if (12 < n) p3 = mfma_f64(sgn * X.t[0][0][3], Y.t[0][0][3], z);
+        acc[0][0] = (acc[0][0] + p1) + (p2 + p3);
+    } else {
 #pragma unroll
-    for (int kt = 0; kt < T; ++kt)
+        for (int kt = 0; kt < T; ++kt)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-            if (16 * kt + 4 * kk < n) {
+            for (int kk = 0; kk < 4; ++kk)
+                if (16 * kt + 4 * kk < n) {
 #pragma unroll
-                for (int a = 0; a < T; ++a)
+                    for (int a = 0; a < T; ++a)
 #pragma unroll
-                    for (int b = 0; b < T; ++b) acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
-            }
+                        for (int b = 0; b < T; ++b)
+                            acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
+                }
+    }
 #else
 #pragma unroll
     for (int a = 0; a < T; ++a)
@@ -776,14 +789,35 @@ __device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, 
 #pragma unroll
     for (int a = 0; a < T; ++a) acc[a] = add ? add->t[a] : d4{0.0, 0.0, 0.0, 0.0};
 #if PDPLQR_TN_CHUNK_OUTER
+    if constexpr (PDPLQR_MFMA_SPLIT && T <= 2) {
+        // T output tiles only: even and odd K chunks on separate accumulators
+        // (two chains of half the length, summed at the end)
+        d4 odd[T];
 #pragma unroll
-    for (int kt = 0; kt < T; ++kt)
+        for (int a = 0; a < T; ++a) odd[a] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-            if (16 * kt + 4 * kk < n) {
+        for (int kt = 0; kt < T; ++kt)
 #pragma unroll
-                for (int a = 0; a < T; ++a) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
-            }
+            for (int kk = 0; kk < 4; ++kk)
+                if (16 * kt + 4 * kk < n) {
+#pragma unroll
+                    for (int a = 0; a < T; ++a) {
+                        if (kk & 1) odd[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], odd[a]);
+                        else acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
+                    }
+                }
+#pragma unroll
+        for (int a = 0; a < T; ++a) acc[a] += odd[a];
+    } else {
+#pragma unroll
+        for (int kt = 0; kt < T; ++kt)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                if (16 * kt + 4 * kk < n) {
+#pragma unroll
+                    for (int a = 0; a < T; ++a) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
+                }
+    }
 #else
 #pragma unroll
     for (int a = 0; a < T; ++a)
