@@ -408,7 +408,9 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         }
         double w, luq[4];
         GainOut go;
-        bool ok = schur_block_pivots<MM, true>(Mn, lpr, w, luq, g, c, &go, sm.col, sm.lu4);
+        // (LPW: lu rides in W's column 0 -- the cache's w slot is read on the
+        // x columns only, and go.T still carries Luu^{-1} for it)
+        bool ok = schur_block_pivots<MM, true, (bool)PDPLQR_SCHUR_LPW>(Mn, lpr, w, luq, g, c, &go, sm.col, sm.lu4);
         Pm = Mn;
 #pragma unroll
         for (int r = 0; r < 4; ++r) prow[r] = lpr[r];
