@@ -69,18 +69,43 @@ struct KKTRicArgs {
     int nc_last;              // constraint rows of the terminal stage
 };
 
-// record per stage: K~ (m x n row-major) | k~ (m) | p_{k+1} (n) | P~_{k+1}
-// (fp64; packed lower, pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full
-// matrix row-major: three unmasked stores a lane, no index arithmetic)
+// Record per stage (PDPLQR_KKT_EHAT = 1, default):
+//     K~ (m x n row-major) | k~ (m) | E^ = (I - rho_dyn P~_{k+1}) E~ | c^
+// with c^ = (I - rho_dyn P~_{k+1})(c - rho_dyn p_{k+1}): the lambda
+// correction x+ = v - rho_dyn (P~ (v - rho_dyn p) + p), v = A x + B u + c, is
+// x+ = (I - rho_dyn P~)(v - rho_dyn p) = E^ [u; x] + c^, so the forward is a
+// plain gain-form rollout on E^, c^ (one group sum and no LDS round trip less
+// per stage, and E, c are not read again).  E^ is stored in the backward's C
+// layout: element 64 (r - 1) + 16 g + c = E^[x row 4 (r - 1) + g][tile column c].
+// 256 doubles = two 16-byte DMA instructions per lane.
+// PDPLQR_KKT_EHAT = 0: K~ | k~ | p_{k+1} (n) | P~_{k+1} (fp64; packed lower,
+// pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full matrix row-major), the
+// forward applying the correction itself.
+#ifndef PDPLQR_KKT_EHAT
+#define PDPLQR_KKT_EHAT 1
+#endif
 #ifndef PDPLQR_KKT_PT_FULL
 #define PDPLQR_KKT_PT_FULL 0
 #endif
 template <int NN, int MM>
 struct KRecShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
-    static constexpr int OK = 0, OKQ = n * m, OPV = OKQ + m, OPT = OPV + n;
-    static constexpr int FS = OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);  // doubles per stage
+    static constexpr int OK = 0, OKQ = n * m;
+    static constexpr int OEH = OKQ + m, OCH = OEH + 3 * 64;  // (EHAT)
+    static constexpr int OPV = OKQ + m, OPT = OPV + n;        // (!EHAT)
+    static constexpr int FS = PDPLQR_KKT_EHAT ? OCH + n
+                                              : OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);  // doubles per stage
+    static_assert(!PDPLQR_KKT_EHAT || (NN == 12 && MM == 4), "E^ record: 12/4");
 };
+
+// c^ store of the EHAT record: lanes (g, c >= 4) hold c^[c - 4] (column
+// layout); lanes (g, c < 4) take lane c + 4's value (DPP row_shl:4 on bank 0)
+// and write the same address as it, so every lane stores and duplicates agree
+__device__ __forceinline__ void kkt_store_chat(double *Rk_och, double v, int c) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), 0x104, 0xF, 0x1, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x104, 0xF, 0x1, false);
+    gstore(Rk_och + (c < 4 ? c : c - 4), __hiloint2double(hi, lo));
+}
 
 // Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
 // backward when KKTRicArgs::cache is set), per stage six 64-lane slots:
@@ -90,7 +115,11 @@ struct KRecShape {
 //   5     rho D (lane (g, c): rho_g D[g][c], stage 0 without the x columns)
 // so that lp = h~ + q + E^^T p - (rho D)^T g, lu' = T lu, k~ = T^T lu',
 // p_k = lp_x - Lxu lu': the right-hand-side dependent part of the backward.
-constexpr int KKT_CF = 6 * 64;
+// With the E^ record (PDPLQR_KKT_EHAT) the pass also rewrites
+// c^ = c0 - rho_dyn M^ p_{k+1}, from
+//   4     lanes 32..47: c0 = M^ c (column layout, lane 32 + c: c0[c - 4])
+//   6..8  M^ = I - rho_dyn P~ (x rows 4 (r - 1) + g, r = 1..3, lane (g, c))
+constexpr int KKT_CF = (PDPLQR_KKT_EHAT ? 9 : 6) * 64;
 
 // Stage record streamed by the backward: E | c | h~ | packed H~ | D | inv_rho | g
 template <int NN, int MM, int NC>
@@ -342,7 +371,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         d4 Pt;
         const bool pt_ok = ptilde_12(Pm, rd, g, c, Pt);
         // ---- record part 1: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]) and P~_{k+1} ----
-        {
+        if constexpr (!PDPLQR_KKT_EHAT) {
             // every lane stores (duplicates carry the same value): one store
             // instruction per part, no exec-mask branch
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
@@ -379,7 +408,25 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             part = -dgc * rq * gq;                 // -(D^T rho g)[c]
         }
         double *Ck = cache ? cache + ((long long)b * N + k) * KKT_CF : nullptr;
-        double qcol = 0.0;
+        double qcol = 0.0, c0col = 0.0;
+        d4 Mh;  // (EHAT) M^ = I - rho_dyn P~, x rows
+        if constexpr (PDPLQR_KKT_EHAT) {
+            // ---- record part 1: E^ = E~ - rho_dyn P~ E~ (= E~ - rho_dyn G), c^ ----
+            double cv = 0.0;
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                gstore(Rk + RS::OEH + 64 * (r - 1) + lane, __builtin_fma(-rd, G[r], in.E[r]));
+                Mh[r] = __builtin_fma(-rd, Pt[r], (4 * r + g == c) ? 1.0 : 0.0);
+                cv = __builtin_fma(Mh[r], __builtin_fma(-rd, prow[r], in.ct[r]), cv);  // M^ (c - rho_dyn p)
+            }
+            kkt_store_chat(Rk + RS::OCH, sum_groups(cv), c);
+            if (Ck) {
+                double v0 = 0.0;
+#pragma unroll
+                for (int r = 1; r < 4; ++r) v0 = __builtin_fma(Mh[r], in.ct[r], v0);
+                c0col = sum_groups(v0);
+            }
+        }
         if (Ck) {  // wave-uniform: the linear pass's copy of this stage's factor
 #pragma unroll
             for (int kk = 1; kk < 4; ++kk) {
@@ -388,6 +435,10 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             }
             qcol = sum_groups(qcol);
             gstore(Ck + 5 * 64 + lane, rhoD);
+            if constexpr (PDPLQR_KKT_EHAT) {
+#pragma unroll
+                for (int r = 1; r < 4; ++r) gstore(Ck + 64 * (5 + r) + lane, Mh[r]);
+            }
         }
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk) {
@@ -437,7 +488,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 #pragma unroll
                 for (int j = 0; j <= i; ++j) tv = (lane == 16 + 4 * i + j) ? go.T[i][j] : tv;
             gstore(Ck + 3 * 64 + lane, w);
-            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : tv);
+            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : ((PDPLQR_KKT_EHAT && g == 2) ? c0col : tv));
         }
         wave_sync();  // stage k's LDS reads retire before slot reuse
     };
@@ -520,6 +571,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     struct Set {
         double e[3], w, q, rd, h, gv;
         double T[10];
+        double mh[3], c0;  // (EHAT) M^ x rows, c0 = M^ c (loaded only with the E^ record)
     };
     // The three register sets are loaded by asm (global_load_dwordx2) and
     // waited for by an explicit vmcnt with the set's registers as operands:
@@ -527,7 +579,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     // rotates the sets through register copies).  LV loads per set; each
     // stage issues 2 stores; a set is waited for with at most 2 LV younger ops
     // outstanding (conservative in steady state, where 2 LV + 4 are).
-    constexpr int LV = 18;
+    constexpr int LV = PDPLQR_KKT_EHAT ? 22 : 18;
     auto gl = [](double &x, const double *p) {
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
     };
@@ -542,6 +594,11 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         gl(X.rd, Ck + 5 * 64 + lane);  // (zeros when NC = 0)
         gl(X.h, hb + (long long)k * s + c);
         gl(X.gv, NC > 0 ? gb + (long long)k * NC + (g < NC ? g : 0) : hb);
+        if constexpr (PDPLQR_KKT_EHAT) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) gl(X.mh[r], Ck + 64 * (6 + r) + lane);
+            gl(X.c0, Ck + 4 * 64 + 32 + c);
+        }
     };
     auto wait = [&](Set &X) {
         asm volatile("s_waitcnt vmcnt(%18)"
@@ -550,6 +607,8 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
                        "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
                      : "n"(2 * LV)
                      : "memory");
+        if constexpr (PDPLQR_KKT_EHAT)  // (same wait: ties the set's other registers to it)
+            asm volatile("" : "+v"(X.mh[0]), "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0));
     };
     // every set landed (the sets the tail does not read are dead to the
     // compiler, which would reuse their registers under the loads in flight)
@@ -564,12 +623,21 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
                      "+v"(Y.T[8]), "+v"(Y.T[9]));
         asm volatile("" : "+v"(Z.T[0]), "+v"(Z.T[1]), "+v"(Z.T[2]), "+v"(Z.T[3]), "+v"(Z.T[4]), "+v"(Z.T[5]),
                      "+v"(Z.T[6]), "+v"(Z.T[7]), "+v"(Z.T[8]), "+v"(Z.T[9]));
+        if constexpr (PDPLQR_KKT_EHAT)
+            asm volatile("" : "+v"(X.mh[0]), "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0), "+v"(Y.mh[0]), "+v"(Y.mh[1]),
+                         "+v"(Y.mh[2]), "+v"(Y.c0), "+v"(Z.mh[0]), "+v"(Z.mh[1]), "+v"(Z.mh[2]), "+v"(Z.c0));
     };
+    const double rdn = A.rho_dyn;
     auto stage = [&](Set &X, int k) {
         wait(X);
         if (NC == 0) X.rd = X.gv = 0.0;
         double *Rk = RB + (long long)k * RS::FS;
-        {  // record: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
+        if constexpr (PDPLQR_KKT_EHAT) {  // record: c^ = c0 - rho_dyn M^ p_{k+1}
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) v = __builtin_fma(X.mh[r], prow[r + 1], v);
+            kkt_store_chat(Rk + RS::OCH, __builtin_fma(-rdn, sum_groups(v), X.c0), c);
+        } else {  // record: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
             const double pv = __builtin_fma(prow[1], (double)(cp == 1), __builtin_fma(prow[2], (double)(cp == 2),
                                                                                        prow[3] * (double)(cp == 3)));
@@ -656,12 +724,15 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
     constexpr int n = 12, m = 4, s = 16, NC = 4;
     using RS = KRecShape<n, m>;
     constexpr int FS = RS::FS;
-    constexpr int OE = 0, OC = n * s, OF = OC + n, OW = OF + FS, OD = OW + s, OZ = OD + NC * s, OY = OZ + NC,
-                  OLB = OY + NC, OUB = OLB + NC, ORH = OUB + NC, OIR = ORH + NC, OH = OIR + NC;
+    // ring record: [E | c |] F (the rollout record) [| ADMM rows]; with the E^
+    // record (PDPLQR_KKT_EHAT) E and c are not read (E^, c^ carry them)
+    constexpr bool EH = PDPLQR_KKT_EHAT;
+    constexpr int OE = 0, OC = EH ? 0 : n * s, OF = EH ? 0 : OC + n, OW = OF + FS, OD = OW + s, OZ = OD + NC * s,
+                  OY = OZ + NC, OLB = OY + NC, OUB = OLB + NC, ORH = OUB + NC, OIR = ORH + NC, OH = OIR + NC;
     constexpr int REC = UPD ? OH + s : OW, CH = REC / 2, NI = (CH + 63) / 64;
     constexpr int TAIL = CH - (NI - 1) * 64;
     constexpr int NQ = 3;
-    static_assert(REC % 2 == 0 && OW % 2 == 0 && (NI == 3 || NI == 4 || NI == 5), "record layout");
+    static_assert(REC % 2 == 0 && OW % 2 == 0 && (NI >= 2 && NI <= 5), "record layout");
     // vm ops per stage: NI DMA + the stores (plain: the w~ store; UPD: z, y, w
     // [+ g, h~ with FUSE], each an instruction with live lanes)
     constexpr int ST = UPD ? (FUSE ? 5 : 3) : 1;
@@ -763,18 +834,25 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
         const double g0 = (g == 0) ? 1.0 : 0.0;
         double kx[NQ], ex[NQ], eu[m], xt[NQ];
         double pt[NQ];
+        // (EH) E^ row cn: element 64 (cn >> 2) + 16 (cn & 3) + tile column
+        const int eh = RS::OEH + 64 * (cn >> 2) + 16 * (cn & 3);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int t = 4 * q + g;
             kx[q] = F[RS::OK + cm * n + t];
-            ex[q] = R[OE + (m + t) * n + cn];
-            pt[q] = F[RS::OPT + (PDPLQR_KKT_PT_FULL ? t * n + cn : t >= cn ? pidx(t, cn, n) : pidx(cn, t, n))];  // P~[4 q + g][cl]
+            if constexpr (EH) {
+                ex[q] = F[eh + m + t];
+                pt[q] = 0.0;
+            } else {
+                ex[q] = R[OE + (m + t) * n + cn];
+                pt[q] = F[RS::OPT + (PDPLQR_KKT_PT_FULL ? t * n + cn : t >= cn ? pidx(t, cn, n) : pidx(cn, t, n))];  // P~[4 q + g][cl]
+            }
         }
 #pragma unroll
-        for (int i = 0; i < m; ++i) eu[i] = g0 * R[OE + i * n + cn];
+        for (int i = 0; i < m; ++i) eu[i] = g0 * (EH ? F[eh + i] : R[OE + i * n + cn]);
         const double kq = F[RS::OKQ + cm];
-        const double cc = R[OC + cn];
-        const double pv = F[RS::OPV + cn];
+        const double cc = EH ? F[RS::OCH + cn] : R[OC + cn];
+        const double pv = EH ? 0.0 : F[RS::OPV + cn];
         // ---- chain ----
         const int lx = UPD ? (cl >= m ? cl - m : 0) : ((lane >= m && lane < s) ? lane - m : 0);
         const double xk = k == 0 ? sx0[lx] : sx[lx];  // ws[0]'s x part is the call's x0
@@ -794,17 +872,20 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
             if (cl == i) myu = ui;
             a = __builtin_fma(eu[i], ui, a);
         }
-        a = sum_groups(a) + cc;  // v = A x + B u + c (every group)
+        a = sum_groups(a) + cc;  // v = A x + B u + c (every group); EH: x+ = E^ [u; x] + c^
         if constexpr (UPD) upd(R, k, (cl < m) ? myu : xk);  // every group holds w~_k[cl]
         else if (lane < s) gstore(wb + (long long)k * s + lane, (lane < m) ? myu : xk);
-        // ---- lambda correction: x+ = v - rho_dyn (P~ (v - rho_dyn p) + p) ----
-        if (g == 0 && cl < n) sz[cl] = __builtin_fma(-rho_dyn, pv, a);
-        wave_sync();
-        double y = 0.0;
+        double xn = a;
+        if constexpr (!EH) {
+            // ---- lambda correction: x+ = v - rho_dyn (P~ (v - rho_dyn p) + p) ----
+            if (g == 0 && cl < n) sz[cl] = __builtin_fma(-rho_dyn, pv, a);
+            wave_sync();
+            double y = 0.0;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) y = __builtin_fma(pt[q], sz[4 * q + g], y);
-        y = sum_groups(y);
-        const double xn = __builtin_fma(-rho_dyn, y + pv, a);
+            for (int q = 0; q < NQ; ++q) y = __builtin_fma(pt[q], sz[4 * q + g], y);
+            y = sum_groups(y);
+            xn = __builtin_fma(-rho_dyn, y + pv, a);
+        }
         wave_sync();  // all reads of x_k done before it is overwritten
         if (g == 0 && cl < n) sx[cl] = xn;
         wave_sync();
