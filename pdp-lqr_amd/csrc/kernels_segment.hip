@@ -226,12 +226,20 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
 #pragma unroll
             for (int bt = 0; bt < 2; ++bt) {
                 G[a][bt] = d4{0.0, 0.0, 0.0, 0.0};
-                if (a < T && bt < T && 16 * a < s && 16 * bt < s)
+                // one [u; x] tile (s <= 16, C2's 12/4): odd K chunks on a second
+                // accumulator -- the tile's chain is the only one in flight
+                constexpr bool SPL = PDPLQR_MFMA_SPLIT && CT && NN + MM <= 16;
+                d4 Go = d4{0.0, 0.0, 0.0, 0.0};
+                if (a < T && bt < T && 16 * a < s && 16 * bt < s) {
 #pragma unroll
                     for (int kk = 0; kk < 8; ++kk)
-                        if ((kk >> 2) < T && kk >= k0 && kk <= k1)
-                            G[a][bt] = mfma_f64(Q[(kk >> 2) < T ? (kk >> 2) : 0][a < T ? a : 0][kk & 3],
-                                                in.E[kk][bt], G[a][bt]);
+                        if ((kk >> 2) < T && kk >= k0 && kk <= k1) {
+                            const double av = Q[(kk >> 2) < T ? (kk >> 2) : 0][a < T ? a : 0][kk & 3];
+                            if (SPL && (kk & 1)) Go = mfma_f64(av, in.E[kk][bt], Go);
+                            else G[a][bt] = mfma_f64(av, in.E[kk][bt], G[a][bt]);
+                        }
+                    if (SPL) G[a][bt] += Go;
+                }
             }
         // ---- aug column in column layout (reads the old y columns = F^T):
         //      [u; x]: h~ + G^T c~ + E~^T p~ ; y: F c (+ f below, row layout) ----
@@ -262,13 +270,17 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
                 if (a < T && 16 * a < s) {
                     const d4 h0 = (bt < 2) ? in.H[a][bt < 2 ? bt : 0] : d4{0.0, 0.0, 0.0, 0.0};
                     acc[a] = cux ? h0 : d4{0.0, 0.0, 0.0, 0.0};
+                    constexpr bool SPL = PDPLQR_MFMA_SPLIT && CT && NN + MM <= 16;
+                    d4 ao = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                     for (int kk = 0; kk < 8; ++kk)
                         if ((kk >> 2) < T && kk >= k0 && kk <= k1) {
                             const double qv = Q[(kk >> 2) < T ? (kk >> 2) : 0][bt][kk & 3];
                             const double bop = (bt < 2 && cux) ? G[kk >> 2][bt < 2 ? bt : 0][kk & 3] : qv;
-                            acc[a] = mfma_f64(in.E[kk][a], bop, acc[a]);
+                            if (SPL && (kk & 1)) ao = mfma_f64(in.E[kk][a], bop, ao);
+                            else acc[a] = mfma_f64(in.E[kk][a], bop, acc[a]);
                         }
+                    if (SPL) acc[a] += ao;
                 }
             }
 #pragma unroll
@@ -593,10 +605,25 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                     avP[a][q] = hx * (Xq[ii + (kx - m) * XLD] + Xq[(kx - m) + ii * XLD]);
                 }
             }
+            if constexpr (PDPLQR_MFMA_SPLIT) {
+                // even / odd K chunks on separate accumulators: four chains of
+                // NK / 2 instead of two of NK (a dependent f64 MFMA waits ~186 cycles)
+                d4 Go[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
-            for (int q = 0; q < NK; ++q)
+                for (int q = 0; q < NK; ++q)
 #pragma unroll
-                for (int a = 0; a < 2; ++a) G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
+                    for (int a = 0; a < 2; ++a) {
+                        if (q & 1) Go[a] = mfma_f64(avP[a][q], bvE[q], Go[a]);
+                        else G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
+                    }
+#pragma unroll
+                for (int a = 0; a < 2; ++a) G[a] += Go[a];
+            } else {
+#pragma unroll
+                for (int q = 0; q < NK; ++q)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
+            }
         }
         AUG_MARK(2);
         // ---- rows [u; x]: H~ + E~^T G ([u; x] columns), E~^T Q[x, col] (y / aug columns) ----
@@ -623,13 +650,20 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                     const int ic = on ? i : 0, jc = on ? col : 0;
                     Mu[a][r] = (on ? 1.0 : 0.0) * Hs[ic >= jc ? pidx(ic, jc, s) : pidx(jc, ic, s)];
                 }
+            d4 Mo[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
             for (int q = 0; q < NK; ++q) {
                 const int kk = K0 + q;
                 const double bv = cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3];
 #pragma unroll
-                for (int a = 0; a < 2; ++a) Mu[a] = mfma_f64(avE[a][q], bv, Mu[a]);
+                for (int a = 0; a < 2; ++a) {
+                    if (PDPLQR_MFMA_SPLIT && (q & 1)) Mo[a] = mfma_f64(avE[a][q], bv, Mo[a]);
+                    else Mu[a] = mfma_f64(avE[a][q], bv, Mu[a]);
+                }
             }
+            if constexpr (PDPLQR_MFMA_SPLIT)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) Mu[a] += Mo[a];
         }
         // ---- aug pieces: lpa[col] = h~ + G^T c ([u; x] columns), fcv = F c (y columns) ----
         {
