@@ -975,8 +975,7 @@ struct SegRec {
     static constexpr int n = NN, m = MM, s = NN + MM, FRS = s * m + m;
     static constexpr int OE = 0, OC = n * s, OF = OC + n, OG = OF + FRS, REC = OG + m * n;
     static constexpr int CH = REC / 2, NI = (CH + 63) / 64, TAIL = CH - (NI - 1) * 64;
-    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FRS % 2 == 0 && (m * n) % 2 == 0 && s > 16 &&
-                               s <= 32;
+    static constexpr bool ok = (n * s) % 2 == 0 && n % 2 == 0 && FRS % 2 == 0 && (m * n) % 2 == 0 && s <= 32;
 };
 
 template <int NN, int MM, int D>
@@ -985,7 +984,7 @@ __global__ __launch_bounds__(64) void k_seg_fwd_dma(Shape sh, const double *__re
                                                     double *__restrict__ ws, SegFwd sf) {
     using SR = SegRec<NN, MM>;
     static_assert(SR::ok, "segment rollout record layout");
-    constexpr int R = 2, NJ = 4 * R, n = NN, m = MM, s = NN + MM, NI = SR::NI;
+    constexpr int R = NN + MM <= 16 ? 1 : 2, NJ = 4 * R, n = NN, m = MM, s = NN + MM, NI = SR::NI;
     constexpr int VM = (1 + R) + (D - 2) * (NI + 1 + R) + NI;  // vm ops younger than stage k's DMA
     static_assert(VM <= 63, "vmcnt range");
     __shared__ __attribute__((aligned(16))) double ring[D][SR::REC];
@@ -1305,6 +1304,16 @@ int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c
                                double *ws, hipStream_t st) {
     if (sh.n == 24 && sh.m == 8 && segfwd_aligned(sh, E, c, FR, sf) && !getenv("PDPLQR_NO_DMA")) {
         hipLaunchKernelGGL((k_seg_fwd_dma<24, 8, 3>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
+                           FR, ws, sf);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        return PDPLQR_OK;
+    }
+    // 12/4 (C2's one-problem solve: segments of a few stages): a 5-deep ring
+    // puts a whole short segment's records in flight at once -- one memory
+    // latency per segment instead of one per stage (k_riccati_fwd prefetches
+    // one stage ahead)
+    if (sh.n == 12 && sh.m == 4 && segfwd_aligned(sh, E, c, FR, sf) && !getenv("PDPLQR_NO_DMA")) {
+        hipLaunchKernelGGL((k_seg_fwd_dma<12, 4, 5>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
                            FR, ws, sf);
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
