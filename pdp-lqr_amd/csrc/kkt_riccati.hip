@@ -600,16 +600,32 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
             gl(X.c0, Ck + 4 * 64 + 32 + c);
         }
     };
-    auto wait = [&](Set &X) {
-        asm volatile("s_waitcnt vmcnt(%18)"
-                     : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
-                       "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
-                       "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
-                     : "n"(2 * LV)
-                     : "memory");
-        if constexpr (PDPLQR_KKT_EHAT)  // (same wait: ties the set's other registers to it)
-            asm volatile("" : "+v"(X.mh[0]), "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0));
+    // "X landed" with exactly the vm ops issued after X's loads still allowed
+    // in flight: the other two sets' loads (2 LV) and the stores of the stages
+    // in between (2 per stage) -- 2 LV at the first stage, 2 LV + 2 at the
+    // second, 2 LV + 4 from the third on (a looser count would also wait for
+    // the next set's first loads and cut the lookahead from three stages to two)
+    auto wait = [&](Set &X, auto cnt) {
+        if constexpr (PDPLQR_KKT_EHAT)
+            asm volatile("s_waitcnt vmcnt(%22)"
+                         : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
+                           "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
+                           "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv), "+v"(X.mh[0]),
+                           "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0)
+                         : "n"(decltype(cnt)::value)
+                         : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%18)"
+                         : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
+                           "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
+                           "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
+                         : "n"(decltype(cnt)::value)
+                         : "memory");
     };
+    using W0 = std::integral_constant<int, 2 * LV>;
+    using W1 = std::integral_constant<int, 2 * LV + 2>;
+    using W2 = std::integral_constant<int, 2 * LV + 4>;
+    static_assert(2 * LV + 4 <= 63, "vmcnt range");
     // every set landed (the sets the tail does not read are dead to the
     // compiler, which would reuse their registers under the loads in flight)
     auto wait_all = [&](Set &X, Set &Y, Set &Z) {
@@ -628,8 +644,8 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
                          "+v"(Y.mh[2]), "+v"(Y.c0), "+v"(Z.mh[0]), "+v"(Z.mh[1]), "+v"(Z.mh[2]), "+v"(Z.c0));
     };
     const double rdn = A.rho_dyn;
-    auto stage = [&](Set &X, int k) {
-        wait(X);
+    auto stage = [&](Set &X, int k, auto cnt) {
+        wait(X, cnt);
         if (NC == 0) X.rd = X.gv = 0.0;
         double *Rk = RB + (long long)k * RS::FS;
         if constexpr (PDPLQR_KKT_EHAT) {  // record: c^ = c0 - rho_dyn M^ p_{k+1}
@@ -688,17 +704,26 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     load(X1, N >= 2 ? N - 2 : 0);
     load(X2, N >= 3 ? N - 3 : 0);
     int k = N - 1;
-    for (; k >= 2; k -= 3) {
-        stage(X0, k);
+    if (k >= 2) {  // first trip: fewer younger ops than in the steady state
+        stage(X0, k, W0{});
         load(X0, k >= 3 ? k - 3 : 0);
-        stage(X1, k - 1);
+        stage(X1, k - 1, W1{});
         load(X1, k >= 4 ? k - 4 : 0);
-        stage(X2, k - 2);
+        stage(X2, k - 2, W2{});
+        load(X2, k >= 5 ? k - 5 : 0);
+        k -= 3;
+    }
+    for (; k >= 2; k -= 3) {
+        stage(X0, k, W2{});
+        load(X0, k >= 3 ? k - 3 : 0);
+        stage(X1, k - 1, W2{});
+        load(X1, k >= 4 ? k - 4 : 0);
+        stage(X2, k - 2, W2{});
         load(X2, k >= 5 ? k - 5 : 0);
     }
     wait_all(X0, X1, X2);
-    if (k >= 0) stage(X0, k);
-    if (k >= 1) stage(X1, k - 1);
+    if (k >= 0) stage(X0, k, W0{});
+    if (k >= 1) stage(X1, k - 1, W0{});
 }
 
 // ---------------------------------------------------------------------------
