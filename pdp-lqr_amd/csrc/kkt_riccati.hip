@@ -258,7 +258,11 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     using SH = KBwdShape<NN, MM, NC>;
     using RS = KRecShape<NN, MM>;
     constexpr int NI = SH::NI, n = NN, m = MM, s = NN + MM;
-    constexpr int ST = 3;  // record stores per stage: [K~ | k~], p_{k+1}, P~_{k+1}
+    // record store instructions per stage, all issued every stage (the counts
+    // below are exact without the ADMM cache; its extra stores only make the
+    // waits stricter): [K~ | k~] + E^ (3) + c^, or [K~ | k~] + p_{k+1} + P~ (3)
+    // (the packed P~ stores are lane-masked but every instruction has live lanes)
+    constexpr int ST = 5;
     __shared__ SchurSmem sm;
     __shared__ __attribute__((aligned(16))) double stg[2][SH::SLOT];
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
