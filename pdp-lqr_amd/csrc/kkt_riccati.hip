@@ -99,12 +99,12 @@ struct KRecShape {
 };
 
 // c^ store of the EHAT record: lanes (g, c >= 4) hold c^[c - 4] (column
-// layout); lanes (g, c < 4) take lane c + 4's value (DPP row_shl:4 on bank 0)
-// and write the same address as it, so every lane stores and duplicates agree
+// layout); lanes (g, c < 4) take lane c + 4's value and write the same address
+// as it, so every lane stores and duplicates agree (off the chain: one
+// ds_bpermute)
 __device__ __forceinline__ void kkt_store_chat(double *Rk_och, double v, int c) {
-    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), 0x104, 0xF, 0x1, false);
-    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x104, 0xF, 0x1, false);
-    gstore(Rk_och + (c < 4 ? c : c - 4), __hiloint2double(hi, lo));
+    const double u = __shfl_down(v, 4, 16);
+    gstore(Rk_och + (c < 4 ? c : c - 4), c < 4 ? u : v);
 }
 
 // Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
