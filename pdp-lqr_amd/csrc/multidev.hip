@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -79,18 +80,24 @@ struct Rccl {
     fn_group group_start = nullptr, group_end = nullptr;
     fn_destroy destroy = nullptr;
     fn_err err = nullptr;
+    // once per process (handles may be created on several threads)
     bool load() {
-        if (so) return true;
+        static std::once_flag once;
+        std::call_once(once, [this] { resolve(); });
+        return ok;
+    }
+    bool ok = false;
+    void resolve() {
         so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!so) return false;
+        if (!so) return;
         init_all = (fn_init_all)dlsym(so, "ncclCommInitAll");
         all_gather = (fn_all_gather)dlsym(so, "ncclAllGather");
         group_start = (fn_group)dlsym(so, "ncclGroupStart");
         group_end = (fn_group)dlsym(so, "ncclGroupEnd");
         destroy = (fn_destroy)dlsym(so, "ncclCommDestroy");
         err = (fn_err)dlsym(so, "ncclGetErrorString");
-        return init_all && all_gather && group_start && group_end && destroy;
+        ok = init_all && all_gather && group_start && group_end && destroy;
     }
 };
 Rccl g_rccl;
