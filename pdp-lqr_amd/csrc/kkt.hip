@@ -1572,7 +1572,7 @@ int kkt_backward_linear(pdplqr_handle h, const double *inv_rho) {
     KKTState *ks = h->kkt;
     const Shape &sh = h->sh;
     return launch_kkt_ric_nofact(sh, ks->ric, ks->Df ? ks->Df : h->D, h->hw, h->gw, inv_rho, h->d_off, h->y_off,
-                                 h->ncs[sh.N], ks->ncache, ks->rec, h->stream);
+                                 h->ncs[sh.N], h->cfg.rho_dyn, ks->ncache, ks->rec, h->stream);
 }
 
 int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {

@@ -1274,7 +1274,7 @@ size_t kkt_ric_cache_doubles(const Shape &sh, int ric) {
 }
 
 int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double *hw, const double *gw,
-                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last,
+                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn,
                           const double *cache, double *rec, hipStream_t st) {
     if (nc != 0 && nc != 4) return PDPLQR_ERR_UNSUPPORTED;
     KKTRicArgs a;
@@ -1289,7 +1289,7 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
     a.rec = rec;
     a.cache = const_cast<double *>(cache);
     a.status = nullptr;
-    a.rho_dyn = 0.0;
+    a.rho_dyn = rho_dyn;  // (the E^ record's c^ = M^ c - rho_dyn M^ p)
     a.nc_last = nc_last;
     if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_nofact<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
     else hipLaunchKernelGGL(k_kkt_ric_nofact<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);

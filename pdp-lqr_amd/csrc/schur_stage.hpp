@@ -82,14 +82,16 @@ struct SchurSmem {
 // substitution with Luu (no explicit T = Luu^{-1}, 16 fewer uniform VALU a
 // stage); PDPLQR_SCHUR_DPP: per-row-group picks and the column-0 merge as
 // masked DPP moves (row_mask / bank_mask) instead of v_cndmask pairs (m = 4)
+// (default on: same-box A/B r4f, headline backward 3.22 -> 2.96 ms with LPW,
+// C5 KKT 1.297 -> 1.260 ms, C5 Riccati 0.913 -> 0.872 ms)
 #ifndef PDPLQR_SCHUR_SUBST
-#define PDPLQR_SCHUR_SUBST 0
+#define PDPLQR_SCHUR_SUBST 1
 #endif
 #ifndef PDPLQR_SCHUR_DPP
 #define PDPLQR_SCHUR_DPP 0
 #endif
 #ifndef PDPLQR_SCHUR_LPW
-#define PDPLQR_SCHUR_LPW 0
+#define PDPLQR_SCHUR_LPW 1
 #endif
 
 // G = P E~ and M = H~ + E~^T G as independent per-chunk MFMAs summed by VALU

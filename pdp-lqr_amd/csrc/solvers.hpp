@@ -51,7 +51,7 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
 // linear-only pass on the factor cache the backward wrote (ric 0 / 4 only)
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric);  // per problem; 0 where unsupported
 int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double *hw, const double *gw,
-                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last,
+                          const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn,
                           const double *cache, double *rec, hipStream_t st);
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
                            double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric);
