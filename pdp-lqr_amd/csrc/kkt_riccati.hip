@@ -626,9 +626,12 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
                          : "n"(decltype(cnt)::value)
                          : "memory");
     };
+#ifndef PDPLQR_KKT_LV_EXACT
+#define PDPLQR_KKT_LV_EXACT 1
+#endif
     using W0 = std::integral_constant<int, 2 * LV>;
-    using W1 = std::integral_constant<int, 2 * LV + 2>;
-    using W2 = std::integral_constant<int, 2 * LV + 4>;
+    using W1 = std::integral_constant<int, 2 * LV + (PDPLQR_KKT_LV_EXACT ? 2 : 0)>;
+    using W2 = std::integral_constant<int, 2 * LV + (PDPLQR_KKT_LV_EXACT ? 4 : 0)>;
     static_assert(2 * LV + 4 <= 63, "vmcnt range");
     // every set landed (the sets the tail does not read are dead to the
     // compiler, which would reuse their registers under the loads in flight)
