@@ -88,9 +88,12 @@ def load_pmc_traffic(workload_tag, kernel=None):
     rocprofv3 PMC summary, or None.  Only a summary collected on the same
     workload AND the same backward kernel counts."""
     best = None
+    names = [kernel] if kernel else []
+    if kernel and kernel.endswith(", 0>"):  # pre-round-4 name of the same kernel
+        names.append(kernel[:-4] + ">")
     for d in _pmc_summaries():
         if (d.get("workload") == workload_tag and "bytes_per_launch" in d
-                and (kernel is None or d.get("dominant_kernel", "").endswith(kernel))):
+                and (kernel is None or any(d.get("dominant_kernel", "").endswith(k) for k in names))):
             best = d
     return best
 
@@ -762,8 +765,9 @@ def bwd_kernel_name(n, m, keep):
     kernels_riccati.hip launch_riccati_backward)."""
     s = n + m
     if not keep and s <= 16:
-        if (n, m) == (12, 4):  # the record form rides in the template (kernels_schur.hip GAIN)
-            return f"k_riccati_bwd_schur<12, 4, {'false' if os.environ.get('PDPLQR_REC_L') else 'true'}>"
+        if (n, m) == (12, 4):  # the record form rides in the template (kernels_schur.hip GAIN; NC = 0:
+            # no fused penalty rows -- summaries before round 4 name it without that argument)
+            return f"k_riccati_bwd_schur<12, 4, {'false' if os.environ.get('PDPLQR_REC_L') else 'true'}, 0>"
         return "k_riccati_bwd_schur<0, 0, false>"
     if (n, m) == (12, 4):
         return f"k_riccati_bwd_fast<1, 12, 4, {str(bool(keep)).lower()}>"
