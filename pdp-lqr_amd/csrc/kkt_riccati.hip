@@ -99,12 +99,13 @@ struct KRecShape {
 };
 
 // c^ store of the EHAT record: lanes (g, c >= 4) hold c^[c - 4] (column
-// layout); lanes (g, c < 4) take lane c + 4's value and write the same address
-// as it, so every lane stores and duplicates agree (off the chain: one
-// ds_bpermute)
+// layout) and store it (the four row groups write equal values); lanes c < 4
+// are masked off.  One store instruction with live lanes every stage, so the
+// callers' fixed vm-op counts hold; the loads in flight are asm-issued, so the
+// exec-mask region cannot make the compiler drain them.  (A cross-lane copy
+// for lanes c < 4 cost an LDS round trip a stage in the linear ADMM pass.)
 __device__ __forceinline__ void kkt_store_chat(double *Rk_och, double v, int c) {
-    const double u = __shfl_down(v, 4, 16);
-    gstore(Rk_och + (c < 4 ? c : c - 4), c < 4 ? u : v);
+    if (c >= 4) gstore(Rk_och + (c - 4), v);
 }
 
 // Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
@@ -534,6 +535,14 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 // wave per problem; the cache slots are read three stages ahead into registers
 // (three sets, the loop unrolled by three so no register set is copied).
 // ---------------------------------------------------------------------------
+// global_load_dwordx2 with an immediate byte offset (signed 13 bits), asm-issued
+// like the other staging loads (the waits are explicit)
+template <int OFF>
+__device__ __forceinline__ void gl_at(double &x, const double *p) {
+    static_assert(OFF >= -4096 && OFF < 4096, "global offset range");
+    asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(x) : "v"(p), "n"(OFF) : "memory");
+}
+
 template <int NC>
 __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     constexpr int n = 12, m = 4, s = 16;
@@ -587,21 +596,38 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     auto gl = [](double &x, const double *p) {
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
     };
+    // the cache slots by three base addresses and the loads' immediate byte
+    // offsets (one address computation per base instead of one per load: at
+    // one wave per SIMD every VALU instruction of the pass is on its time)
     auto load = [&](Set &X, int k) {
         const double *Ck = Cb + (long long)k * KKT_CF;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) gl(X.e[r], Ck + 64 * r + lane);
-        gl(X.w, Ck + 3 * 64 + lane);
-        gl(X.q, Ck + 4 * 64 + c);
-#pragma unroll
-        for (int t = 0; t < 10; ++t) gl(X.T[t], Ck + 4 * 64 + 16 + (t < 1 ? 0 : t < 3 ? t + 3 : t < 6 ? t + 5 : t + 6));
-        gl(X.rd, Ck + 5 * 64 + lane);  // (zeros when NC = 0)
+        const double *B1 = Ck + 4 * 64 + lane;  // lane-indexed slots, around slot 4
+        const double *B2 = Ck + 4 * 64 + c;     // column-indexed entries of slot 4
+        const double *B3 = Ck + 4 * 64 + 16;    // T (wave-uniform)
+        gl_at<-4 * 512>(X.e[0], B1);
+        gl_at<-3 * 512>(X.e[1], B1);
+        gl_at<-2 * 512>(X.e[2], B1);
+        gl_at<-1 * 512>(X.w, B1);
+        gl_at<0>(X.q, B2);
+        // T[i][j] at 4 i + j
+        gl_at<0>(X.T[0], B3);
+        gl_at<8 * 4>(X.T[1], B3);
+        gl_at<8 * 5>(X.T[2], B3);
+        gl_at<8 * 8>(X.T[3], B3);
+        gl_at<8 * 9>(X.T[4], B3);
+        gl_at<8 * 10>(X.T[5], B3);
+        gl_at<8 * 12>(X.T[6], B3);
+        gl_at<8 * 13>(X.T[7], B3);
+        gl_at<8 * 14>(X.T[8], B3);
+        gl_at<8 * 15>(X.T[9], B3);
+        gl_at<512>(X.rd, B1);  // (zeros when NC = 0)
         gl(X.h, hb + (long long)k * s + c);
         gl(X.gv, NC > 0 ? gb + (long long)k * NC + (g < NC ? g : 0) : hb);
         if constexpr (PDPLQR_KKT_EHAT) {
-#pragma unroll
-            for (int r = 0; r < 3; ++r) gl(X.mh[r], Ck + 64 * (6 + r) + lane);
-            gl(X.c0, Ck + 4 * 64 + 32 + c);
+            gl_at<2 * 512>(X.mh[0], B1);
+            gl_at<3 * 512>(X.mh[1], B1);
+            gl_at<4 * 512>(X.mh[2], B1);
+            gl_at<8 * 32>(X.c0, B2);
         }
     };
     // "X landed" with exactly the vm ops issued after X's loads still allowed
