@@ -501,7 +501,7 @@ def bench_single(local, dev, dist, steps=10, warmup=3):
     return res
 
 
-def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
+def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024, admm=True):
     """C5: conic (box-constrained u) LQ, N = 512, 12/4, nc = 4 (D = [I 0]) on
     every stage but the terminal, batch 1024, rho = 0.1, random y, z, w-bar.
     One ADMM inner solve = backward + forward, timed for the KKT path
@@ -555,6 +555,10 @@ def bench_conic(local, dev, dist, steps=5, warmup=2, N=512, batch=1024):
             "roofline": roofline_block(bst, N * batch, t * 1e3, f"C5_N{N}_b{batch}", kern,
                                        kernel_desc="backward + forward")}
         bs.close()
+    if not admm:  # (scripts/prof_secondary.py c5solve: PMC passes of the solves alone)
+        del E, H, D
+        torch.cuda.empty_cache()
+        return res
     # the ADMM outer loop on the same data (pdplqr_admm_solve): |u| <= 0.5,
     # rho = 1, from a cold start.  (a) 100 fixed iterations (eps = 0, one
     # termination test at the end): iterations/s of the batch; (b) a run to

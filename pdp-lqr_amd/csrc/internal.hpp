@@ -121,7 +121,9 @@ struct pdplqr_handle_s {
     // update_problem_data calls with the same sigma, re-formed after set_model
     // or clear_workspace
     bool hw_cached = false;
-    // the last serial backward left the gain-form rollout record (schur_gain_record)
+    // the last backward left the gain-form rollout record: the serial path's
+    // [K~|k~] (schur_gain_record) or the KKT path's E^ record (kkt_ric_rec_ehat;
+    // a cache-writing ADMM backward leaves the P~ record, rec_gain false)
     bool rec_gain = false;
     bool graph_rec_gain = false;  // record form the captured forward graph reads
     double hw_sigma = 0.0;

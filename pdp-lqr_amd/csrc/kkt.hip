@@ -1554,6 +1554,7 @@ int kkt_backward_cached(pdplqr_handle h, const double *inv_rho) {
     const Shape &sh = h->sh;
     int rc;
     if (!ks->ncache && (rc = kalloc(h, &ks->ncache, sh.batch * kkt_ric_cache_doubles(sh, ks->ric)))) return rc;
+    h->rec_gain = false;  // the cache-writing backward leaves the P~ record (pdplqr_handle_s::rec_gain)
     rc = launch_kkt_ric_backward(sh, ks->ric, ks->Ef ? ks->Ef : h->E, h->c, ks->Df ? ks->Df : h->D, h->Hw, h->hw,
                                  h->gw, inv_rho, h->d_off, h->y_off, h->ncs[sh.N], h->cfg.rho_dyn, ks->rec, h->status,
                                  h->stream, ks->ncache);
@@ -1580,7 +1581,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
     const Shape &sh = h->sh;
     if (ks->ric >= 0)
         return launch_kkt_ric_forward(sh, ks->Ef ? ks->Ef : h->E, h->c, ks->rec, x0, ks->x0acc, ws, h->cfg.rho_dyn,
-                                      h->stream, ks->ric);
+                                      h->stream, ks->ric, h->rec_gain);
     KKTArgs a = kkt_args(h);
     const size_t P = ks->P, PP = P * P;
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), probs((unsigned)sh.batch), wave(64);
@@ -1605,7 +1606,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
 
 int kkt_forward_admm(pdplqr_handle h, const double *x0, const AdmmArgs &q, bool fuse, bool check) {
     KKTState *ks = h->kkt;
-    if (!ks || ks->ric != 4) return PDPLQR_ERR_UNSUPPORTED;
+    if (!ks || ks->ric != 4 || h->rec_gain) return PDPLQR_ERR_UNSUPPORTED;
     return launch_kkt_ric_forward_admm(h->sh, ks->Ef ? ks->Ef : h->E, h->c, ks->rec, x0, ks->x0acc, h->cfg.rho_dyn,
                                        q, fuse, check, h->stream);
 }
@@ -1613,5 +1614,8 @@ int kkt_forward_admm(pdplqr_handle h, const double *x0, const AdmmArgs &q, bool 
 int kkt_dim(pdplqr_handle h) { return h->kkt ? h->kkt->dim : 0; }
 
 bool kkt_ric_active(pdplqr_handle h) { return h->kkt && h->kkt->ric >= 0; }
+
+// a plain backward of this handle's KKT path leaves the E^ record
+bool kkt_plain_rec_ehat(pdplqr_handle h) { return h->kkt && h->kkt->ric >= 0 && kkt_ric_rec_ehat(h->kkt->ric); }
 
 }  // namespace pdplqr

@@ -78,9 +78,14 @@ struct KKTRicArgs {
 // per stage, and E, c are not read again).  E^ is stored in the backward's C
 // layout: element 64 (r - 1) + 16 g + c = E^[x row 4 (r - 1) + g][tile column c].
 // 256 doubles = two 16-byte DMA instructions per lane.
-// PDPLQR_KKT_EHAT = 0: K~ | k~ | p_{k+1} (n) | P~_{k+1} (fp64; packed lower,
-// pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full matrix row-major), the
-// forward applying the correction itself.
+// The ADMM runs (a backward that writes the linear pass's cache, then the
+// linear pass) keep the P~ record K~ | k~ | p_{k+1} (n) | P~_{k+1} (fp64;
+// packed lower, pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full matrix
+// row-major) and the forward applies the correction itself: rewriting c^ in the
+// linear pass costs that pass more (one wave per SIMD: every instruction is on
+// its time) than the forward saves (profiles/r04).  Both forms share the
+// 256-double stage stride; the handle records which one the last backward
+// left (KKTState::rec_ehat).  PDPLQR_KKT_EHAT = 0: the P~ record always.
 #ifndef PDPLQR_KKT_EHAT
 #define PDPLQR_KKT_EHAT 1
 #endif
@@ -91,10 +96,10 @@ template <int NN, int MM>
 struct KRecShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
     static constexpr int OK = 0, OKQ = n * m;
-    static constexpr int OEH = OKQ + m, OCH = OEH + 3 * 64;  // (EHAT)
-    static constexpr int OPV = OKQ + m, OPT = OPV + n;        // (!EHAT)
-    static constexpr int FS = PDPLQR_KKT_EHAT ? OCH + n
-                                              : OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);  // doubles per stage
+    static constexpr int OEH = OKQ + m, OCH = OEH + 3 * 64;  // E^ record
+    static constexpr int OPV = OKQ + m, OPT = OPV + n;        // P~ record
+    static constexpr int FS_EH = OCH + n, FS_PT = OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);
+    static constexpr int FS = PDPLQR_KKT_EHAT ? (FS_EH > FS_PT ? FS_EH : FS_PT) : FS_PT;  // stage stride
     static_assert(!PDPLQR_KKT_EHAT || (NN == 12 && MM == 4), "E^ record: 12/4");
 };
 
@@ -116,11 +121,8 @@ __device__ __forceinline__ void kkt_store_chat(double *Rk_och, double v, int c) 
 //   5     rho D (lane (g, c): rho_g D[g][c], stage 0 without the x columns)
 // so that lp = h~ + q + E^^T p - (rho D)^T g, lu' = T lu, k~ = T^T lu',
 // p_k = lp_x - Lxu lu': the right-hand-side dependent part of the backward.
-// With the E^ record (PDPLQR_KKT_EHAT) the pass also rewrites
-// c^ = c0 - rho_dyn M^ p_{k+1}, from
-//   4     lanes 32..47: c0 = M^ c (column layout, lane 32 + c: c0[c - 4])
-//   6..8  M^ = I - rho_dyn P~ (x rows 4 (r - 1) + g, r = 1..3, lane (g, c))
-constexpr int KKT_CF = (PDPLQR_KKT_EHAT ? 9 : 6) * 64;
+// (ADMM runs keep the P~ record: the pass rewrites k~ and p_{k+1}.)
+constexpr int KKT_CF = 6 * 64;
 
 // Stage record streamed by the backward: E | c | h~ | packed H~ | D | inv_rho | g
 template <int NN, int MM, int NC>
@@ -280,6 +282,8 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     double *RB = A.rec + b * (long long)N * RS::FS;
     const double rd = A.rho_dyn;
     double *const cache = A.cache;  // (a member read inside the stage lambda would put A in scratch)
+    // the E^ record for a plain solve, the P~ record when the ADMM cache is written
+    const bool ehat = PDPLQR_KKT_EHAT && cache == nullptr;
     int fail_stage = -1;
 
     // ---- terminal: P_N = H~_N + D_N^T rho D_N, p_N = h~_N - D_N^T rho g_N ----
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         d4 Pt;
         const bool pt_ok = ptilde_12(Pm, rd, g, c, Pt);
         // ---- record part 1: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]) and P~_{k+1} ----
-        if constexpr (!PDPLQR_KKT_EHAT) {
+        if (!ehat) {  // (wave-uniform)
             // every lane stores (duplicates carry the same value): one store
             // instruction per part, no exec-mask branch
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
@@ -413,24 +417,17 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             part = -dgc * rq * gq;                 // -(D^T rho g)[c]
         }
         double *Ck = cache ? cache + ((long long)b * N + k) * KKT_CF : nullptr;
-        double qcol = 0.0, c0col = 0.0;
-        d4 Mh;  // (EHAT) M^ = I - rho_dyn P~, x rows
-        if constexpr (PDPLQR_KKT_EHAT) {
+        double qcol = 0.0;
+        if (ehat) {
             // ---- record part 1: E^ = E~ - rho_dyn P~ E~ (= E~ - rho_dyn G), c^ ----
             double cv = 0.0;
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
                 gstore(Rk + RS::OEH + 64 * (r - 1) + lane, __builtin_fma(-rd, G[r], in.E[r]));
-                Mh[r] = __builtin_fma(-rd, Pt[r], (4 * r + g == c) ? 1.0 : 0.0);
-                cv = __builtin_fma(Mh[r], __builtin_fma(-rd, prow[r], in.ct[r]), cv);  // M^ (c - rho_dyn p)
+                const double mh = __builtin_fma(-rd, Pt[r], (4 * r + g == c) ? 1.0 : 0.0);  // M^ = I - rho_dyn P~
+                cv = __builtin_fma(mh, __builtin_fma(-rd, prow[r], in.ct[r]), cv);      // M^ (c - rho_dyn p)
             }
             kkt_store_chat(Rk + RS::OCH, sum_groups(cv), c);
-            if (Ck) {
-                double v0 = 0.0;
-#pragma unroll
-                for (int r = 1; r < 4; ++r) v0 = __builtin_fma(Mh[r], in.ct[r], v0);
-                c0col = sum_groups(v0);
-            }
         }
         if (Ck) {  // wave-uniform: the linear pass's copy of this stage's factor
 #pragma unroll
@@ -440,10 +437,6 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             }
             qcol = sum_groups(qcol);
             gstore(Ck + 5 * 64 + lane, rhoD);
-            if constexpr (PDPLQR_KKT_EHAT) {
-#pragma unroll
-                for (int r = 1; r < 4; ++r) gstore(Ck + 64 * (5 + r) + lane, Mh[r]);
-            }
         }
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk) {
@@ -493,7 +486,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 #pragma unroll
                 for (int j = 0; j <= i; ++j) tv = (lane == 16 + 4 * i + j) ? go.T[i][j] : tv;
             gstore(Ck + 3 * 64 + lane, w);
-            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : ((PDPLQR_KKT_EHAT && g == 2) ? c0col : tv));
+            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : tv);
         }
         wave_sync();  // stage k's LDS reads retire before slot reuse
     };
@@ -584,7 +577,6 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     struct Set {
         double e[3], w, q, rd, h, gv;
         double T[10];
-        double mh[3], c0;  // (EHAT) M^ x rows, c0 = M^ c (loaded only with the E^ record)
     };
     // The three register sets are loaded by asm (global_load_dwordx2) and
     // waited for by an explicit vmcnt with the set's registers as operands:
@@ -592,7 +584,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     // rotates the sets through register copies).  LV loads per set; each
     // stage issues 2 stores; a set is waited for with at most 2 LV younger ops
     // outstanding (conservative in steady state, where 2 LV + 4 are).
-    constexpr int LV = PDPLQR_KKT_EHAT ? 22 : 18;
+    constexpr int LV = 18;
     auto gl = [](double &x, const double *p) {
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
     };
@@ -623,12 +615,6 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         gl_at<512>(X.rd, B1);  // (zeros when NC = 0)
         gl(X.h, hb + (long long)k * s + c);
         gl(X.gv, NC > 0 ? gb + (long long)k * NC + (g < NC ? g : 0) : hb);
-        if constexpr (PDPLQR_KKT_EHAT) {
-            gl_at<2 * 512>(X.mh[0], B1);
-            gl_at<3 * 512>(X.mh[1], B1);
-            gl_at<4 * 512>(X.mh[2], B1);
-            gl_at<8 * 32>(X.c0, B2);
-        }
     };
     // "X landed" with exactly the vm ops issued after X's loads still allowed
     // in flight: the other two sets' loads (2 LV) and the stores of the stages
@@ -636,16 +622,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     // second, 2 LV + 4 from the third on (a looser count would also wait for
     // the next set's first loads and cut the lookahead from three stages to two)
     auto wait = [&](Set &X, auto cnt) {
-        if constexpr (PDPLQR_KKT_EHAT)
-            asm volatile("s_waitcnt vmcnt(%22)"
-                         : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
-                           "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
-                           "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv), "+v"(X.mh[0]),
-                           "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0)
-                         : "n"(decltype(cnt)::value)
-                         : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(%18)"
+        asm volatile("s_waitcnt vmcnt(%18)"
                          : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
                            "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
                            "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
@@ -672,21 +649,12 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
                      "+v"(Y.T[8]), "+v"(Y.T[9]));
         asm volatile("" : "+v"(Z.T[0]), "+v"(Z.T[1]), "+v"(Z.T[2]), "+v"(Z.T[3]), "+v"(Z.T[4]), "+v"(Z.T[5]),
                      "+v"(Z.T[6]), "+v"(Z.T[7]), "+v"(Z.T[8]), "+v"(Z.T[9]));
-        if constexpr (PDPLQR_KKT_EHAT)
-            asm volatile("" : "+v"(X.mh[0]), "+v"(X.mh[1]), "+v"(X.mh[2]), "+v"(X.c0), "+v"(Y.mh[0]), "+v"(Y.mh[1]),
-                         "+v"(Y.mh[2]), "+v"(Y.c0), "+v"(Z.mh[0]), "+v"(Z.mh[1]), "+v"(Z.mh[2]), "+v"(Z.c0));
     };
-    const double rdn = A.rho_dyn;
     auto stage = [&](Set &X, int k, auto cnt) {
         wait(X, cnt);
         if (NC == 0) X.rd = X.gv = 0.0;
         double *Rk = RB + (long long)k * RS::FS;
-        if constexpr (PDPLQR_KKT_EHAT) {  // record: c^ = c0 - rho_dyn M^ p_{k+1}
-            double v = 0.0;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) v = __builtin_fma(X.mh[r], prow[r + 1], v);
-            kkt_store_chat(Rk + RS::OCH, __builtin_fma(-rdn, sum_groups(v), X.c0), c);
-        } else {  // record: p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
+        {  // record (the P~ form of ADMM runs): p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
             const double pv = __builtin_fma(prow[1], (double)(cp == 1), __builtin_fma(prow[2], (double)(cp == 2),
                                                                                        prow[3] * (double)(cp == 3)));
@@ -774,18 +742,20 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
 // maxima, then admm_decide).  Rows: exactly Q.uni = 4 per stage k < N, none
 // at the terminal.
 // ---------------------------------------------------------------------------
-template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false>
+template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false, bool EH = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
                                                     const double *__restrict__ x0, double *__restrict__ x0acc,
                                                     double *__restrict__ ws, double rho_dyn, AdmmArgs Q) {
     constexpr int n = 12, m = 4, s = 16, NC = 4;
     using RS = KRecShape<n, m>;
-    constexpr int FS = RS::FS;
-    // ring record: [E | c |] F (the rollout record) [| ADMM rows]; with the E^
-    // record (PDPLQR_KKT_EHAT) E and c are not read (E^, c^ carry them)
-    constexpr bool EH = PDPLQR_KKT_EHAT;
-    constexpr int OE = 0, OC = EH ? 0 : n * s, OF = EH ? 0 : OC + n, OW = OF + FS, OD = OW + s, OZ = OD + NC * s,
+    constexpr int FS = RS::FS;  // stage stride of the record in HBM
+    // ring record: [E | c |] F (the rollout record, FRL doubles) [| ADMM rows];
+    // EH (the E^ record of a plain solve): E and c are not read (E^, c^ carry
+    // them); otherwise the P~ record and the correction applied here
+    static_assert(!EH || !UPD, "ADMM runs keep the P~ record");
+    constexpr int FRL = EH ? RS::FS_EH : RS::FS_PT;
+    constexpr int OE = 0, OC = EH ? 0 : n * s, OF = EH ? 0 : OC + n, OW = OF + FRL, OD = OW + s, OZ = OD + NC * s,
                   OY = OZ + NC, OLB = OY + NC, OUB = OLB + NC, ORH = OUB + NC, OIR = ORH + NC, OH = OIR + NC;
     constexpr int REC = UPD ? OH + s : OW, CH = REC / 2, NI = (CH + 63) / 64;
     constexpr int TAIL = CH - (NI - 1) * 64;
@@ -1298,6 +1268,8 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     return PDPLQR_OK;
 }
 
+bool kkt_ric_rec_ehat(int ric) { return PDPLQR_KKT_EHAT && ric != KKT_RIC_WIDE; }
+
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric) {
     return ric == 0 || ric == 4 ? (size_t)sh.N * KKT_CF : 0;
 }
@@ -1327,15 +1299,19 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
 }
 
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
-                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric) {
+                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric, bool ehat) {
     if (ric == KKT_RIC_WIDE) {
         hipLaunchKernelGGL(k_kkt_ric_fwd_wide, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc,
                            ws, rho_dyn);
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    hipLaunchKernelGGL(k_kkt_ric_fwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
-                       rho_dyn, AdmmArgs{});
+    if (ehat)
+        hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, (bool)PDPLQR_KKT_EHAT>), dim3((unsigned)sh.batch),
+                           dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws, rho_dyn, AdmmArgs{});
+    else
+        hipLaunchKernelGGL((k_kkt_ric_fwd<4>), dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
+                           rho_dyn, AdmmArgs{});
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

@@ -461,7 +461,8 @@ static int uniform_nc(pdplqr_handle h) {
 int solver_backward(pdplqr_handle h, const double *rho) {
     if (h->cfg.solver == PDPLQR_SOLVER_PARALLEL) h->shard_last = 1;
     // the record form is host state: set outside the (replayable) launch sequence
-    h->rec_gain = h->cfg.solver == PDPLQR_SOLVER_SERIAL && schur_gain_record(riccati_args(h));
+    h->rec_gain = (h->cfg.solver == PDPLQR_SOLVER_SERIAL && schur_gain_record(riccati_args(h))) ||
+                  (h->cfg.solver == PDPLQR_SOLVER_KKT && kkt_plain_rec_ehat(h));
     // the record form selects the backward kernel: it is part of the graph key
     // (a replay of the other form's capture would leave the record in the
     // layout the forward does not read)

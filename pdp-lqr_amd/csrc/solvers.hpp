@@ -39,6 +39,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws);
 int kkt_dim(pdplqr_handle h);
 int kkt_before_model(pdplqr_handle h);  // set_model on a formed KKT handle: keep the frozen matrix
 bool kkt_ric_active(pdplqr_handle h);  // the Riccati-ordered path serves this handle
+bool kkt_plain_rec_ehat(pdplqr_handle h);  // a plain KKT backward leaves the E^ record (kept in rec_gain)
 // Riccati-ordered KKT path (kkt_riccati.hip): nc of the uniform 12/4 row
 // layout, KKT_RIC_WIDE for the LDS kernels (any ncs, n + m <= 64), or -1
 constexpr int KKT_RIC_WIDE = 1000;
@@ -50,11 +51,12 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
                             int32_t *status, hipStream_t st, double *cache = nullptr);
 // linear-only pass on the factor cache the backward wrote (ric 0 / 4 only)
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric);  // per problem; 0 where unsupported
+bool kkt_ric_rec_ehat(int ric);  // a plain backward of this path leaves the E^ record
 int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double *hw, const double *gw,
                           const double *irho, const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn,
                           const double *cache, double *rec, hipStream_t st);
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
-                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric);
+                           double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric, bool ehat);
 // num_devices > 1 (multidev.hip): the horizon split over the devices of one process
 int md_create(pdplqr_handle h, const pdplqr_config &C);
 void md_release(pdplqr_handle h);

@@ -1,5 +1,5 @@
 """One secondary bench workload on its own (for rocprofv3 kernel traces and PMC
-passes of exactly that workload): c2 | c3 | c5 | c4 [N] | wide.
+passes of exactly that workload): c2 | c3 | c5 | c5solve | c4 [N] | wide.
 Prints the bench's JSON for it."""
 import json
 import os
@@ -23,6 +23,8 @@ def main():
         r = bench.bench_batched_c3(0, dev, None, steps=5, warmup=2)
     elif which == "c5":
         r = bench.bench_conic(0, dev, None, steps=3, warmup=1)
+    elif which == "c5solve":  # the KKT and Riccati solves only (no ADMM runs through the same kernels)
+        r = bench.bench_conic(0, dev, None, steps=3, warmup=1, admm=False)
     elif which == "c4":
         r = bench.bench_horizon(0, dev, None, 1, 0, int(sys.argv[2]) if len(sys.argv) > 2 else 65536, steps=3,
                                 warmup=1)
