@@ -29,6 +29,16 @@ inline void append(std::vector<double> &dst, const Dense &a) {
     if (k) dst.insert(dst.end(), a.data(), a.data() + k);
 }
 
+// does `a` equal packed[off, off + a.size())?  advances off
+template <typename Dense>
+inline bool same_at(const std::vector<double> &packed, size_t &off, const Dense &a) {
+    const size_t k = static_cast<size_t>(a.size());
+    if (off + k > packed.size()) return false;
+    const bool eq = k == 0 || std::memcmp(packed.data() + off, a.data(), k * sizeof(double)) == 0;
+    off += k;
+    return eq;
+}
+
 // The model in the boundary layout of pdplqr.h (Eigen column-major blocks,
 // stage-major): E [N][n s], c [N][n], H [N][s s] + [n n], h [N][s] + [n],
 // D ragged [nc_k x dim_k].  Node k of the model is nodes[k].
@@ -55,6 +65,34 @@ struct PackedModel {
             if (mask & PDPLQR_MODEL_HV) append(h, nd.h);
             if ((mask & PDPLQR_MODEL_D) && nd.n_con > 0) append(D, nd.D_con);
         }
+    }
+
+    // the arrays in `mask` whose packed contents differ from `model`, compared
+    // in place (no packing pass, no allocation; an array stops at its first
+    // differing block)
+    int differs(const LQRModel &model, int mask) const {
+        const int N = model.N;
+        if (static_cast<int>(model.nodes.size()) != N + 1) return mask;
+        int out = 0;
+        size_t oE = 0, oc = 0, oH = 0, oh = 0, oD = 0;
+        for (int k = 0; k <= N && (mask & ~out); ++k) {
+            const Node &nd = model.nodes[static_cast<size_t>(k)];
+            const int live = mask & ~out;
+            if (k < N) {
+                if ((live & PDPLQR_MODEL_E) && !same_at(E, oE, nd.E)) out |= PDPLQR_MODEL_E;
+                if ((live & PDPLQR_MODEL_C) && !same_at(c, oc, nd.c)) out |= PDPLQR_MODEL_C;
+            }
+            if ((live & PDPLQR_MODEL_H) && !same_at(H, oH, nd.H)) out |= PDPLQR_MODEL_H;
+            if ((live & PDPLQR_MODEL_HV) && !same_at(h, oh, nd.h)) out |= PDPLQR_MODEL_HV;
+            if ((live & PDPLQR_MODEL_D) && nd.n_con > 0 && !same_at(D, oD, nd.D_con)) out |= PDPLQR_MODEL_D;
+        }
+        // a model that shrank leaves packed entries unmatched
+        if ((mask & PDPLQR_MODEL_E) && oE != E.size()) out |= PDPLQR_MODEL_E;
+        if ((mask & PDPLQR_MODEL_C) && oc != c.size()) out |= PDPLQR_MODEL_C;
+        if ((mask & PDPLQR_MODEL_H) && oH != H.size()) out |= PDPLQR_MODEL_H;
+        if ((mask & PDPLQR_MODEL_HV) && oh != h.size()) out |= PDPLQR_MODEL_HV;
+        if ((mask & PDPLQR_MODEL_D) && oD != D.size()) out |= PDPLQR_MODEL_D;
+        return out & mask;
     }
 };
 
@@ -109,32 +147,33 @@ public:
     // Uploads the arrays of `model` in `mask` (PDPLQR_MODEL_*) that differ from
     // what the device holds: the reference reads its model lazily (H, h at
     // update_problem_data, E, c, D_con at backward / forward), so each facade
-    // call syncs exactly what that call reads.  An unchanged model costs a host
-    // packing pass and a compare of the arrays in `mask` only, no host ->
-    // device copy.
+    // call syncs exactly what that call reads.  With tracking on (the default)
+    // an unchanged model costs one in-place compare of the arrays in `mask`
+    // (no packing, no host -> device copy); with tracking off the compare is
+    // skipped too and only arrays declared by model_changed() are re-read.
     void sync(const LQRModel &model, int mask) {
         if (!synced_) mask = PDPLQR_MODEL_ALL;
-        fresh_.pack(model, mask);
-        int need = synced_ ? 0 : PDPLQR_MODEL_ALL;
-        if (synced_) {
-            if ((mask & PDPLQR_MODEL_E) && fresh_.E != packed_.E) need |= PDPLQR_MODEL_E;
-            if ((mask & PDPLQR_MODEL_C) && fresh_.c != packed_.c) need |= PDPLQR_MODEL_C;
-            if ((mask & PDPLQR_MODEL_H) && fresh_.H != packed_.H) need |= PDPLQR_MODEL_H;
-            if ((mask & PDPLQR_MODEL_HV) && fresh_.h != packed_.h) need |= PDPLQR_MODEL_HV;
-            if ((mask & PDPLQR_MODEL_D) && fresh_.D != packed_.D) need |= PDPLQR_MODEL_D;
-        }
+        int need;
+        if (!synced_) need = PDPLQR_MODEL_ALL;
+        else if (tracking_) need = packed_.differs(model, mask);
+        else need = pending_ & mask;
         if (!need) return;
-        check(pdplqr_set_model_arrays(h_, need, fresh_.E.data(), fresh_.c.data(), fresh_.H.data(), fresh_.h.data(),
-                                      fresh_.D.empty() ? nullptr : fresh_.D.data(), PDPLQR_MEM_HOST),
+        packed_.pack(model, need);
+        check(pdplqr_set_model_arrays(h_, need, packed_.E.data(), packed_.c.data(), packed_.H.data(),
+                                      packed_.h.data(), packed_.D.empty() ? nullptr : packed_.D.data(),
+                                      PDPLQR_MEM_HOST),
               "set_model");
-        if (need & PDPLQR_MODEL_E) packed_.E = fresh_.E;
-        if (need & PDPLQR_MODEL_C) packed_.c = fresh_.c;
-        if (need & PDPLQR_MODEL_H) packed_.H = fresh_.H;
-        if (need & PDPLQR_MODEL_HV) packed_.h = fresh_.h;
-        if (need & PDPLQR_MODEL_D) packed_.D = fresh_.D;
+        pending_ &= ~need;
         synced_ = true;
     }
     void upload(const LQRModel &model) { sync(model, PDPLQR_MODEL_ALL); }
+
+    // MPC loops whose model rarely changes: with tracking off the protocol calls
+    // do no per-call host work on the model; the caller declares edits with
+    // model_changed(mask), and each declared array is re-read at the next call
+    // that reads it (the lazy semantics above are kept)
+    void set_tracking(bool on) { tracking_ = on; }
+    void model_changed(int mask) { pending_ |= mask & PDPLQR_MODEL_ALL; }
 
     long long upload_bytes() const {
         int64_t b = 0;
@@ -181,8 +220,9 @@ private:
     pdplqr_handle h_ = nullptr;
     int n_ = 0, m_ = 0, N_ = 0;
     std::vector<int32_t> ncs_, devs_;
-    PackedModel packed_, fresh_;  // what the device holds / the model as packed now
-    bool synced_ = false;
+    PackedModel packed_;  // what the device holds
+    bool synced_ = false, tracking_ = true;
+    int pending_ = 0;  // arrays declared changed (tracking off)
     std::vector<double> w_, y_, z_, r_;
 };
 

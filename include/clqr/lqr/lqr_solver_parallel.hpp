@@ -65,6 +65,14 @@ public:
     // unchanged model uploads nothing after the constructor)
     long long model_upload_bytes() const { return hd_.upload_bytes(); }
 
+    // this build: model change tracking.  On (default), every protocol call
+    // compares the model arrays it reads with what the device holds (host work
+    // O(N s^2), no copy when unchanged).  Off, the calls skip that compare and
+    // the caller declares edits: model_changed(PDPLQR_MODEL_E | ...) before the
+    // call that should read them (detail::Handle::sync).
+    void set_model_tracking(bool on) { hd_.set_tracking(on); }
+    void model_changed(int mask = PDPLQR_MODEL_ALL) { hd_.model_changed(mask); }
+
     int num_segments() const { return num_segments_; }
 
     // segment boundaries of the reference segmentation (idx_start, Nseg)

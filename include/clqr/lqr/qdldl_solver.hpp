@@ -45,6 +45,14 @@ public:
 
     long long model_upload_bytes() const { return hd_.upload_bytes(); }
 
+    // this build: model change tracking.  On (default), every protocol call
+    // compares the model arrays it reads with what the device holds (host work
+    // O(N s^2), no copy when unchanged).  Off, the calls skip that compare and
+    // the caller declares edits: model_changed(PDPLQR_MODEL_E | ...) before the
+    // call that should read them (detail::Handle::sync).
+    void set_model_tracking(bool on) { hd_.set_tracking(on); }
+    void model_changed(int mask = PDPLQR_MODEL_ALL) { hd_.model_changed(mask); }
+
     // qdldl_solver.hpp:19,47-78: the QDLDL workspace (elimination tree, column
     // counts, factor buffers) of a KKT matrix, e.g. KKTSystem::get_KKT_csc_matrix's.
     // Host-side; the GPU factorisation does not use it.

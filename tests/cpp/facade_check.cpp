@@ -3,7 +3,7 @@
 // Eigen-style blocks element by element, and runs one of the three solver
 // classes through update_problem_data -> backward -> forward.
 //
-//   facade_check <problem.bin> <out.bin> <solver> [num_segments condensed] [nofact|mutate|mpc]
+//   facade_check <problem.bin> <out.bin> <solver> [num_segments condensed] [nofact|mutate|mpc|declared]
 //   solver: serial | parallel | qdldl
 // problem.bin (little endian): int32 n, m, N, ncs[N+1]; then float64 arrays in
 // the boundary layout of pdplqr.h: E, c, H, h, D, x0, sigma, ws, ys, zs, rho, inv_rho.
@@ -15,7 +15,10 @@
 // at backward / forward and H at update_problem_data, so the answer is that of
 // the model with the new E and the old H.  With `mpc` the protocol runs 5 more
 // times on the unchanged model and the model bytes uploaded host -> device
-// during those iterations are printed ("uploads <bytes>").
+// during those iterations are printed ("uploads <bytes>").  With `declared`
+// model tracking is off: the same 5 iterations, then the `mutate` edit with only
+// E declared (model_changed(PDPLQR_MODEL_E)) before one more solve, whose answer
+// is again the model with the new E and the old H.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -108,7 +111,8 @@ int main(int argc, char **argv) {
     const std::string kind = argv[3];
     const bool nofact = std::string(argv[argc - 1]) == "nofact";
     const bool mutate = std::string(argv[argc - 1]) == "mutate";
-    const bool mpc = std::string(argv[argc - 1]) == "mpc";
+    const bool declared = std::string(argv[argc - 1]) == "declared";
+    const bool mpc = declared || std::string(argv[argc - 1]) == "mpc";
     auto edit = [&]() {
         lqr::Node &a = model.get_node(N / 2);
         for (int j = 0; j < s; ++j)
@@ -125,6 +129,7 @@ int main(int argc, char **argv) {
     try {
         if (kind == "serial") {
             lqr::LQRSolver sol(model);
+            if (declared) sol.set_model_tracking(false);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
             if (mutate) edit();
             sol.backward(rhov);
@@ -137,6 +142,13 @@ int main(int argc, char **argv) {
                     sol.forward(x0, out);
                 }
                 uploads = sol.model_upload_bytes() - b0;
+            }
+            if (declared) {
+                sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+                edit();
+                sol.model_changed(PDPLQR_MODEL_E);  // H's edit is not declared: the device keeps the old H
+                sol.backward(rhov);
+                sol.forward(x0, out);
             }
             if (nofact) {
                 sol.update_problem_data(ws2, ysv, zsv, irv, sigma);
@@ -160,6 +172,7 @@ int main(int argc, char **argv) {
                 }
             }
             lqr::LQRParallelSolver sol(model, ns, true, ty, devs);
+            if (declared) sol.set_model_tracking(false);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
             if (mutate) edit();
             sol.backward(rhov);
@@ -173,6 +186,13 @@ int main(int argc, char **argv) {
                 }
                 uploads = sol.model_upload_bytes() - b0;
             }
+            if (declared) {
+                sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
+                edit();
+                sol.model_changed(PDPLQR_MODEL_E);  // H's edit is not declared: the device keeps the old H
+                sol.backward(rhov);
+                sol.forward(x0, out);
+            }
             if (nofact) {
                 sol.update_problem_data(ws2, ysv, zsv, irv, sigma);
                 sol.backward_without_factorization(rhov);
@@ -180,6 +200,7 @@ int main(int argc, char **argv) {
             }
         } else if (kind == "qdldl") {
             lqr::QDLDLSolver sol(model);
+            if (declared) sol.set_model_tracking(false);
             sol.update_problem_data(wsv, ysv, zsv, irv, sigma);
             sol.backward(irv);
             sol.forward(x0, out);

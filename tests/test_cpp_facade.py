@@ -174,3 +174,45 @@ def test_cpp_facade_mpc_loop_uploads_no_model(facade_bin, tmp_path, args):
     assert r.returncode == 0, r.stdout + r.stderr
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("uploads")]
     assert line and int(line[0].split()[1]) == 0, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["serial", "declared"], ["parallel", "4", "CHOLESKY", "declared"]])
+def test_cpp_facade_declared_model_changes(facade_bin, tmp_path, args):
+    """Model tracking off (set_model_tracking(false)): the
+    MPC loop does no per-call compare and uploads nothing; after the `mutate`
+    edit only E is declared (model_changed(PDPLQR_MODEL_E)), so the solve sees
+    the new E and the old H -- the same answer as the tracked `mutate` run."""
+    from oracle.oracle import OracleParallel, OracleSerial
+    from pdplqr.model import PackedModel
+
+    pm, d, w = _run(facade_bin, str(tmp_path), "random_n12_m4_N64_nc4", args)
+    n, m, N = pm.n, pm.m, pm.N
+    s = n + m
+    E = pm.E.copy()
+    k = N // 2
+    E[k * n * s:(k + 1) * n * s] *= 1.01
+    pm2 = PackedModel(n, m, N, pm.ncs, E, pm.c, pm.H, pm.h, pm.D)
+    o = OracleSerial(pm2) if args[0] == "serial" else OracleParallel(pm2, int(args[1]), True, args[2])
+    o.update_problem_data(d["ws"], d["ys"], d["zs"], d["inv_rho"], float(d["sigma"]))
+    o.backward(d["rho"])
+    assert rel_err(w, o.forward(d["x0"])) < 1e-9
+    prob, out = os.path.join(str(tmp_path), "p.bin"), os.path.join(str(tmp_path), "p.out")
+    _write_problem(prob, pm, d)
+    r = subprocess.run([facade_bin, prob, out] + args, capture_output=True, text=True, timeout=300)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("uploads")]
+    assert r.returncode == 0 and line and int(line[0].split()[1]) == 0, r.stdout + r.stderr
+
+
+def test_facade_model_change_detection(tmp_path):
+    """CPU: PackedModel::differs (the facade's in-place compare) reports exactly
+    the arrays an edit touched (host-only program, no library call)."""
+    if shutil.which("g++") is None:
+        pytest.skip("g++ missing")
+    exe = str(tmp_path / "packed_model_check")
+    b = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(CPP, "packed_model_check.cpp"), "-o", exe], capture_output=True, text=True,
+                       timeout=300)
+    assert b.returncode == 0, b.stdout + b.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
