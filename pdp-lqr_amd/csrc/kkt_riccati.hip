@@ -114,15 +114,22 @@ __device__ __forceinline__ void kkt_store_chat(double *Rk_och, double v, int c) 
 }
 
 // Factor cache of the linear-only pass (k_kkt_ric_nofact; written by the
-// backward when KKTRicArgs::cache is set), per stage six 64-lane slots:
-//   0..2  E^ = E~ - rho_dyn G (x rows 4 r + g, r = 1..3; G = P~ E~)
-//   3     w = Lxu (lane (g, c): L(c, g))
-//   4     lanes 0..15: q = G^T c~ (per column), lanes 16..31: T = Luu^{-1} (16 + 4 i + j)
-//   5     rho D (lane (g, c): rho_g D[g][c], stage 0 without the x columns)
+// backward when KKTRicArgs::cache is set), per stage three lane-interleaved
+// pair slots (lane L's two doubles at 2 L: one 16-byte load per lane, 1 KB
+// contiguous per instruction) and the packed Luu^{-1}:
+//   KC_EE  (e0, e1)  E^ = E~ - rho_dyn G, x rows 4 + g and 8 + g (G = P~ E~)
+//   KC_EW  (e2, w)   x row 12 + g of E^;  w = Lxu (lane (g, c): L(c, g))
+//   KC_QR  (q, rD)   q = G^T c~ (column c);  rho D (lane (g, c): rho_g D[g][c],
+//                    stage 0 without the x columns)
+//   KC_T   T = Luu^{-1} packed lower, t = i (i + 1) / 2 + j (10 doubles, read
+//          wave-uniform by five 16-byte loads)
 // so that lp = h~ + q + E^^T p - (rho D)^T g, lu' = T lu, k~ = T^T lu',
 // p_k = lp_x - Lxu lu': the right-hand-side dependent part of the backward.
+// Ten load instructions a stage let the pass keep five stages in flight
+// within the 63 outstanding vector-memory operations a wave may have.
 // (ADMM runs keep the P~ record: the pass rewrites k~ and p_{k+1}.)
-constexpr int KKT_CF = 6 * 64;
+constexpr int KC_EE = 0, KC_EW = 128, KC_QR = 256, KC_T = 384;
+constexpr int KKT_CF = 400;
 
 // Stage record streamed by the backward: E | c | h~ | packed H~ | D | inv_rho | g
 template <int NN, int MM, int NC>
@@ -417,7 +424,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             part = -dgc * rq * gq;                 // -(D^T rho g)[c]
         }
         double *Ck = cache ? cache + ((long long)b * N + k) * KKT_CF : nullptr;
-        double qcol = 0.0;
+        double qcol = 0.0, e2c = 0.0;
         if (ehat) {
             // ---- record part 1: E^ = E~ - rho_dyn P~ E~ (= E~ - rho_dyn G), c^ ----
             double cv = 0.0;
@@ -430,13 +437,16 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
             kkt_store_chat(Rk + RS::OCH, sum_groups(cv), c);
         }
         if (Ck) {  // wave-uniform: the linear pass's copy of this stage's factor
+            double ev[3];
 #pragma unroll
             for (int kk = 1; kk < 4; ++kk) {
-                gstore(Ck + 64 * (kk - 1) + lane, __builtin_fma(-rd, G[kk], in.E[kk]));
+                ev[kk - 1] = __builtin_fma(-rd, G[kk], in.E[kk]);
                 qcol = __builtin_fma(G[kk], in.ct[kk], qcol);
             }
             qcol = sum_groups(qcol);
-            gstore(Ck + 5 * 64 + lane, rhoD);
+            gstore2(Ck + KC_EE + 2 * lane, d2v{ev[0], ev[1]});
+            gstore2(Ck + KC_QR + 2 * lane, d2v{qcol, rhoD});
+            e2c = ev[2];
         }
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk) {
@@ -484,9 +494,9 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 #pragma unroll
             for (int i = 0; i < MM; ++i)
 #pragma unroll
-                for (int j = 0; j <= i; ++j) tv = (lane == 16 + 4 * i + j) ? go.T[i][j] : tv;
-            gstore(Ck + 3 * 64 + lane, w);
-            gstore(Ck + 4 * 64 + lane, lane < 16 ? qcol : tv);
+                for (int j = 0; j <= i; ++j) tv = (lane == i * (i + 1) / 2 + j) ? go.T[i][j] : tv;
+            gstore2(Ck + KC_EW + 2 * lane, d2v{e2c, w});
+            if (lane < MM * (MM + 1) / 2) gstore(Ck + KC_T + lane, tv);
         }
         wave_sync();  // stage k's LDS reads retire before slot reuse
     };
@@ -525,8 +535,9 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 //     lp = h~ + q + E^^T p_{k+1} - (rho D)^T g,   lu' = T lu,   k~ = T^T lu',
 //     p_k = lp_x - Lxu lu'
 // and the rollout record's k~ and p_{k+1} are rewritten (K~, P~ stay).  One
-// wave per problem; the cache slots are read three stages ahead into registers
-// (three sets, the loop unrolled by three so no register set is copied).
+// wave per problem (one per SIMD at C5, so the pass is bound by the memory
+// latency its lookahead covers): the cache of PDPLQR_KKT_NF_DEPTH stages is in
+// flight into registers at a time.
 // ---------------------------------------------------------------------------
 // global_load_dwordx2 with an immediate byte offset (signed 13 bits), asm-issued
 // like the other staging loads (the waits are explicit)
@@ -535,6 +546,25 @@ __device__ __forceinline__ void gl_at(double &x, const double *p) {
     static_assert(OFF >= -4096 && OFF < 4096, "global offset range");
     asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(x) : "v"(p), "n"(OFF) : "memory");
 }
+
+template <int OFF>
+__device__ __forceinline__ void gl4_at(d2v &x, const double *p) {
+    static_assert(OFF >= -4096 && OFF < 4096, "global offset range");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(x) : "v"(p), "n"(OFF) : "memory");
+}
+
+// f(integral_constant<int, I>) for I = B .. E - 1 (compile-time set indices)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+#ifndef PDPLQR_KKT_NF_DEPTH
+#define PDPLQR_KKT_NF_DEPTH 5
+#endif
 
 template <int NC>
 __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
@@ -574,85 +604,61 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
     double sel[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sel[j] = (g == j) ? 1.0 : 0.0;
+    // One register set per stage in flight: the cache pair slots (three
+    // 16-byte loads), Luu^{-1} (five, wave-uniform), h~ and g.  The sets are
+    // loaded by asm and waited for by an explicit vmcnt with the set's
+    // registers as operands (compiler-placed waits drained every set at the top
+    // of the loop).  DEPTH sets, the loop unrolled by DEPTH so no set is copied.
+    constexpr int DEPTH = PDPLQR_KKT_NF_DEPTH, LV = 10, STS = 2;  // loads per set, stores per stage
+    // "set j landed" with exactly the vm ops issued after its loads still in
+    // flight: the other sets' loads, and the stores and reloads of the stages
+    // in between -- (DEPTH - 1) LV + STS j in the first trip, (DEPTH - 1)(LV + STS)
+    // from then on (a looser count would wait for younger loads too and cut
+    // the lookahead)
+    static_assert((DEPTH - 1) * (LV + STS) + LV <= 63, "vmcnt range");
     struct Set {
-        double e[3], w, q, rd, h, gv;
-        double T[10];
+        d2v ee, ew, qr, t[5];
+        double h, gv;
     };
-    // The three register sets are loaded by asm (global_load_dwordx2) and
-    // waited for by an explicit vmcnt with the set's registers as operands:
-    // compiler-placed waits drained every set at the top of the loop (it
-    // rotates the sets through register copies).  LV loads per set; each
-    // stage issues 2 stores; a set is waited for with at most 2 LV younger ops
-    // outstanding (conservative in steady state, where 2 LV + 4 are).
-    constexpr int LV = 18;
     auto gl = [](double &x, const double *p) {
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
     };
-    // the cache slots by three base addresses and the loads' immediate byte
-    // offsets (one address computation per base instead of one per load: at
-    // one wave per SIMD every VALU instruction of the pass is on its time)
     auto load = [&](Set &X, int k) {
         const double *Ck = Cb + (long long)k * KKT_CF;
-        const double *B1 = Ck + 4 * 64 + lane;  // lane-indexed slots, around slot 4
-        const double *B2 = Ck + 4 * 64 + c;     // column-indexed entries of slot 4
-        const double *B3 = Ck + 4 * 64 + 16;    // T (wave-uniform)
-        gl_at<-4 * 512>(X.e[0], B1);
-        gl_at<-3 * 512>(X.e[1], B1);
-        gl_at<-2 * 512>(X.e[2], B1);
-        gl_at<-1 * 512>(X.w, B1);
-        gl_at<0>(X.q, B2);
-        // T[i][j] at 4 i + j
-        gl_at<0>(X.T[0], B3);
-        gl_at<8 * 4>(X.T[1], B3);
-        gl_at<8 * 5>(X.T[2], B3);
-        gl_at<8 * 8>(X.T[3], B3);
-        gl_at<8 * 9>(X.T[4], B3);
-        gl_at<8 * 10>(X.T[5], B3);
-        gl_at<8 * 12>(X.T[6], B3);
-        gl_at<8 * 13>(X.T[7], B3);
-        gl_at<8 * 14>(X.T[8], B3);
-        gl_at<8 * 15>(X.T[9], B3);
-        gl_at<512>(X.rd, B1);  // (zeros when NC = 0)
+        const double *B1 = Ck + 2 * lane;  // lane-interleaved pair slots
+        const double *B3 = Ck + KC_T;      // T (wave-uniform)
+        gl4_at<8 * KC_EE>(X.ee, B1);
+        gl4_at<8 * KC_EW>(X.ew, B1);
+        gl4_at<8 * KC_QR>(X.qr, B1);
+        gl4_at<0>(X.t[0], B3);
+        gl4_at<16>(X.t[1], B3);
+        gl4_at<32>(X.t[2], B3);
+        gl4_at<48>(X.t[3], B3);
+        gl4_at<64>(X.t[4], B3);
         gl(X.h, hb + (long long)k * s + c);
         gl(X.gv, NC > 0 ? gb + (long long)k * NC + (g < NC ? g : 0) : hb);
     };
-    // "X landed" with exactly the vm ops issued after X's loads still allowed
-    // in flight: the other two sets' loads (2 LV) and the stores of the stages
-    // in between (2 per stage) -- 2 LV at the first stage, 2 LV + 2 at the
-    // second, 2 LV + 4 from the third on (a looser count would also wait for
-    // the next set's first loads and cut the lookahead from three stages to two)
     auto wait = [&](Set &X, auto cnt) {
-        asm volatile("s_waitcnt vmcnt(%18)"
-                         : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q), "+v"(X.T[0]), "+v"(X.T[1]),
-                           "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]), "+v"(X.T[6]), "+v"(X.T[7]),
-                           "+v"(X.T[8]), "+v"(X.T[9]), "+v"(X.rd), "+v"(X.h), "+v"(X.gv)
+        asm volatile("s_waitcnt vmcnt(%10)"
+                         : "+v"(X.ee), "+v"(X.ew), "+v"(X.qr), "+v"(X.t[0]), "+v"(X.t[1]), "+v"(X.t[2]), "+v"(X.t[3]),
+                           "+v"(X.t[4]), "+v"(X.h), "+v"(X.gv)
                          : "n"(decltype(cnt)::value)
                          : "memory");
     };
-#ifndef PDPLQR_KKT_LV_EXACT
-#define PDPLQR_KKT_LV_EXACT 1
-#endif
-    using W0 = std::integral_constant<int, 2 * LV>;
-    using W1 = std::integral_constant<int, 2 * LV + (PDPLQR_KKT_LV_EXACT ? 2 : 0)>;
-    using W2 = std::integral_constant<int, 2 * LV + (PDPLQR_KKT_LV_EXACT ? 4 : 0)>;
-    static_assert(2 * LV + 4 <= 63, "vmcnt range");
-    // every set landed (the sets the tail does not read are dead to the
-    // compiler, which would reuse their registers under the loads in flight)
-    auto wait_all = [&](Set &X, Set &Y, Set &Z) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(X.e[0]), "+v"(X.e[1]), "+v"(X.e[2]), "+v"(X.w), "+v"(X.q),
-                     "+v"(X.rd), "+v"(X.h), "+v"(X.gv), "+v"(Y.e[0]), "+v"(Y.e[1]), "+v"(Y.e[2]), "+v"(Y.w),
-                     "+v"(Y.q), "+v"(Y.rd), "+v"(Y.h), "+v"(Y.gv), "+v"(Z.e[0]), "+v"(Z.e[1]), "+v"(Z.e[2]),
-                     "+v"(Z.w), "+v"(Z.q), "+v"(Z.rd), "+v"(Z.h), "+v"(Z.gv)::"memory");
-        asm volatile("" : "+v"(X.T[0]), "+v"(X.T[1]), "+v"(X.T[2]), "+v"(X.T[3]), "+v"(X.T[4]), "+v"(X.T[5]),
-                     "+v"(X.T[6]), "+v"(X.T[7]), "+v"(X.T[8]), "+v"(X.T[9]), "+v"(Y.T[0]), "+v"(Y.T[1]),
-                     "+v"(Y.T[2]), "+v"(Y.T[3]), "+v"(Y.T[4]), "+v"(Y.T[5]), "+v"(Y.T[6]), "+v"(Y.T[7]),
-                     "+v"(Y.T[8]), "+v"(Y.T[9]));
-        asm volatile("" : "+v"(Z.T[0]), "+v"(Z.T[1]), "+v"(Z.T[2]), "+v"(Z.T[3]), "+v"(Z.T[4]), "+v"(Z.T[5]),
-                     "+v"(Z.T[6]), "+v"(Z.T[7]), "+v"(Z.T[8]), "+v"(Z.T[9]));
+    // (registers of a set touched after a wait: the compiler must not reuse
+    // them under loads still in flight)
+    auto touch = [&](Set &X) {
+        asm volatile("" : "+v"(X.ee), "+v"(X.ew), "+v"(X.qr), "+v"(X.t[0]), "+v"(X.t[1]), "+v"(X.t[2]), "+v"(X.t[3]),
+                     "+v"(X.t[4]), "+v"(X.h), "+v"(X.gv));
     };
     auto stage = [&](Set &X, int k, auto cnt) {
         wait(X, cnt);
-        if (NC == 0) X.rd = X.gv = 0.0;
+        const double e[3] = {X.ee.x, X.ee.y, X.ew.x};
+        const double xw = X.ew.y, xq = X.qr.x;
+        const double xrd = NC > 0 ? X.qr.y : 0.0, xgv = NC > 0 ? X.gv : 0.0;
+        double T[10];
+#pragma unroll
+        for (int t = 0; t < 10; ++t) T[t] = (t & 1) ? X.t[t >> 1].y : X.t[t >> 1].x;
         double *Rk = RB + (long long)k * RS::FS;
         {  // record (the P~ form of ADMM runs): p_{k+1} (lanes (g, c = 1..3): p[4 c + g - m]), as the backward writes it
             const int cp = c < 1 ? 1 : (c > 3 ? 3 : c);
@@ -662,9 +668,9 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         }
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) part = __builtin_fma(X.e[r], prow[r + 1], part);
-        if (NC > 0) part = __builtin_fma(-X.rd, X.gv, part);
-        const double lp = X.h + X.q + sum_groups(part);  // lp[c], every group
+        for (int r = 0; r < 3; ++r) part = __builtin_fma(e[r], prow[r + 1], part);
+        if (NC > 0) part = __builtin_fma(-xrd, xgv, part);
+        const double lp = X.h + xq + sum_groups(part);  // lp[c], every group
         double lu[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) lu[j] = readlane_f64(lp, j);
@@ -674,14 +680,14 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         for (int i = 0; i < 4; ++i) {
             double v = 0.0;
 #pragma unroll
-            for (int j = 0; j <= i; ++j) v = __builtin_fma(X.T[i * (i + 1) / 2 + j], lu[j], v);
+            for (int j = 0; j <= i; ++j) v = __builtin_fma(T[i * (i + 1) / 2 + j], lu[j], v);
             luq[i] = v;
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             double v = 0.0;
 #pragma unroll
-            for (int l = i; l < 4; ++l) v = __builtin_fma(X.T[l * (l + 1) / 2 + i], luq[l], v);
+            for (int l = i; l < 4; ++l) v = __builtin_fma(T[l * (l + 1) / 2 + i], luq[l], v);
             kq[i] = v;
         }
         const double kv = lane == 0 ? kq[0] : lane == 1 ? kq[1] : lane == 2 ? kq[2] : kq[3];
@@ -689,42 +695,43 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
         double lq = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) lq = __builtin_fma(sel[j], luq[j], lq);
-        const double pcol = lp - sum_groups(X.w * lq);  // p_k[c - m] on c >= m
+        const double pcol = lp - sum_groups(xw * lq);  // p_k[c - m] on c >= m
         if (g == 0) pc[c] = pcol;
         wave_sync();
 #pragma unroll
         for (int r = 1; r < 4; ++r) prow[r] = pc[4 * r + g];
         wave_sync();
     };
-    // three register sets in flight: a stage's chain is ~0.3 us, HBM latency
-    // ~1 us (one set ahead: 0.91 us per stage, latency-bound)
     // (loads unconditional, at clamped stages: a load inside a branch made the
     // wait-count pass drain every set in flight at the top of the loop)
-    Set X0, X1, X2;
-    load(X0, N - 1);
-    load(X1, N >= 2 ? N - 2 : 0);
-    load(X2, N >= 3 ? N - 3 : 0);
+    Set X[DEPTH];
+    static_for<0, DEPTH>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        load(X[j], N - 1 - j >= 0 ? N - 1 - j : 0);
+    });
     int k = N - 1;
-    if (k >= 2) {  // first trip: fewer younger ops than in the steady state
-        stage(X0, k, W0{});
-        load(X0, k >= 3 ? k - 3 : 0);
-        stage(X1, k - 1, W1{});
-        load(X1, k >= 4 ? k - 4 : 0);
-        stage(X2, k - 2, W2{});
-        load(X2, k >= 5 ? k - 5 : 0);
-        k -= 3;
+    if (k >= DEPTH - 1) {  // first trip: fewer younger ops than in the steady state
+        static_for<0, DEPTH>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            stage(X[j], k - j, std::integral_constant<int, (DEPTH - 1) * LV + STS * j>{});
+            load(X[j], k - j - DEPTH >= 0 ? k - j - DEPTH : 0);
+        });
+        k -= DEPTH;
     }
-    for (; k >= 2; k -= 3) {
-        stage(X0, k, W2{});
-        load(X0, k >= 3 ? k - 3 : 0);
-        stage(X1, k - 1, W2{});
-        load(X1, k >= 4 ? k - 4 : 0);
-        stage(X2, k - 2, W2{});
-        load(X2, k >= 5 ? k - 5 : 0);
+    for (; k >= DEPTH - 1; k -= DEPTH) {
+        static_for<0, DEPTH>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            stage(X[j], k - j, std::integral_constant<int, (DEPTH - 1) * (LV + STS)>{});
+            load(X[j], k - j - DEPTH >= 0 ? k - j - DEPTH : 0);
+        });
     }
-    wait_all(X0, X1, X2);
-    if (k >= 0) stage(X0, k, W0{});
-    if (k >= 1) stage(X1, k - 1, W0{});
+    // the last k + 1 < DEPTH stages: every set landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    static_for<0, DEPTH>([&](auto J) { touch(X[decltype(J)::value]); });
+    static_for<0, DEPTH - 1>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (k - j >= 0) stage(X[j], k - j, std::integral_constant<int, (DEPTH - 1) * LV>{});
+    });
 }
 
 // ---------------------------------------------------------------------------

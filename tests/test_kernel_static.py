@@ -22,3 +22,18 @@ def test_schur_staging_has_no_inflight_hazard(tmp_path, src):
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 hazards" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="hipcc not installed")
+def test_kkt_linear_pass_vmcnt_waits(tmp_path):
+    """k_kkt_ric_nofact keeps PDPLQR_KKT_NF_DEPTH register sets in flight with
+    hand-counted vmcnt waits: no instruction touches a set before the wait that
+    retires it (scripts/asm_vmcnt_check.py models the counter in issue order)."""
+    asm = str(tmp_path / "kkt.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Iinclude",
+                    "--cuda-device-only", "-S", os.path.join(ROOT, "pdp-lqr_amd", "csrc", "kkt_riccati.hip"), "-o",
+                    asm], cwd=ROOT, check=True, capture_output=True, timeout=600)
+    for sym in ("k_kkt_ric_nofactILi4E", "k_kkt_ric_nofactILi0E"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "asm_vmcnt_check.py"), asm, sym],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr
