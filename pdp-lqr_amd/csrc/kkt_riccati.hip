@@ -749,6 +749,10 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
 // maxima, then admm_decide).  Rows: exactly Q.uni = 4 per stage k < N, none
 // at the terminal.
 // ---------------------------------------------------------------------------
+// ring depth of the ADMM (UPD) rollout: stages in flight
+#ifndef PDPLQR_KKT_UPD_RING
+#define PDPLQR_KKT_UPD_RING 3
+#endif
 template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false, bool EH = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
@@ -1336,16 +1340,16 @@ int launch_kkt_ric_forward_admm(const Shape &sh, const double *E, const double *
         return PDPLQR_ERR_UNSUPPORTED;
     const dim3 grid((unsigned)sh.batch), blk(64);
     if (fuse && check)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, true, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, true, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
                            (double *)nullptr, rho_dyn, q);
     else if (fuse)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, true, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, true, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
                            (double *)nullptr, rho_dyn, q);
     else if (check)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, false, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, false, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
                            (double *)nullptr, rho_dyn, q);
     else
-        hipLaunchKernelGGL((k_kkt_ric_fwd<3, true, false, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
+        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, false, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
                            (double *)nullptr, rho_dyn, q);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
