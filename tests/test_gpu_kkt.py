@@ -388,3 +388,68 @@ def test_kkt_h_upload_keeps_protocol_state():
         assert np.all(bs.status() == 0)
         outs.append(out)
     assert rel_err(outs[1], outs[0]) < 1e-13
+
+
+def test_record_form_follows_last_backward_kkt():
+    """The 12/4 KKT path writes the E^ record in a plain backward and the P~
+    record in an ADMM run's cache-writing backward; the forward follows the
+    last one (pdplqr_handle_s::rec_gain).  Plain solve -> ADMM run -> plain
+    solve on one handle, with and without hipGraph replay (PDPLQR_GRAPH=1 is
+    read at library load: child processes): both plain answers match OracleKKT."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    code = textwrap.dedent(r"""
+        import os, sys, numpy as np
+        sys.path[:0] = [os.environ["ROOT"], os.path.join(os.environ["ROOT"], "pdp-lqr_amd")]
+        from oracle.oracle import OracleKKT
+        from pdplqr import BatchedLQRSolver
+        from pdplqr.model import PackedModel
+        from pdplqr.problems import random_batch_arrays
+        n, m, N, batch, nc = 12, 4, 37, 3, 4
+        s = n + m
+        E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 1234)
+        g = np.random.default_rng(5)
+        ncs = np.full(N + 1, nc, dtype=np.int32)
+        ncs[N] = 0
+        D = np.concatenate([g.standard_normal((batch, nc * s)) for _ in range(N)], axis=1)
+        ny = int(ncs.sum())
+        ws = g.standard_normal((batch, N * s + n))
+        ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+        irho = 0.05 + g.random((batch, ny))
+        refs = []
+        for b in range(batch):
+            o = OracleKKT(PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b]))
+            o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+            o.backward(irho[b])
+            refs.append(o.forward(x0[b]))
+        bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+        bs.set_model(E, c, H, h, D)
+        worst = 0.0
+        for step in ("plain", "admm", "plain", "admm", "plain"):
+            if step == "admm":
+                lb, ub = np.full((batch, ny), -0.5), np.full((batch, ny), 0.5)
+                w, y, z = np.zeros((batch, N * s + n)), np.zeros((batch, ny)), np.zeros((batch, ny))
+                bs.admm_solve(x0, lb, ub, np.full((batch, ny), 3.0), w, y, z, max_iter=6, eps_abs=0.0, eps_rel=0.0)
+                assert np.all(np.isfinite(w))
+                continue
+            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+            bs.backward(irho)
+            out = np.zeros((batch, N * s + n))
+            bs.forward(x0, out)
+            assert np.all(bs.status() == 0)
+            for b in range(batch):
+                worst = max(worst, np.linalg.norm(out[b] - refs[b]) / np.linalg.norm(refs[b]))
+        print("worst", worst)
+        assert worst < 1e-8, worst
+    """)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for graph in ("0", "1"):
+        env = dict(os.environ, ROOT=root)
+        if graph == "1":
+            env["PDPLQR_GRAPH"] = "1"
+        else:
+            env.pop("PDPLQR_GRAPH", None)
+        subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
