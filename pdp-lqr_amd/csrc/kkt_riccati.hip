@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
 // ---------------------------------------------------------------------------
 // ring depth of the ADMM (UPD) rollout: stages in flight
 #ifndef PDPLQR_KKT_UPD_RING
-#define PDPLQR_KKT_UPD_RING 3
+#define PDPLQR_KKT_UPD_RING 4
 #endif
 template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false, bool EH = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
