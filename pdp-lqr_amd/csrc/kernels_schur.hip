@@ -80,6 +80,9 @@ using SymOff = std::integral_constant<bool, false>;
 // the fused-penalty instance has the registers (2 waves per SIMD) for G and M
 // on three independent MFMA accumulators each (schur_stage SPLIT = 1); C5 runs
 // it at one wave per SIMD, where the stage chain is what bounds it
+#ifndef PDPLQR_PEN_SPARSE_WB
+#define PDPLQR_PEN_SPARSE_WB 1
+#endif
 #ifndef PDPLQR_PEN_SPLIT
 #define PDPLQR_PEN_SPLIT 1
 #endif
@@ -269,15 +272,24 @@ __global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_S
                 // write-back stores below (each entry from both of its lanes) carry equal bits
                 const double dgc = R[SH::LOD + g + c * NC], rq = R[SH::LOR + g], gq = R[SH::LOG + g];
                 const double a = sqrt(fabs(rq)) * dgc;
+                const d4 H0 = in.H;
+                const double h0 = in.h;
                 in.H = mfma_f64(a, rq < 0.0 ? -a : a, in.H);
                 in.h -= sum_groups(dgc * (rq * gq));  // h~ -= D^T (rho o g)
                 double *Hk = A.Hw + b * sh.perHw + (long long)k * SH::ps;
+                // PDPLQR_PEN_SPARSE_WB: only entries whose bits the penalty
+                // changed are written back (a box on u changes the u block
+                // alone); lane 0 always stores, so every store instruction has a
+                // live lane and the fixed vm-op counts of the waits hold
+                auto changed = [&](double x, double y) {
+                    return !PDPLQR_PEN_SPARSE_WB || lane == 0 || __double_as_longlong(x) != __double_as_longlong(y);
+                };
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int i = 4 * r + g;
-                    gstore(Hk + (i >= c ? pidx(i, c, SH::s) : pidx(c, i, SH::s)), in.H[r]);
+                    if (changed(in.H[r], H0[r])) gstore(Hk + (i >= c ? pidx(i, c, SH::s) : pidx(c, i, SH::s)), in.H[r]);
                 }
-                gstore(A.hw + b * sh.perh + (long long)k * SH::s + c, in.h);
+                if (changed(in.h, h0)) gstore(A.hw + b * sh.perh + (long long)k * SH::s + c, in.h);
             }
             double w, luq[4];
             GainOut go;

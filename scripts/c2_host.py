@@ -1,0 +1,73 @@
+"""C2 (one N = 1024 12/4 problem, LQRParallelSolver path) host-issue study:
+per-solve wall time of backward + forward with
+  own      the handle's own stream, torch stream joins per call (bench.py)
+  shared   the handle on torch's current stream (no joins)
+  raw      shared + the C ABI called directly through ctypes (no wrapper)
+and the host-only issue time of the raw calls (no synchronisation inside the
+loop).  PDPLQR_GRAPH=1 in the environment replays captured graphs."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pdp-lqr_amd")]
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from pdplqr import BatchedLQRSolver  # noqa: E402
+from pdplqr._lib import lib  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n, m, N = 12, 4, 1024
+    E, c, H, h, x0 = bench.gen_batch_device(n, m, N, 1, seed=77, device=dev)
+    ws0 = torch.zeros(1, N * (n + m) + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    bs = BatchedLQRSolver(n, m, N, 1, solver="parallel", num_segments=8, keep_factors=True, device=0)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    res = {"graph": os.environ.get("PDPLQR_GRAPH", "0")}
+
+    def wrapped():
+        bs.backward(None)
+        bs.forward(x0, out)
+
+    L = lib()
+    hx, ho = C.c_void_p(x0.data_ptr()), C.c_void_p(out.data_ptr())
+
+    def raw():
+        L.pdplqr_backward(bs.h, None, 1)
+        L.pdplqr_forward(bs.h, hx, ho, 1)
+
+    def timed(fn, steps=200, warm=20):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    res["own_ms"] = timed(wrapped)
+    bs.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    res["shared_ms"] = timed(wrapped)
+    res["raw_ms"] = timed(raw)
+    # host issue time alone (the queue absorbs 50 solves)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        raw()
+    res["raw_issue_ms"] = (time.perf_counter() - t0) / 50 * 1e3
+    torch.cuda.synchronize()
+    res["status_ok"] = bool((bs.status() == 0).all())
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

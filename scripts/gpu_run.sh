@@ -12,6 +12,7 @@
 #   pytest-all                                           the whole -m gpu suite
 #   py:<script args, comma separated>                    e.g. py:scripts/prof_c5.py
 #   trace:<script args, comma separated>                 rocprofv3 --kernel-trace --stats of that script
+#   rtrace:<script args, comma separated>                the same plus the HIP runtime API trace (host-side call times)
 #   bench:<bench.py args, comma separated>               e.g. bench:--no-cpu,--steps,20
 #   lat                                                  scripts/ubench/lat_bench
 #   pmc:<tag>,<dominant kernel>,<script args...>         PMC passes of one workload (scripts/collect_pmc.sh)
@@ -43,6 +44,8 @@ for step in "$@"; do
       timeout -k 10 600 python -u $args > "$log" 2>&1 ;;
     trace)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$i" -o run -- python -u $args > "$log" 2>&1 ;;
+    rtrace)
+      timeout -k 10 600 rocprofv3 --runtime-trace --kernel-trace --stats --output-format csv -d "$O/rtrace_$i" -o run -- python -u $args > "$log" 2>&1 ;;
     bench)
       timeout -k 10 600 python -u bench.py $args > "$log" 2>&1 ;;
     lat)
