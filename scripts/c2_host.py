@@ -41,8 +41,8 @@ def main():
     hx, ho = C.c_void_p(x0.data_ptr()), C.c_void_p(out.data_ptr())
 
     def raw():
-        L.pdplqr_backward(bs.h, None, 1)
-        L.pdplqr_forward(bs.h, hx, ho, 1)
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
 
     def timed(fn, steps=200, warm=20):
         for _ in range(warm):
@@ -55,7 +55,7 @@ def main():
         return (time.perf_counter() - t0) / steps * 1e3
 
     res["own_ms"] = timed(wrapped)
-    bs.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    bs.handle.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     res["shared_ms"] = timed(wrapped)
     res["raw_ms"] = timed(raw)
     # host issue time alone (the queue absorbs 50 solves)
