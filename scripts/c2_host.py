@@ -54,10 +54,31 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / steps * 1e3
 
+    def raw_hostmem():  # backward with mem = HOST (no rho), as the wrapper passes it
+        L.pdplqr_backward(bs.handle.h, None, 0)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+
+    def wb_rf():
+        bs.backward(None)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+
+    def rb_wf():
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        bs.forward(x0, out)
+
+    res["raw_first_ms"] = timed(raw)
     res["own_ms"] = timed(wrapped)
     bs.handle.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     res["shared_ms"] = timed(wrapped)
     res["raw_ms"] = timed(raw)
+    res["raw_hostmem_ms"] = timed(raw_hostmem)
+    res["wrapped_bwd_raw_fwd_ms"] = timed(wb_rf)
+    res["raw_bwd_wrapped_fwd_ms"] = timed(rb_wf)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        wrapped()
+    res["wrapped_issue_ms"] = (time.perf_counter() - t0) / 50 * 1e3
     # host issue time alone (the queue absorbs 50 solves)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
