@@ -78,6 +78,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
     const int n = sh.n, m = sh.m, s = sh.s, S = A.S;
     const long long b = blockIdx.x / S;
     const int seg = blockIdx.x % S;
+    if (A.flag && seg == 0 && lane == 0) A.flag[b] = 0;
     const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
     const bool last = (seg == S - 1) && A.last_is_terminal;
     const long long frs = (long long)s * m + m;

@@ -157,6 +157,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
     const int k0 = m >> 2, k1 = (s - 1) >> 2;  // K chunks holding x rows
     const long long bi = blockIdx.x / S;
     const int seg = blockIdx.x % S;
+    if (A.flag && seg == 0 && lane == 0) A.flag[bi] = 0;
     const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
     const bool last = (seg == S - 1) && A.last_is_terminal;
     const long long frs = (long long)s * m + m;
@@ -489,6 +490,7 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
     const int S = A.S;
     const long long bi = blockIdx.x / S;
     const int seg = blockIdx.x % S;
+    if (A.flag && seg == 0 && tid == 0) A.flag[bi] = 0;
     const int N0 = A.seg_start[seg], N1 = N0 + A.seg_len[seg];
     const bool last = (seg == S - 1) && A.last_is_terminal;
     const long long frs = (long long)s * m + m;

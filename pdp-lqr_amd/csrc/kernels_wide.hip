@@ -434,6 +434,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     const int n = sh.n, m = sh.m, s = n + m, S = A.S;
     const long long bi = blockIdx.x / S;
     const int seg = blockIdx.x % S;
+    if (A.flag && !A.serial && seg == 0 && tid == 0) A.flag[bi] = 0;
     const int N0 = A.serial ? 0 : A.seg_start[seg], N1 = A.serial ? sh.N : N0 + A.seg_len[seg];
     const bool last = A.serial || ((seg == S - 1) && A.last_is_terminal);
     const long long frs = (long long)s * m + m;

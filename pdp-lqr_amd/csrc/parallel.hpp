@@ -17,6 +17,8 @@ struct SegArgs {
     int32_t *seg_status;       // [b][S]
     int serial = 0;            // k_seg_bwd_wide as the serial value-form backward: one segment [0, N),
                                // no element, status per problem (seg_start / seg_len unused)
+    int *flag = nullptr;       // [b] the scans' / maps' failure flag: zeroed by segment 0's block
+                               // (the later kernels of the solve set it; no memset launch)
 };
 
 struct ScanArgs {

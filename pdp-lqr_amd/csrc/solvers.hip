@@ -248,7 +248,7 @@ static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = 
     a.lpc = h->lpc;
     a.elem = ps->elem;
     a.seg_status = ps->seg_status;
-    PDPLQR_HIP_TRY(hipMemsetAsync(ps->flag, 0, (size_t)sh.batch * sizeof(int), h->stream));
+    a.flag = ps->flag;  // reset by the segment backward itself
     int rc = fact ? launch_seg_backward(a, h->stream) : launch_seg_backward_nofact(a, h->stream);
     if (rc) return rc;
     return parallel_scans(h, last_is_terminal);

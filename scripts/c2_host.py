@@ -79,6 +79,30 @@ def main():
     for _ in range(50):
         wrapped()
     res["wrapped_issue_ms"] = (time.perf_counter() - t0) / 50 * 1e3
+
+    def spin(us):
+        t = time.perf_counter() + us * 1e-6
+        while time.perf_counter() < t:
+            pass
+
+    def raw_spin_fwd():  # host time before the forward call (no Python API work)
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        spin(25)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+
+    def raw_spin_bwd():  # host time before the backward call
+        spin(25)
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+
+    def raw_curstream():
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        torch.cuda.current_stream(dev)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+
+    res["raw_spin25_before_fwd_ms"] = timed(raw_spin_fwd)
+    res["raw_spin25_before_bwd_ms"] = timed(raw_spin_bwd)
+    res["raw_current_stream_ms"] = timed(raw_curstream)
     # host issue time alone (the queue absorbs 50 solves)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
