@@ -100,6 +100,31 @@ def main():
         torch.cuda.current_stream(dev)
         L.pdplqr_forward(bs.handle.h, hx, ho, 1)
 
+    from pdplqr.solvers import _ptr, _mem_of
+
+    def raw_ptr():  # the wrapper's pointer conversion, then the raw call
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        ps = [_ptr(x0, "x0"), _ptr(out, "ws")]
+        L.pdplqr_forward(bs.handle.h, ps[0][0], ps[1][0], _mem_of(*ps))
+
+    def raw_enter():  # the wrapper's stream join check, then the raw call
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        cur = bs.handle._enter(x0, out)
+        L.pdplqr_forward(bs.handle.h, hx, ho, 1)
+        bs.handle._leave(cur)
+
+    def handle_fwd():  # _Handle.forward directly
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        bs.handle.forward(x0, out)
+
+    def fresh_ptr():  # new c_void_p objects from data_ptr() every call
+        L.pdplqr_backward(bs.handle.h, None, 1)
+        L.pdplqr_forward(bs.handle.h, C.c_void_p(x0.data_ptr()), C.c_void_p(out.data_ptr()), 1)
+
+    res["raw_ptr_ms"] = timed(raw_ptr)
+    res["raw_enter_ms"] = timed(raw_enter)
+    res["handle_fwd_ms"] = timed(handle_fwd)
+    res["fresh_ptr_ms"] = timed(fresh_ptr)
     res["raw_spin25_before_fwd_ms"] = timed(raw_spin_fwd)
     res["raw_spin25_before_bwd_ms"] = timed(raw_spin_bwd)
     res["raw_current_stream_ms"] = timed(raw_curstream)
