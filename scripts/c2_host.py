@@ -125,6 +125,12 @@ def main():
     res["raw_enter_ms"] = timed(raw_enter)
     res["handle_fwd_ms"] = timed(handle_fwd)
     res["fresh_ptr_ms"] = timed(fresh_ptr)
+    side = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    bs.handle.set_stream(side.cuda_stream)
+    with torch.cuda.stream(side):
+        res["wrapped_on_callers_stream_ms"] = timed(wrapped)
+    torch.cuda.synchronize()
     res["raw_spin25_before_fwd_ms"] = timed(raw_spin_fwd)
     res["raw_spin25_before_bwd_ms"] = timed(raw_spin_bwd)
     res["raw_current_stream_ms"] = timed(raw_curstream)
