@@ -658,7 +658,14 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
         def step():
             sh.backward(elem[0], True)
             sh.forward(x0, elem, 1, 0, out)
-    t = _timed(step, steps, warmup, dev, dist)
+    # the shard on the caller's (side) stream: backward, all-gather and forward
+    # in stream order, no cross-stream event joins (solve_distributed fast path)
+    sh.synchronize()
+    side = torch.cuda.Stream(device=dev)
+    sh.set_stream(side.cuda_stream)
+    with torch.cuda.stream(side):
+        t = _timed(step, steps, warmup, dev, dist)
+    torch.cuda.synchronize(dev)
     ok = bool(torch.isfinite(out).all().item())
     sh.close()
     oerr = None

@@ -122,6 +122,11 @@ class HorizonShard:
     def stream(self) -> int:
         return self._hd.stream()
 
+    def set_stream(self, stream_ptr: int):
+        """Run the shard's launches on `stream_ptr` (e.g. torch's current side
+        stream: solve_distributed then needs no cross-stream joins)."""
+        self._hd.set_stream(stream_ptr)
+
     def close(self):
         self._hd.close()
 
@@ -138,6 +143,16 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     elem = torch.empty(shard.batch, shard.es, dtype=torch.float64, device=dev)
+    if on_gpu and shard.stream() == torch.cuda.current_stream().cuda_stream:
+        # the shard runs on torch's current stream (set_stream): stream order
+        # alone sequences backward, the all-gather (ProcessGroupNCCL orders its
+        # stream after the current one) and forward -- no event joins, which
+        # cost ~19 us of GPU timeline each (profiles/r04/c2_host.log)
+        shard.backward(elem, rank == world - 1, rho)
+        gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(gathered, elem, group=group)
+        shard.forward(x0, gathered, world, rank, ws_out)
+        return ws_out
     if on_gpu:
         # Device-side ordering between the handle's stream and torch's current
         # stream (which ProcessGroupNCCL orders the all-gather against): events,

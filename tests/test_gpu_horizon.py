@@ -168,9 +168,12 @@ def _nccl_worker(port, q):
         outs = []
         from pdplqr.horizon import solve_distributed
 
-        for it in range(2):  # torch's default stream, then a side stream
-            if it:
+        for it in range(3):  # torch's default stream, a side stream, the shard on that side stream
+            if it == 1:
                 torch.cuda.set_stream(torch.cuda.Stream())
+            if it == 2:  # solve_distributed's no-join path
+                sh.synchronize()
+                sh.set_stream(torch.cuda.current_stream().cuda_stream)
             out = torch.full((2, N * (n + m) + n), float("nan"), dtype=torch.float64, device=dev)
             solve_distributed(sh, torch.from_numpy(x0).to(dev), out)
             torch.cuda.synchronize()
@@ -197,4 +200,4 @@ def test_single_rank_nccl_device_path():
     for got in outs:
         for b in range(2):
             assert rel_err(got[b], ref[b]) < TOL, b
-    assert np.array_equal(outs[0], outs[1])
+    assert len(outs) == 3 and np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
