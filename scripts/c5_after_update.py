@@ -3,6 +3,7 @@
   update   update_problem_data, then backward + forward (the protocol)
   stream   a 512 MB device copy (another kernel's traffic), then backward + forward
   idle     the device idle for 2 ms, then backward + forward
+  update_copy / update_idle   update_problem_data, then the copy / the idle time
 Backward kernel time from events on the solver's stream, median of 5."""
 import json
 import os
@@ -52,7 +53,7 @@ def main():
         r = irho if solver == "kkt" else rho
         out_s = {}
         with torch.cuda.stream(side):
-            for mode in ("repeat", "update", "stream", "idle", "repeat"):
+            for mode in ("repeat", "update", "stream", "idle", "update_copy", "update_idle", "repeat"):
                 ts = []
                 for _ in range(5):
                     if mode == "update":
@@ -60,6 +61,13 @@ def main():
                     elif mode == "stream":
                         big_b.copy_(big_a)
                     elif mode == "idle":
+                        torch.cuda.synchronize()
+                        time.sleep(0.002)
+                    elif mode == "update_copy":
+                        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+                        big_b.copy_(big_a)
+                    elif mode == "update_idle":
+                        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
                         torch.cuda.synchronize()
                         time.sleep(0.002)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
