@@ -20,7 +20,45 @@ import bench  # noqa: E402
 from pdplqr import BatchedLQRSolver  # noqa: E402
 
 
+def head():
+    """The same probe at the headline config (N = 1024, batch 4096, no constraints)."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n, m, N, B = 12, 4, 1024, 4096
+    E, c, H, h, x0 = bench.gen_batch_device(n, m, N, B, seed=1234, device=dev)
+    ws0 = torch.zeros(B, N * (n + m) + n, dtype=torch.float64, device=dev)
+    out = torch.empty_like(ws0)
+    big_a = torch.ones(64 << 20, dtype=torch.float64, device=dev)
+    big_b = torch.empty_like(big_a)
+    bs = BatchedLQRSolver(n, m, N, B, device=0)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.synchronize()
+    side = torch.cuda.Stream(device=dev)
+    bs.handle.set_stream(side.cuda_stream)
+    res = {}
+    with torch.cuda.stream(side):
+        for mode in ("repeat", "update", "stream", "update_copy", "repeat"):
+            ts = []
+            for _ in range(5):
+                if mode in ("update", "update_copy"):
+                    bs.update_problem_data(ws0, sigma=1e-6)
+                if mode in ("stream", "update_copy"):
+                    big_b.copy_(big_a)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+                bs.backward()
+                e1.record(side)
+                bs.forward(x0, out)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            res[mode + ("2" if mode in res else "")] = round(float(np.median(ts)), 4)
+    print(json.dumps({"head": res}), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "head":
+        return head()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     n, m, nc, N, batch = 12, 4, 4, 512, 1024
