@@ -93,10 +93,13 @@ typedef struct {
                                 LQRParallelSolver, lqr_solver_parallel.hpp:22-25,102-113):
                                 slice backward on every device, one RCCL all-gather of
                                 the slice elements (3 nx^2 + 2 nx doubles per problem),
-                                slice forward.  0 or 1: one device (`device`).  With
-                                num_devices > 1 backward_without_factorization, admm_solve,
-                                the shard_* calls and set_stream are unsupported, and
-                                `device` is ignored.  num_devices = 1 with a non-NULL
+                                slice forward.  0 or 1: one device (`device`).
+                                backward_without_factorization all-gathers only the
+                                slices' (f, p) (2 nx doubles per problem,
+                                lqr_solver_parallel.hpp:207-210); admm_solve runs its
+                                vectors on the first device around the slices' protocol
+                                calls.  With num_devices > 1 the shard_* calls and
+                                set_stream are unsupported, and `device` is ignored.  num_devices = 1 with a non-NULL
                                 `devices` runs the same split with one slice (RCCL
                                 communicator of one rank). */
     const int32_t *devices;  /* num_devices HIP ordinals, or NULL = 0 .. num_devices - 1.
@@ -207,6 +210,13 @@ int pdplqr_get_segments(pdplqr_handle h, int32_t *idx_start, int32_t *Nseg);
 /* ---------------------------------------------------------------------- */
 int pdplqr_shard_element_size(pdplqr_handle h);
 int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem);
+/* LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:148-154,190-211)
+ * on the slice: keep_factors = 1 and a preceding pdplqr_shard_backward with the same
+ * is_last_shard.  Writes the whole element; only its f and p differ from the
+ * factorising call's (F, C, P bit-identical), so ranks need to exchange only
+ * f, p (2n doubles per problem) and keep the rest of the last all-gather. */
+int pdplqr_shard_backward_without_factorization(pdplqr_handle h, const double *rho, int is_last_shard,
+                                                double *elem_out, int mem);
 int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_all, int32_t num_shards,
                          int32_t shard_id, double *ws, int mem);
 

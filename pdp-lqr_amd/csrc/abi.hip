@@ -18,6 +18,21 @@ static thread_local std::string g_last_error;
 
 void set_error(const std::string &msg) { g_last_error = msg; }
 
+int device_simds(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    return 4 * cus;  // CDNA: four SIMDs per CU
+}
+
+int x1_mask() {
+    static const int m = getenv("PDPLQR_X1_MASK") ? atoi(getenv("PDPLQR_X1_MASK")) : -1;
+    return m;
+}
+
+bool one_wave_per_simd(int device, long long waves) {
+    return waves <= device_simds(device) && !getenv("PDPLQR_NO_X1");
+}
+
 static int invalid(const std::string &msg) {
     set_error(msg);
     return PDPLQR_ERR_INVALID;
@@ -175,6 +190,7 @@ int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out) {
         return PDPLQR_ERR_HIP;
     }
     h->stream = h->own_stream;
+    sh.x1 = one_wave_per_simd(C.device, sh.batch);
     const long long B = sh.batch;
 #define ALLOC(ptr, cnt)                                  \
     do {                                                 \
@@ -242,7 +258,11 @@ fail:
 int pdplqr_destroy(pdplqr_handle h) {
     if (!h) return PDPLQR_OK;
     if (h->md) {
+        const int d0 = md_primary_device(h);
         md_release(h);
+        (void)hipSetDevice(d0);  // admm_solve's vectors (allocated on the first device)
+        admm_release(h);
+        for (void *p : h->allocs) (void)hipFree(p);
         delete h;
         return PDPLQR_OK;
     }
@@ -377,13 +397,7 @@ static int backward_common(pdplqr_handle h, const double *rho, int mem, bool fac
         set_error("backward_without_factorization needs a preceding backward");
         return PDPLQR_ERR_STATE;
     }
-    if (h->md) {
-        if (!fact) {
-            set_error("backward_without_factorization: not supported with num_devices > 1");
-            return PDPLQR_ERR_UNSUPPORTED;
-        }
-        return md_backward(h, rho, mem);
-    }
+    if (h->md) return md_backward(h, rho, mem, fact);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     h->host_staged = false;
     const Shape &sh = h->sh;

@@ -345,6 +345,142 @@ void admm_release(pdplqr_handle h) {
     h->admm = nullptr;
 }
 
+// admm_solve on a num_devices > 1 handle (multidev.hip): the ADMM vectors and
+// the update pass live on the first device; every x-update is the reference
+// protocol on the slices -- update_problem_data, then backward (iteration 1 and
+// after a rho change) or backward_without_factorization (its exchange is the
+// slices' (f, p) only), then forward -- with device pointers on the first
+// device (the slices copy their rows peer-to-peer).  The update pass is
+// k_admm_update (the unfused form: h~, g are re-formed by the next
+// update_problem_data on the slices).
+static int md_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const double *x0, const double *lb,
+                         const double *ub, const double *rho, double *ws, double *ys, double *zs, int mem) {
+    const Shape &sh = h->sh;
+    const int dev0 = md_primary_device(h);
+    hipStream_t S = reinterpret_cast<hipStream_t>(md_stream(h));
+    PDPLQR_HIP_TRY(hipSetDevice(dev0));
+    int rc = admm_alloc(h);
+    if (rc) return rc;
+    AdmmState *s = h->admm;
+    const long long B = sh.batch, W = B * sh.perh, Y = B * sh.ny;
+    const hipMemcpyKind kin = mem == PDPLQR_MEM_DEVICE ? hipMemcpyDefault : hipMemcpyHostToDevice;
+    if (mem == PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipDeviceSynchronize());  // inputs made on another stream
+    PDPLQR_HIP_TRY(hipMemcpyAsync(s->w, ws, W * sizeof(double), kin, S));
+    PDPLQR_HIP_TRY(hipMemcpyAsync(s->x0, x0, B * sh.n * sizeof(double), kin, S));
+    if (Y > 0) {
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->y, ys, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->z, zs, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->lb, lb, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->ub, ub, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->rho, rho, Y * sizeof(double), kin, S));
+        PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
+        hipLaunchKernelGGL(k_admm_validate, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, s->lb, s->ub,
+                           s->rho, s->active);
+        hipLaunchKernelGGL(k_admm_init, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, s->rho, s->irho);
+        PDPLQR_HIP_TRY(hipGetLastError());
+        PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, sizeof(int32_t), hipMemcpyDeviceToHost, S));
+        PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+        if (s->active_h[0] != 0) {
+            set_error("admm_solve: " + std::to_string(s->active_h[0]) +
+                      " constraint rows with e_lb > e_ub, or rho not in (0, inf)");
+            return PDPLQR_ERR_INVALID;
+        }
+    }
+    PDPLQR_HIP_TRY(hipMemsetAsync(s->done, 0, B * sizeof(int32_t), S));
+    PDPLQR_HIP_TRY(hipMemsetAsync(s->conv, 0, B * sizeof(int32_t), S));
+    PDPLQR_HIP_TRY(hipMemsetAsync(s->iters, 0, B * sizeof(int32_t), S));
+    PDPLQR_HIP_TRY(hipMemsetAsync(s->prim, 0, B * sizeof(double), S));
+    PDPLQR_HIP_TRY(hipMemsetAsync(s->dual, 0, B * sizeof(double), S));
+    PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+    AdmmArgs a;
+    a.sh = sh;
+    md_admm_view(h, &a.D, &a.d_off, &a.y_off);
+    a.hv = nullptr;  // (unfused: h~ and g are re-formed by update_problem_data)
+    a.hw = a.gw = nullptr;
+    a.wt = s->wt;
+    a.lb = s->lb;
+    a.ub = s->ub;
+    a.rho = s->rho;
+    a.irho = s->irho;
+    a.w = s->w;
+    a.y = s->y;
+    a.z = s->z;
+    a.done = s->done;
+    a.iters = s->iters;
+    a.conv = s->conv;
+    a.active = s->active;
+    a.prim = s->prim;
+    a.dual = s->dual;
+    a.rscale = s->rscale;
+    a.adaptive = st->adaptive_rho ? 1 : 0;
+    a.rho_tol = st->adaptive_rho_tolerance;
+    a.alpha = st->alpha;
+    a.sigma = st->sigma;
+    a.eps_abs = st->eps_abs;
+    a.eps_rel = st->eps_rel;
+    a.max_nc = h->max_nc;
+    a.no_penalty = 0;
+    {
+        const int c0 = sh.N > 0 ? h->ncs[0] : 0;
+        bool uni = c0 > 0 && h->ncs[sh.N] == 0;
+        for (int k = 0; k < sh.N && uni; ++k) uni = h->ncs[k] == c0;
+        a.uni = uni ? c0 : 0;
+    }
+    const dim3 ugrid((unsigned)B), ublk(256);
+    const double *irho_or_null = Y > 0 ? s->irho : nullptr;
+    int it = 1, rho_updates = 0;
+    bool refactor = true;
+    for (;; ++it) {
+        if ((rc = md_update(h, s->w, Y > 0 ? s->y : nullptr, Y > 0 ? s->z : nullptr, irho_or_null, st->sigma,
+                            PDPLQR_MEM_DEVICE)))
+            return rc;
+        h->updated = true;
+        if ((rc = md_backward(h, Y > 0 ? s->rho : nullptr, PDPLQR_MEM_DEVICE, refactor))) return rc;
+        h->factored = true;
+        refactor = false;
+        if ((rc = md_forward(h, s->x0, s->wt, PDPLQR_MEM_DEVICE))) return rc;  // (returns with the slices drained)
+        PDPLQR_HIP_TRY(hipSetDevice(dev0));
+        if (Y == 0) {  // nothing to split: one LQ solve is the answer
+            PDPLQR_HIP_TRY(hipMemcpyAsync(s->w, s->wt, W * sizeof(double), hipMemcpyDeviceToDevice, S));
+            std::vector<int32_t> one(B, 1);
+            PDPLQR_HIP_TRY(hipMemcpyAsync(s->iters, one.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, S));
+            PDPLQR_HIP_TRY(hipMemcpyAsync(s->conv, one.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, S));
+            PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+            break;
+        }
+        const bool last = it >= st->max_iter;
+        const bool check = last || it % st->check_every == 0;
+        a.it = it;
+        if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
+        if ((rc = launch_admm_update(a, sh.s <= 16 ? 16 : (sh.s <= 32 ? 32 : 64), false, check, ugrid, ublk, S)))
+            return rc;
+        if (check) {
+            PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
+            PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+            if (s->active_h[0] == 0) break;
+            if (s->active_h[1] && !last) {
+                hipLaunchKernelGGL(k_admm_rescale, dim3((unsigned)((Y + 255) / 256)), dim3(256), 0, S, Y, sh.ny,
+                                   s->rscale, s->rho, s->irho);
+                PDPLQR_HIP_TRY(hipGetLastError());
+                refactor = true;
+                ++rho_updates;
+            }
+        }
+        if (last) break;
+        PDPLQR_HIP_TRY(hipStreamSynchronize(S));  // the next update reads w, y, z on the slices' streams
+    }
+    const hipMemcpyKind kout = mem == PDPLQR_MEM_DEVICE ? hipMemcpyDefault : hipMemcpyDeviceToHost;
+    PDPLQR_HIP_TRY(hipMemcpyAsync(ws, s->w, W * sizeof(double), kout, S));
+    if (Y > 0) {
+        PDPLQR_HIP_TRY(hipMemcpyAsync(ys, s->y, Y * sizeof(double), kout, S));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(zs, s->z, Y * sizeof(double), kout, S));
+    }
+    PDPLQR_HIP_TRY(hipStreamSynchronize(S));
+    h->admm_iters = it;
+    h->admm_rho_updates = rho_updates;
+    return PDPLQR_OK;
+}
+
 }  // namespace pdplqr
 
 using namespace pdplqr;
@@ -366,10 +502,6 @@ void pdplqr_admm_settings_init(pdplqr_admm_settings *s) {
 int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const double *x0, const double *lb,
                       const double *ub, const double *rho, double *ws, double *ys, double *zs, int mem) {
     if (!h || !st) return PDPLQR_ERR_INVALID;
-    if (h->md) {
-        set_error("admm_solve: not supported with num_devices > 1");
-        return PDPLQR_ERR_UNSUPPORTED;
-    }
     if (!h->model_set) {
         set_error("admm_solve before set_model");
         return PDPLQR_ERR_STATE;
@@ -389,6 +521,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
                   "adaptive_rho_tolerance >= 1)");
         return PDPLQR_ERR_INVALID;
     }
+    if (h->md) return md_admm_solve(h, st, x0, lb, ub, rho, ws, ys, zs, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     int rc = admm_alloc(h);
     if (rc) return rc;
@@ -583,8 +716,8 @@ int pdplqr_admm_info(pdplqr_handle h, int32_t *iters, int32_t *converged, double
         set_error("admm_info before admm_solve");
         return PDPLQR_ERR_STATE;
     }
-    PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
-    PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
+    PDPLQR_HIP_TRY(hipSetDevice(h->md ? md_primary_device(h) : h->cfg.device));
+    PDPLQR_HIP_TRY(hipStreamSynchronize(h->md ? reinterpret_cast<hipStream_t>(md_stream(h)) : h->stream));
     AdmmState *s = h->admm;
     const size_t B = (size_t)h->sh.batch;
     if (iters) PDPLQR_HIP_TRY(hipMemcpy(iters, s->iters, B * sizeof(int32_t), hipMemcpyDeviceToHost));

@@ -35,6 +35,59 @@ __device__ __forceinline__ d4 mfma_f64_x3(double a1, double b1, double a2, doubl
 #endif
 }
 
+// One wave per SIMD (X1).  A one-wave-per-problem kernel whose waves are
+// latency-bound runs each problem's stage chain alone on a SIMD when the batch
+// fits the device's SIMDs once -- but only if the hardware places the waves
+// that way.  With <= 256 registers per wave a SIMD can host two of them, and
+// the dispatcher does pair waves on one SIMD while another SIMD of the same CU
+// idles (after some preceding kernels, e.g. update_problem_data's: measured
+// 65-86 of 1024 SIMDs doubled, those waves 1.3x slower, the kernel span 1.5x;
+// scripts/c5_placement.py).  X1 = true makes the wave
+// claim the SIMD's whole register file (an AGPR clobber raises the kernel's
+// register count past 256), so no second wave fits and the placement is one
+// per SIMD by construction.  Launchers pick X1 when grid <= SIMDs (Shape::x1).
+template <bool X1>
+__device__ __forceinline__ void simd_exclusive() {
+    if constexpr (X1) asm volatile("; one wave per SIMD" ::: "a255");
+}
+
+// Wave placement probe (diagnostic variant only, -DPDPLQR_HWID_PROBE=1): lane 0
+// of every block records where it ran -- (XCC, SE, SH, CU, SIMD) from the
+// HW_ID / XCC_ID hardware registers -- and its start / end on the 100 MHz
+// constant clock into a per-translation-unit device array, read back by
+// pdplqr_probe_read_<tu>() (scripts/c5_placement.py).
+#ifndef PDPLQR_HWID_PROBE
+#define PDPLQR_HWID_PROBE 0
+#endif
+#if PDPLQR_HWID_PROBE
+#define PDPLQR_PROBE_SLOTS 16384
+static __device__ long long g_wave_probe[PDPLQR_PROBE_SLOTS * 3];
+#define PDPLQR_PROBE_DEFINE(tu)                                                                    \
+    extern "C" int pdplqr_probe_read_##tu(long long *out) {                                       \
+        return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_probe), sizeof(g_wave_probe), 0,   \
+                                        hipMemcpyDeviceToHost);                                    \
+    }
+__device__ __forceinline__ long long hw_place() {
+    // hwreg(id, offset 0, size 32): id | (size - 1) << 11
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID[3:0]
+    // simd [5:4], cu [11:8], sh [12], se [15:13]
+    return (long long)(((xcc & 15u) << 16) | (((hw >> 13) & 7u) << 9) | (((hw >> 12) & 1u) << 8) |
+                       (((hw >> 8) & 15u) << 4) | ((hw >> 4) & 3u));
+}
+#define PDPLQR_PROBE_BEGIN const long long probe_t0_ = wall_clock64();
+#define PDPLQR_PROBE_END(lane, blk)                                                                \
+    if ((lane) == 0 && (blk) < PDPLQR_PROBE_SLOTS) {                                               \
+        g_wave_probe[3 * (blk)] = hw_place();                                                      \
+        g_wave_probe[3 * (blk) + 1] = probe_t0_;                                                   \
+        g_wave_probe[3 * (blk) + 2] = wall_clock64();                                              \
+    }
+#else
+#define PDPLQR_PROBE_DEFINE(tu)
+#define PDPLQR_PROBE_BEGIN
+#define PDPLQR_PROBE_END(lane, blk)
+#endif
+
 // packed lower (column-major) index of (i, j), i >= j, dimension d
 __device__ __forceinline__ int pidx(int i, int j, int d) { return j * d - ((j * (j - 1)) >> 1) + (i - j); }
 

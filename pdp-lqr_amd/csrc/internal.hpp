@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "pdplqr.h"
@@ -40,7 +41,22 @@ struct Shape {
     int ndD;            // sum_k nc_k * dim_k
     long long perE, perc, perH, perh, perHw, perKD;
     int mw = 1;  // PARALLEL: the 4-wave horizon kernels may run (parallel_init's family choice)
+    // the batch fits the device's SIMDs once: the one-wave-per-problem kernels
+    // launch their one-wave-per-SIMD instance (simd_exclusive, device_common.hpp)
+    int x1 = 0;
 };
+
+// f(std::true_type{}) or f(std::false_type{}): a launcher's generic lambda picks
+// the X1 instance of its kernel from Shape::x1
+int x1_mask();  // diagnostic: PDPLQR_X1_MASK limits X1 to kernel families (bits below)
+enum { X1_SCHUR = 1, X1_ROLL = 2, X1_NOFACT = 4, X1_KKT_BWD = 8, X1_KKT_FWD = 16, X1_KKT_NOFACT = 32 };
+template <typename F>
+inline void with_x1(int x1, int fam, F &&f) {
+    if (x1 && (x1_mask() & fam)) f(std::true_type{});
+    else f(std::false_type{});
+}
+int device_simds(int device);  // SIMDs of the device (4 per CU)
+bool one_wave_per_simd(int device, long long waves);  // waves <= SIMDs (PDPLQR_NO_X1: never)
 
 // Riccati (serial, batched) kernels: kernels_riccati.hip
 struct RiccatiArgs {

@@ -92,8 +92,9 @@ __device__ __forceinline__ double nofact_q(const double *R, int oe, int oc, cons
 #define PDPLQR_NOFACT_ADMM_DEPTH 4
 #endif
 
-template <int NN, int MM, int D>
+template <int NN, int MM, int D, bool X1 = false>
 __global__ __launch_bounds__(64) void k_nofact_dma(RiccatiArgs A) {
+    simd_exclusive<X1>();
     using SH = NofactShape<NN, MM>;
     constexpr int n = SH::n, m = SH::m, s = SH::s, NI = SH::NI;
     static_assert(SH::ok, "nofact DMA layout");
@@ -223,8 +224,9 @@ struct NofactAdmmShape {
     static constexpr bool ok = s == 16 && NC == 4 && n % 2 == 0 && (n * s) % 2 == 0 && ps % 2 == 0;
 };
 
-template <int NN, int MM, int NC, int D, bool CHECK>
+template <int NN, int MM, int NC, int D, bool CHECK, bool X1 = false>
 __global__ __launch_bounds__(64) void k_nofact_admm_dma(RiccatiArgs A, AdmmArgs Q) {
+    simd_exclusive<X1>();
     using SH = NofactAdmmShape<NN, MM, NC>;
     constexpr int n = SH::n, m = SH::m, s = SH::s, NI = SH::NI;
     static_assert(SH::ok, "fused nofact / ADMM layout");
@@ -402,12 +404,15 @@ int launch_nofact_admm(const RiccatiArgs &a, const AdmmArgs &q, bool check, hipS
         !al(q.y) || !al(q.lb) || !al(q.ub) || !al(q.rho) || !al(q.irho) || sh.perE % 2 || sh.perc % 2 ||
         sh.perh % 2 || sh.perHw % 2 || sh.ndD % 2 || sh.ny % 2)
         return PDPLQR_ERR_UNSUPPORTED;
-    if (check)
-        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st,
-                           a, q);
-    else
-        hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, false>), dim3(sh.batch), dim3(64), 0,
-                           st, a, q);
+    with_x1(sh.x1, X1_NOFACT, [&](auto x1) {
+        constexpr bool X = decltype(x1)::value;
+        if (check)
+            hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, true, X>), dim3(sh.batch),
+                               dim3(64), 0, st, a, q);
+        else
+            hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, false, X>), dim3(sh.batch),
+                               dim3(64), 0, st, a, q);
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -424,7 +429,10 @@ int launch_nofact_dma(const RiccatiArgs &a, hipStream_t st) {
     const Shape &sh = a.sh;
     if (!a.Lc || !a.lpc || getenv("PDPLQR_NO_DMA") || !nofact_aligned(a)) return PDPLQR_ERR_UNSUPPORTED;
     if (sh.n == 12 && sh.m == 4)
-        hipLaunchKernelGGL((k_nofact_dma<12, 4, PDPLQR_NOFACT_DEPTH>), dim3(sh.batch), dim3(64), 0, st, a);
+        with_x1(sh.x1, X1_NOFACT, [&](auto x1) {
+            hipLaunchKernelGGL((k_nofact_dma<12, 4, PDPLQR_NOFACT_DEPTH, decltype(x1)::value>), dim3(sh.batch),
+                               dim3(64), 0, st, a);
+        });
     else
         return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());

@@ -43,10 +43,11 @@ struct RollShape {
 #define PDPLQR_ROLL_DEPTH 4
 #endif
 
-template <int NN, int MM, int D, bool GAIN = false>
+template <int NN, int MM, int D, bool GAIN = false, bool X1 = false>
 __global__ __launch_bounds__(64) void k_rollout_dma(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
                                                     const double *__restrict__ x0, double *__restrict__ ws) {
+    simd_exclusive<X1>();
     using SH = RollShape<NN, MM, GAIN>;
     constexpr int n = SH::n, m = SH::m, s = SH::s, NI = SH::NI;
     constexpr int NQ = (n + 3) / 4;  // row / column chunks of the x block over g
@@ -165,15 +166,19 @@ int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const 
                        double *ws, hipStream_t st, bool gain) {
     if (gain) {
         if (!(sh.n == 12 && sh.m == 4 && roll_aligned(sh, E, c, FR))) return PDPLQR_ERR_UNSUPPORTED;
-        hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, true>), dim3(sh.batch), dim3(64), 0, st, sh, E,
-                           c, FR, x0, ws);
+        with_x1(sh.x1, X1_ROLL, [&](auto x1) {
+            hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, true, decltype(x1)::value>), dim3(sh.batch),
+                               dim3(64), 0, st, sh, E, c, FR, x0, ws);
+        });
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
     if (getenv("PDPLQR_NO_DMA") || !roll_aligned(sh, E, c, FR)) return PDPLQR_ERR_UNSUPPORTED;
     if (sh.n == 12 && sh.m == 4)
-        hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH>), dim3(sh.batch), dim3(64), 0, st, sh, E, c, FR,
-                           x0, ws);
+        with_x1(sh.x1, X1_ROLL, [&](auto x1) {
+            hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, false, decltype(x1)::value>), dim3(sh.batch),
+                               dim3(64), 0, st, sh, E, c, FR, x0, ws);
+        });
     else
         return PDPLQR_ERR_UNSUPPORTED;
     PDPLQR_HIP_TRY(hipGetLastError());

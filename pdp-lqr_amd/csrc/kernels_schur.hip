@@ -95,9 +95,11 @@ using SymOff = std::integral_constant<bool, false>;
 // penalised H~_k + D^T rho D and h~_k - D^T rho g feed the stage and are written
 // back in place (the reference's data.H += / data.h -= semantics, so a second
 // backward without update_problem_data penalises again, as there).
-template <int NN, int MM, bool GAIN = false, int NC = 0>
-__global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_SCHUR_WAVES) : 3)) void k_riccati_bwd_schur(
+template <int NN, int MM, bool GAIN = false, int NC = 0, bool X1 = false>
+__global__ __launch_bounds__(64, (X1 ? 1 : NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_SCHUR_WAVES) : 3)) void k_riccati_bwd_schur(
     RiccatiArgs A) {
+    PDPLQR_PROBE_BEGIN
+    simd_exclusive<X1>();
     static_assert(!GAIN || (NN == 12 && MM == 4 && PDPLQR_SCHUR_BLOCK), "gain-form record: 12/4 block path");
     static_assert(NC == 0 || (GAIN && NC == 4), "fused penalty: 12/4 gain-form path, 4 rows per stage");
     constexpr bool CT = NN > 0;
@@ -360,7 +362,10 @@ __global__ __launch_bounds__(64, (NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES : PDPLQR_S
         }
     }
     if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+    PDPLQR_PROBE_END(lane, b)
 }
+
+PDPLQR_PROBE_DEFINE(schur)
 
 static bool schur_aligned(const RiccatiArgs &a) {
     const Shape &sh = a.sh;
@@ -391,7 +396,10 @@ int launch_riccati_backward_pen(const RiccatiArgs &a, int nc, hipStream_t st) {
     if (nc != 4 || a.nc_last > 4 || !schur_gain_record(a) || getenv("PDPLQR_NO_PEN_FUSE") || !a.D || !a.rho ||
         !a.gw || !al(a.D) || !al(a.rho) || !al(a.gw) || sh.ny % 2 || sh.ndD % 2)
         return PDPLQR_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, true, 4>), dim3(sh.batch), dim3(64), 0, st, a);
+    with_x1(sh.x1, X1_SCHUR, [&](auto x1) {
+        hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, true, 4, decltype(x1)::value>), dim3(sh.batch), dim3(64), 0, st,
+                           a);
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -401,8 +409,11 @@ int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st) {
     const Shape &sh = a.sh;
     if (a.Lc || sh.s > 16 || getenv("PDPLQR_NO_SCHUR")) return PDPLQR_ERR_UNSUPPORTED;
     if (schur_gain_record(a))
-        hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4>), dim3(sh.batch),
-                           dim3(64), 0, st, a);
+        with_x1(sh.x1, X1_SCHUR, [&](auto x1) {
+            hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4, 0,
+                                                    decltype(x1)::value>),
+                               dim3(sh.batch), dim3(64), 0, st, a);
+        });
     else if (schur_ct(a))
         hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4>), dim3(sh.batch), dim3(64), 0, st, a);
     else

@@ -262,8 +262,10 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
     return true;
 }
 
-template <int NC>
+template <int NC, bool X1 = false>
 __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
+    PDPLQR_PROBE_BEGIN
+    simd_exclusive<X1>();
     constexpr int NN = 12, MM = 4;
     using SH = KBwdShape<NN, MM, NC>;
     using RS = KRecShape<NN, MM>;
@@ -525,7 +527,10 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     }
     if (k == 0) process(0, true);
     if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+    PDPLQR_PROBE_END(lane, b)
 }
+
+PDPLQR_PROBE_DEFINE(kkt)
 
 // ---------------------------------------------------------------------------
 // The right-hand-side part of the backward on a cached factor (the KKT
@@ -566,8 +571,9 @@ __device__ __forceinline__ void static_for(F &&f) {
 #define PDPLQR_KKT_NF_DEPTH 5
 #endif
 
-template <int NC>
+template <int NC, bool X1 = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
+    simd_exclusive<X1>();
     constexpr int n = 12, m = 4, s = 16;
     using RS = KRecShape<n, m>;
     __shared__ double pc[16];
@@ -753,11 +759,12 @@ __global__ __launch_bounds__(64) void k_kkt_ric_nofact(KKTRicArgs A) {
 #ifndef PDPLQR_KKT_UPD_RING
 #define PDPLQR_KKT_UPD_RING 4
 #endif
-template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false, bool EH = false>
+template <int D, bool UPD = false, bool FUSE = false, bool CHECK = false, bool EH = false, bool X1 = false>
 __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__restrict__ E,
                                                     const double *__restrict__ c, const double *__restrict__ FR,
                                                     const double *__restrict__ x0, double *__restrict__ x0acc,
                                                     double *__restrict__ ws, double rho_dyn, AdmmArgs Q) {
+    simd_exclusive<X1>();
     constexpr int n = 12, m = 4, s = 16, NC = 4;
     using RS = KRecShape<n, m>;
     constexpr int FS = RS::FS;  // stage stride of the record in HBM
@@ -1273,8 +1280,11 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     a.rho_dyn = rho_dyn;
     a.nc_last = nc_last;
     a.cache = cache;
-    if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_bwd<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(k_kkt_ric_bwd<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    with_x1(sh.x1, X1_KKT_BWD, [&](auto x1) {
+        constexpr bool X = decltype(x1)::value;
+        if (nc == 4) hipLaunchKernelGGL((k_kkt_ric_bwd<4, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+        else hipLaunchKernelGGL((k_kkt_ric_bwd<0, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -1303,8 +1313,11 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
     a.status = nullptr;
     a.rho_dyn = rho_dyn;  // (the E^ record's c^ = M^ c - rho_dyn M^ p)
     a.nc_last = nc_last;
-    if (nc == 4) hipLaunchKernelGGL(k_kkt_ric_nofact<4>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(k_kkt_ric_nofact<0>, dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    with_x1(sh.x1, X1_KKT_NOFACT, [&](auto x1) {
+        constexpr bool X = decltype(x1)::value;
+        if (nc == 4) hipLaunchKernelGGL((k_kkt_ric_nofact<4, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+        else hipLaunchKernelGGL((k_kkt_ric_nofact<0, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -1317,12 +1330,16 @@ int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, co
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    if (ehat)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, (bool)PDPLQR_KKT_EHAT>), dim3((unsigned)sh.batch),
-                           dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws, rho_dyn, AdmmArgs{});
-    else
-        hipLaunchKernelGGL((k_kkt_ric_fwd<4>), dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws,
-                           rho_dyn, AdmmArgs{});
+    with_x1(sh.x1, X1_KKT_FWD, [&](auto x1) {
+        constexpr bool X = decltype(x1)::value;
+        if (ehat)
+            hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, (bool)PDPLQR_KKT_EHAT, X>),
+                               dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws, rho_dyn,
+                               AdmmArgs{});
+        else
+            hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, false, X>), dim3((unsigned)sh.batch), dim3(64),
+                               0, st, sh, E, c, rec, x0, x0acc, ws, rho_dyn, AdmmArgs{});
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }
@@ -1339,18 +1356,23 @@ int launch_kkt_ric_forward_admm(const Shape &sh, const double *E, const double *
         sh.perh % 2 || sh.ndD % 2 || sh.ny % 2)
         return PDPLQR_ERR_UNSUPPORTED;
     const dim3 grid((unsigned)sh.batch), blk(64);
-    if (fuse && check)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, true, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
-                           (double *)nullptr, rho_dyn, q);
-    else if (fuse)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, true, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
-                           (double *)nullptr, rho_dyn, q);
-    else if (check)
-        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, false, true>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
-                           (double *)nullptr, rho_dyn, q);
-    else
-        hipLaunchKernelGGL((k_kkt_ric_fwd<PDPLQR_KKT_UPD_RING, true, false, false>), grid, blk, 0, st, sh, E, c, rec, x0, x0acc,
-                           (double *)nullptr, rho_dyn, q);
+    with_x1(sh.x1, X1_KKT_FWD, [&](auto x1) {
+        constexpr bool X = decltype(x1)::value;
+        constexpr int RG = PDPLQR_KKT_UPD_RING;
+        double *const nows = nullptr;
+        if (fuse && check)
+            hipLaunchKernelGGL((k_kkt_ric_fwd<RG, true, true, true, false, X>), grid, blk, 0, st, sh, E, c, rec, x0,
+                               x0acc, nows, rho_dyn, q);
+        else if (fuse)
+            hipLaunchKernelGGL((k_kkt_ric_fwd<RG, true, true, false, false, X>), grid, blk, 0, st, sh, E, c, rec, x0,
+                               x0acc, nows, rho_dyn, q);
+        else if (check)
+            hipLaunchKernelGGL((k_kkt_ric_fwd<RG, true, false, true, false, X>), grid, blk, 0, st, sh, E, c, rec, x0,
+                               x0acc, nows, rho_dyn, q);
+        else
+            hipLaunchKernelGGL((k_kkt_ric_fwd<RG, true, false, false, false, X>), grid, blk, 0, st, sh, E, c, rec, x0,
+                               x0acc, nows, rho_dyn, q);
+    });
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

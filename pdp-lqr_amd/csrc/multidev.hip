@@ -111,9 +111,15 @@ struct MultiDev {
     std::vector<MdSlice> plan;
     std::vector<pdplqr_handle> sh;
     std::vector<hipStream_t> st;
-    std::vector<hipEvent_t> ev;  // elem ready on its shard's stream (device-copy exchange)
-    // per shard, on its device: model staging (set_model), vectors, elements
-    std::vector<double *> ws, ys, zs, ir, rho, x0, elem, gathered, wout;
+    std::vector<hipEvent_t> ev;   // elem / fp ready on its shard's stream (device-copy exchange)
+    std::vector<hipEvent_t> xev;  // shard r's exchange copies done (they read every other shard's buffers)
+    bool xpending = false;        // a device-copy exchange was issued since the last backward
+    // per shard, on its device: model staging (set_model), vectors, elements,
+    // the (f, p) parts of the element and their gather (backward_without_factorization)
+    std::vector<double *> ws, ys, zs, ir, rho, x0, elem, gathered, wout, fp, gathered_fp;
+    // on the first device: the full D and row / D offsets (admm_solve's update pass)
+    double *Dfull = nullptr;
+    int32_t *d_off = nullptr, *y_off = nullptr;
     std::vector<ncclComm_t> comm;
     bool rccl = false;
     std::vector<std::vector<void *>> allocs;
@@ -180,6 +186,7 @@ void md_release(pdplqr_handle h) {
     for (int r = 0; r < md->R; ++r) {
         (void)hipSetDevice(md->dev[r]);
         if (r < (int)md->ev.size() && md->ev[r]) (void)hipEventDestroy(md->ev[r]);
+        if (r < (int)md->xev.size() && md->xev[r]) (void)hipEventDestroy(md->xev[r]);
         if (r < (int)md->sh.size() && md->sh[r]) (void)pdplqr_destroy(md->sh[r]);
         for (void *p : md->allocs[r]) (void)hipFree(p);
     }
@@ -219,6 +226,9 @@ int md_create(pdplqr_handle h, const pdplqr_config &C) {
     md->sh.assign(R, nullptr);
     md->st.assign(R, nullptr);
     md->ev.assign(R, nullptr);
+    md->xev.assign(R, nullptr);
+    md->fp.assign(R, nullptr);
+    md->gathered_fp.assign(R, nullptr);
     md->ws.assign(R, nullptr);
     md->ys.assign(R, nullptr);
     md->zs.assign(R, nullptr);
@@ -253,10 +263,25 @@ int md_create(pdplqr_handle h, const pdplqr_config &C) {
             (rc = md_alloc(md, r, &md->ys[r], B * ny)) || (rc = md_alloc(md, r, &md->zs[r], B * ny)) ||
             (rc = md_alloc(md, r, &md->ir[r], B * ny)) || (rc = md_alloc(md, r, &md->rho[r], B * ny)) ||
             (rc = md_alloc(md, r, &md->x0[r], B * n)) || (rc = md_alloc(md, r, &md->elem[r], B * es)) ||
-            (rc = md_alloc(md, r, &md->gathered[r], (long long)R * B * es)))
+            (rc = md_alloc(md, r, &md->gathered[r], (long long)R * B * es)) ||
+            (rc = md_alloc(md, r, &md->fp[r], B * 2 * n)) ||
+            (rc = md_alloc(md, r, &md->gathered_fp[r], (long long)R * B * 2 * n)))
             return rc;
         PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
         PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->ev[r], hipEventDisableTiming));
+        PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->xev[r], hipEventDisableTiming));
+    }
+    // admm_solve's update pass runs on the first device over the whole horizon
+    {
+        double *p = nullptr;
+        if ((rc = md_alloc(md, 0, &md->Dfull, B * h->sh.ndD))) return rc;
+        if ((rc = md_alloc(md, 0, &p, (C.N + 2 + 1) / 2 * 2))) return rc;  // (int32 offsets in double-sized slots)
+        md->d_off = reinterpret_cast<int32_t *>(p);
+        if ((rc = md_alloc(md, 0, &p, (C.N + 2 + 1) / 2 * 2))) return rc;
+        md->y_off = reinterpret_cast<int32_t *>(p);
+        PDPLQR_HIP_TRY(hipSetDevice(md->dev[0]));
+        PDPLQR_HIP_TRY(hipMemcpy(md->d_off, h->d_off_h.data(), (C.N + 2) * sizeof(int32_t), hipMemcpyHostToDevice));
+        PDPLQR_HIP_TRY(hipMemcpy(md->y_off, h->y_off_h.data(), (C.N + 2) * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     // peer access between distinct devices (the 2D slice copies, the device-copy exchange)
     for (int a = 0; a < R; ++a)
@@ -356,6 +381,20 @@ int md_set_model(pdplqr_handle h, int mask, const double *E, const double *c, co
         for (void *v : tmp) (void)hipFree(v);
         if (rc) return rc;
     }
+    if ((mask & PDPLQR_MODEL_D) && g.ndD > 0) {  // the full D for admm_solve's update pass (first device)
+        PDPLQR_HIP_TRY(hipSetDevice(md->dev[0]));
+        PDPLQR_HIP_TRY(hipMemcpyAsync(md->Dfull, D, (size_t)Bi * g.ndD * sizeof(double), kind, md->st[0]));
+        PDPLQR_HIP_TRY(hipStreamSynchronize(md->st[0]));
+    }
+    if (mem != PDPLQR_MEM_DEVICE) {  // host bytes this upload moved (pdplqr_get_model_upload_bytes)
+        long long bytes = 0;
+        if (mask & PDPLQR_MODEL_E) bytes += (long long)Bi * g.perE;
+        if (mask & PDPLQR_MODEL_C) bytes += (long long)Bi * g.perc;
+        if (mask & PDPLQR_MODEL_H) bytes += (long long)Bi * g.perH;
+        if (mask & PDPLQR_MODEL_HV) bytes += (long long)Bi * g.perh;
+        if (mask & PDPLQR_MODEL_D) bytes += (long long)Bi * g.ndD;
+        h->model_upload_bytes += bytes * (long long)sizeof(double);
+    }
     h->model_set = true;
     if (mask & (PDPLQR_MODEL_H | PDPLQR_MODEL_HV)) h->updated = false;
     return PDPLQR_OK;
@@ -407,14 +446,30 @@ int md_update(pdplqr_handle h, const double *ws, const double *ys, const double 
     return PDPLQR_OK;
 }
 
-int md_backward(pdplqr_handle h, const double *rho, int mem) {
+// backward (fact) or backward_without_factorization: the slice backwards, then
+// the exchange -- the whole slice elements (3n^2 + 2n doubles per problem) after
+// a factorising backward, only their (f, p) (2n) without factorization
+// (reduction_without_factorization's update_segment_data(p, f, id),
+// lqr_solver_parallel.hpp:207-210): F, C, P of the last gather stay valid.
+int md_backward(pdplqr_handle h, const double *rho, int mem, bool fact) {
     MultiDev *md = h->md;
     const Shape &g = h->sh;
-    const int N = g.N, Bi = g.batch;
-    const long long es = 3LL * g.n * g.n + 2LL * g.n, cnt = (long long)Bi * es;
+    const int N = g.N, Bi = g.batch, n = g.n;
+    const long long es = 3LL * n * n + 2LL * n;
+    const long long cnt = (long long)Bi * (fact ? es : 2LL * n);
     const hipMemcpyKind kind = md_kind(mem, true);
     int rc;
     if ((rc = md_inputs_ready(md, mem))) return rc;
+    // the last device-copy exchange read every slice's element / (f, p) buffer
+    // on the reading slice's stream: no slice rewrites its buffer before all of
+    // those copies are done
+    if (md->xpending) {
+        for (int q = 0; q < md->R; ++q) {
+            PDPLQR_HIP_TRY(hipSetDevice(md->dev[q]));
+            for (int r = 0; r < md->R; ++r) PDPLQR_HIP_TRY(hipStreamWaitEvent(md->st[q], md->xev[r], 0));
+        }
+        md->xpending = false;
+    }
     for (int r = 0; r < md->R; ++r) {
         const MdSlice &p = md->plan[r];
         const long long ny = p.ny_st + p.nc_term;
@@ -429,19 +484,37 @@ int md_backward(pdplqr_handle h, const double *rho, int mem) {
                              md->st[r])))
                 return rc;
         }
-        if ((rc = pdplqr_shard_backward(md->sh[r], ny ? md->rho[r] : nullptr, p.last ? 1 : 0, md->elem[r],
-                                        PDPLQR_MEM_DEVICE)))
-            return rc;
+        const double *rr = ny ? md->rho[r] : nullptr;
+        if (fact) rc = pdplqr_shard_backward(md->sh[r], rr, p.last ? 1 : 0, md->elem[r], PDPLQR_MEM_DEVICE);
+        else
+            rc = pdplqr_shard_backward_without_factorization(md->sh[r], rr, p.last ? 1 : 0, md->elem[r],
+                                                             PDPLQR_MEM_DEVICE);
+        if (rc) return rc;
+        if (!fact) {  // pack [f | p] per problem (element offsets 2n^2 and 3n^2 + n)
+            if ((rc = md_copy2d(md->fp[r], 2 * n, md->elem[r] + 2LL * n * n, es, n, Bi, hipMemcpyDeviceToDevice,
+                                md->st[r])) ||
+                (rc = md_copy2d(md->fp[r] + n, 2 * n, md->elem[r] + 3LL * n * n + n, es, n, Bi,
+                                hipMemcpyDeviceToDevice, md->st[r])))
+                return rc;
+        }
         PDPLQR_HIP_TRY(hipEventRecord(md->ev[r], md->st[r]));
     }
-    // the exchange: every shard receives [R][batch][3n^2+2n] (rank-major)
+    const std::vector<double *> &src = fact ? md->elem : md->fp;
+    const std::vector<double *> &dst = fact ? md->gathered : md->gathered_fp;
+    // the exchange: every slice receives [R][batch][width] (rank-major)
     if (md->rccl) {
         int e = g_rccl.group_start();
-        for (int r = 0; r < md->R && e == 0; ++r) {
-            PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
-            e = g_rccl.all_gather(md->elem[r], md->gathered[r], (size_t)cnt, NCCL_FLOAT64, md->comm[r], md->st[r]);
+        hipError_t he = hipSuccess;
+        for (int r = 0; r < md->R && e == 0 && he == hipSuccess; ++r) {
+            he = hipSetDevice(md->dev[r]);
+            if (he == hipSuccess)
+                e = g_rccl.all_gather(src[r], dst[r], (size_t)cnt, NCCL_FLOAT64, md->comm[r], md->st[r]);
         }
-        const int e2 = g_rccl.group_end();
+        const int e2 = g_rccl.group_end();  // always closes the group, also after an error inside it
+        if (he != hipSuccess) {
+            set_error(std::string("hipSetDevice: ") + hipGetErrorString(he));
+            return PDPLQR_ERR_HIP;
+        }
         if (e || e2) {
             set_error("ncclAllGather: " + nccl_msg(e ? e : e2));
             return PDPLQR_ERR_HIP;
@@ -451,13 +524,28 @@ int md_backward(pdplqr_handle h, const double *rho, int mem) {
             PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
             for (int q = 0; q < md->R; ++q) {
                 PDPLQR_HIP_TRY(hipStreamWaitEvent(md->st[r], md->ev[q], 0));
-                PDPLQR_HIP_TRY(hipMemcpyAsync(md->gathered[r] + q * cnt, md->elem[q], (size_t)cnt * sizeof(double),
+                PDPLQR_HIP_TRY(hipMemcpyAsync(dst[r] + q * cnt, src[q], (size_t)cnt * sizeof(double),
                                               hipMemcpyDefault, md->st[r]));
+            }
+            PDPLQR_HIP_TRY(hipEventRecord(md->xev[r], md->st[r]));
+        }
+        md->xpending = true;
+    }
+    if (!fact) {  // scatter the gathered (f, p) into the element slots of the last full gather
+        for (int r = 0; r < md->R; ++r) {
+            PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
+            for (int q = 0; q < md->R; ++q) {
+                double *eq = md->gathered[r] + (long long)q * Bi * es;
+                const double *fq = md->gathered_fp[r] + (long long)q * Bi * 2 * n;
+                if ((rc = md_copy2d(eq + 2LL * n * n, es, fq, 2 * n, n, Bi, hipMemcpyDeviceToDevice, md->st[r])) ||
+                    (rc = md_copy2d(eq + 3LL * n * n + n, es, fq + n, 2 * n, n, Bi, hipMemcpyDeviceToDevice,
+                                    md->st[r])))
+                    return rc;
             }
         }
     }
     if (mem != PDPLQR_MEM_DEVICE && (rc = md_sync(md))) return rc;
-    h->factored = true;
+    if (fact) h->factored = true;
     return PDPLQR_OK;
 }
 
@@ -524,6 +612,14 @@ int md_clear(pdplqr_handle h) {
 }
 
 void *md_stream(pdplqr_handle h) { return h->md->R > 0 ? reinterpret_cast<void *>(h->md->st[0]) : nullptr; }
+
+int md_primary_device(pdplqr_handle h) { return h->md->dev[0]; }
+
+void md_admm_view(pdplqr_handle h, const double **D, const int32_t **d_off, const int32_t **y_off) {
+    *D = h->md->Dfull;
+    *d_off = h->md->d_off;
+    *y_off = h->md->y_off;
+}
 
 }  // namespace pdplqr
 

@@ -604,7 +604,8 @@ int pdplqr_shard_element_size(pdplqr_handle h) {
 // Horizon shards: this handle holds one slice of the
 // horizon.  Backward = segment recursion + local scans; the slice element is the
 // suffix-scan entry 0 (e_0 (x) ... (x) e_{S-1}).  Elements: [batch][3n^2+2n].
-int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem) {
+static int shard_backward_common(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem,
+                                 bool fact) {
     if (!h || !elem_out) return PDPLQR_ERR_INVALID;
     if (h->cfg.solver != PDPLQR_SOLVER_PARALLEL || !h->par) {
         set_error("shard_backward needs a PARALLEL handle");
@@ -613,6 +614,14 @@ int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard,
     if (!h->updated) {
         set_error("shard_backward before update_problem_data");
         return PDPLQR_ERR_STATE;
+    }
+    if (!fact && (!h->factored || !h->Lc)) {
+        set_error("shard_backward_without_factorization needs keep_factors = 1 and a preceding shard_backward");
+        return PDPLQR_ERR_STATE;
+    }
+    if (!fact && (is_last_shard ? 1 : 0) != h->shard_last) {
+        set_error("shard_backward_without_factorization: is_last_shard differs from the factorising call's");
+        return PDPLQR_ERR_INVALID;
     }
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     const Shape &sh = h->sh;
@@ -623,23 +632,37 @@ int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard,
         else PDPLQR_HIP_TRY(hipMemcpyAsync(h->st_rho, rho, (size_t)sh.batch * sh.ny * sizeof(double),
                                            hipMemcpyHostToDevice, h->stream));
     }
-    int rc = launch_penalty(sh, h->D, drho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, 1,
+    // backward: H~ += D^T rho D and h~ -= D^T rho g; without factorization only
+    // the linear term (lqr_kernel.hpp:106-112, 150-158)
+    int rc = launch_penalty(sh, h->D, drho, h->gw, h->Hw, h->hw, h->d_off, h->y_off, h->tab_s, h->tab_n, fact ? 1 : 0,
                             h->max_nc, h->stream);
     if (rc) return rc;
-    if ((rc = parallel_backward(h, is_last_shard ? 1 : 0))) return rc;
+    if ((rc = parallel_backward(h, is_last_shard ? 1 : 0, fact))) return rc;
     h->shard_last = is_last_shard ? 1 : 0;
     ParallelState *ps = h->par;
     const long long es = 3LL * sh.n * sh.n + 2LL * sh.n;
-    // suffix entry 0 of every problem: suf_final[b][0]
-    for (int b = 0; b < sh.batch; ++b) {
-        const double *src = ps->suf_final + (long long)b * ps->S * es;
-        PDPLQR_HIP_TRY(hipMemcpyAsync(elem_out + b * es, src, es * sizeof(double),
-                                      mem == PDPLQR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                                      h->stream));
-    }
+    // suffix entry 0 of every problem: suf_final[b][0] (rows of es at pitch S es)
+    PDPLQR_HIP_TRY(hipMemcpy2DAsync(elem_out, (size_t)es * sizeof(double), ps->suf_final,
+                                    (size_t)ps->S * es * sizeof(double), (size_t)es * sizeof(double),
+                                    (size_t)sh.batch,
+                                    mem == PDPLQR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                    h->stream));
     if (mem != PDPLQR_MEM_DEVICE) PDPLQR_HIP_TRY(hipStreamSynchronize(h->stream));
-    h->factored = true;
+    if (fact) h->factored = true;
     return PDPLQR_OK;
+}
+
+int pdplqr_shard_backward(pdplqr_handle h, const double *rho, int is_last_shard, double *elem_out, int mem) {
+    return shard_backward_common(h, rho, is_last_shard, elem_out, mem, true);
+}
+
+// LQRParallelSolver::backward_without_factorization (lqr_solver_parallel.hpp:
+// 148-154,190-211) on one slice: the segment factorizations and the condensed
+// (F, C, P) are reused; the element's f, p are new (F, C, P bit-identical to
+// the factorising call's), so a rank exchange needs only f, p (2n doubles).
+int pdplqr_shard_backward_without_factorization(pdplqr_handle h, const double *rho, int is_last_shard,
+                                                double *elem_out, int mem) {
+    return shard_backward_common(h, rho, is_last_shard, elem_out, mem, false);
 }
 
 // elems_all: [num_shards][batch][3n^2+2n] (rank-major, the all-gather output).

@@ -64,10 +64,12 @@ int md_set_model(pdplqr_handle h, int mask, const double *E, const double *c, co
                  const double *D, int mem);
 int md_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho, double sigma,
               int mem);
-int md_backward(pdplqr_handle h, const double *rho, int mem);
+int md_backward(pdplqr_handle h, const double *rho, int mem, bool fact = true);
 int md_forward(pdplqr_handle h, const double *x0, double *ws, int mem);
 int md_status(pdplqr_handle h, int32_t *flags);
 int md_synchronize(pdplqr_handle h);
 int md_clear(pdplqr_handle h);
 void *md_stream(pdplqr_handle h);
+int md_primary_device(pdplqr_handle h);  // the device admm_solve's vectors live on
+void md_admm_view(pdplqr_handle h, const double **D, const int32_t **d_off, const int32_t **y_off);
 }  // namespace pdplqr

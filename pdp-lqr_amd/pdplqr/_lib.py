@@ -30,7 +30,8 @@ EXPORTS = [
     "pdplqr_get_model_upload_bytes", "pdplqr_update_problem_data",
     "pdplqr_backward", "pdplqr_backward_without_factorization", "pdplqr_forward", "pdplqr_clear_workspace",
     "pdplqr_get_value_function", "pdplqr_get_status", "pdplqr_get_segments", "pdplqr_shard_element_size",
-    "pdplqr_shard_backward", "pdplqr_shard_forward", "pdplqr_device_count",
+    "pdplqr_shard_backward", "pdplqr_shard_backward_without_factorization", "pdplqr_shard_forward",
+    "pdplqr_device_count",
     "pdplqr_admm_settings_init", "pdplqr_admm_solve", "pdplqr_admm_info", "pdplqr_multidev_plan",
 ]
 
@@ -102,6 +103,8 @@ def lib() -> C.CDLL:
     L.pdplqr_get_segments.argtypes = [vp, ip, ip]
     L.pdplqr_shard_element_size.argtypes = [vp]
     L.pdplqr_shard_backward.argtypes = [vp, dp, C.c_int, dp, C.c_int]
+    if hasattr(L, "pdplqr_shard_backward_without_factorization"):  # (absent from pre-round-5 A/B variants)
+        L.pdplqr_shard_backward_without_factorization.argtypes = [vp, dp, C.c_int, dp, C.c_int]
     L.pdplqr_shard_forward.argtypes = [vp, dp, dp, i32, i32, dp, C.c_int]
     L.pdplqr_device_count.argtypes = [ip]
     L.pdplqr_admm_settings_init.argtypes = [C.POINTER(AdmmSettings)]

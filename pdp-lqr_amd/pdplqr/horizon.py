@@ -7,6 +7,10 @@ nx = 24, nu = 8 over 8 x MI355X).  Each rank
   2. all-gathers the R elements (3n^2 + 2n doubles each) over RCCL/xGMI
   3. folds the global prefix (ranks < r) and suffix (ranks > r), computes the
      boundary states of its segments and rolls out      -> pdplqr_shard_forward
+backward_without_factorization (an ADMM iteration with rho unchanged,
+lqr_solver_parallel.hpp:148-154,190-211) reuses every factorization: only the
+elements' (f, p) change, so step 2 exchanges 2n doubles per problem instead of
+3n^2 + 2n and the rest of the last full gather is kept   -> solve_distributed(..., factorize=False)
 This is the multi-GPU form of the reference's condensed segment system
 (condensed_system.hpp:8-299), whose serial fold over OpenMP segments is
 replaced by the associative combine.
@@ -109,6 +113,18 @@ class HorizonShard:
         check(lib().pdplqr_shard_backward(self._hd.h, pr[0], int(bool(is_last)), pe[0], mem))
         return elem_out
 
+    def backward_without_factorization(self, elem_out, is_last: bool, rho=None):
+        """Slice backward reusing the factorizations of the last backward (same
+        is_last); writes the whole element, of which only f and p are new."""
+        pr, pe = _ptr(rho, "rho"), _ptr(elem_out, "elem")
+        check(lib().pdplqr_shard_backward_without_factorization(self._hd.h, pr[0], int(bool(is_last)), pe[0], pe[1]))
+        return elem_out
+
+    def fp_slices(self):
+        """(f, p) positions inside an element (layout F C f P p, include/pdplqr.h)."""
+        n = self.n
+        return slice(2 * n * n, 2 * n * n + n), slice(3 * n * n + n, 3 * n * n + 2 * n)
+
     def forward(self, x0, elems_all, num_shards: int, shard_id: int, ws_out):
         """elems_all: [num_shards, batch, 3n^2+2n] (rank-major all-gather output)."""
         p0, pe, pw = _ptr(x0, "x0"), _ptr(elems_all, "elems"), _ptr(ws_out, "ws")
@@ -131,10 +147,13 @@ class HorizonShard:
         self._hd.close()
 
 
-def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
+def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None, factorize: bool = True):
     """backward -> all-gather of slice elements -> forward, on the current
     torch.distributed process group.  With the nccl backend (RCCL) the
-    elements stay on the GPU; with gloo they are gathered through host memory."""
+    elements stay on the GPU; with gloo they are gathered through host memory.
+    factorize=False: backward_without_factorization; the all-gather carries only
+    every rank's (f, p) (2n doubles per problem, lqr_solver_parallel.hpp:207-210),
+    written into the full gather kept from the last factorising call."""
     import torch
     import torch.distributed as dist
 
@@ -142,15 +161,50 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
     rank = dist.get_rank(group)
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    last = rank == world - 1
+    if not factorize and getattr(shard, "_gathered", None) is None:
+        raise RuntimeError("solve_distributed(factorize=False) needs a preceding factorising solve")
+    fs, ps = shard.fp_slices()
+
+    def exchange(elem):
+        """The all-gather: the whole elements, or their (f, p) into the kept gather."""
+        if factorize:
+            g = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=elem.device)
+            if on_gpu:
+                dist.all_gather_into_tensor(g, elem, group=group)
+            else:
+                parts = [torch.empty_like(elem) for _ in range(world)]
+                dist.all_gather(parts, elem, group=group)
+                g = torch.stack(parts).contiguous()
+            shard._gathered = g
+            return g
+        fp = torch.cat([elem[:, fs], elem[:, ps]], dim=1).contiguous()
+        gfp = torch.empty(world, shard.batch, 2 * shard.n, dtype=torch.float64, device=fp.device)
+        if on_gpu:
+            dist.all_gather_into_tensor(gfp, fp, group=group)
+        else:
+            parts = [torch.empty_like(fp) for _ in range(world)]
+            dist.all_gather(parts, fp, group=group)
+            gfp = torch.stack(parts)
+        g = shard._gathered
+        g[:, :, fs] = gfp[:, :, :shard.n]
+        g[:, :, ps] = gfp[:, :, shard.n:]
+        return g
+
+    def bwd(elem):
+        if factorize:
+            shard.backward(elem, last, rho)
+        else:
+            shard.backward_without_factorization(elem, last, rho)
+
     elem = torch.empty(shard.batch, shard.es, dtype=torch.float64, device=dev)
     if on_gpu and shard.stream() == torch.cuda.current_stream().cuda_stream:
         # the shard runs on torch's current stream (set_stream): stream order
         # alone sequences backward, the all-gather (ProcessGroupNCCL orders its
         # stream after the current one) and forward -- no event joins, which
         # cost ~19 us of GPU timeline each (profiles/r04/c2_host.log)
-        shard.backward(elem, rank == world - 1, rho)
-        gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(gathered, elem, group=group)
+        bwd(elem)
+        gathered = exchange(elem)
         shard.forward(x0, gathered, world, rank, ws_out)
         return ws_out
     if on_gpu:
@@ -161,24 +215,20 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None):
         cur = torch.cuda.current_stream()
         hs.wait_stream(cur)  # x0 / ws_out / rho produced on the current stream
         elem.record_stream(hs)
-        shard.backward(elem, rank == world - 1, rho)
+        bwd(elem)
         cur.wait_stream(hs)
-        gathered = torch.empty(world, shard.batch, shard.es, dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(gathered, elem, group=group)
+        gathered = exchange(elem)
         hs.wait_stream(cur)
         gathered.record_stream(hs)
         shard.forward(x0, gathered, world, rank, ws_out)
         cur.wait_stream(hs)  # ws_out is read on the current stream
         return ws_out
-    else:
-        e_np = np.zeros((shard.batch, shard.es))
-        shard.backward(e_np, rank == world - 1, None if rho is None else rho)
-        elem = torch.from_numpy(e_np)
-        parts = [torch.empty_like(elem) for _ in range(world)]
-        dist.all_gather(parts, elem, group=group)
-        gathered = torch.stack(parts).contiguous()
-        if isinstance(ws_out, np.ndarray):
-            gathered = gathered.numpy()
-        elif getattr(ws_out, "is_cuda", False):
-            gathered = gathered.to(ws_out.device)
-    return shard.forward(x0, gathered, world, rank, ws_out)
+    e_np = np.zeros((shard.batch, shard.es))
+    bwd(e_np)
+    gathered = exchange(torch.from_numpy(e_np))
+    if isinstance(ws_out, np.ndarray):
+        gathered = gathered.numpy()
+    elif getattr(ws_out, "is_cuda", False):
+        gathered = gathered.to(ws_out.device)
+    return shard.forward(x0, np.ascontiguousarray(gathered) if isinstance(gathered, np.ndarray) else gathered,
+                         world, rank, ws_out)

@@ -181,6 +181,12 @@ class _Handle:
     def clear_workspace(self):
         check(lib().pdplqr_clear_workspace(self.h))
 
+    def model_upload_bytes(self) -> int:
+        """Host -> device model bytes since creation (pdplqr_get_model_upload_bytes)."""
+        v = C.c_int64(0)
+        check(lib().pdplqr_get_model_upload_bytes(self.h, C.byref(v)))
+        return int(v.value)
+
     def synchronize(self):
         check(lib().pdplqr_synchronize(self.h))
 
