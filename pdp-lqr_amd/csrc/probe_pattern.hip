@@ -49,7 +49,33 @@ __global__ __launch_bounds__(256) void k_probe_pattern(const double2 *__restrict
     if (acc == 1234.5) sink[0] = acc;  // keeps the loads live
 }
 
+// Streaming copy with 16-byte loads / stores (the guide's float4 copy, 6.29
+// TB/s measured): every thread keeps four loads in flight, grid-stride over
+// the buffer.  The achievable-HBM reference the roofline lines quote beside the
+// 8 TB/s spec (torch's copy_ runs the runtime's blit kernel instead).
+__global__ __launch_bounds__(256) void k_probe_copy(const double2 *__restrict__ a, double2 *__restrict__ b,
+                                                    size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const double2 v0 = a[i], v1 = a[i + stride], v2 = a[i + 2 * stride], v3 = a[i + 3 * stride];
+        b[i] = v0;
+        b[i + stride] = v1;
+        b[i + 2 * stride] = v2;
+        b[i + 3 * stride] = v3;
+    }
+    for (; i < n; i += stride) b[i] = a[i];
+}
+
 }  // namespace
+
+// 16-byte streaming copy of nbytes (a multiple of 16); returns 0 or a hipError_t.
+extern "C" int pdplqr_probe_copy(const void *src, void *dst, size_t nbytes, int blocks, void *stream) {
+    if (nbytes % 16 || blocks < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_probe_copy, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const double2 *)src,
+                       (double2 *)dst, nbytes / 16);
+    return (int)hipGetLastError();
+}
 
 // Chunks are 16 bytes; r0, r1, r2 in [1, 128], rw in [0, 64].  Returns 0 or a
 // hipError_t.  Buffers hold P * N records of their size.

@@ -19,8 +19,10 @@ independent problems of one shape, host numpy or device (torch) buffers.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import enum
+import weakref
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -65,6 +67,23 @@ def _mem_of(*ps):
     return mems.pop() if mems else _lib.PDPLQR_MEM_HOST
 
 
+_LIVE = weakref.WeakSet()  # open handles, closed by _close_all at interpreter exit
+_ATEXIT = False
+
+
+def _close_all():
+    """Destroy every handle still open when the interpreter exits, while the
+    HIP runtime (torch's, which libpdplqr.so binds to) is fully alive: this
+    hook is registered after torch is imported, so it runs before torch's own
+    exit hooks and long before the runtime's static destructors in exit()
+    (teardown order)."""
+    for hd in list(_LIVE):
+        try:
+            hd.close()
+        except Exception:
+            pass
+
+
 class _Handle:
     """Owns one pdplqr_handle."""
 
@@ -99,6 +118,11 @@ class _Handle:
         h = C.c_void_p()
         check(L.pdplqr_create(C.byref(cfg), C.byref(h)))
         self.h = h
+        global _ATEXIT
+        if not _ATEXIT:  # (lib() imported torch first: this hook runs before torch's)
+            atexit.register(_close_all)
+            _ATEXIT = True
+        _LIVE.add(self)
         self.nx, self.nu, self.N, self.batch = int(nx), int(nu), int(N), int(batch)
         self.ncs = self._ncs if self._ncs is not None else np.zeros(N + 1, dtype=np.int32)
         self.ny = int(np.sum(self.ncs))
