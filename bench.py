@@ -344,7 +344,7 @@ def pattern_ceiling_ms(dev, n, m, N, batch, reps=5):
     s = n + m
     ch = lambda doubles: (doubles + 1) // 2  # noqa: E731
     # rollout record: gain form [K~ | k~] on the 12/4 value-form path, else [L(:, 0:m) | lu']
-    gain = (n, m) == (12, 4) and not os.environ.get("PDPLQR_REC_L")
+    gain = (n, m) == (12, 4)
     rE, rH, rc, rR, rw = ch(n * s), ch(s * (s + 1) // 2 + s), ch(n), ch(n * m + m if gain else s * m + m), ch(s)
     st = N * batch
     bufs = [torch.zeros(st * r * 2, dtype=torch.float64, device=dev) for r in (rE, rH, rc, rR)]
@@ -836,7 +836,7 @@ def bwd_kernel_name(n, m, keep):
     if not keep and s <= 16:
         if (n, m) == (12, 4):  # the record form rides in the template (kernels_schur.hip GAIN; NC = 0:
             # no fused penalty rows -- summaries before round 4 name it without that argument)
-            return f"k_riccati_bwd_schur<12, 4, {'false' if os.environ.get('PDPLQR_REC_L') else 'true'}, 0>"
+            return "k_riccati_bwd_schur<12, 4, true, 0>"
         return "k_riccati_bwd_schur<0, 0, false>"
     if (n, m) == (12, 4):
         return f"k_riccati_bwd_fast<1, 12, 4, {str(bool(keep)).lower()}>"

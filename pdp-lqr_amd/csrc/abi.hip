@@ -24,11 +24,6 @@ int device_simds(int device) {
     return 4 * cus;  // CDNA: four SIMDs per CU
 }
 
-int x1_mask() {
-    static const int m = getenv("PDPLQR_X1_MASK") ? atoi(getenv("PDPLQR_X1_MASK")) : -1;
-    return m;
-}
-
 bool one_wave_per_simd(int device, long long waves) {
     return waves <= device_simds(device) && !getenv("PDPLQR_NO_X1");
 }

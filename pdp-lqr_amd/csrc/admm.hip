@@ -594,7 +594,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
     a.no_penalty = kkt ? 1 : 0;
     {
         const int c0 = sh.N > 0 ? h->ncs[0] : 0;
-        bool uni = c0 > 0 && h->ncs[sh.N] == 0 && !getenv("PDPLQR_ADMM_NO_UNI");
+        bool uni = c0 > 0 && h->ncs[sh.N] == 0;
         for (int k = 0; k < sh.N && uni; ++k) uni = h->ncs[k] == c0;
         a.uni = uni ? c0 : 0;
     }

@@ -40,9 +40,6 @@ namespace pdplqr {
 // Phase B: R^T C_a u and R^T v1 on wave 3 (idle there otherwise) instead of
 // after R^T F_a on wave 1, the slowest wave of the phase (comb_ab.log: the
 // block waited 2.5 us for it).  0: on wave 1 (A/B).
-#ifndef PDPLQR_MW_VEC_W3
-#define PDPLQR_MW_VEC_W3 1
-#endif
 
 struct MwSmem {
     int ld;
@@ -84,13 +81,7 @@ __device__ __forceinline__ void mw_col_load(d4 (&B)[T][1], const double *p, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g, jj = 16 * j + c;
-#if PDPLQR_BF_LOAD
-            const bool in = i < n && jj < n;
-            const double v = p[(in ? i : 0) + (in ? jj : 0) * PL];  // branch-free (see wm_load)
-            B[a][0][r] = in ? v : 0.0;
-#else
             B[a][0][r] = (i < n && jj < n) ? p[i + jj * PL] : 0.0;
-#endif
         }
 }
 
@@ -114,13 +105,7 @@ __device__ __forceinline__ void mw_vec2_load(d4 (&B)[T][1], const double *p, int
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g;
-#if PDPLQR_BF_LOAD
-            const bool in = i < n && c < 2;
-            const double v = p[(in ? i : 0) + (in ? c : 0) * P];  // branch-free (see wm_load)
-            B[a][0][r] = in ? v : 0.0;
-#else
             B[a][0][r] = (i < n && c < 2) ? p[i + c * P] : 0.0;
-#endif
         }
 }
 
@@ -267,10 +252,8 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wm_tn(B, R, Fa, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // R^T F_a
             wm_store(B, sm.B1, PL, n, g, c);
         }
-#if PDPLQR_MW_VEC_W3
     } else if (wv == 3) {  // the two vector products on the wave phase B leaves idle
         wm_load(R, sm.S, PL, n, true, 1.0, g, c);
-#endif
         WV<T> cu, v1, y;
         wv_load(cu, sm.bv + n, n, g, c);
         if (fcf) wv_load(v1, sm.bv, n, g, c);

@@ -65,12 +65,6 @@ struct CombSmem {
 // combine (profiles/r03/comb_ab.log): chunk-outer 1824 -> 1676 ticks, the
 // branch-free loads 1728 -> 1824 (they also read the all-padding registers a
 // guard skips as a whole), so they stay off here.
-#ifndef PDPLQR_BF_LOAD
-#define PDPLQR_BF_LOAD 0
-#endif
-#ifndef PDPLQR_TN_CHUNK_OUTER
-#define PDPLQR_TN_CHUNK_OUTER 1
-#endif
 
 template <int T>
 __device__ __forceinline__ void wm_load(WM<T> &M, const double *p, int ld, int n, bool trans, double pad, int g,
@@ -85,16 +79,9 @@ __device__ __forceinline__ void wm_load(WM<T> &M, const double *p, int ld, int n
                 // select (a guarded read compiles to an exec-mask region with its
                 // own wait per element)
                 const int i = 16 * a + 4 * r + g, j = 16 * b + c;
-#if PDPLQR_BF_LOAD
-                const bool in = i < n && j < n;
-                const int ic = in ? i : 0, jc = in ? j : 0;
-                const double x = trans ? p[jc + ic * ld] : p[ic + jc * ld];
-                M.t[a][b][r] = in ? x : ((i == j) ? pad : 0.0);
-#else
                 double v = (i == j) ? pad : 0.0;
                 if (i < n && j < n) v = trans ? p[j + i * ld] : p[i + j * ld];
                 M.t[a][b][r] = v;
-#endif
             }
 }
 
@@ -143,8 +130,7 @@ __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, 
                 const int i = 16 * a + 4 * r + g, j = 16 * b + c;
                 acc[a][b][r] = (add ? add->t[a][b][r] : 0.0) + (i == j ? diag : 0.0);
             }
-#if PDPLQR_TN_CHUNK_OUTER
-    if constexpr (T == 1 && PDPLQR_MFMA_SPLIT) {
+    if constexpr (T == 1) {
         // one output tile: its K chunks would be ONE dependent chain (~186
         // cycles a link); on separate accumulators they issue back to back
         const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -167,17 +153,6 @@ __device__ __forceinline__ void wm_tn(WM<T> &C, const WM<T> &X, const WM<T> &Y, 
                             acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
                 }
     }
-#else
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b)
-#pragma unroll
-            for (int kt = 0; kt < T; ++kt)
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                    if (16 * kt + 4 * kk < n) acc[a][b] = mfma_f64(sgn * X.t[kt][a][kk], Y.t[kt][b][kk], acc[a][b]);
-#endif
 #pragma unroll
     for (int a = 0; a < T; ++a)
 #pragma unroll
@@ -319,14 +294,8 @@ __device__ __forceinline__ bool elim_regs_n(WM<T> &M, d4 (&B)[T][TB], int n_rt, 
 // once per block (lane (g, c) supplies A[c][g]); each tile then costs one
 // MFMA instead of four row-group broadcasts, ten FMAs and a select chain.
 // PDPLQR_T4_MFMA=0 keeps the broadcast form (A/B diagnostics).
-#ifndef PDPLQR_T4_MFMA
-#define PDPLQR_T4_MFMA 1
-#endif
 // Blocked-Cholesky trailing update on the upper tiles only, the next block's
 // diagonal tile first (PDPLQR_CHOL_UPPER=0: every tile pair, row order; A/B)
-#ifndef PDPLQR_CHOL_UPPER
-#define PDPLQR_CHOL_UPPER 1
-#endif
 
 // The lane picks are products with 0/1 weights (loop-invariant per lane), not
 // selects: a select chain over values used nowhere else was turned into
@@ -395,42 +364,11 @@ __device__ __forceinline__ bool chol_blk4_aug(d4 &M, d4 (&B)[TB], int g, int c) 
                 T[i][j] = -v * inv[i];
             }
         }
-#if PDPLQR_T4_MFMA
         const double top = t4_operand(T, g, c);
         const double v = t4_apply(top, M[blk]);
         const double vt = (c >= j0 + 4) ? v : 0.0;  // panel, trailing rows only
 #pragma unroll
         for (int tb = 0; tb < TB; ++tb) B[tb][blk] = t4_apply(top, B[tb][blk]);  // T4 B_block
-#else
-        // row-block values M[j0 + k][c] (register blk, row group k) -> V
-        double ml[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ml[k] = bcast_group(M[blk], k);
-        double v = 0.0;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k <= jj; ++k) s = __builtin_fma(T[jj][k], ml[k], s);
-            v = (g == jj) ? s : v;
-        }
-        const double vt = (c >= j0 + 4) ? v : 0.0;  // trailing rows only
-#pragma unroll
-        for (int tb = 0; tb < TB; ++tb) {  // block rows of B: T4 B_block (in place, register blk)
-            double bl[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) bl[k] = bcast_group(B[tb][blk], k);
-            double s4 = 0.0;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k <= jj; ++k) s = __builtin_fma(T[jj][k], bl[k], s);
-                s4 = (g == jj) ? s : s4;
-            }
-            B[tb][blk] = s4;
-        }
-#endif
         if (blk < 3) M = mfma_f64(-vt, vt, M);
 #pragma unroll
         for (int tb = 0; tb < TB; ++tb) B[tb] = mfma_f64(-vt, B[tb][blk], B[tb]);
@@ -482,28 +420,12 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
             }
         }
         double vt[T];
-#if PDPLQR_T4_MFMA
         const double top = t4_operand(Ti, g, c);
-#endif
 #pragma unroll
         for (int ta = 0; ta < T; ++ta) {
             vt[ta] = 0.0;
             if (ta < tj) continue;
-#if PDPLQR_T4_MFMA
             const double v = t4_apply(top, M.t[tj][ta][rj]);  // (T M_rows)[g][16 ta + c]
-#else
-            double ml[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ml[k] = bcast_group(M.t[tj][ta][rj], k);  // M[j0 + k][16 ta + c]
-            double v = 0.0;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k <= jj; ++k) s = __builtin_fma(Ti[jj][k], ml[k], s);
-                v = (g == jj) ? s : v;
-            }
-#endif
             const int col = 16 * ta + c;
             vt[ta] = (col >= j0 + 4) ? v : 0.0;  // trailing rows of the panel
             if (KEEP) M.t[tj][ta][rj] = (col >= j0) ? v : 0.0;  // row block of C^T, final
@@ -511,29 +433,13 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
         if (AUG) {
 #pragma unroll
             for (int tb = 0; tb < TB; ++tb) {  // block rows of B: T4 B_block (register rj of tile row tj)
-#if PDPLQR_T4_MFMA
                 B[tj][tb][rj] = t4_apply(top, B[tj][tb][rj]);
-#else
-                double bl[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) bl[k] = bcast_group(B[tj][tb][rj], k);
-                double s4 = 0.0;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    double s = 0.0;
-#pragma unroll
-                    for (int k = 0; k <= jj; ++k) s = __builtin_fma(Ti[jj][k], bl[k], s);
-                    s4 = (g == jj) ? s : s4;
-                }
-                B[tj][tb][rj] = s4;
-#endif
             }
         }
         // Trailing update, upper tiles only (the panels read M's row blocks
         // M.t[tj][ta], ta >= tj, and the diagonal tiles; a lower tile is never
         // read again).  The next block's diagonal tile goes first: its
         // readlanes wait on that one product.
-#if PDPLQR_CHOL_UPPER
         const int ntj = (blk + 1) >> 2;
         if (ntj < T) M.t[ntj][ntj] = mfma_f64(-vt[ntj], vt[ntj], M.t[ntj][ntj]);
 #pragma unroll
@@ -542,13 +448,6 @@ __device__ __forceinline__ bool chol_blk4(WM<T> &M, d4 (&B)[T][TB], int n, int g
             for (int tb = 0; tb < T; ++tb)
                 if (ta >= tj && tb >= ta && !(ta == ntj && tb == ntj))
                     M.t[ta][tb] = mfma_f64(-vt[ta], vt[tb], M.t[ta][tb]);
-#else
-#pragma unroll
-        for (int ta = 0; ta < T; ++ta)
-#pragma unroll
-            for (int tb = 0; tb < T; ++tb)
-                if (ta >= tj && tb >= tj) M.t[ta][tb] = mfma_f64(-vt[ta], vt[tb], M.t[ta][tb]);
-#endif
         if (AUG)
 #pragma unroll
             for (int ta = 0; ta < T; ++ta)
@@ -598,9 +497,6 @@ __device__ __forceinline__ bool wm_chol_regs(WM<T> &M, int n, int g, int c) {
 //     R = chol(P_b), S = I + R^T C_a R = Q Q^T, U = Q^{-1} R^T, Y = U^T U
 // U comes out of the elimination of S carrying R^T as extra columns (row i
 // scaled by 1/sqrt(d_i) at the end), so no triangular solve is needed.
-#ifndef PDPLQR_COMB_BLK4
-#define PDPLQR_COMB_BLK4 1
-#endif
 
 template <int T>
 __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const WM<T> &Ca, const double *Pb, int n,
@@ -609,7 +505,6 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     const int g = lane >> 4, c = lane & 15;
     WM<T> R, S, U;
     COMB_MARK(1);
-#if PDPLQR_COMB_BLK4
     // blocked factors (chol_blk4): R^T comes out directly, R through LDS
     wm_load(U, Pb, n, n, false, 1.0, g, c);
     bool ok = chol_blk4<T, false, T>(U, U.t, n, g, c);  // U = R^T
@@ -625,30 +520,6 @@ __device__ __forceinline__ bool comb_core(WM<T> &Y, WM<T> &Z, WM<T> &Zt, const W
     COMB_MARK(3);
     ok = chol_blk4<T, true, T>(S, U.t, n, g, c) && ok;  // U = Q^{-1} R^T
     COMB_MARK(4);
-#else
-    wm_load(R, Pb, n, n, false, 1.0, g, c);
-    bool ok = wm_chol_regs(R, n, g, c);
-    COMB_MARK(2);
-    {
-        WM<T> T1;
-        wm_tn(T1, Ca, R, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a R
-        wm_tn(S, R, T1, n, 1.0, 1.0, (const WM<T> *)nullptr, g, c);   // I + R^T C_a R
-    }
-    // R^T through LDS (identity padding)
-    wm_store(R, sm.B, PL, n, g, c);
-    wave_sync();
-    wm_load(U, sm.B, PL, n, true, 1.0, g, c);
-    COMB_MARK(3);
-    double colinv[T], rowinv[T][4];
-    ok = elim_regs<T, true>(S, U.t, n, colinv, rowinv, g, c) && ok;
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int b = 0; b < T; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) U.t[a][b][r] *= rowinv[a][r];
-    COMB_MARK(4);
-#endif
     COMB_MARK(5);
     wm_tn(Y, U, U, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Y = U^T U
     wm_tn(Z, Ca, Y, n, -1.0, 1.0, (const WM<T> *)nullptr, g, c);  // Z = I - C_a Y
@@ -760,12 +631,7 @@ __device__ __forceinline__ void wv_load(WV<T> &x, const double *p, int n, int g,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * a + 4 * r + g;
-#if PDPLQR_BF_LOAD
-            const double v = p[i < n ? i : 0];  // branch-free (see wm_load)
-            x.t[a][r] = (c == 0 && i < n) ? v : 0.0;
-#else
             x.t[a][r] = (c == 0 && i < n) ? p[i] : 0.0;
-#endif
         }
 }
 
@@ -788,8 +654,7 @@ __device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, 
     d4 acc[T];  // chunk outermost (see wm_tn)
 #pragma unroll
     for (int a = 0; a < T; ++a) acc[a] = add ? add->t[a] : d4{0.0, 0.0, 0.0, 0.0};
-#if PDPLQR_TN_CHUNK_OUTER
-    if constexpr (PDPLQR_MFMA_SPLIT && T <= 2) {
+    if constexpr (T <= 2) {
         // T output tiles only: even and odd K chunks on separate accumulators
         // (two chains of half the length, summed at the end)
         d4 odd[T];
@@ -818,15 +683,6 @@ __device__ __forceinline__ void wv_tn(WV<T> &y, const WM<T> &X, const WV<T> &x, 
                     for (int a = 0; a < T; ++a) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
                 }
     }
-#else
-#pragma unroll
-    for (int a = 0; a < T; ++a)
-#pragma unroll
-        for (int kt = 0; kt < T; ++kt)
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                if (16 * kt + 4 * kk < n) acc[a] = mfma_f64(sgn * X.t[kt][a][kk], x.t[kt][kk], acc[a]);
-#endif
 #pragma unroll
     for (int a = 0; a < T; ++a) y.t[a] = acc[a];
 }

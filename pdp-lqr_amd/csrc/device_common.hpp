@@ -20,19 +20,11 @@ __device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
 // independent ones issue every 64 (scripts/ubench/lat_bench.hip), so a
 // three-deep accumulation chain becomes one product deep plus two v_add_f64
 // (different rounding order from the chain)
-// (PDPLQR_MFMA_SPLIT = 0: the plain accumulation chain, A/B)
-#ifndef PDPLQR_MFMA_SPLIT
-#define PDPLQR_MFMA_SPLIT 1
-#endif
 __device__ __forceinline__ d4 mfma_f64_x3(double a1, double b1, double a2, double b2, double a3, double b3,
                                           const d4 &acc) {
-#if PDPLQR_MFMA_SPLIT
     const d4 z = {0.0, 0.0, 0.0, 0.0};
     const d4 p1 = mfma_f64(a1, b1, acc), p2 = mfma_f64(a2, b2, z), p3 = mfma_f64(a3, b3, z);
     return (p1 + p2) + p3;
-#else
-    return mfma_f64(a3, b3, mfma_f64(a2, b2, mfma_f64(a1, b1, acc)));
-#endif
 }
 
 // One wave per SIMD (X1).  A one-wave-per-problem kernel whose waves are
@@ -220,23 +212,12 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // prefetch.  Callers own the vmcnt accounting (loads retire in issue order).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; it is only live inside this asm
-// PDPLQR_NT_STREAM=1: once-read stage records carry the non-temporal hint
-// (MI355X_MICROARCH.md nt-weights: issued -> landed about 18 % shorter).
-#ifndef PDPLQR_NT_STREAM
-#define PDPLQR_NT_STREAM 0
-#endif
-#if PDPLQR_NT_STREAM
-#define PDPLQR_NT_SUFFIX " nt"
-#else
-#define PDPLQR_NT_SUFFIX ""
-#endif
-
 __device__ __forceinline__ void dma16(const void *src, const void *lds_dst) {
     const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)lds_dst;
     asm volatile(
         "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, off" PDPLQR_NT_SUFFIX ::"v"(src),
+        "global_load_lds_dwordx4 %0, off" ::"v"(src),
         "s"(__builtin_amdgcn_readfirstlane(base))
         : "memory", "m0");
 }

@@ -48,11 +48,9 @@ struct Shape {
 
 // f(std::true_type{}) or f(std::false_type{}): a launcher's generic lambda picks
 // the X1 instance of its kernel from Shape::x1
-int x1_mask();  // diagnostic: PDPLQR_X1_MASK limits X1 to kernel families (bits below)
-enum { X1_SCHUR = 1, X1_ROLL = 2, X1_NOFACT = 4, X1_KKT_BWD = 8, X1_KKT_FWD = 16, X1_KKT_NOFACT = 32 };
 template <typename F>
-inline void with_x1(int x1, int fam, F &&f) {
-    if (x1 && (x1_mask() & fam)) f(std::true_type{});
+inline void with_x1(int x1, F &&f) {
+    if (x1) f(std::true_type{});
     else f(std::false_type{});
 }
 int device_simds(int device);  // SIMDs of the device (4 per CU)

@@ -308,7 +308,7 @@ int launch_riccati_backward_value_wide(const RiccatiArgs &r, hipStream_t st);  /
 
 int launch_riccati_backward_big(const RiccatiArgs &a, hipStream_t st) {
     // keep_factors = 0: the value form (m pivots a stage, MFMA products)
-    if (!a.Lc && !getenv("PDPLQR_BIG_LFORM")) return launch_riccati_backward_value_wide(a, st);
+    if (!a.Lc) return launch_riccati_backward_value_wide(a, st);
     hipLaunchKernelGGL(k_riccati_bwd_big, dim3(a.sh.batch), dim3(BT), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;

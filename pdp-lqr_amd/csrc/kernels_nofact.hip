@@ -404,7 +404,7 @@ int launch_nofact_admm(const RiccatiArgs &a, const AdmmArgs &q, bool check, hipS
         !al(q.y) || !al(q.lb) || !al(q.ub) || !al(q.rho) || !al(q.irho) || sh.perE % 2 || sh.perc % 2 ||
         sh.perh % 2 || sh.perHw % 2 || sh.ndD % 2 || sh.ny % 2)
         return PDPLQR_ERR_UNSUPPORTED;
-    with_x1(sh.x1, X1_NOFACT, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         constexpr bool X = decltype(x1)::value;
         if (check)
             hipLaunchKernelGGL((k_nofact_admm_dma<12, 4, 4, PDPLQR_NOFACT_ADMM_DEPTH, true, X>), dim3(sh.batch),
@@ -427,9 +427,9 @@ static bool nofact_aligned(const RiccatiArgs &a) {
 // PDPLQR_ERR_UNSUPPORTED: shape / alignment not covered (the generic kernel runs)
 int launch_nofact_dma(const RiccatiArgs &a, hipStream_t st) {
     const Shape &sh = a.sh;
-    if (!a.Lc || !a.lpc || getenv("PDPLQR_NO_DMA") || !nofact_aligned(a)) return PDPLQR_ERR_UNSUPPORTED;
+    if (!a.Lc || !a.lpc || !nofact_aligned(a)) return PDPLQR_ERR_UNSUPPORTED;
     if (sh.n == 12 && sh.m == 4)
-        with_x1(sh.x1, X1_NOFACT, [&](auto x1) {
+        with_x1(sh.x1, [&](auto x1) {
             hipLaunchKernelGGL((k_nofact_dma<12, 4, PDPLQR_NOFACT_DEPTH, decltype(x1)::value>), dim3(sh.batch),
                                dim3(64), 0, st, a);
         });

@@ -824,19 +824,15 @@ static size_t mw_maps_bytes(int n) { return (size_t)(mw_smem_doubles(n) + 3 * el
 // constant: every bounds guard of the tile loads / stores folds away (the
 // runtime-n scan kernel is ~14 k instructions, past the instruction cache a
 // 4-wave block with four different phase paths cycles through).
-// PDPLQR_CT_N24=0: runtime n everywhere (A/B).
-#ifndef PDPLQR_CT_N24
-#define PDPLQR_CT_N24 1
-#endif
-static inline bool ct_n24(int n) { return PDPLQR_CT_N24 && n == 24; }
+static inline bool ct_n24(int n) { return n == 24; }
 // n = 12 (the C2 / headline state size) likewise for the n <= 16 kernels
-static inline bool ct_n12(int n) { return PDPLQR_CT_N24 && n == 12; }
+static inline bool ct_n12(int n) { return n == 12; }
 
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
 bool seg_scan_mw(int n, bool lu, int mw) {
-    if (!mw || lu || getenv("PDPLQR_SCAN_1WAVE")) return false;
-    return tile_order(n) == 2 || (tile_order(n) == 1 && getenv("PDPLQR_SCAN_MW"));
+    if (!mw || lu) return false;
+    return tile_order(n) == 2;
 }
 
 // Resident scan combines the device holds for this shape.
@@ -862,10 +858,7 @@ static int tile_order(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 0); }
 
 // T = 1 only: at T = 2 two waves' combine LDS (~75 KB a block) halves the
 // resident blocks, and C4's scans need every slot.
-#ifndef PDPLQR_SCAN4
-#define PDPLQR_SCAN4 1
-#endif
-bool seg_scan4_supported(int n) { return PDPLQR_SCAN4 && tile_order(n) == 1; }
+bool seg_scan4_supported(int n) { return tile_order(n) == 1; }
 
 int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(128);
@@ -908,7 +901,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
     if (wide_state(a.n)) return launch_seg_maps_wide(a, batch, st);
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
-    if (seg_scan_mw(a.n, a.lu, a.mw) && !getenv("PDPLQR_MAPS_1WAVE")) {
+    if (seg_scan_mw(a.n, a.lu, a.mw)) {
         const size_t sm = mw_maps_bytes(a.n);
         if (T == 1) hipLaunchKernelGGL(k_seg_maps_mw<1>, grid, dim3(256), sm, st, a);
         else if (ct_n24(a.n)) hipLaunchKernelGGL((k_seg_maps_mw<2, 24>), grid, dim3(256), sm, st, a);

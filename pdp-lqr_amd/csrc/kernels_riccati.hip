@@ -645,15 +645,15 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         const int rc = launch_riccati_backward_schur(a, st);  // keep_factors = 0, n + m <= 16
         if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
     }
-    const bool fast_ok = fast_aligned(a) && !getenv("PDPLQR_NO_FAST");
+    const bool fast_ok = fast_aligned(a);
     if (fast_ok && a.sh.n == 12 && a.sh.m == 4) {
         launch_fast<1, 12, 4>(a, st);
     } else if (fast_ok && a.sh.n == 24 && a.sh.m == 8) {
         launch_fast<2, 24, 8>(a, st);
-    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16 && !getenv("PDPLQR_NO_T3")) {
+    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16) {
         // s = 40 on 3 x 3 register tiles (one wave per problem) instead of the
         // block-wide LDS kernels of kernels_big.hip / kernels_wide.hip
-        if (!a.Lc && !getenv("PDPLQR_NO_VF3"))
+        if (!a.Lc)
             hipLaunchKernelGGL((k_riccati_bwd_vf3<24, 16>), dim3(a.sh.batch), dim3(64), 0, st, a);
         else launch_fast<3, 24, 16>(a, st);
     } else if (a.sh.s <= 16) {
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(64) void k_riccati_bwd_nofact(RiccatiArgs A) {
 
 int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st) {
     // compile-time shapes: the streamed vector recursion (kernels_nofact.hip)
-    if (!getenv("PDPLQR_NO_NOFACT_DMA")) {
+    {
         const int rc = launch_nofact_dma(a, st);
         if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
     }
@@ -1259,13 +1259,12 @@ template <bool SEG>
 static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                       double *ws, const SegFwd &sf, hipStream_t st) {
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
-    if (!SEG && sh.n == 24 && sh.m == 16 && ser3_aligned(sh, E, c, FR) && !getenv("PDPLQR_NO_T3") &&
-        !getenv("PDPLQR_NO_DMA")) {
+    if (!SEG && sh.n == 24 && sh.m == 16 && ser3_aligned(sh, E, c, FR)) {
         hipLaunchKernelGGL((k_rollout_dma3<24, 16, 3>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    if (!SEG && sh.s > 32 && sh.s <= 48 && sh.m <= 16 && !getenv("PDPLQR_NO_T3")) {
+    if (!SEG && sh.s > 32 && sh.s <= 48 && sh.m <= 16) {
         // 32 < s <= 48: the register rollout on 3 row tiles (one wave per problem)
         hipLaunchKernelGGL((k_riccati_fwd<3, 16, false>), grid, blk, 0, st, sh, E, c, FR, x0, ws, sf);
         PDPLQR_HIP_TRY(hipGetLastError());
@@ -1302,7 +1301,7 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st) {
-    if (sh.n == 24 && sh.m == 8 && segfwd_aligned(sh, E, c, FR, sf) && !getenv("PDPLQR_NO_DMA")) {
+    if (sh.n == 24 && sh.m == 8 && segfwd_aligned(sh, E, c, FR, sf)) {
         hipLaunchKernelGGL((k_seg_fwd_dma<24, 8, 3>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
                            FR, ws, sf);
         PDPLQR_HIP_TRY(hipGetLastError());
@@ -1312,7 +1311,7 @@ int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c
     // puts a whole short segment's records in flight at once -- one memory
     // latency per segment instead of one per stage (k_riccati_fwd prefetches
     // one stage ahead)
-    if (sh.n == 12 && sh.m == 4 && segfwd_aligned(sh, E, c, FR, sf) && !getenv("PDPLQR_NO_DMA")) {
+    if (sh.n == 12 && sh.m == 4 && segfwd_aligned(sh, E, c, FR, sf)) {
         hipLaunchKernelGGL((k_seg_fwd_dma<12, 4, 5>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
                            FR, ws, sf);
         PDPLQR_HIP_TRY(hipGetLastError());

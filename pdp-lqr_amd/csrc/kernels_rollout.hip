@@ -166,16 +166,16 @@ int launch_rollout_dma(const Shape &sh, const double *E, const double *c, const 
                        double *ws, hipStream_t st, bool gain) {
     if (gain) {
         if (!(sh.n == 12 && sh.m == 4 && roll_aligned(sh, E, c, FR))) return PDPLQR_ERR_UNSUPPORTED;
-        with_x1(sh.x1, X1_ROLL, [&](auto x1) {
+        with_x1(sh.x1, [&](auto x1) {
             hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, true, decltype(x1)::value>), dim3(sh.batch),
                                dim3(64), 0, st, sh, E, c, FR, x0, ws);
         });
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    if (getenv("PDPLQR_NO_DMA") || !roll_aligned(sh, E, c, FR)) return PDPLQR_ERR_UNSUPPORTED;
+    if (!roll_aligned(sh, E, c, FR)) return PDPLQR_ERR_UNSUPPORTED;
     if (sh.n == 12 && sh.m == 4)
-        with_x1(sh.x1, X1_ROLL, [&](auto x1) {
+        with_x1(sh.x1, [&](auto x1) {
             hipLaunchKernelGGL((k_rollout_dma<12, 4, PDPLQR_ROLL_DEPTH, false, decltype(x1)::value>), dim3(sh.batch),
                                dim3(64), 0, st, sh, E, c, FR, x0, ws);
         });

@@ -27,9 +27,6 @@
 
 namespace pdplqr {
 
-#ifndef PDPLQR_SCHUR_BLOCK
-#define PDPLQR_SCHUR_BLOCK 1
-#endif
 
 // Stage-record layout of the LDS-DMA variant (compile-time shapes).
 // HBM record = E (n x s, column-major), c, h~, packed H~ (offsets OE..OP).
@@ -47,7 +44,7 @@ struct SchurShape {
     static constexpr int OE = 0, OC = n * s, OH = OC + n, OP = OH + s, OD = OP + ps, OR = OD + NC * s, OG = OR + NC,
                          Q = OG + NC;
     static constexpr int CH = Q / 2, NI = (CH + 63) / 64;
-    static constexpr int LDE = PDPLQR_LDS_PAD ? ((n / 2) % 2 == 1 ? n : n + 2) : n;
+    static constexpr int LDE = n;
     static constexpr int LSH = (LDE - n) * s;  // shift of everything after E in the LDS copy
     static constexpr int LOC = OC + LSH, LOH = OH + LSH, LOP = OP + LSH, LOD = OD + LSH, LOR = OR + LSH,
                          LOG = OG + LSH;
@@ -63,9 +60,6 @@ struct SchurShape {
 using SymOn = std::integral_constant<bool, true>;
 using SymOff = std::integral_constant<bool, false>;
 
-#ifndef PDPLQR_REC_DIRECT
-#define PDPLQR_REC_DIRECT 1
-#endif
 
 #ifndef PDPLQR_SCHUR_WAVES
 #define PDPLQR_SCHUR_WAVES 4
@@ -80,12 +74,6 @@ using SymOff = std::integral_constant<bool, false>;
 // the fused-penalty instance has the registers (2 waves per SIMD) for G and M
 // on three independent MFMA accumulators each (schur_stage SPLIT = 1); C5 runs
 // it at one wave per SIMD, where the stage chain is what bounds it
-#ifndef PDPLQR_PEN_SPARSE_WB
-#define PDPLQR_PEN_SPARSE_WB 1
-#endif
-#ifndef PDPLQR_PEN_SPLIT
-#define PDPLQR_PEN_SPLIT 1
-#endif
 
 // NN = MM = 0: runtime shape, register prefetch of the next stage.
 // NN, MM > 0 : compile-time shape, stage records streamed by LDS-DMA
@@ -100,7 +88,8 @@ __global__ __launch_bounds__(64, (X1 ? 1 : NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES :
     RiccatiArgs A) {
     PDPLQR_PROBE_BEGIN
     simd_exclusive<X1>();
-    static_assert(!GAIN || (NN == 12 && MM == 4 && PDPLQR_SCHUR_BLOCK), "gain-form record: 12/4 block path");
+    static_assert(!GAIN || (NN == 12 && MM == 4), "gain-form record: 12/4 block path");
+    static_assert(NN == 0 || GAIN, "the compile-time shape writes the gain-form record");
     static_assert(NC == 0 || (GAIN && NC == 4), "fused penalty: 12/4 gain-form path, 4 rows per stage");
     constexpr bool CT = NN > 0;
     using SH = SchurShape<(CT ? NN : 2), (CT ? MM : 2), NC>;
@@ -208,16 +197,15 @@ __global__ __launch_bounds__(64, (X1 ? 1 : NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES :
                 // issued through asm: the compiler's waitcnt pass would otherwise
                 // wait for every outstanding load at the first use (its loop
                 // model merges the guarded loads); the waits are explicit below
-                asm volatile("global_load_dwordx4 %0, %1, off" PDPLQR_NT_SUFFIX : "=v"(R[q]) : "v"(src) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[q]) : "v"(src) : "memory");
             }
         };
         // R's loads have landed once at most `after` younger vm ops are
         // outstanding.  One immediate per call site: a branchy wait made the
         // compiler copy R (still in flight) into other registers.
-        // store instructions per stage (all unconditional): the record (1, or 2
-        // with PDPLQR_REC_DIRECT's L form), plus with NC > 0 the in-place
-        // write-back of h~ (1) and of the packed H~ (4)
-        constexpr int ST = ((PDPLQR_REC_DIRECT && !GAIN) ? 2 : 1) + (NC > 0 ? 5 : 0);
+        // store instructions per stage (all unconditional): the record (1),
+        // plus with NC > 0 the in-place write-back of h~ (1) and of the packed H~ (4)
+        constexpr int ST = 1 + (NC > 0 ? 5 : 0);
         static_assert(NI == 3 || NI == 4, "register staging");
         auto vwait5 = [&](d2v(&R)[NI]) {  // steady state
             if constexpr (NI == 3)
@@ -279,12 +267,12 @@ __global__ __launch_bounds__(64, (X1 ? 1 : NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES :
                 in.H = mfma_f64(a, rq < 0.0 ? -a : a, in.H);
                 in.h -= sum_groups(dgc * (rq * gq));  // h~ -= D^T (rho o g)
                 double *Hk = A.Hw + b * sh.perHw + (long long)k * SH::ps;
-                // PDPLQR_PEN_SPARSE_WB: only entries whose bits the penalty
-                // changed are written back (a box on u changes the u block
-                // alone); lane 0 always stores, so every store instruction has a
-                // live lane and the fixed vm-op counts of the waits hold
+                // only entries whose bits the penalty changed are written back
+                // (a box on u changes the u block alone); lane 0 always stores,
+                // so every store instruction has a live lane and the fixed
+                // vm-op counts of the waits hold
                 auto changed = [&](double x, double y) {
-                    return !PDPLQR_PEN_SPARSE_WB || lane == 0 || __double_as_longlong(x) != __double_as_longlong(y);
+                    return lane == 0 || __double_as_longlong(x) != __double_as_longlong(y);
                 };
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -295,18 +283,12 @@ __global__ __launch_bounds__(64, (X1 ? 1 : NN > 0 ? (NC > 0 ? PDPLQR_PEN_WAVES :
             }
             double w, luq[4];
             GainOut go;
-            const bool ok =
-                schur_stage<PDPLQR_SCHUR_BLOCK ? SH::m : 0, decltype(sym)::value, GAIN, GAIN && PDPLQR_SCHUR_LPW,
-                            (NC > 0 ? PDPLQR_PEN_SPLIT : PDPLQR_SCHUR_SPLIT)>(Pm, prow, in, sm, m, s, g, c, w, luq,
-                                                                             sym_rt, &go);
+            // the fused-penalty instance (2 waves per SIMD launch bounds) has
+            // the registers for G and M on three accumulators each (SPLIT = 1)
+            const bool ok = schur_stage<SH::m, decltype(sym)::value, GAIN, GAIN, (NC > 0 ? 1 : 0)>(
+                Pm, prow, in, sm, m, s, g, c, w, luq, sym_rt, &go);
             fail_stage = (!ok && fail_stage < 0) ? k : fail_stage;
-            if constexpr (GAIN)
-                schur_store_record_gain<SH::m, SH::s>(FRb + (long long)k * frs, go, g, c);
-            else if (PDPLQR_SCHUR_BLOCK && PDPLQR_REC_DIRECT)
-                schur_store_record_direct<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, g, c);
-            else if (PDPLQR_SCHUR_BLOCK)
-                schur_store_record_staged<SH::m, SH::s>(FRb + (long long)k * frs, w, luq, sm, g, c);
-            else schur_store_record_tile<SH::m, SH::s>(FRb + (long long)k * frs, Pm, sm, g, c);
+            schur_store_record_gain<SH::m, SH::s>(FRb + (long long)k * frs, go, g, c);
             wave_sync();  // stage k's LDS reads retire before slot reuse
         };
         auto step = [&](int k, d2v(&X)[NI], bool first, auto sym, bool sym_rt) {  // X: stage k - 1 on entry, k - 3 on exit
@@ -376,16 +358,12 @@ static bool schur_aligned(const RiccatiArgs &a) {
 
 static bool schur_ct(const RiccatiArgs &a) {  // the compile-time 12/4 kernel applies
     const Shape &sh = a.sh;
-    return !a.Lc && !getenv("PDPLQR_NO_SCHUR") && sh.n == 12 && sh.m == 4 && schur_aligned(a) &&
-           !getenv("PDPLQR_NO_DMA");
+    return !a.Lc && sh.n == 12 && sh.m == 4 && schur_aligned(a);
 }
 
 // The backward for these arguments leaves the gain-form record [K~ | k~]
 // (the forward must then run launch_rollout_dma(..., gain = true)).
-// PDPLQR_REC_L: keep the [L(:, 0:m) | lu'] record (A/B).
-bool schur_gain_record(const RiccatiArgs &a) {
-    return PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4 && schur_ct(a) && !getenv("PDPLQR_REC_L");
-}
+bool schur_gain_record(const RiccatiArgs &a) { return schur_ct(a); }
 
 // The fused-penalty backward applies: the 12/4 gain-form kernel, nc = 4 rows on
 // every stage k < N (the C5 layout), nc_N <= 4, 16-byte aligned per-problem
@@ -393,10 +371,10 @@ bool schur_gain_record(const RiccatiArgs &a) {
 int launch_riccati_backward_pen(const RiccatiArgs &a, int nc, hipStream_t st) {
     const Shape &sh = a.sh;
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (nc != 4 || a.nc_last > 4 || !schur_gain_record(a) || getenv("PDPLQR_NO_PEN_FUSE") || !a.D || !a.rho ||
+    if (nc != 4 || a.nc_last > 4 || !schur_gain_record(a) || !a.D || !a.rho ||
         !a.gw || !al(a.D) || !al(a.rho) || !al(a.gw) || sh.ny % 2 || sh.ndD % 2)
         return PDPLQR_ERR_UNSUPPORTED;
-    with_x1(sh.x1, X1_SCHUR, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, true, 4, decltype(x1)::value>), dim3(sh.batch), dim3(64), 0, st,
                            a);
     });
@@ -407,15 +385,12 @@ int launch_riccati_backward_pen(const RiccatiArgs &a, int nc, hipStream_t st) {
 // Returns PDPLQR_ERR_UNSUPPORTED when the shape / options need the full-factor kernels.
 int launch_riccati_backward_schur(const RiccatiArgs &a, hipStream_t st) {
     const Shape &sh = a.sh;
-    if (a.Lc || sh.s > 16 || getenv("PDPLQR_NO_SCHUR")) return PDPLQR_ERR_UNSUPPORTED;
+    if (a.Lc || sh.s > 16) return PDPLQR_ERR_UNSUPPORTED;
     if (schur_gain_record(a))
-        with_x1(sh.x1, X1_SCHUR, [&](auto x1) {
-            hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, PDPLQR_SCHUR_BLOCK && !PDPLQR_SCHUR_T4, 0,
-                                                    decltype(x1)::value>),
-                               dim3(sh.batch), dim3(64), 0, st, a);
+        with_x1(sh.x1, [&](auto x1) {
+            hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4, true, 0, decltype(x1)::value>), dim3(sh.batch), dim3(64), 0,
+                               st, a);
         });
-    else if (schur_ct(a))
-        hipLaunchKernelGGL((k_riccati_bwd_schur<12, 4>), dim3(sh.batch), dim3(64), 0, st, a);
     else
         hipLaunchKernelGGL((k_riccati_bwd_schur<0, 0>), dim3(sh.batch), dim3(64), 0, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
                 G[a][bt] = d4{0.0, 0.0, 0.0, 0.0};
                 // one [u; x] tile (s <= 16, C2's 12/4): odd K chunks on a second
                 // accumulator -- the tile's chain is the only one in flight
-                constexpr bool SPL = PDPLQR_MFMA_SPLIT && CT && NN + MM <= 16;
+                constexpr bool SPL = CT && NN + MM <= 16;
                 d4 Go = d4{0.0, 0.0, 0.0, 0.0};
                 if (a < T && bt < T && 16 * a < s && 16 * bt < s) {
 #pragma unroll
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
                 if (a < T && 16 * a < s) {
                     const d4 h0 = (bt < 2) ? in.H[a][bt < 2 ? bt : 0] : d4{0.0, 0.0, 0.0, 0.0};
                     acc[a] = cux ? h0 : d4{0.0, 0.0, 0.0, 0.0};
-                    constexpr bool SPL = PDPLQR_MFMA_SPLIT && CT && NN + MM <= 16;
+                    constexpr bool SPL = CT && NN + MM <= 16;
                     d4 ao = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                     for (int kk = 0; kk < 8; ++kk)
@@ -607,25 +607,18 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                     avP[a][q] = hx * (Xq[ii + (kx - m) * XLD] + Xq[(kx - m) + ii * XLD]);
                 }
             }
-            if constexpr (PDPLQR_MFMA_SPLIT) {
-                // even / odd K chunks on separate accumulators: four chains of
-                // NK / 2 instead of two of NK (a dependent f64 MFMA waits ~186 cycles)
-                d4 Go[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
+            // even / odd K chunks on separate accumulators: four chains of
+            // NK / 2 instead of two of NK (a dependent f64 MFMA waits ~186 cycles)
+            d4 Go[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
-                for (int q = 0; q < NK; ++q)
+            for (int q = 0; q < NK; ++q)
 #pragma unroll
-                    for (int a = 0; a < 2; ++a) {
-                        if (q & 1) Go[a] = mfma_f64(avP[a][q], bvE[q], Go[a]);
-                        else G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
-                    }
+                for (int a = 0; a < 2; ++a) {
+                    if (q & 1) Go[a] = mfma_f64(avP[a][q], bvE[q], Go[a]);
+                    else G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
+                }
 #pragma unroll
-                for (int a = 0; a < 2; ++a) G[a] += Go[a];
-            } else {
-#pragma unroll
-                for (int q = 0; q < NK; ++q)
-#pragma unroll
-                    for (int a = 0; a < 2; ++a) G[a] = mfma_f64(avP[a][q], bvE[q], G[a]);
-            }
+            for (int a = 0; a < 2; ++a) G[a] += Go[a];
         }
         AUG_MARK(2);
         // ---- rows [u; x]: H~ + E~^T G ([u; x] columns), E~^T Q[x, col] (y / aug columns) ----
@@ -659,13 +652,12 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                 const double bv = cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3];
 #pragma unroll
                 for (int a = 0; a < 2; ++a) {
-                    if (PDPLQR_MFMA_SPLIT && (q & 1)) Mo[a] = mfma_f64(avE[a][q], bv, Mo[a]);
+                    if (q & 1) Mo[a] = mfma_f64(avE[a][q], bv, Mo[a]);
                     else Mu[a] = mfma_f64(avE[a][q], bv, Mu[a]);
                 }
             }
-            if constexpr (PDPLQR_MFMA_SPLIT)
 #pragma unroll
-                for (int a = 0; a < 2; ++a) Mu[a] += Mo[a];
+            for (int a = 0; a < 2; ++a) Mu[a] += Mo[a];
         }
         // ---- aug pieces: lpa[col] = h~ + G^T c ([u; x] columns), fcv = F c (y columns) ----
         {
@@ -865,7 +857,7 @@ static const void *aug_kernel(const Shape &sh) {
 }
 
 // the 4-wave stage for 24/8 (PDPLQR_AUG_1WAVE: the one-wave k_seg_bwd_aug, A/B)
-static bool aug_mw(const Shape &sh) { return sh.mw && sh.n == 24 && sh.m == 8 && !getenv("PDPLQR_AUG_1WAVE"); }
+static bool aug_mw(const Shape &sh) { return sh.mw && sh.n == 24 && sh.m == 8; }
 
 int seg_backward_slots(const Shape &sh, int device) {
     if (wide_stage(sh)) return wide_seg_backward_slots(sh, device);

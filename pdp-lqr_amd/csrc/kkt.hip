@@ -679,158 +679,14 @@ __global__ void k_kkt_bvec16(KKTArgs A, double *__restrict__ bvec) {
 // dimensions -- only two tiles and the y diagonal, loaded two groups ahead.
 // PDPLQR_KKT_BLK4: the per-group factorisation as 4-pivot blocks with MFMA
 // trailing updates (chol_blk4_aug) instead of 16 single pivots (elim_regs).
-#ifndef PDPLQR_KKT_BLK4
-#define PDPLQR_KKT_BLK4 1
-#endif
 
-__global__ __launch_bounds__(64) void k_kkt_factor16(KKTArgs A, const double *__restrict__ dpk,
-                                                     const double *__restrict__ dreg) {
-    const Shape &sh = A.sh;
-    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
-    const TriLane tl = tri_lane(g, c, false);  // packed L^{-1} tiles
-    const long long b = blockIdx.x;
-    const double *tiles = dpk + b * (N + 1) * 512LL;
-    const double *dg = dreg + b * (N + 1) * 16LL;
-    int fail = 0;
-    WM<1> X;
-    X.t[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-    d4 D1 = tn_load(tiles, lane), B1 = tn_load(tiles + 256, lane);
-    d4 D2 = tn_load(tiles + (N > 0 ? 512 : 0), lane), B2 = tn_load(tiles + (N > 0 ? 768 : 256), lane);
-    double r1[4], r2[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        r1[r] = dg[4 * r + g];
-        r2[r] = dg[(N > 0 ? 16 : 0) + 4 * r + g];
-    }
-    for (int k = 0; k <= N; ++k) {
-        WM<1> M, D;
-        d4 B[1][2];
-        D.t[0][0] = D1;
-        B[0][0] = B1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) D.t[0][0][r] += (4 * r + g == c) ? r1[r] : 0.0;
-        D1 = D2;
-        B1 = B2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) r1[r] = r2[r];
-        const int kn = min(k + 2, N);  // (re)loads the last group past the end: harmless
-        D2 = tn_load(tiles + kn * 512LL, lane);
-        B2 = tn_load(tiles + kn * 512LL + 256, lane);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) r2[r] = dg[kn * 16 + 4 * r + g];
-        if (k > 0) wm_tn<1>(M, X, X, 16, -1.0, 0.0, &D, g, c);  // D_k - L_{k,k-1} L_{k,k-1}^T
-        else M = D;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) B[0][1][r] = (4 * r + g == c) ? 1.0 : 0.0;
-        d4 Linv;
-#if PDPLQR_KKT_BLK4
-        const bool ok = chol_blk4_aug<2>(M.t[0][0], B[0], g, c);  // B <- C^{-1} B, final
-        if (!ok && !fail) fail = k + 1;
-        X.t[0][0] = B[0][0];
-        Linv = B[0][1];
-#else
-        double colinv[1], rowinv[1][4];
-        const bool ok = elim_regs<1, true, 2>(M, B, 16, colinv, rowinv, g, c);
-        if (!ok && !fail) fail = k + 1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            X.t[0][0][r] = B[0][0][r] * rowinv[0][r];
-            Linv[r] = B[0][1][r] * rowinv[0][r];
-        }
-#endif
-        // block LDL^T form for the solve (see k_kkt_solve2_16): T_k = M_k^{-1} Bt_k
-        // = Lkk^{-T} X_{k+1}, and Lkk^{-1} (packed) for M_k^{-1} = Lkk^{-T} Lkk^{-1}
-        WM<1> Li, Tm;
-        Li.t[0][0] = Linv;
-        wm_tn<1>(Tm, Li, X, 16, 1.0, 0.0, (const WM<1> *)nullptr, g, c);
-        double *fk = A.fac + (b * (N + 1) + k) * 3LL * 256;
-        tn_store(fk + 256, lane, Tm.t[0][0]);
-        tri_store(fk + 512, tl, Linv);
-    }
-    if (lane == 0) A.status[b] = fail ? fail : (A.pstat[b] ? N + 2 : 0);
-}
 
-// forward phase 2, P = 16, in block LDL^T form -S = L~ D L~^T with unit lower
-// blocks L~_{k+1,k} = T_k^T (T_k = M_k^{-1} Bt_k) and D = diag(M_k):
-//     forward  z_k   = bvec_k - T_{k-1}^T z_{k-1}      (one product, no M^{-1})
-//     backward lam_k = M_k^{-1} z_k - T_k lam_{k+1}    (M^{-1} z off the chain)
-// the same solution as L y = bvec, L^T lam = y with the Cholesky blocks, with
-// one tile less read in the forward sweep (single-column MFMA products over
-// the full padded tile; inputs loaded two steps ahead)
-__global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *__restrict__ bvec) {
-    __shared__ double tt[16 * 17];
-    const Shape &sh = A.sh;
-    const int N = sh.N, lane = wave_lane(), g = lane >> 4, c = lane & 15;
-    const TriLane tl = tri_lane(g, c, false);  // packed Lkk^{-1} tiles
-    const long long b = blockIdx.x;
-    double *wvb = A.wv + b * (N + 1) * 4LL * 16;
-    const double *fb = A.fac + b * (N + 1) * 3LL * 256;
-    const double *bv = bvec + b * (N + 1) * 16LL;
-    struct In {
-        d4 T, L;
-        double v[4];
-    };
-    // forward (unit lower block L~): z_k = bvec_k - T_{k-1}^T z_{k-1}, T_{k-1} stored by group k - 1
-    auto fload = [&](In &in, int k) {
-        in.T = tn_load(fb + (long long)max(k - 1, 0) * 768 + 256, lane);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) in.v[r] = bv[k * 16 + 4 * r + g];
-    };
-    WV<1> z;
-    z.t[0] = d4{0.0, 0.0, 0.0, 0.0};
-    In nx1, nx2;
-    fload(nx1, 0);
-    fload(nx2, min(1, N));
-    for (int k = 0; k <= N; ++k) {
-        const In in = nx1;
-        nx1 = nx2;
-        fload(nx2, min(k + 2, N));
-        WM<1> Tk;
-        Tk.t[0][0] = in.T;
-        WV<1> v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
-        if (k > 0) wv_tn<1>(v, Tk, z, 16, -1.0, &v);
-        z = v;
-        wv_store<1>(z, wvb + (long long)k * 64 + 48, 16, g, c);
-    }
-    // backward: lam_k = M_k^{-1} z_k - T_k lam_{k+1}; z_k was written by this
-    // wave above (same lanes: wv_store / the loads below touch lanes c == 0 only)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    auto bload = [&](In &in, int k) {
-        in.T = tn_load(fb + (long long)min(k, N - 1) * 768 + 256, lane);
-        in.L = tri_load(fb + (long long)k * 768 + 512, tl);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) in.v[r] = wvb[(long long)k * 64 + 48 + 4 * r + g];
-    };
-    WV<1> lam;
-    lam.t[0] = d4{0.0, 0.0, 0.0, 0.0};
-    bload(nx1, N);
-    bload(nx2, max(N - 1, 0));
-    for (int k = N; k >= 0; --k) {
-        const In in = nx1;
-        nx1 = nx2;
-        bload(nx2, max(k - 2, 0));
-        WM<1> TkT, Linv, LinvT;
-        TkT.t[0][0] = tile_transpose(in.T, tt, g, c);
-        Linv.t[0][0] = in.L;
-        LinvT.t[0][0] = tile_transpose(in.L, tt, g, c);
-        WV<1> v, y, w;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v.t[0][r] = (c == 0) ? in.v[r] : 0.0;
-        wv_tn<1>(y, LinvT, v, 16, 1.0, (const WV<1> *)nullptr);  // Lkk^{-1} z_k
-        wv_tn<1>(w, Linv, y, 16, 1.0, (const WV<1> *)nullptr);   // M_k^{-1} z_k
-        if (k < N) wv_tn<1>(w, TkT, lam, 16, -1.0, &w);      // - T_k lam_{k+1}
-        lam = w;
-        wv_store<1>(lam, wvb + (long long)k * 64 + 48, 16, g, c);
-    }
-}
 
 // ---------------------------------------------------------------------------
 // P = 16, two waves per problem: the TWISTED block factorisation of -S.
 // The serial chain above walks all N + 1 dual groups with one wave per problem
 // (one wave per SIMD at C5's batch 1024: latency-bound).  Here wave 0
-// eliminates groups 0 .. p-1 top-down exactly as k_kkt_factor16 and wave 1
+// eliminates groups 0 .. p-1 top-down (the natural-order chain) and wave 1
 // eliminates groups N .. p+1 bottom-up (the same recursion on the reversed
 // system, whose coupling block is Bt_{k-1}^T):
 //     M'_k = D_k - Z_k^T Z_k,  L'_kk = chol(M'_k),  Z_{k-1} = L'_kk^{-1} Bt_{k-1}^T
@@ -842,9 +698,6 @@ __global__ __launch_bounds__(64) void k_kkt_solve2_16(KKTArgs A, const double *_
 // k < p as before (X_{k+1}, Lkk^{-1}); group k > p: Z_{k-1} at +256,
 // L'_kk^{-1} at +512; group p: L_pp^{-1} at +512.
 // ---------------------------------------------------------------------------
-#ifndef PDPLQR_KKT_TWIST
-#define PDPLQR_KKT_TWIST 1
-#endif
 
 __device__ __forceinline__ d4 tile_identity(int g, int c) {
     d4 v;
@@ -881,13 +734,8 @@ __device__ __forceinline__ void wv_store_rows(const WV<1> &v, double *p, int g) 
 // A scheduling barrier after each load group keeps the loads where they are
 // written (the machine scheduler would otherwise sink them towards their use,
 // shortening the prefetch distance).
-#ifndef PDPLQR_SWEEP_SCHED_BARRIER
-#define PDPLQR_SWEEP_SCHED_BARRIER 1
-#endif
 __device__ __forceinline__ void sweep_fence() {
-#if PDPLQR_SWEEP_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
-#endif
 }
 
 template <class In, class LD, class ST>
@@ -1462,7 +1310,7 @@ int kkt_on_model(pdplqr_handle h) {
     KKTArgs a = kkt_args(h);
     const size_t smem = 4 * (size_t)ks->P * ks->P * sizeof(double);
     const dim3 stages((unsigned)(sh.batch * (sh.N + 1))), wave(64);
-    if (ks->P == 16 && !getenv("PDPLQR_KKT_STAGE_GENERIC")) {
+    if (ks->P == 16) {
         hipLaunchKernelGGL(k_kkt_stage16, stages, wave, 0, h->stream, a);
         hipLaunchKernelGGL(k_kkt_pack16d, stages, wave, 0, h->stream, a, ks->dpk);
     } else {
@@ -1531,11 +1379,7 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
         const long long total = (long long)sh.batch * (sh.N + 1) * 16;
         const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
         hipLaunchKernelGGL(k_kkt_dreg16, dim3(grid), dim3(256), 0, h->stream, a, inv_rho, ks->dreg);
-        if (PDPLQR_KKT_TWIST && !getenv("PDPLQR_KKT_NO_TWIST"))
-            hipLaunchKernelGGL(k_kkt_factor16_tw, dim3((unsigned)sh.batch), dim3(128), 0, h->stream, a, ks->dpk,
-                               ks->dreg);
-        else
-            hipLaunchKernelGGL(k_kkt_factor16, dim3((unsigned)sh.batch), dim3(64), 0, h->stream, a, ks->dpk, ks->dreg);
+        hipLaunchKernelGGL(k_kkt_factor16_tw, dim3((unsigned)sh.batch), dim3(128), 0, h->stream, a, ks->dpk, ks->dreg);
     }
     else hipLaunchKernelGGL(k_kkt_factor, dim3((unsigned)sh.batch), dim3(64), smem, h->stream, a, inv_rho);
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -1592,10 +1436,7 @@ int kkt_forward(pdplqr_handle h, const double *x0, double *ws) {
         const long long total = (long long)sh.batch * (sh.N + 1) * 16;
         const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
         hipLaunchKernelGGL(k_kkt_bvec16, dim3(grid), dim3(256), 0, h->stream, a, ks->bvec);
-        if (PDPLQR_KKT_TWIST && !getenv("PDPLQR_KKT_NO_TWIST"))
-            hipLaunchKernelGGL(k_kkt_solve2_16_tw, probs, dim3(128), 0, h->stream, a, (const double *)ks->bvec);
-        else
-            hipLaunchKernelGGL(k_kkt_solve2_16, probs, wave, 0, h->stream, a, (const double *)ks->bvec);
+        hipLaunchKernelGGL(k_kkt_solve2_16_tw, probs, dim3(128), 0, h->stream, a, (const double *)ks->bvec);
     }
     else hipLaunchKernelGGL(k_kkt_solve2, probs, wave, (2 * PP + 2 * P) * sizeof(double), h->stream, a);
     if (P == 16) hipLaunchKernelGGL(k_kkt_solve3_16, stages, wave, 0, h->stream, a, x0, ws);

@@ -80,27 +80,20 @@ struct KKTRicArgs {
 // 256 doubles = two 16-byte DMA instructions per lane.
 // The ADMM runs (a backward that writes the linear pass's cache, then the
 // linear pass) keep the P~ record K~ | k~ | p_{k+1} (n) | P~_{k+1} (fp64;
-// packed lower, pidx(i, j, n), or with PDPLQR_KKT_PT_FULL the full matrix
-// row-major) and the forward applies the correction itself: rewriting c^ in the
-// linear pass costs that pass more (one wave per SIMD: every instruction is on
-// its time) than the forward saves (profiles/r04).  Both forms share the
-// 256-double stage stride; the handle records which one the last backward
-// left (KKTState::rec_ehat).  PDPLQR_KKT_EHAT = 0: the P~ record always.
-#ifndef PDPLQR_KKT_EHAT
-#define PDPLQR_KKT_EHAT 1
-#endif
-#ifndef PDPLQR_KKT_PT_FULL
-#define PDPLQR_KKT_PT_FULL 0
-#endif
+// packed lower, pidx(i, j, n)) and the forward applies the correction itself:
+// rewriting c^ in the linear pass costs that pass more (one wave per SIMD:
+// every instruction is on its time) than the forward saves (profiles/r04).
+// Both forms share the 256-double stage stride; the handle records which one
+// the last backward left (KKTState::rec_ehat).
 template <int NN, int MM>
 struct KRecShape {
     static constexpr int n = NN, m = MM, s = NN + MM;
     static constexpr int OK = 0, OKQ = n * m;
     static constexpr int OEH = OKQ + m, OCH = OEH + 3 * 64;  // E^ record
     static constexpr int OPV = OKQ + m, OPT = OPV + n;        // P~ record
-    static constexpr int FS_EH = OCH + n, FS_PT = OPT + (PDPLQR_KKT_PT_FULL ? n * n : n * (n + 1) / 2);
-    static constexpr int FS = PDPLQR_KKT_EHAT ? (FS_EH > FS_PT ? FS_EH : FS_PT) : FS_PT;  // stage stride
-    static_assert(!PDPLQR_KKT_EHAT || (NN == 12 && MM == 4), "E^ record: 12/4");
+    static constexpr int FS_EH = OCH + n, FS_PT = OPT + n * (n + 1) / 2;
+    static constexpr int FS = FS_EH > FS_PT ? FS_EH : FS_PT;  // stage stride
+    static_assert(NN == 12 && MM == 4, "E^ record: 12/4");
 };
 
 // c^ store of the EHAT record: lanes (g, c >= 4) hold c^[c - 4] (column
@@ -196,9 +189,6 @@ __device__ __forceinline__ bool ptilde_exact(const d4 &P, double rd, int g, int 
 // P~ of the x block for the 12/4 kernels: the Neumann series while it has
 // converged to rounding (e <= PDPLQR_KKT_NEUMANN_MAX, wave-uniform), the exact
 // inversion above otherwise.  False: S = I + rho_dyn P was not SPD.
-#ifndef PDPLQR_KKT_POW_TREE
-#define PDPLQR_KKT_POW_TREE 1
-#endif
 __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c, d4 &Pt) {
     double f = 0.0;
 #pragma unroll
@@ -208,7 +198,6 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
     // J terms (-rho_dyn)^j P^{j+1}, j = 1..J, while e^j > 1e-16 (wave-uniform)
     int J = 0;
     for (double ej = e; J < 8 && ej > 1e-16; ej *= e) ++J;
-#if PDPLQR_KKT_POW_TREE
     // the powers by a product tree instead of a chain of J products:
     // P^2 | P^3 = P^2 P, P^4 = P^2 P^2 | P^5..P^8 = P^4 P^{1..4} | P^9 = P^8 P,
     // so J = 3 (rho_dyn ||P|| ~ 1e-4) is two dependent products, not three
@@ -247,18 +236,6 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
         }
         acc(Q2, r1);
     }
-#else
-    Pt = Pm;
-    d4 T = Pm, Pneg;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Pneg[r] = -rd * Pm[r];
-    for (int j = 0; j < J; ++j) {  // wave-uniform
-        const d4 z = {0.0, 0.0, 0.0, 0.0};
-        T = mfma_f64_x3(Pneg[1], T[1], Pneg[2], T[2], Pneg[3], T[3], z);  // (-rho_dyn P) T (x rows)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Pt[r] += T[r];
-    }
-#endif
     return true;
 }
 
@@ -292,7 +269,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
     const double rd = A.rho_dyn;
     double *const cache = A.cache;  // (a member read inside the stage lambda would put A in scratch)
     // the E^ record for a plain solve, the P~ record when the ADMM cache is written
-    const bool ehat = PDPLQR_KKT_EHAT && cache == nullptr;
+    const bool ehat = cache == nullptr;
     int fail_stage = -1;
 
     // ---- terminal: P_N = H~_N + D_N^T rho D_N, p_N = h~_N - D_N^T rho g_N ----
@@ -403,8 +380,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
 #pragma unroll
                 for (int r = 1; r < 4; ++r) {
                     const int i = 4 * (r - 1) + g, j = c - m;
-                    if (PDPLQR_KKT_PT_FULL) gstore(Rk + RS::OPT + i * n + j, Pt[r]);
-                    else if (i >= j) gstore(Rk + RS::OPT + pidx(i, j, n), Pt[r]);
+                    if (i >= j) gstore(Rk + RS::OPT + pidx(i, j, n), Pt[r]);
                 }
             }
         }
@@ -471,7 +447,7 @@ __global__ __launch_bounds__(64, 1) void k_kkt_ric_bwd(KKTRicArgs A) {
         GainOut go;
         // (LPW: lu rides in W's column 0 -- the cache's w slot is read on the
         // x columns only, and go.T still carries Luu^{-1} for it)
-        bool ok = schur_block_pivots<MM, true, (bool)PDPLQR_SCHUR_LPW>(Mn, lpr, w, luq, g, c, &go, sm.col, sm.lu4);
+        bool ok = schur_block_pivots<MM, true, true>(Mn, lpr, w, luq, g, c, &go, sm.col, sm.lu4);
         Pm = Mn;
 #pragma unroll
         for (int r = 0; r < 4; ++r) prow[r] = lpr[r];
@@ -891,7 +867,7 @@ __global__ __launch_bounds__(64) void k_kkt_ric_fwd(Shape sh, const double *__re
                 pt[q] = 0.0;
             } else {
                 ex[q] = R[OE + (m + t) * n + cn];
-                pt[q] = F[RS::OPT + (PDPLQR_KKT_PT_FULL ? t * n + cn : t >= cn ? pidx(t, cn, n) : pidx(cn, t, n))];  // P~[4 q + g][cl]
+                pt[q] = F[RS::OPT + (t >= cn ? pidx(t, cn, n) : pidx(cn, t, n))];  // P~[4 q + g][cl]
             }
         }
 #pragma unroll
@@ -1280,7 +1256,7 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     a.rho_dyn = rho_dyn;
     a.nc_last = nc_last;
     a.cache = cache;
-    with_x1(sh.x1, X1_KKT_BWD, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         constexpr bool X = decltype(x1)::value;
         if (nc == 4) hipLaunchKernelGGL((k_kkt_ric_bwd<4, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
         else hipLaunchKernelGGL((k_kkt_ric_bwd<0, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
@@ -1289,7 +1265,7 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     return PDPLQR_OK;
 }
 
-bool kkt_ric_rec_ehat(int ric) { return PDPLQR_KKT_EHAT && ric != KKT_RIC_WIDE; }
+bool kkt_ric_rec_ehat(int ric) { return ric != KKT_RIC_WIDE; }
 
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric) {
     return ric == 0 || ric == 4 ? (size_t)sh.N * KKT_CF : 0;
@@ -1313,7 +1289,7 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
     a.status = nullptr;
     a.rho_dyn = rho_dyn;  // (the E^ record's c^ = M^ c - rho_dyn M^ p)
     a.nc_last = nc_last;
-    with_x1(sh.x1, X1_KKT_NOFACT, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         constexpr bool X = decltype(x1)::value;
         if (nc == 4) hipLaunchKernelGGL((k_kkt_ric_nofact<4, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
         else hipLaunchKernelGGL((k_kkt_ric_nofact<0, X>), dim3((unsigned)sh.batch), dim3(64), 0, st, a);
@@ -1330,10 +1306,10 @@ int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, co
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }
-    with_x1(sh.x1, X1_KKT_FWD, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         constexpr bool X = decltype(x1)::value;
         if (ehat)
-            hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, (bool)PDPLQR_KKT_EHAT, X>),
+            hipLaunchKernelGGL((k_kkt_ric_fwd<4, false, false, false, true, X>),
                                dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc, ws, rho_dyn,
                                AdmmArgs{});
         else
@@ -1356,7 +1332,7 @@ int launch_kkt_ric_forward_admm(const Shape &sh, const double *E, const double *
         sh.perh % 2 || sh.ndD % 2 || sh.ny % 2)
         return PDPLQR_ERR_UNSUPPORTED;
     const dim3 grid((unsigned)sh.batch), blk(64);
-    with_x1(sh.x1, X1_KKT_FWD, [&](auto x1) {
+    with_x1(sh.x1, [&](auto x1) {
         constexpr bool X = decltype(x1)::value;
         constexpr int RG = PDPLQR_KKT_UPD_RING;
         double *const nows = nullptr;

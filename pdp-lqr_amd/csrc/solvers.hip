@@ -110,7 +110,6 @@ static int parallel_init(pdplqr_handle h) {
     // per-composition latencies of one wave (profiles/r01 c4_v12: a ~10 us,
     // b ~45 us, c ~5.5 us at 24/8; a ~10 us, b ~15 us for s <= 16).
     int Lsub = h->cfg.segment_len;
-    if (Lsub <= 0 && getenv("PDPLQR_SEGMENT_LEN")) Lsub = atoi(getenv("PDPLQR_SEGMENT_LEN"));  // diagnostics
     const bool auto_len = Lsub <= 0;
     for (int family = 0; family < 2 && auto_len; ++family) {
         // family 0: the 4-wave kernels where they apply (Shape::mw); family 1
@@ -126,7 +125,7 @@ static int parallel_init(pdplqr_handle h) {
             for (int i = 0; i < ns; ++i)
                 longest = std::max(longest, (ps->ref_len[i] + ((ps->ref_len[i] + Lsub - 1) / Lsub) - 1) /
                                                 ((ps->ref_len[i] + Lsub - 1) / Lsub));
-            if (longest <= 64 || getenv("PDPLQR_MW_ALWAYS")) break;
+            if (longest <= 64) break;
             h->sh.mw = 0;
         }
         const double a = 10.0, b = sh.s <= 16 ? 15.0 : 45.0, cm = sh.s <= 16 ? 4.0 : 5.5;
@@ -199,7 +198,7 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->seg_status, B * S)) || (rc = palloc(h, &ps->G, B * sh.N * sh.m * sh.n)) ||
         (rc = palloc(h, &ps->elem, B * S * es)) || (rc = palloc(h, &ps->bufA, B * S * es)) ||
         (rc = palloc(h, &ps->bufB, B * S * es)) || (rc = palloc(h, &ps->xhat, B * (S + 1) * sh.n)) ||
-        (seg_scan4_supported(sh.n) && !getenv("PDPLQR_NO_SCAN4") && (rc = palloc(h, &ps->scan4, B * S * 2 * es))) ||
+        (seg_scan4_supported(sh.n) && (rc = palloc(h, &ps->scan4, B * S * 2 * es))) ||
         (rc = palloc(h, &ps->lam, B * (S + 1) * sh.n)) || (rc = palloc(h, &ps->flag, B)) ||
         (rc = palloc(h, &ps->mapA, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
         (rc = palloc(h, &ps->mapB, B * (S + 1) * (sh.n * sh.n + sh.n))) ||
@@ -225,7 +224,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal);
 static bool scan_sklansky(const Shape &sh) {
     // (n <= 16 with PDPLQR_NO_SCAN4: radix-2 Hillis-Steele, the bit-exact
     // reference of k_seg_scan4; PDPLQR_SCAN_SK=1 takes Sklansky there, A/B only)
-    return !wide_state(sh.n) && (!seg_scan4_supported(sh.n) || getenv("PDPLQR_SCAN_SK")) && !getenv("PDPLQR_SCAN_HS");
+    return !wide_state(sh.n) && !seg_scan4_supported(sh.n);
 }
 void graph_release(pdplqr_handle h);
 
@@ -380,7 +379,7 @@ int solver_on_model(pdplqr_handle h) {
 int solver_update(pdplqr_handle h, const double *ws, const double *ys, const double *zs, const double *irho,
                   double sigma) {
     if (h->cfg.solver == PDPLQR_SOLVER_KKT) return kkt_update(h, ws, ys, zs, irho, sigma);
-    const bool cacheable = h->max_nc <= 0 && !getenv("PDPLQR_NO_HCACHE");
+    const bool cacheable = h->max_nc <= 0;
     const bool skipH = cacheable && h->hw_cached && h->hw_sigma == sigma;
     const int rc = launch_update_problem_data(h->sh, h->H, h->h, ws, ys, zs, irho, sigma, h->Hw, h->hw, h->gw,
                                               h->tab_s, h->tab_n, h->stream, skipH);

@@ -206,13 +206,13 @@ def test_kkt_protocol():
 
 
 @pytest.mark.parametrize("N", [1, 2, 3, 4, 65, 200])
-def test_twisted_factor_equals_natural_order(N):
-    """P = 16 (12/4, nc = 4): the two-wave twisted factorisation and solve
-    (k_kkt_factor16_tw / k_kkt_solve2_16_tw, the default) agree with the
-    natural-order one-wave kernels (PDPLQR_KKT_NO_TWIST) to 1e-11 and with the
-    oracle to 1e-8; short horizons put the middle group at 0 and 1."""
-    import os
-
+def test_twisted_ldl_equals_riccati_order(N, monkeypatch):
+    """P = 16 (12/4, nc = 4): QDLDL's natural-order elimination on the GPU
+    (PDPLQR_KKT_LDL=1: the two-wave twisted block factorisation and solve,
+    k_kkt_factor16_tw / k_kkt_solve2_16_tw) and the default Riccati-order
+    elimination of the same KKT matrix (kkt_riccati.hip) agree to 1e-10 and
+    each matches the oracle to 1e-8; short horizons put the twist's middle
+    group at 0 and 1."""
     from oracle.oracle import OracleKKT
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
@@ -230,38 +230,38 @@ def test_twisted_factor_equals_natural_order(N):
     ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
     irho = 0.05 + g.random((batch, ny))
     outs = {}
-    for mode in ("twist", "natural"):
-        if mode == "natural":
-            os.environ["PDPLQR_KKT_NO_TWIST"] = "1"
-        try:
-            bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
-            bs.set_model(E, c, H, h, D)
-            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
-            bs.backward(irho)
-            out = np.zeros((batch, N * s + n))
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0)
-            outs[mode] = out
-            bs.close()
-        finally:
-            os.environ.pop("PDPLQR_KKT_NO_TWIST", None)
-    d = np.linalg.norm(outs["twist"] - outs["natural"], axis=1) / np.linalg.norm(outs["natural"], axis=1)
-    assert float(d.max()) < 1e-11, float(d.max())
+    for mode in ("ldl", "riccati"):
+        if mode == "ldl":
+            monkeypatch.setenv("PDPLQR_KKT_LDL", "1")  # read at handle creation
+        else:
+            monkeypatch.delenv("PDPLQR_KKT_LDL", raising=False)
+        bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+        bs.set_model(E, c, H, h, D)
+        bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+        bs.backward(irho)
+        out = np.zeros((batch, N * s + n))
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0)
+        outs[mode] = out
+        bs.close()
+    d = np.linalg.norm(outs["ldl"] - outs["riccati"], axis=1) / np.linalg.norm(outs["riccati"], axis=1)
+    assert float(d.max()) < 1e-10, float(d.max())
     for b in (0, batch - 1):
         pm = PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b])
         o = OracleKKT(pm)
         o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
         o.backward(irho[b])
-        assert rel_err(outs["twist"][b], o.forward(x0[b])) < TOL, b
+        ref = o.forward(x0[b])
+        assert rel_err(outs["ldl"][b], ref) < TOL and rel_err(outs["riccati"][b], ref) < TOL, b
 
 
-def test_register_tile_stage_equals_generic():
-    """P = 16 model setup on register tiles (k_kkt_stage16 + k_kkt_pack16d, the
-    default) against the generic LDS kernels (PDPLQR_KKT_STAGE_GENERIC): the
-    same solution to 1e-12 on a batch with varying constraint counts."""
-    import os
-
+def test_register_tile_stage_varying_rows():
+    """P = 16 model setup on register tiles (k_kkt_stage16 + k_kkt_pack16d) on
+    a batch with varying constraint counts (the QDLDL-order path: the
+    Riccati-order one needs a uniform row layout) against the oracle."""
+    from oracle.oracle import OracleKKT
     from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
     from pdplqr.problems import random_batch_arrays
 
     n, m, N, batch = 12, 4, 37, 4
@@ -276,24 +276,20 @@ def test_register_tile_stage_equals_generic():
     ws = g.standard_normal((batch, N * s + n))
     ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
     irho = 0.05 + g.random((batch, ny))
-    outs = {}
-    for mode in ("tiles", "generic"):
-        if mode == "generic":
-            os.environ["PDPLQR_KKT_STAGE_GENERIC"] = "1"
-        try:
-            bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
-            bs.set_model(E, c, H, h, D)
-            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
-            bs.backward(irho)
-            out = np.zeros((batch, N * s + n))
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0)
-            outs[mode] = out
-            bs.close()
-        finally:
-            os.environ.pop("PDPLQR_KKT_STAGE_GENERIC", None)
-    d = np.linalg.norm(outs["tiles"] - outs["generic"], axis=1) / np.linalg.norm(outs["generic"], axis=1)
-    assert float(d.max()) < 1e-12, float(d.max())
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=ncs)
+    bs.set_model(E, c, H, h, D)
+    bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+    bs.backward(irho)
+    out = np.zeros((batch, N * s + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    bs.close()
+    for b in range(batch):
+        pm = PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b])
+        o = OracleKKT(pm)
+        o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
+        o.backward(irho[b])
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
 
 
 @pytest.mark.parametrize("name", ["e0.05_state_cost", "e0.5_state_box", "e3_rho_dyn", "wide_e0.5", "wide_e3"])

@@ -161,80 +161,35 @@ def test_parallel_backward_without_factorization(name, ns, condensed, seglen):
         ws2 = ws2 + 0.05 * g.standard_normal(ws2.shape)
 
 
-@pytest.mark.parametrize("N,batch,seglen,condensed", [(1024, 1, 0, "CHOLESKY"), (1024, 1, 0, "LU"),
-                                                      (96, 3, 5, "CHOLESKY"), (40, 2, 2, "LU"), (7, 2, 3, "CHOLESKY"),
-                                                      (12, 1, 4, "CHOLESKY")])
-def test_radix4_scan_equals_radix2(N, batch, seglen, condensed, monkeypatch):
-    """k_seg_scan4 (two Hillis-Steele rounds per launch, T = 1 shapes) performs
-    the same combines in the same order as two k_seg_scan rounds: the solutions
-    are bit-identical.  PDPLQR_NO_SCAN4 (read at handle creation) keeps radix 2.
-    Segment counts 1..~200 cover every case of the two-level round (i + d, i + 2d,
+@pytest.mark.parametrize("n,m,N,batch,seglen,condensed",
+                         [(12, 4, 1024, 1, 0, "CHOLESKY"), (12, 4, 1024, 1, 0, "LU"), (12, 4, 96, 3, 5, "CHOLESKY"),
+                          (12, 4, 40, 2, 2, "LU"), (12, 4, 7, 2, 3, "CHOLESKY"), (12, 4, 12, 1, 4, "CHOLESKY"),
+                          (24, 8, 96, 2, 5, "CHOLESKY"), (24, 8, 40, 1, 3, "CHOLESKY"), (24, 8, 7, 2, 3, "CHOLESKY"),
+                          (24, 8, 512, 1, 0, "CHOLESKY"), (20, 6, 130, 2, 4, "LU"), (24, 8, 12, 1, 4, "CHOLESKY"),
+                          (18, 4, 33, 3, 2, "CHOLESKY"), (24, 8, 96, 1, 5, "LU")])
+def test_scan_forms_match_serial(n, m, N, batch, seglen, condensed):
+    """Every suffix-scan form on the shapes that take it, against the serial
+    solve and so the oracle: n <= 16 CHOLESKY takes the radix-4 Hillis-Steele
+    launches (k_seg_scan4, two rounds per launch); LU takes Sklansky rounds
+    through the one-wave combine, in place after the first (tcombine_parts'
+    aliasing contract, combine_tiles.hpp); 16 < n <= 32 CHOLESKY takes
+    Sklansky rounds on the 4-wave combine.  Segment counts 1..~200 cover the
+    partial upper halves, every case of the two-level round (i + d, i + 2d,
     i + 3d past the end) and the terminal element's (P, p)-only combines."""
     from pdplqr import BatchedLQRSolver
     from pdplqr.problems import random_batch_arrays
 
-    n, m = 12, 4
-    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 1000 + N)
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 2000 + N + n)
     ws0 = np.zeros((batch, N * (n + m) + n))
-    outs = []
-    for off in (False, True):
-        if off:
-            monkeypatch.setenv("PDPLQR_NO_SCAN4", "1")
-        bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=True,
-                              segment_len=seglen, condensed=condensed)
-        bs.set_model(E, c, H, h)
-        bs.update_problem_data(ws0, sigma=1e-6)
-        bs.backward()
-        out = np.zeros_like(ws0)
-        bs.forward(x0, out)
-        assert np.all(bs.status() == 0)
-        outs.append(out)
-        bs.close()
-    assert np.array_equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("n,m,N,batch,seglen,condensed,one_wave,force_sk",
-                         [(24, 8, 96, 2, 5, "CHOLESKY", False, False), (24, 8, 40, 1, 3, "CHOLESKY", False, False),
-                          (24, 8, 7, 2, 3, "CHOLESKY", False, False), (24, 8, 512, 1, 0, "CHOLESKY", False, False),
-                          (24, 8, 96, 2, 5, "CHOLESKY", True, False), (20, 6, 130, 2, 4, "LU", False, False),
-                          (24, 8, 12, 1, 4, "CHOLESKY", False, False), (18, 4, 33, 3, 2, "CHOLESKY", True, False),
-                          # in-place rounds through the one-wave combine (tcombine_parts'
-                          # aliasing contract, combine_tiles.hpp) in LU form at T = 2 and
-                          # T = 1, the latter forced off the 4-way scan by PDPLQR_SCAN_SK
-                          (20, 6, 130, 2, 4, "LU", True, False), (24, 8, 96, 1, 5, "LU", True, False),
-                          (12, 4, 96, 2, 5, "LU", True, True), (12, 4, 40, 1, 2, "CHOLESKY", True, True)])
-def test_sklansky_scan_matches_hillis_steele(n, m, N, batch, seglen, condensed, one_wave, force_sk, monkeypatch):
-    """The suffix scan's Sklansky rounds (n <= 32: the first round into a
-    buffer, the later ones in place, half the combines per round) give the
-    Hillis-Steele rounds' solution (PDPLQR_SCAN_HS=1) to rounding -- the same
-    elements associated differently -- and both match the serial oracle.
-    Segment counts 3..~130 cover partial upper halves and the terminal
-    element's (P, p)-only combines; one_wave forces the one-wave combine,
-    force_sk the Sklansky rounds where the 4-way scan would run (n <= 16)."""
-    from pdplqr import BatchedLQRSolver
-    from pdplqr.problems import random_batch_arrays
-
-    if one_wave:
-        monkeypatch.setenv("PDPLQR_SCAN_1WAVE", "1")
-    if force_sk:
-        monkeypatch.setenv("PDPLQR_SCAN_SK", "1")
-    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 2000 + N)
-    ws0 = np.zeros((batch, N * (n + m) + n))
-    outs = []
-    for hs in (False, True):
-        if hs:
-            monkeypatch.setenv("PDPLQR_SCAN_HS", "1")
-        bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=False,
-                              segment_len=seglen if seglen else 16, condensed=condensed)
-        bs.set_model(E, c, H, h)
-        bs.update_problem_data(ws0, sigma=1e-6)
-        bs.backward()
-        out = np.zeros_like(ws0)
-        bs.forward(x0, out)
-        assert np.all(bs.status() == 0)
-        outs.append(out)
-        bs.close()
-    assert rel_err(outs[0], outs[1]) < 1e-11
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, keep_factors=False,
+                          segment_len=seglen, condensed=condensed)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws0, sigma=1e-6)
+    bs.backward()
+    out = np.zeros_like(ws0)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    bs.close()
     ser = BatchedLQRSolver(n, m, N, batch, solver="serial")
     ser.set_model(E, c, H, h)
     ser.update_problem_data(ws0, sigma=1e-6)
@@ -242,7 +197,7 @@ def test_sklansky_scan_matches_hillis_steele(n, m, N, batch, seglen, condensed, 
     ref = np.zeros_like(ws0)
     ser.forward(x0, ref)
     ser.close()
-    assert rel_err(outs[0], ref) < TOL
+    assert rel_err(out, ref) < TOL
 
 
 def test_graph_replay_matches_direct():

@@ -124,13 +124,13 @@ def test_value_form_batched_shapes(n, m, N, batch):
 
 @pytest.mark.parametrize("N,batch", [(1, 2), (2, 3), (5, 2), (64, 7), (301, 4)])
 def test_rollout_record_forms(N, batch):
-    """The 12/4 value-form backward writes the gain-form record [K~ | k~]
-    (K~ = Luu^-T Lxu^T, k~ = Luu^-T lu', 52 doubles per stage) read by the
-    gain rollout; PDPLQR_REC_L keeps the reference's [L(:, 0:m) | lu'] record
-    (68 doubles, back substitution in the rollout).  Both against the oracle
-    and against each other, horizons shorter and longer than the rings."""
-    import os
-
+    """The two rollout records: keep_factors = 0 runs the 12/4 value-form
+    backward, which writes the gain-form record [K~ | k~] (K~ = Luu^-T Lxu^T,
+    k~ = Luu^-T lu', 52 doubles per stage) read by the gain rollout;
+    keep_factors = 1 runs the full factor, which writes the reference's
+    [L(:, 0:m) | lu'] record (68 doubles, back substitution in the rollout).
+    Both against the oracle and against each other, horizons shorter and
+    longer than the rings."""
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
@@ -140,20 +140,16 @@ def test_rollout_record_forms(N, batch):
     E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 7 + N)
     ws0 = np.zeros((batch, N * (n + m) + n))
     outs = {}
-    for form in ("gain", "L"):
-        if form == "L":
-            os.environ["PDPLQR_REC_L"] = "1"
-        try:
-            bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
-            bs.set_model(E, c, H, h)
-            bs.update_problem_data(ws0, sigma=1e-6)
-            bs.backward()
-            out = np.zeros_like(ws0)
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0), form
-            outs[form] = out
-        finally:
-            os.environ.pop("PDPLQR_REC_L", None)
+    for form, keep in (("gain", False), ("L", True)):
+        bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+        bs.backward()
+        out = np.zeros_like(ws0)
+        bs.forward(x0, out)
+        assert np.all(bs.status() == 0), form
+        outs[form] = out
+        bs.close()
     for b in range(batch):
         pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
         o = OracleSerial(pm)
@@ -165,14 +161,11 @@ def test_rollout_record_forms(N, batch):
         assert rel_err(outs["gain"][b], outs["L"][b]) < 1e-12, b
 
 
-def test_record_form_follows_last_backward():
-    """One handle alternating backward kernels: the forward must read the
-    record in the form the LAST backward left (gain form from the 12/4
-    value-form kernel, L form from the runtime-shape kernel under
-    PDPLQR_NO_DMA), and a forward repeated without a new backward is
-    idempotent."""
-    import os
-
+def test_repeated_forward_is_idempotent():
+    """A forward repeated without a new backward gives the same trajectory
+    (a documented deviation: the reference's condensed forward mutates p, c),
+    for both record forms (keep_factors 0: gain form, 1: L form), over
+    several backward / forward rounds of one handle."""
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
@@ -188,30 +181,26 @@ def test_record_form_follows_last_backward():
         o.update_problem_data(ws0[b], None, None, None, 1e-6)
         o.backward(None)
         refs.append(o.forward(x0[b]))
-    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
-    bs.set_model(E, c, H, h)
-    bs.update_problem_data(ws0, sigma=1e-6)
-    for generic in (False, True, False, True):
-        if generic:
-            os.environ["PDPLQR_NO_DMA"] = "1"
-        try:
+    for keep in (False, True):
+        bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+        bs.set_model(E, c, H, h)
+        bs.update_problem_data(ws0, sigma=1e-6)
+        for _ in range(3):
             bs.backward()
-        finally:
-            os.environ.pop("PDPLQR_NO_DMA", None)
-        for _ in range(2):
-            out = np.zeros_like(ws0)
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0)
-            for b in range(batch):
-                assert rel_err(out[b], refs[b]) < TOL, (generic, b)
+            for _ in range(2):
+                out = np.zeros_like(ws0)
+                bs.forward(x0, out)
+                assert np.all(bs.status() == 0)
+                for b in range(batch):
+                    assert rel_err(out[b], refs[b]) < TOL, (keep, b)
+        bs.close()
 
 
 def test_record_form_follows_last_backward_graph():
-    """The same alternation with protocol calls replayed from captured hipGraphs
-    (PDPLQR_GRAPH=1 is read at library load: child process).  The backward
-    graph is keyed on the record form, so a replay never runs the other form's
-    captured kernel; PDPLQR_NO_DMA is read per call, so it is toggled in the
-    child around each backward."""
+    """Protocol calls replayed from captured hipGraphs (PDPLQR_GRAPH=1 is read
+    at library load: child process) on handles of both record forms (the
+    backward graph is keyed on the record form), repeated backward / forward
+    rounds, against the oracle."""
     import os
     import subprocess
     import sys
@@ -237,17 +226,13 @@ def test_record_form_follows_last_backward_graph():
             refs.append(o.forward(x0[b]))
         dev = torch.device("cuda", 0)
         t = lambda a: torch.as_tensor(a, device=dev)
-        bs = BatchedLQRSolver(n, m, N, batch, keep_factors=False)
-        bs.set_model(t(E), t(c), t(H), t(h))
-        bs.update_problem_data(t(ws0), sigma=1e-6)
         worst = 0.0
-        for generic in (False, True, False, True, False):
-            if generic:
-                os.environ["PDPLQR_NO_DMA"] = "1"
-            try:
-                bs.backward()
-            finally:
-                os.environ.pop("PDPLQR_NO_DMA", None)
+        for keep in (False, True, False):
+          bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+          bs.set_model(t(E), t(c), t(H), t(h))
+          bs.update_problem_data(t(ws0), sigma=1e-6)
+          for _ in range(3):
+            bs.backward()
             for _ in range(2):
                 out = torch.zeros(batch, N * (n + m) + n, dtype=torch.float64, device=dev)
                 bs.forward(t(x0), out)
@@ -486,44 +471,32 @@ def test_full_size_properties():
         assert rel_err(out[b], o.forward(x0[b])) < TOL
 
 
-@pytest.mark.parametrize("N,batch", [(1, 3), (2, 5), (300, 37)])
-def test_nofact_streamed_kernel_batched(N, batch):
-    """backward_without_factorization at 12/4 takes the streamed vector kernel
-    (kernels_nofact.hip, k_nofact_dma): equal to the generic LDS kernel
-    (PDPLQR_NO_NOFACT_DMA) to 1e-12 and to the oracle to 1e-9 on a batch with
-    new w-bar between the two backwards; short horizons cover the ring prologue."""
-    import os
-
+@pytest.mark.parametrize("n,m,N,batch", [(12, 4, 1, 3), (12, 4, 2, 5), (12, 4, 300, 37), (4, 2, 50, 6),
+                                         (12, 6, 33, 4)])
+def test_nofact_streamed_kernel_batched(n, m, N, batch):
+    """backward_without_factorization: at 12/4 the streamed vector kernel
+    (kernels_nofact.hip, k_nofact_dma), at other shapes the generic LDS
+    kernel; against the oracle to 1e-9 on a batch with new w-bar between the
+    two backwards; short horizons cover the ring prologue."""
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
     from pdplqr.problems import random_batch_arrays
 
-    n, m = 12, 4
     E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 77 + N)
     g = np.random.default_rng(N)
     ws1 = g.standard_normal((batch, N * (n + m) + n))
     ws2 = g.standard_normal((batch, N * (n + m) + n))
-    outs = {}
-    for mode in ("dma", "generic"):
-        if mode == "generic":
-            os.environ["PDPLQR_NO_NOFACT_DMA"] = "1"
-        try:
-            bs = BatchedLQRSolver(n, m, N, batch, keep_factors=True)
-            bs.set_model(E, c, H, h)
-            bs.update_problem_data(ws1, sigma=0.5)
-            bs.backward()
-            bs.update_problem_data(ws2, sigma=0.5)
-            bs.backward_without_factorization()
-            out = np.zeros_like(ws1)
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0)
-            outs[mode] = out
-            bs.close()
-        finally:
-            os.environ.pop("PDPLQR_NO_NOFACT_DMA", None)
-    d = np.linalg.norm(outs["dma"] - outs["generic"], axis=1) / np.linalg.norm(outs["generic"], axis=1)
-    assert float(d.max()) < 1e-12, float(d.max())
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=True)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(ws1, sigma=0.5)
+    bs.backward()
+    bs.update_problem_data(ws2, sigma=0.5)
+    bs.backward_without_factorization()
+    out = np.zeros_like(ws1)
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    bs.close()
     for b in sorted({0, batch - 1, batch // 2}):
         pm = PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0))
         o = OracleSerial(pm)
@@ -531,20 +504,19 @@ def test_nofact_streamed_kernel_batched(N, batch):
         o.backward(None)
         o.update_problem_data(ws2[b], None, None, None, 0.5)
         o.backward_without_factorization(None)
-        assert rel_err(outs["dma"][b], o.forward(x0[b])) < TOL, b
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
 
 
 @pytest.mark.parametrize("N,ncN,backwards", [(64, 0, 1), (64, 4, 1), (37, 4, 2), (1, 0, 1), (2, 4, 2), (3, 0, 2),
-                                             (8, 2, 1)])
+                                             (8, 2, 1), (37, -1, 2), (9, -1, 1)])
 def test_fused_penalty_backward(N, ncN, backwards):
     """12/4 with four rows on every stage (C5's layout), keep_factors = 0: the
     rho penalty runs inside the streamed value-form backward
-    (k_riccati_bwd_schur<12, 4, true, 4>) instead of the k_penalty pass.  Same
-    answer as the separate pass (PDPLQR_NO_PEN_FUSE) and as the oracle; a second
-    backward without update_problem_data penalises H~, h~ again in place, as
-    the reference's data.H += / data.h -= (lqr_kernel.hpp:106-112)."""
-    import os
-
+    (k_riccati_bwd_schur<12, 4, true, 4>); a layout with one stage of three
+    rows (ncN = -1 below: the k_penalty pass, then the backward) is the
+    separate form.  Both against the oracle; a second backward without
+    update_problem_data penalises H~, h~ again in place, as the reference's
+    data.H += / data.h -= (lqr_kernel.hpp:106-112)."""
     from oracle.oracle import OracleSerial
     from pdplqr import BatchedLQRSolver
     from pdplqr.model import PackedModel
@@ -554,7 +526,9 @@ def test_fused_penalty_backward(N, ncN, backwards):
     s = n + m
     E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 91 + N)
     g = np.random.default_rng(92 + N)
-    ncs = np.array([nc] * N + [ncN], dtype=np.int32)
+    ncs = np.array([nc] * N + [max(ncN, 0)], dtype=np.int32)
+    if ncN < 0:
+        ncs[N // 2] = 3  # non-uniform rows: the separate penalty pass
     dims = [s] * N + [n]
     D = np.concatenate([g.standard_normal((batch, int(ncs[k]) * dims[k])) for k in range(N + 1)], axis=1)
     ny = int(ncs.sum())
@@ -562,27 +536,18 @@ def test_fused_penalty_backward(N, ncN, backwards):
     ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
     rho = 0.1 + g.random((batch, ny))
     irho = 1.0 / rho
-    outs = {}
-    for mode in ("fused", "separate"):
-        if mode == "separate":
-            os.environ["PDPLQR_NO_PEN_FUSE"] = "1"
-        try:
-            bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=False, ncs=ncs)
-            bs.set_model(E, c, H, h, D)
-            bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
-            for _ in range(backwards):
-                bs.backward(rho)
-            out = np.zeros((batch, N * s + n))
-            bs.forward(x0, out)
-            assert np.all(bs.status() == 0)
-            outs[mode] = out
-            bs.close()
-        finally:
-            os.environ.pop("PDPLQR_NO_PEN_FUSE", None)
-    assert rel_err(outs["fused"], outs["separate"]) < 1e-11
+    bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=False, ncs=ncs)
+    bs.set_model(E, c, H, h, D)
+    bs.update_problem_data(ws, ys, zs, irho, sigma=1e-6)
+    for _ in range(backwards):
+        bs.backward(rho)
+    out = np.zeros((batch, N * s + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    bs.close()
     for b in range(batch):
         o = OracleSerial(PackedModel(n, m, N, ncs, E[b], c[b], H[b], h[b], D[b]))
         o.update_problem_data(ws[b], ys[b], zs[b], irho[b], 1e-6)
         for _ in range(backwards):
             o.backward(rho[b])
-        assert rel_err(outs["fused"][b], o.forward(x0[b])) < TOL, b
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b

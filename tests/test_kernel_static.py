@@ -37,3 +37,21 @@ def test_kkt_linear_pass_vmcnt_waits(tmp_path):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "asm_vmcnt_check.py"), asm, sym],
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr
+
+
+def test_runtime_switches_are_the_documented_seven():
+    """The library reads exactly these environment switches (DESIGN.md section
+    6a, each with a GPU test), nothing that selects a retired A/B variant."""
+    import glob
+    import re
+
+    found = set()
+    for p in glob.glob(os.path.join(ROOT, "pdp-lqr_amd", "csrc", "*.hip")) + \
+            glob.glob(os.path.join(ROOT, "pdp-lqr_amd", "csrc", "*.hpp")):
+        found |= set(re.findall(r'getenv\("(PDPLQR_[A-Z0-9_]+)"\)', open(p).read()))
+    expected = {"PDPLQR_GRAPH", "PDPLQR_KKT_LDL", "PDPLQR_KKT_NO_LINEAR", "PDPLQR_MD_P2P", "PDPLQR_NO_ADMM_FUSE",
+                "PDPLQR_NO_X1", "PDPLQR_SHARD_FOLD"}
+    assert found == expected, found ^ expected
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    for v in expected:
+        assert v in design, v
