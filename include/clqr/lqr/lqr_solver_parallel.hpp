@@ -29,7 +29,8 @@ public:
     // MI355X extension: `devices` (HIP ordinals) splits the horizon into one
     // slice per GPU, driven by this one object -- slice backward on every device,
     // one RCCL all-gather of the slice elements, slice forward (pdplqr.h
-    // num_devices; backward_without_factorization is unsupported there).
+    // num_devices; backward_without_factorization exchanges only the slices'
+    // (f, p), lqr_solver_parallel.hpp:207-210).
     LQRParallelSolver(const LQRModel &model, int num_segments, bool load_balancing,
                       CondensedSystemSolverType solver_type, const std::vector<int> &devices)
         : model_(model),
