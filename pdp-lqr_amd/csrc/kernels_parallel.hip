@@ -775,32 +775,43 @@ __device__ __forceinline__ void map_scan4_block(const MapScanArgs &A, long long 
         for (int q = lane; q < n; q += 64) out[(long long)j * mw + nn + q] = in[(long long)j * mw + nn + q];
         return;
     }
-    WM<T> PaccT;
-    WV<T> pacc;
+    // partners j - d, ..., j - K d; the K-th is anchored (index < d) when j / d <= 3.
+    // Every operand is loaded up front (none depends on the running map), so
+    // the round pays one memory latency, not one per partner.
+    const int K = j / d < 3 ? j / d : 3;
+    const bool anch = j / d <= 3;
+    WM<T> PaccT, Pa[3];
+    WV<T> pacc, pa[3];
     wm_load(PaccT, in + (long long)j * mw, n, n, true, 0.0, g, c);
     wv_load(pacc, in + (long long)j * mw + nn, n, g, c);
-#pragma unroll 1
-    for (int k = 1; k <= 3; ++k) {
-        const int ia = j - k * d;  // >= 0: the previous partner was not anchored (>= d)
-        const double *ea = in + (long long)ia * mw;
-        WV<T> pa, po;
-        wv_load(pa, ea + nn, n, g, c);
-        wv_tn(po, PaccT, pa, n, 1.0, &pacc);  // Phi_acc phi_a + phi_acc
-        if (ia < d) {  // anchored partner: po = x_j
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double *ea = in + (long long)(j - (k + 1) * d) * mw;
+        if (k < K) wv_load(pa[k], ea + nn, n, g, c);
+        if (k < K - (anch ? 1 : 0)) wm_load(Pa[k], ea, n, n, false, 0.0, g, c);
+    }
+    WM<T> Pv;
+    WV<T> pv;
+    const double *v = A.vfun + (b * J + j) * (long long)mw;
+    if (anch) {
+        wm_load(Pv, v, n, n, false, 0.0, g, c);
+        wv_load(pv, v + nn, n, g, c);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= K) break;
+        WV<T> po;
+        wv_tn(po, PaccT, pa[k], n, 1.0, &pacc);  // Phi_acc phi_a + phi_acc
+        if (anch && k == K - 1) {  // anchored partner: po = x_j
             wv_store(po, out + (long long)j * mw + nn, n, g, c);
             wv_store(po, A.xhat + (b * J + j) * (long long)n, n, g, c);
-            const double *v = A.vfun + (b * J + j) * (long long)mw;
-            WM<T> Pv;
-            WV<T> pv, lam;
-            wm_load(Pv, v, n, n, false, 0.0, g, c);
-            wv_load(pv, v + nn, n, g, c);
+            WV<T> lam;
             wv_tn(lam, Pv, po, n, 1.0, &pv);
             wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
             return;
         }
-        WM<T> Pa, Pn;
-        wm_load(Pa, ea, n, n, false, 0.0, g, c);
-        wm_tn(Pn, Pa, PaccT, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi_a^T Phi_acc^T = (Phi_acc Phi_a)^T
+        WM<T> Pn;
+        wm_tn(Pn, Pa[k], PaccT, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi_a^T Phi_acc^T = (Phi_acc Phi_a)^T
         PaccT = Pn;
         pacc = po;
     }
@@ -1115,6 +1126,62 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
     } else {
         return PDPLQR_ERR_UNSUPPORTED;
     }
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+// One level of the rank-fold trees (RankTreeArgs) on 4-wave blocks: block
+// (b, q) combines one pair of the prefix list (q < its block count) or of the
+// suffix list with mw_combine, both operands staged in LDS first (the scan
+// round's body).  A suffix pair whose right operand is the list's last partial
+// holds the real terminal: P, p only, [F | C | f] zeroed (k_seg_maps reads
+// only the suffix's value function, the prefix's (F, C, f)).  Depth
+// max(ceil(log2 r), ceil(log2(R - 1 - r))) combines, against ceil(log2 R)
+// scan rounds plus the boundary-map round and the map chain of the scan form.
+template <int T, int NC = 0>
+__global__ __launch_bounds__(256) void k_rank_tree_mw(RankTreeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double mwbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = NC ? NC : A.n, nn = n * n, es = 3 * nn + 2 * n;
+    const int mp0 = A.r, ms0 = A.R - 1 - A.r;
+    const int bp = rank_tree_blocks(mp0, A.level), bs = rank_tree_blocks(ms0, A.level);
+    const long long b = blockIdx.x / (bp + bs);
+    const int q = blockIdx.x % (bp + bs);
+    const bool suf = q >= bp;  // block-uniform
+    const int k = suf ? q - bp : q, m0 = suf ? ms0 : mp0;
+    const int m = rank_tree_len(m0, A.level);
+    const int base = suf ? A.r + 1 : 0, soff = suf ? A.R / 2 : 0;
+    const double *ia = A.level == 0 ? A.gathered + (long long)(base + 2 * k) * A.gstride + b * es
+                                    : A.in + (b * A.R + soff + 2 * k) * (long long)es;
+    double *o = rank_tree_len(m0, A.level + 1) == 1 ? (suf ? A.right : A.left) + b * es
+                                                    : A.out + (b * A.R + soff + k) * (long long)es;
+    if (2 * k + 1 >= m) {  // odd last partial: carried to the next level
+        if (wv == 0) elem_copy(o, ia, n, lane);
+        return;
+    }
+    const double *ib = A.level == 0 ? ia + A.gstride : ia + es;
+    const bool fcf = !(suf && 2 * k + 1 == m - 1);
+    const MwSmem sm = mw_smem(mwbuf, n);
+    double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
+    stage_range_blk(ea, ia, es);
+    stage_range_blk(eb, ib, es);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
+                                  elem_in(eb, n), n, fcf, sm);
+    if (!fcf && wv == 1)
+        for (int p = lane; p < 2 * nn + n; p += 64) o[p] = 0.0;  // [F | C | f]
+    if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, suf ? 8 : 4);
+}
+
+int launch_rank_tree(const RankTreeArgs &a, int batch, hipStream_t st) {
+    const int per = rank_tree_blocks(a.r, a.level) + rank_tree_blocks(a.R - 1 - a.r, a.level);
+    if (per == 0) return PDPLQR_OK;
+    if (!seg_scan_mw(a.n, false) || wide_state(a.n)) return PDPLQR_ERR_UNSUPPORTED;
+    const dim3 grid((unsigned)(batch * per));
+    const size_t sm = mw_scan_bytes(a.n);
+    if (ct_n24(a.n)) hipLaunchKernelGGL((k_rank_tree_mw<2, 24>), grid, dim3(256), sm, st, a);
+    else hipLaunchKernelGGL(k_rank_tree_mw<2>, grid, dim3(256), sm, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
 }

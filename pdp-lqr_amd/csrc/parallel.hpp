@@ -86,6 +86,34 @@ struct MapScanArgs {
     double *xhat, *lam;
 };
 
+// Rank fold of a horizon shard as two pairwise reduction trees over the
+// all-gathered rank elements (k_rank_tree_mw): the prefix list e_0 .. e_{r-1}
+// and the suffix list e_{r+1} .. e_{R-1} of rank r, one launch per level.
+// At level l a list of m partials pairs entries (2k, 2k + 1); an odd last
+// entry is carried.  Partials of level l > 0 live in `in` [b][R][es] at slot
+// k (prefix) or R / 2 + k (suffix); a list's last level writes `left` /
+// `right` [b][es].
+struct RankTreeArgs {
+    int n, R, r, level;
+    const double *gathered;    // [R][b][es] (rank-major all-gather)
+    long long gstride;         // rank stride of `gathered` (b * es)
+    const double *in;          // level l > 0: the partials of level l - 1
+    double *out;               // partials of this level
+    double *left, *right;      // [b][es] prefix (F, C, f) / suffix (P, p) results
+    int *flag;
+};
+
+__host__ __device__ inline int rank_tree_len(int m0, int level) {
+    int m = m0;
+    for (int l = 0; l < level; ++l) m = (m + 1) >> 1;
+    return m;
+}
+// blocks per problem of a list at `level` (0 when the list is done or empty)
+__host__ __device__ inline int rank_tree_blocks(int m0, int level) {
+    const int m = rank_tree_len(m0, level);
+    return m > 1 ? (m + 1) >> 1 : 0;
+}
+
 struct SegFwd {
     int S;
     const int32_t *seg_start, *seg_len;
@@ -114,6 +142,7 @@ int launch_fold_shards(const double *elems, int R, int r, int n, int batch, doub
                        int *has_suf, int *flag, bool lu, hipStream_t st);
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
                           double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
+int launch_rank_tree(const RankTreeArgs &a, int batch, hipStream_t st);
 // wide shapes (kernels_wide.hip): 32 < n + m <= 64 stage kernels, 32 < n element kernels
 bool wide_state(int n);
 bool wide_stage(const Shape &sh);

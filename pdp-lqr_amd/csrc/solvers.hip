@@ -705,21 +705,56 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
     // the prefix / suffix chains, max(r - 1, R - r - 2) sequential combines.
     // Scan: the rank suffix scan (ceil(log2 R) rounds of k_seg_scan, every
     // suffix entry) plus, for r > 0, the rank boundary maps (one combine-sized
-    // round) and their matrix-vector chain.  The shorter one runs;
-    // PDPLQR_SHARD_FOLD=chain|scan forces one (diagnostics and tests).
+    // round) and their matrix-vector chain.  Tree (4-wave combines, CHOLESKY
+    // form): the prefix and suffix lists reduced pairwise, max(ceil(log2 r),
+    // ceil(log2(R - 1 - r))) levels and nothing after them (k_seg_maps maps x0
+    // through the prefix as in the chain form).  The shortest one runs;
+    // PDPLQR_SHARD_FOLD=chain|scan|tree forces one (diagnostics and tests).
     const int R = num_shards, r = shard_id;
+    const bool lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
     int lgR = 0;
     while ((1 << lgR) < R) ++lgR;
     bool use_scan = lgR + (r > 0 ? 1 : 0) < std::max(r - 1, R - r - 2);
     // with the 4-wave scan rounds (seg_scan_mw) a round costs about half a
-    // one-wave chain combine: the log-depth form wins for every rank
-    if (R > 1 && seg_scan_mw(sh.n, h->cfg.condensed_type == PDPLQR_CONDENSED_LU)) use_scan = true;
-    if (const char *f = getenv("PDPLQR_SHARD_FOLD")) use_scan = R > 1 && f[0] == 's';
+    // one-wave chain combine: the log-depth forms win for every rank
+    bool use_tree = R > 1 && seg_scan_mw(sh.n, lu) && !wide_state(sh.n);
+    if (const char *f = getenv("PDPLQR_SHARD_FOLD")) {
+        use_tree = use_tree && f[0] == 't';
+        use_scan = R > 1 && f[0] == 's';
+    }
     if (wide_state(sh.n)) use_scan = R > 1;  // the n > 32 element kernels fold by the scan form only
     int rc;
     const double *left = nullptr, *right = nullptr;
     long long rstride = 0;
-    if (use_scan) {
+    if (use_tree) {
+        if (ps->rcap < R) {
+            if ((rc = palloc(h, &ps->rscan[0], (long long)sh.batch * R * es)) ||
+                (rc = palloc(h, &ps->rscan[1], (long long)sh.batch * R * es)) ||
+                (rc = palloc(h, &ps->rmaps, (long long)sh.batch * R * (sh.n * sh.n + sh.n))))
+                return rc;
+            ps->rcap = R;
+        }
+        const long long gstride = (long long)sh.batch * es;
+        RankTreeArgs ta;
+        ta.n = sh.n;
+        ta.R = R;
+        ta.r = r;
+        ta.gathered = delems;
+        ta.gstride = gstride;
+        ta.left = ps->left;
+        ta.right = ps->right;
+        ta.flag = ps->flag;
+        for (ta.level = 0; rank_tree_blocks(r, ta.level) + rank_tree_blocks(R - 1 - r, ta.level) > 0; ++ta.level) {
+            ta.in = ps->rscan[(ta.level + 1) & 1];
+            ta.out = ps->rscan[ta.level & 1];
+            if ((rc = launch_rank_tree(ta, sh.batch, h->stream))) return rc;
+        }
+        // a one-element list is the gathered element itself
+        if (r == 1) left = delems;
+        else if (r > 1) left = ps->left;
+        if (r == R - 2) right = delems + (long long)(R - 1) * gstride;
+        else if (r < R - 2) right = ps->right;
+    } else if (use_scan) {
         if (ps->rcap < R) {
             if ((rc = palloc(h, &ps->rscan[0], (long long)sh.batch * R * es)) ||
                 (rc = palloc(h, &ps->rscan[1], (long long)sh.batch * R * es)) ||
@@ -742,7 +777,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
             }
             sa.out = ps->rscan[round & 1];
             sa.flag = ps->flag;
-            sa.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
+            sa.lu = lu;
             if ((rc = launch_seg_scan(sa, sh.batch, h->stream))) return rc;
             sin = sa.out;
         }

@@ -3,7 +3,7 @@ virtual ranks (each rank's slice solved in turn on the same device): prints,
 per rank, the slice backward and the shard forward (fold of the gathered
 elements + boundary maps + rollout) in ms, and the slowest rank's total -- what
 an R-GPU run takes per solve, less the all-gather.
-usage: python scripts/prof_shards.py [Ntot=65536] [R=8] [reps=5]"""
+usage: python scripts/prof_shards.py [Ntot=65536] [R=8] [reps=5] [segment_len=0 (automatic)]"""
 import json
 import os
 import sys
@@ -21,6 +21,7 @@ def main():
     Ntot = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    seglen = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     n, m = 24, 8
     s = n + m
     dev = torch.device("cuda", 0)
@@ -35,7 +36,7 @@ def main():
         if r < R - 1:
             H[:, Nl * s * s:] = 0.0
             h[:, Nl * s:] = 0.0
-        sh = HorizonShard(n, m, Nl, 1, device=0)
+        sh = HorizonShard(n, m, Nl, 1, segment_len=seglen, device=0)
         sh.set_model(E, c, H, h)
         sh.update_problem_data(torch.zeros(1, Nl * s + n, dtype=torch.float64, device=dev), sigma=1e-6)
         sh.handle.set_stream(st.cuda_stream)
@@ -69,7 +70,7 @@ def main():
     per = [{"rank": r, "bwd_ms": med(res["bwd"][r]), "fwd_ms": med(res["fwd"][r])} for r in range(R)]
     ok = all(bool(torch.isfinite(o).all().item()) for o in outs)
     print(json.dumps({"Ntot": Ntot, "R": R, "ranks": per, "max_rank_ms": max(p["bwd_ms"] + p["fwd_ms"] for p in per),
-                      "finite": ok, "lib": os.environ.get("PDPLQR_LIB", "in-tree")}), flush=True)
+                      "finite": ok, "segment_len": seglen, "fold": os.environ.get("PDPLQR_SHARD_FOLD", "auto"), "lib": os.environ.get("PDPLQR_LIB", "in-tree")}), flush=True)
     for sh in shards:
         sh.close()
 

@@ -83,14 +83,18 @@ def test_virtual_ranks_match_oracle(n, m, N, batch, R, seglen):
         assert rel_err(got[b], ref[b]) < TOL, b
 
 
-@pytest.mark.parametrize("fold", ["scan", "chain"])
+@pytest.mark.parametrize("fold", ["scan", "chain", "tree"])
 @pytest.mark.parametrize("n,m,N,batch,R,seglen", [(12, 4, 200, 2, 3, 7), (12, 4, 320, 3, 8, 8),
                                                   (24, 8, 128, 1, 8, 4), (24, 8, 150, 2, 5, 6),
+                                                  (20, 6, 133, 2, 7, 5), (24, 8, 96, 3, 2, 6),
                                                   (4, 2, 60, 2, 6, 3)])
 def test_virtual_ranks_fold_variants(n, m, N, batch, R, seglen, fold, monkeypatch):
-    """Both folds of the gathered rank elements (PDPLQR_SHARD_FOLD): the
-    sequential prefix / suffix chains and the log-depth rank suffix scan with
-    rank boundary maps (rank-major strides exercised by batch > 1)."""
+    """The folds of the gathered rank elements (PDPLQR_SHARD_FOLD): the
+    sequential prefix / suffix chains, the log-depth rank suffix scan with
+    rank boundary maps, and the pairwise prefix / suffix trees (4-wave
+    combines, 16 < n <= 32; the chain form elsewhere).  Rank-major strides are
+    exercised by batch > 1; R = 5, 7, 8 give carried odd partials and one-
+    element lists."""
     monkeypatch.setenv("PDPLQR_SHARD_FOLD", fold)
     got, ref = _run_virtual(n, m, N, batch, R, seglen, seed=5)
     for b in range(batch):
