@@ -127,3 +127,21 @@ extern "C" int pdplqr_debug_rsqrt(int n, const double *x, double *y) {
     (void)hipFree(d);
     return PDPLQR_OK;
 }
+
+// Host-side plan of the rank-fold trees (parallel.hpp rank_tree_op, the
+// indexing k_rank_tree_mw runs): out[6] = {suf, carry, fcf, a, b, dst} of
+// block q at `level` for rank r of R; returns the block count of that level
+// (tests/test_rank_tree_plan.py simulates the trees on CPU with it).
+extern "C" int pdplqr_debug_rank_tree(int R, int r, int level, int q, int *out) {
+    const int per = pdplqr::rank_tree_blocks(r, level) + pdplqr::rank_tree_blocks(R - 1 - r, level);
+    if (q >= 0 && q < per && out) {
+        const pdplqr::RankTreeOp op = pdplqr::rank_tree_op(R, r, level, q);
+        out[0] = op.suf;
+        out[1] = op.carry;
+        out[2] = op.fcf;
+        out[3] = op.a;
+        out[4] = op.b;
+        out[5] = op.dst;
+    }
+    return per;
+}

@@ -45,15 +45,17 @@ __device__ __forceinline__ void simd_exclusive() {
 
 // Wave placement probe (diagnostic variant only, -DPDPLQR_HWID_PROBE=1): lane 0
 // of every block records where it ran -- (XCC, SE, SH, CU, SIMD) from the
-// HW_ID / XCC_ID hardware registers -- and its start / end on the 100 MHz
-// constant clock into a per-translation-unit device array, read back by
-// pdplqr_probe_read_<tu>() (scripts/c5_placement.py).
+// HW_ID / XCC_ID hardware registers -- its start / end on the 100 MHz
+// constant clock and on the shader clock counter (s_memtime: the effective
+// core clock is their ratio) into a per-translation-unit device array, read
+// back by pdplqr_probe_read_<tu>() (scripts/c5_placement.py).
 #ifndef PDPLQR_HWID_PROBE
 #define PDPLQR_HWID_PROBE 0
 #endif
 #if PDPLQR_HWID_PROBE
 #define PDPLQR_PROBE_SLOTS 16384
-static __device__ long long g_wave_probe[PDPLQR_PROBE_SLOTS * 3];
+#define PDPLQR_PROBE_FIELDS 5
+static __device__ long long g_wave_probe[PDPLQR_PROBE_SLOTS * PDPLQR_PROBE_FIELDS];
 #define PDPLQR_PROBE_DEFINE(tu)                                                                    \
     extern "C" int pdplqr_probe_read_##tu(long long *out) {                                       \
         return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_probe), sizeof(g_wave_probe), 0,   \
@@ -67,12 +69,18 @@ __device__ __forceinline__ long long hw_place() {
     return (long long)(((xcc & 15u) << 16) | (((hw >> 13) & 7u) << 9) | (((hw >> 12) & 1u) << 8) |
                        (((hw >> 8) & 15u) << 4) | ((hw >> 4) & 3u));
 }
-#define PDPLQR_PROBE_BEGIN const long long probe_t0_ = wall_clock64();
+#define PDPLQR_PROBE_BEGIN                                                                         \
+    const long long probe_t0_ = wall_clock64();                                                    \
+    const long long probe_c0_ = (long long)__builtin_amdgcn_s_memtime();
 #define PDPLQR_PROBE_END(lane, blk)                                                                \
     if ((lane) == 0 && (blk) < PDPLQR_PROBE_SLOTS) {                                               \
-        g_wave_probe[3 * (blk)] = hw_place();                                                      \
-        g_wave_probe[3 * (blk) + 1] = probe_t0_;                                                   \
-        g_wave_probe[3 * (blk) + 2] = wall_clock64();                                              \
+        const long long c1_ = (long long)__builtin_amdgcn_s_memtime();                             \
+        long long *q_ = g_wave_probe + PDPLQR_PROBE_FIELDS * (blk);                                \
+        q_[0] = hw_place();                                                                        \
+        q_[1] = probe_t0_;                                                                         \
+        q_[2] = wall_clock64();                                                                    \
+        q_[3] = probe_c0_;                                                                         \
+        q_[4] = c1_;                                                                               \
     }
 #else
 #define PDPLQR_PROBE_DEFINE(tu)

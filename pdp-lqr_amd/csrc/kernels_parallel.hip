@@ -1143,24 +1143,20 @@ __global__ __launch_bounds__(256) void k_rank_tree_mw(RankTreeArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, nn = n * n, es = 3 * nn + 2 * n;
-    const int mp0 = A.r, ms0 = A.R - 1 - A.r;
-    const int bp = rank_tree_blocks(mp0, A.level), bs = rank_tree_blocks(ms0, A.level);
-    const long long b = blockIdx.x / (bp + bs);
-    const int q = blockIdx.x % (bp + bs);
-    const bool suf = q >= bp;  // block-uniform
-    const int k = suf ? q - bp : q, m0 = suf ? ms0 : mp0;
-    const int m = rank_tree_len(m0, A.level);
-    const int base = suf ? A.r + 1 : 0, soff = suf ? A.R / 2 : 0;
-    const double *ia = A.level == 0 ? A.gathered + (long long)(base + 2 * k) * A.gstride + b * es
-                                    : A.in + (b * A.R + soff + 2 * k) * (long long)es;
-    double *o = rank_tree_len(m0, A.level + 1) == 1 ? (suf ? A.right : A.left) + b * es
-                                                    : A.out + (b * A.R + soff + k) * (long long)es;
-    if (2 * k + 1 >= m) {  // odd last partial: carried to the next level
+    const int per = rank_tree_blocks(A.r, A.level) + rank_tree_blocks(A.R - 1 - A.r, A.level);
+    const long long b = blockIdx.x / per;
+    const RankTreeOp op = rank_tree_op(A.R, A.r, A.level, (int)(blockIdx.x % per));  // block-uniform
+    auto src = [&](int i) {
+        return A.level == 0 ? A.gathered + (long long)i * A.gstride + b * es : A.in + (b * A.R + i) * (long long)es;
+    };
+    const double *ia = src(op.a);
+    double *o = op.dst < 0 ? (op.suf ? A.right : A.left) + b * es : A.out + (b * A.R + op.dst) * (long long)es;
+    if (op.carry) {  // odd last partial: carried to the next level
         if (wv == 0) elem_copy(o, ia, n, lane);
         return;
     }
-    const double *ib = A.level == 0 ? ia + A.gstride : ia + es;
-    const bool fcf = !(suf && 2 * k + 1 == m - 1);
+    const double *ib = src(op.b);
+    const bool fcf = op.fcf, suf = op.suf;
     const MwSmem sm = mw_smem(mwbuf, n);
     double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
     stage_range_blk(ea, ia, es);

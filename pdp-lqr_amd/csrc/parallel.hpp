@@ -114,6 +114,32 @@ __host__ __device__ inline int rank_tree_blocks(int m0, int level) {
     return m > 1 ? (m + 1) >> 1 : 0;
 }
 
+// What block q (of one problem) does at `level`: combine operands a (earlier)
+// and b (later) of the prefix (suf = false) or suffix list -- at level 0 rank
+// indices into the all-gather, later the partial slots of `in` -- or carry a
+// alone (carry); the result goes to partial slot dst, or to left / right when
+// dst < 0.  fcf = false: b holds the real terminal (the suffix list's last
+// partial), only P, p are formed.
+struct RankTreeOp {
+    bool suf, carry, fcf;
+    int a, b, dst;
+};
+__host__ __device__ inline RankTreeOp rank_tree_op(int R, int r, int level, int q) {
+    const int mp0 = r, ms0 = R - 1 - r;
+    const int bp = rank_tree_blocks(mp0, level);
+    RankTreeOp op;
+    op.suf = q >= bp;
+    const int k = op.suf ? q - bp : q, m0 = op.suf ? ms0 : mp0;
+    const int m = rank_tree_len(m0, level);
+    const int base = level == 0 ? (op.suf ? r + 1 : 0) : (op.suf ? R / 2 : 0);
+    op.a = base + 2 * k;
+    op.carry = 2 * k + 1 >= m;
+    op.b = op.carry ? -1 : op.a + 1;
+    op.fcf = !(op.suf && 2 * k + 1 == m - 1);
+    op.dst = rank_tree_len(m0, level + 1) == 1 ? -1 : (op.suf ? R / 2 : 0) + k;
+    return op;
+}
+
 struct SegFwd {
     int S;
     const int32_t *seg_start, *seg_len;

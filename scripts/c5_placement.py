@@ -4,14 +4,17 @@ Needs the probe variant: scripts/build_variant.sh hwid -DPDPLQR_HWID_PROBE=1 and
 PDPLQR_LIB=pdp-lqr_amd/build/variants/libpdplqr_hwid.so.  Every block's lane 0
 records (XCC, SE, SH, CU, SIMD) and its start / end on the 100 MHz constant
 clock (device_common.hpp, PDPLQR_PROBE_*).  For the protocol order (update,
-backward, forward) and back-to-back (backward, forward) calls this prints, per
-call: kernel span from the waves, wave durations (min / median / max), how many
-waves shared a SIMD / a CU, and the per-XCC spread of the start times.
+backward, forward), back-to-back (backward, forward), after 2 ms of idle and
+after a read-only sweep of 1 GiB (evicts the dirty lines update leaves in the
+caches) this prints, per call: kernel span from the waves, wave durations (min / median / max), how many
+waves shared a SIMD / a CU, the per-XCC spread of the start times and the
+waves' core clock (MHz, min / median / max).
 usage: python scripts/c5_placement.py [kkt|serial|head]"""
 import ctypes as C
 import json
 import os
 import sys
+import time
 from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,19 +28,21 @@ from pdplqr import BatchedLQRSolver  # noqa: E402
 from pdplqr._lib import lib  # noqa: E402
 
 SLOTS = 16384
+FIELDS = 5
 
 
 def read_probe(tu, nblk):
-    buf = (C.c_longlong * (3 * SLOTS))()
+    buf = (C.c_longlong * (FIELDS * SLOTS))()
     fn = getattr(lib(), "pdplqr_probe_read_" + tu)
     fn.argtypes = [C.c_void_p]
     assert fn(C.cast(buf, C.c_void_p)) == 0
-    a = np.frombuffer(buf, dtype=np.int64).reshape(SLOTS, 3)[:nblk].copy()
+    a = np.frombuffer(buf, dtype=np.int64).reshape(SLOTS, FIELDS)[:nblk].copy()
     return a
 
 
 def summarize(a):
-    place, t0, t1 = a[:, 0], a[:, 1], a[:, 2]
+    place, t0, t1, c0, c1 = a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4]
+    mhz = (c1 - c0) / np.maximum(t1 - t0, 1) * 100.0
     xcc = place >> 16
     cu_key = place >> 2  # (xcc, se, sh, cu)
     simd_cnt = Counter(place.tolist())
@@ -53,6 +58,7 @@ def summarize(a):
                            "dur_max_us": round(float(dur[sel].max()), 1)}
     return {
         "span_us": round(float(span), 1),
+        "clock_mhz": [round(float(mhz.min())), round(float(np.median(mhz))), round(float(mhz.max()))],
         "dur_us": [round(float(dur.min()), 1), round(float(np.median(dur)), 1), round(float(dur.max()), 1)],
         "start_spread_us": round(float(start_rel.max()), 1),
         "simds_used": len(simd_cnt), "waves_per_simd_hist": dict(Counter(simd_cnt.values())),
@@ -106,9 +112,15 @@ def main():
     bs.handle.set_stream(side.cuda_stream)
     res = []
     with torch.cuda.stream(side):
-        for mode in ["repeat"] * 3 + ["update"] * 3 + ["repeat"] * 2:
-            if mode == "update":
+        sweep = torch.ones(1 << 27, dtype=torch.float64, device=dev)  # 1 GiB
+        for mode in ["repeat"] * 3 + ["update"] * 3 + ["repeat"] * 2 + ["update_idle", "update_sweep"] * 2:
+            if mode.startswith("update"):
                 upd()
+            if mode == "update_idle":
+                torch.cuda.synchronize()
+                time.sleep(0.002)
+            elif mode == "update_sweep":
+                float(sweep.sum())  # read-only pass: update's dirty lines leave the caches
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(side)
             if r is None:
