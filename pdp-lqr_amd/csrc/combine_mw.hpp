@@ -20,9 +20,10 @@
 //     p = p_a + F_a^T u - X1^T x4            (u = p_b + P_b f_a)
 // Phases (barriers between them), waves w0..w3:
 //   A  w0: R = chol(P_b) (U = R^T to LDS);  w1: K2 = F_b F_a, C_a u, v1;
-//      w2: K0 = C_a F_b^T;  w3: K1 = F_b C_a F_b^T + C_b, F_b v1 + f_b,
-//      p_a + F_a^T u (inputs only)
-//   B  w0: S;  w1: R^T F_a, R^T v1, R^T C_a u;  w2: R^T K0 (R read from LDS) -> LDS
+//      w2: K0 = C_a F_b^T;  w3: K0 (own copy), F_b v1 + f_b, p_a + F_a^T u
+//      (inputs only)
+//   B  w0: S;  w1: R^T F_a;  w2: R^T K0 (R read from LDS) -> LDS;
+//      w3: R^T C_a u, R^T v1, K1 = F_b K0 + C_b
 //   C  every wave: chol(S) carrying ONE column tile of the right-hand sides
 //   D  w0: P;  w1: F;  w2: C;  w3: f, p                                    -> HBM
 // When the right operand holds the real terminal (F = C = f = 0 there and in
@@ -166,7 +167,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
     // wave costs issue slots the co-resident blocks of a scan round need).
     // Wave 0's factor U = R^T lands in sm.S; S then goes to the staged P_b
     // slot (P_b is dead after phase A), so the R reads and S cannot race.
-    WM<T> R;
+    WM<T> R, K0w3;  // K0w3: wave 3's C_a F_b^T, phase A -> B
     double *Sd = const_cast<double *>(eb.P);  // S, leading dimension n
     if (wv == 0) {
         ok = mw_chol_R<T>(R, eb.P, sm.S, sm.ld, n, g, c);
@@ -219,7 +220,7 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wv_store(t, sm.pv, n, g, c);
         }
         if (fcf) {
-            WM<T> Ca, Fbt, K0;
+            WM<T> Ca, Fbt;
             WV<T> v1, fb, fo;
             wm_load(Ca, ea.C, n, n, false, 0.0, g, c);
             wv_tn(v1, Ca, pb, n, -1.0, &fa);  // v1 = f_a - C_a p_b
@@ -227,11 +228,10 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
             wv_load(fb, eb.f, n, g, c);
             wv_tn(fo, Fbt, v1, n, 1.0, &fb);  // F_b v1 + f_b
             wv_store(fo, sm.fv, n, g, c);
-            wm_tn(K0, Ca, Fbt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a F_b^T
-            WM<T> Cb, K;
-            wm_load(Cb, eb.C, n, n, false, 0.0, g, c);
-            wm_tn(K, Fbt, K0, n, 1.0, 0.0, &Cb, g, c);  // F_b C_a F_b^T + C_b
-            wm_store(K, sm.K1, PL, n, g, c);
+            wm_tn(K0w3, Ca, Fbt, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // C_a F_b^T
+            // F_b K0 + C_b follows in phase B: here it would outlast wave 0's
+            // factorisation and hold the phase-A barrier (comb_phases: full
+            // combines waited ~1.4 us for this wave)
         }
     }
     COMB_MARK(1);  // wave 0: R formed
@@ -262,6 +262,11 @@ __device__ __forceinline__ bool mw_combine(double *oF, double *oC, double *of, d
         if (fcf) {
             wv_tn(y, R, v1, n, 1.0, (const WV<T> *)nullptr);  // R^T v1
             wv_store(y, sm.bv, n, g, c);
+            WM<T> Fbt, Cb, K;
+            wm_load(Fbt, eb.F, n, n, true, 0.0, g, c);
+            wm_load(Cb, eb.C, n, n, false, 0.0, g, c);
+            wm_tn(K, Fbt, K0w3, n, 1.0, 0.0, &Cb, g, c);  // F_b C_a F_b^T + C_b (read in phase D)
+            wm_store(K, sm.K1, PL, n, g, c);
         }
     } else if (wv == 2 && fcf) {
         WM<T> K0, B;

@@ -190,6 +190,19 @@ __device__ __forceinline__ bool ptilde_exact(const d4 &P, double rd, int g, int 
 // converged to rounding (e <= PDPLQR_KKT_NEUMANN_MAX, wave-uniform), the exact
 // inversion above otherwise.  False: S = I + rho_dyn P was not SPD.
 __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c, d4 &Pt) {
+    // the powers by a product tree instead of a chain of J products:
+    // P^2 | P^3 = P^2 P, P^4 = P^2 P^2 | P^5..P^8 = P^4 P^{1..4} | P^9 = P^8 P,
+    // so J = 3 (rho_dyn ||P|| ~ 1e-4) is two dependent products, not three
+    // (every power of the symmetric P is symmetric: its registers serve as the
+    // A operand, read as the transpose, like P's own).  P^2, P^3, P^4 are
+    // issued before the norm that picks J is known: the norm's cross-lane sum
+    // and square root then run beside the products instead of ahead of them
+    // on the stage chain (a smaller J leaves them unused).
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    auto mul = [&](const d4 &X, const d4 &Y) { return mfma_f64_x3(X[1], Y[1], X[2], Y[2], X[3], Y[3], z); };
+    const d4 Q2 = mul(Pm, Pm);
+    const d4 Q3 = mul(Q2, Pm);
+    const d4 Q4 = mul(Q2, Q2);
     double f = 0.0;
 #pragma unroll
     for (int r = 1; r < 4; ++r) f = (c >= 4) ? __builtin_fma(Pm[r], Pm[r], f) : f;
@@ -198,13 +211,6 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
     // J terms (-rho_dyn)^j P^{j+1}, j = 1..J, while e^j > 1e-16 (wave-uniform)
     int J = 0;
     for (double ej = e; J < 8 && ej > 1e-16; ej *= e) ++J;
-    // the powers by a product tree instead of a chain of J products:
-    // P^2 | P^3 = P^2 P, P^4 = P^2 P^2 | P^5..P^8 = P^4 P^{1..4} | P^9 = P^8 P,
-    // so J = 3 (rho_dyn ||P|| ~ 1e-4) is two dependent products, not three
-    // (every power of the symmetric P is symmetric: its registers serve as the
-    // A operand, read as the transpose, like P's own)
-    const d4 z = {0.0, 0.0, 0.0, 0.0};
-    auto mul = [&](const d4 &X, const d4 &Y) { return mfma_f64_x3(X[1], Y[1], X[2], Y[2], X[3], Y[3], z); };
     auto acc = [&](const d4 &Q, double f) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pt[r] = __builtin_fma(f, Q[r], Pt[r]);
@@ -212,11 +218,7 @@ __device__ __forceinline__ bool ptilde_12(const d4 &Pm, double rd, int g, int c,
     const double r1 = -rd, r2 = rd * rd, r3 = -r2 * rd, r4 = r2 * r2;
     Pt = Pm;
     if (J >= 1) {
-        const d4 Q2 = mul(Pm, Pm);
         if (J >= 2) {
-            const d4 Q3 = mul(Q2, Pm);
-            d4 Q4 = z;
-            if (J >= 3) Q4 = mul(Q2, Q2);
             if (J >= 4) {
                 const d4 Q5 = mul(Q4, Pm);
                 d4 Q6 = z, Q7 = z, Q8 = z, Q9 = z;
