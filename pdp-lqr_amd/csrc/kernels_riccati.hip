@@ -632,6 +632,30 @@ __global__ __launch_bounds__(64, 1) void k_riccati_bwd_vf3(RiccatiArgs A) {
     if (lane == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
 }
 
+// The wide shapes the 3 x 3 register-tile kernels are instantiated for: every
+// (n, m) with n % 4 = m % 4 = 0, m <= 16 and 32 < n + m <= 48 (the value-form
+// backward k_riccati_bwd_vf3 and the DMA rollout k_rollout_dma3; other wide
+// shapes keep the block-wide kernels of kernels_big.hip / kernels_wide.hip).
+template <int NN, int MM>
+struct Wide3 {
+    static constexpr int n = NN, m = MM;
+};
+template <typename F>
+static bool wide3_dispatch(int n, int m, F &&f) {
+    bool hit = false;
+    auto one = [&](auto shape) {
+        if (!hit && n == decltype(shape)::n && m == decltype(shape)::m) {
+            f(shape);
+            hit = true;
+        }
+    };
+    one(Wide3<32, 4>{}), one(Wide3<28, 8>{}), one(Wide3<24, 12>{}), one(Wide3<20, 16>{});
+    one(Wide3<36, 4>{}), one(Wide3<32, 8>{}), one(Wide3<28, 12>{}), one(Wide3<24, 16>{});
+    one(Wide3<40, 4>{}), one(Wide3<36, 8>{}), one(Wide3<32, 12>{}), one(Wide3<28, 16>{});
+    one(Wide3<44, 4>{}), one(Wide3<40, 8>{}), one(Wide3<36, 12>{}), one(Wide3<32, 16>{});
+    return hit;
+}
+
 // 16-byte alignment of every per-problem / per-stage block (fast path).
 static bool fast_aligned(const RiccatiArgs &a) {
     const Shape &sh = a.sh;
@@ -650,12 +674,15 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         launch_fast<1, 12, 4>(a, st);
     } else if (fast_ok && a.sh.n == 24 && a.sh.m == 8) {
         launch_fast<2, 24, 8>(a, st);
-    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16) {
-        // s = 40 on 3 x 3 register tiles (one wave per problem) instead of the
-        // block-wide LDS kernels of kernels_big.hip / kernels_wide.hip
-        if (!a.Lc)
-            hipLaunchKernelGGL((k_riccati_bwd_vf3<24, 16>), dim3(a.sh.batch), dim3(64), 0, st, a);
-        else launch_fast<3, 24, 16>(a, st);
+    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16 && a.Lc) {
+        launch_fast<3, 24, 16>(a, st);  // the factor cache: full factor on 3 x 3 tiles
+    } else if (fast_ok && !a.Lc &&
+               wide3_dispatch(a.sh.n, a.sh.m, [&](auto shape) {
+                   using W = decltype(shape);
+                   hipLaunchKernelGGL((k_riccati_bwd_vf3<W::n, W::m>), dim3(a.sh.batch), dim3(64), 0, st, a);
+               })) {
+        // 32 < s <= 48 on 3 x 3 register tiles (one wave per problem) instead of
+        // the block-wide LDS kernels of kernels_big.hip / kernels_wide.hip
     } else if (a.sh.s <= 16) {
         hipLaunchKernelGGL(k_riccati_bwd<1>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (a.sh.s <= 32) {
@@ -1259,8 +1286,10 @@ template <bool SEG>
 static int launch_fwd(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
                       double *ws, const SegFwd &sf, hipStream_t st) {
     const dim3 grid((unsigned)(SEG ? sh.batch * sf.S : sh.batch)), blk(64);
-    if (!SEG && sh.n == 24 && sh.m == 16 && ser3_aligned(sh, E, c, FR)) {
-        hipLaunchKernelGGL((k_rollout_dma3<24, 16, 3>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
+    if (!SEG && ser3_aligned(sh, E, c, FR) && wide3_dispatch(sh.n, sh.m, [&](auto shape) {
+            using W = decltype(shape);
+            hipLaunchKernelGGL((k_rollout_dma3<W::n, W::m, 3>), grid, blk, 0, st, sh, E, c, FR, x0, ws);
+        })) {
         PDPLQR_HIP_TRY(hipGetLastError());
         return PDPLQR_OK;
     }

@@ -16,6 +16,10 @@ from conftest import rel_err
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
 SHAPES = [(32, 16), (40, 20), (50, 10), (20, 30)]
+# the 3 x 3 register-tile instances (kernels_riccati.hip wide3_dispatch):
+# n % 4 = m % 4 = 0, m <= 16, 32 < n + m <= 48
+WIDE3 = [(32, 4), (28, 8), (24, 12), (20, 16), (36, 4), (32, 8), (28, 12), (24, 16), (40, 4), (36, 8), (32, 12),
+         (28, 16), (44, 4), (40, 8), (36, 12), (32, 16)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -82,6 +86,23 @@ def test_wide_serial_matches_oracle(n, m, keep, nc):
     assert np.all(bs.status() == 0)
     for b in range(batch):
         assert rel_err(out[b], _oracle_serial(p, b, n, m, N)) < TOL, b
+
+
+@pytest.mark.parametrize("n,m", WIDE3)
+@pytest.mark.parametrize("nc", [0, 4])
+def test_wide3_register_tile_shapes_match_oracle(n, m, nc):
+    """Every instantiated 3 x 3 register-tile shape (value-form backward
+    k_riccati_bwd_vf3 + DMA rollout k_rollout_dma3), penalties on and off."""
+    from pdplqr import BatchedLQRSolver
+
+    N, batch = 12, 2
+    p = _problem(n, m, N, batch, nc, 7 * n + m + nc)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=False, ncs=p["ncs"])
+    out = _solve(bs, p, nc)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        assert rel_err(out[b], _oracle_serial(p, b, n, m, N)) < TOL, b
+    bs.close()
 
 
 @pytest.mark.parametrize("n,m", SHAPES)
