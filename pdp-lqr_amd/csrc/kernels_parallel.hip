@@ -404,16 +404,8 @@ __device__ __forceinline__ void mw_scan_block(const ScanArgs &A, long long blk, 
     if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, 1);
 }
 
-// PDPLQR_MW_X1 (diagnostic variant only; bit 1 the scan rounds, 2 the boundary
-// maps, 4 the rank-fold trees): those 4-wave combine kernels claim a SIMD's
-// whole register file, so a block's four waves sit on four SIMDs and no other
-// block shares the CU
-#ifndef PDPLQR_MW_X1
-#define PDPLQR_MW_X1 0
-#endif
 template <int T, int NC = 0>
 __global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
-    simd_exclusive<(PDPLQR_MW_X1 & 1) != 0>();
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     mw_scan_block<T, NC>(A, blockIdx.x, mwbuf);
 }
@@ -628,7 +620,6 @@ __device__ __forceinline__ bool mw_map(const ElemIn &e, const double *vP, const 
 // split over the waves by output tile.
 template <int T, int NC = 0>
 __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
-    simd_exclusive<(PDPLQR_MW_X1 & 2) != 0>();
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int n = NC ? NC : A.n, S = A.S, J = S + 1, nn = n * n;
@@ -850,6 +841,8 @@ static inline bool ct_n12(int n) { return n == 12; }
 
 // the 4-wave combine runs the CHOLESKY rounds at T = 2 (PDPLQR_SCAN_1WAVE: the
 // one-wave k_seg_scan; PDPLQR_SCAN_MW=1 also at T = 1, A/B)
+// (n <= 16 keeps the one-wave combines: the 4-wave ones in Sklansky rounds
+// measured C2 0.113 against 0.103 ms with the two-round k_seg_scan4, r5q)
 bool seg_scan_mw(int n, bool lu, int mw) {
     if (!mw || lu) return false;
     return tile_order(n) == 2;
@@ -1149,7 +1142,6 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
 // scan rounds plus the boundary-map round and the map chain of the scan form.
 template <int T, int NC = 0>
 __global__ __launch_bounds__(256) void k_rank_tree_mw(RankTreeArgs A) {
-    simd_exclusive<(PDPLQR_MW_X1 & 4) != 0>();
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, nn = n * n, es = 3 * nn + 2 * n;

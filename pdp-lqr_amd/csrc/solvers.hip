@@ -218,14 +218,10 @@ static int parallel_init(pdplqr_handle h) {
 static int parallel_scans(pdplqr_handle h, int last_is_terminal);
 
 // The suffix scan runs Sklansky rounds (half the combines of a Hillis-Steele
-// round, same depth; PDPLQR_SCAN_HS=1: Hillis-Steele, A/B) on the shapes whose
-// combine kernels stage their operands before storing (n <= 32) and that do
-// not take the two-round k_seg_scan4 launches.
-static bool scan_sklansky(const Shape &sh) {
-    // (n <= 16 with PDPLQR_NO_SCAN4: radix-2 Hillis-Steele, the bit-exact
-    // reference of k_seg_scan4; PDPLQR_SCAN_SK=1 takes Sklansky there, A/B only)
-    return !wide_state(sh.n) && !seg_scan4_supported(sh.n);
-}
+// round, same depth) on the shapes whose combine kernels stage their operands
+// before storing (n <= 32) and that do not take the two-round k_seg_scan4
+// launches (n <= 16: radix-4 Hillis-Steele).
+static bool scan_sklansky(const Shape &sh) { return !wide_state(sh.n) && !seg_scan4_supported(sh.n); }
 void graph_release(pdplqr_handle h);
 
 static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
