@@ -674,12 +674,11 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         launch_fast<1, 12, 4>(a, st);
     } else if (fast_ok && a.sh.n == 24 && a.sh.m == 8) {
         launch_fast<2, 24, 8>(a, st);
-    } else if (fast_ok && a.sh.n == 24 && a.sh.m == 16 && a.Lc) {
-        launch_fast<3, 24, 16>(a, st);  // the factor cache: full factor on 3 x 3 tiles
-    } else if (fast_ok && !a.Lc &&
-               wide3_dispatch(a.sh.n, a.sh.m, [&](auto shape) {
+    } else if (fast_ok && wide3_dispatch(a.sh.n, a.sh.m, [&](auto shape) {
                    using W = decltype(shape);
-                   hipLaunchKernelGGL((k_riccati_bwd_vf3<W::n, W::m>), dim3(a.sh.batch), dim3(64), 0, st, a);
+                   if (a.Lc)  // the factor cache: the full factor
+                       hipLaunchKernelGGL((k_riccati_bwd_fast<3, W::n, W::m, true>), dim3(a.sh.batch), dim3(64), 0, st, a);
+                   else hipLaunchKernelGGL((k_riccati_bwd_vf3<W::n, W::m>), dim3(a.sh.batch), dim3(64), 0, st, a);
                })) {
         // 32 < s <= 48 on 3 x 3 register tiles (one wave per problem) instead of
         // the block-wide LDS kernels of kernels_big.hip / kernels_wide.hip

@@ -90,18 +90,30 @@ def test_wide_serial_matches_oracle(n, m, keep, nc):
 
 @pytest.mark.parametrize("n,m", WIDE3)
 @pytest.mark.parametrize("nc", [0, 4])
-def test_wide3_register_tile_shapes_match_oracle(n, m, nc):
+@pytest.mark.parametrize("keep", [False, True])
+def test_wide3_register_tile_shapes_match_oracle(n, m, nc, keep):
     """Every instantiated 3 x 3 register-tile shape (value-form backward
-    k_riccati_bwd_vf3 + DMA rollout k_rollout_dma3), penalties on and off."""
+    k_riccati_bwd_vf3, or the full factor k_riccati_bwd_fast<3> with the factor
+    cache, + DMA rollout k_rollout_dma3), penalties on and off; with the cache,
+    backward_without_factorization on new linear terms as well."""
     from pdplqr import BatchedLQRSolver
 
     N, batch = 12, 2
     p = _problem(n, m, N, batch, nc, 7 * n + m + nc)
-    bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=False, ncs=p["ncs"])
+    bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=keep, ncs=p["ncs"])
     out = _solve(bs, p, nc)
     assert np.all(bs.status() == 0)
     for b in range(batch):
         assert rel_err(out[b], _oracle_serial(p, b, n, m, N)) < TOL, b
+    if keep:
+        ws2 = 0.5 * p["ws"]
+        bs.update_problem_data(ws2, p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                               sigma=1e-6)
+        bs.backward_without_factorization((1.0 / p["irho"]) if nc else None)
+        out2 = np.zeros_like(p["ws"])
+        bs.forward(p["x0"], out2)
+        for b in range(batch):
+            assert rel_err(out2[b], _oracle_serial(p, b, n, m, N, ws=ws2[b])) < TOL, b
     bs.close()
 
 
