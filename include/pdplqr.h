@@ -111,9 +111,11 @@ typedef struct {
  * CHOLESKY, rho_dyn = kkt_sigma = 1e-6).
  * Shape limits of this build (the reference is size-generic, lqr_kernel.hpp:104-147):
  * nx + nu <= 64 for every solver: up to 32 on MFMA tiles in one wavefront,
- * 33..64 on LDS-resident stage matrices, one 256-thread block per problem /
- * segment / element (kernels_big.hip, kernels_wide.hip); KKT rows per stage
- * <= 64 past the block LDL^T tiles.  pdplqr_create returns
+ * 33..64 on register tiles or LDS-resident stage matrices, one 256-thread
+ * block per problem / segment / element (kernels_big.hip, kernels_wide.hip);
+ * KKT rows per stage <= 64 past the block LDL^T tiles.  The SERIAL solver
+ * goes on to nx + nu <= 256 (kernels_xl.hip: global-memory stage matrices;
+ * every protocol call, pdplqr_admm_solve excepted).  pdplqr_create returns
  * PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 

@@ -89,6 +89,9 @@ static void model_destroy(orc_model *md) {
 /* Dense helpers (Eigen semantics)                                          */
 /* ------------------------------------------------------------------------ */
 
+/* Largest stage size of the serial restatement (the parallel one keeps 64). */
+#define ORC_SMAX 256
+
 /* Eigen llt_inplace<Lower>::unblocked (Eigen/src/Cholesky/LLT.h), used by
  * Eigen for sizes < 32 and restated here for every size.  Writes the lower
  * factor into L (ld = dim) with a zero upper triangle, as
@@ -242,7 +245,7 @@ static void k_linear_tail(const orc_model *md, int k, const orc_stage *nx_, orc_
     int nd = nx_->dim, xo = nd - n; /* bottomRightCorner(n, n) of next L */
     const double *E = md->E + (size_t)k * n * s;
     const double *c = md->c + (size_t)k * n;
-    double Pb_tmp[64], Pb[64];
+    double Pb_tmp[ORC_SMAX], Pb[ORC_SMAX];
     for (j = 0; j < n; ++j) { /* Pb_tmp = Lxx^T c */
         double a = 0.0;
         for (i = 0; i < n; ++i) a += nx_->L[IX(xo + i, xo + j, nd)] * c[i];
@@ -271,7 +274,7 @@ static void k_step_fact(const orc_model *md, int k, const double *rho, const orc
     int n = md->n, m = md->m, s = n + m, i, j, t;
     int nd = nx_->dim, xo = nd - n;
     const double *E = md->E + (size_t)k * n * s;
-    double V[64 * 64], M[64 * 64];
+    double *V = (double *)xcalloc((size_t)s * s, sizeof(double)), *M = (double *)xcalloc((size_t)s * s, sizeof(double));
     stage_penalty(md, k, st, rho, 1);
     for (j = 0; j < n; ++j) /* V = E^T Lxx_next  (s x n) */
         for (i = 0; i < s; ++i) {
@@ -286,6 +289,8 @@ static void k_step_fact(const orc_model *md, int k, const double *rho, const orc
             M[IX(i, j, s)] = st->H[IX(i, j, s)] + a;
         }
     llt_lower(M, st->L, s);
+    free(V);
+    free(M);
     k_linear_tail(md, k, nx_, st);
     (void)m;
 }
@@ -307,7 +312,7 @@ static void k_forward(const orc_model *md, int k, const orc_stage *st, double *w
     double *x = w + m, *u = w;
     int xdim_next = (k + 1 < md->N) ? s : n;
     double *x_next = w_next + (xdim_next - n);
-    double xn[64];
+    double xn[ORC_SMAX];
     for (i = 0; i < m; ++i) {
         double a = -st->lp[i];
         for (j = 0; j < n; ++j) a -= st->L[IX(m + j, i, s)] * x[j];
@@ -337,7 +342,7 @@ void *orc_serial_create(int n, int m, int N, const int *nc, const double *E, con
                         const double *h, const double *D) {
     orc_serial *o;
     int k;
-    if (N < 1 || n < 1 || m < 1 || n + m > 64) return NULL; /* lqr_model.hpp:75-77; s <= 64 here */
+    if (N < 1 || n < 1 || m < 1 || n + m > ORC_SMAX) return NULL; /* lqr_model.hpp:75-77; s <= 256 here */
     o = (orc_serial *)xcalloc(1, sizeof(orc_serial));
     o->md = model_create(n, m, N, nc, E, c, H, h, D);
     o->ws = (orc_stage *)xcalloc(N + 1, sizeof(orc_stage));

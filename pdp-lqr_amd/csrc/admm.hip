@@ -521,6 +521,10 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
                   "adaptive_rho_tolerance >= 1)");
         return PDPLQR_ERR_INVALID;
     }
+    if (sh.s > 64) {  // k_admm_update covers a stage's w with at most 64 lanes
+        set_error("admm_solve: n + m > 64 is not supported by this build (the protocol calls are)");
+        return PDPLQR_ERR_UNSUPPORTED;
+    }
     if (h->md) return md_admm_solve(h, st, x0, lb, ub, rho, ws, ys, zs, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
     int rc = admm_alloc(h);

@@ -71,7 +71,17 @@ struct RiccatiArgs {
     const double *D = nullptr, *rho = nullptr, *gw = nullptr;
     const int32_t *d_off = nullptr, *y_off = nullptr;
     int nc_last = 0;
+    double *xl_ws = nullptr;  // 64 < n + m <= 256: per-problem workspace of kernels_xl.hip
 };
+bool xl_shape(const Shape &sh);           // 64 < n + m <= 256 (kernels_xl.hip)
+// workspace doubles per problem: V (s x n) and two s x s factor buffers
+__host__ __device__ inline long long xl_ws_doubles(const Shape &sh) {
+    return (long long)sh.s * sh.n + 2LL * sh.s * sh.s;
+}
+int launch_riccati_backward_xl(const RiccatiArgs &a, hipStream_t st);
+int launch_riccati_backward_nofact_xl(const RiccatiArgs &a, hipStream_t st);
+int launch_riccati_forward_xl(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                              double *ws, hipStream_t st);
 
 int launch_update_problem_data(const Shape &sh, const double *H, const double *hv, const double *ws,
                                const double *ys, const double *zs, const double *irho, double sigma, double *Hw,
@@ -130,6 +140,7 @@ struct pdplqr_handle_s {
     // workspace
     double *Hw = nullptr, *hw = nullptr, *gw = nullptr;
     double *KD = nullptr, *Lc = nullptr, *lpc = nullptr;
+    double *xl_ws = nullptr;  // SERIAL, 64 < n + m <= 256 (kernels_xl.hip)
     // H~ = H + sigma I (Hw) depends only on the model and sigma when no stage
     // has constraints (no rho penalty is folded into Hw): kept across
     // update_problem_data calls with the same sigma, re-formed after set_model

@@ -688,8 +688,10 @@ int launch_riccati_backward(const RiccatiArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k_riccati_bwd<2>, dim3(a.sh.batch), dim3(64), 0, st, a);
     } else if (big_shape(a.sh)) {
         return launch_riccati_backward_big(a, st);
+    } else if (xl_shape(a.sh)) {
+        return launch_riccati_backward_xl(a, st);
     } else {
-        set_error("backward: n + m > 64 is not supported by this build");
+        set_error("backward: n + m > 256 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     PDPLQR_HIP_TRY(hipGetLastError());
@@ -792,7 +794,8 @@ int launch_riccati_backward_nofact(const RiccatiArgs &a, hipStream_t st) {
         if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
     }
     if (a.sh.s > 64) {
-        set_error("backward_without_factorization: n + m > 64 is not supported by this build");
+        if (xl_shape(a.sh)) return launch_riccati_backward_nofact_xl(a, st);
+        set_error("backward_without_factorization: n + m > 256 is not supported by this build");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     if (a.sh.s <= 32) hipLaunchKernelGGL(k_riccati_bwd_nofact<32>, dim3(a.sh.batch), dim3(64), 0, st, a);
@@ -1300,6 +1303,7 @@ static int launch_fwd(const Shape &sh, const double *E, const double *c, const d
     }
     if (sh.s > 32) {
         if (!SEG && big_shape(sh)) return launch_riccati_forward_big(sh, E, c, FR, x0, ws, st);
+        if (!SEG && xl_shape(sh)) return launch_riccati_forward_xl(sh, E, c, FR, x0, ws, st);
         if (SEG && big_shape(sh)) return launch_riccati_forward_seg_big(sh, E, c, FR, sf, ws, st);
         set_error(SEG ? "segment forward: n + m > 32 is not supported by this build"
                       : "forward: n + m > 64 is not supported by this build");

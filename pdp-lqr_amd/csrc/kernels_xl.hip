@@ -1,0 +1,337 @@
+// kernels_xl.hip -- the serial solver (LQRSolver) for stage sizes
+// 64 < n + m <= 256: one 256-thread block per problem, the stage matrices in
+// a per-problem global-memory workspace (L2-resident; too large for LDS),
+// products by the block-wide MFMA routine of blk_la.hpp on 64 x 64 output
+// blocks.  A generality path: the reference is dynamic-size
+// (lqr_kernel.hpp:104-147 on Eigen::MatrixXd), and these kernels restate it
+// literally, in its own factor form:
+//   * k_riccati_bwd_xl: terminal_step_with_factorization (lqr_kernel.hpp:80-91)
+//     and step_with_factorization (:104-147) --
+//         V = E~^T Lxx_{k+1},  M = H~ + V V^T,  L = llt(M)
+//         lp = h~ + E~^T (Lxx (Lxx^T c) + p_{k+1}),  lu <- Luu^{-1} lu,
+//         p_k = lp_x - Lxu lu
+//     with Eigen's LLT stop (a non-positive reduced pivot leaves its column
+//     and every later one at the input values, device_common.hpp
+//     chol_restore_tail; here the factorisation is left-looking, so only the
+//     failing column is restored) and the same status as every backward.
+//     Records FR_k = [L(:, 0:m) | lu'], the factor cache (packed L_k, lp_k)
+//     when it exists;
+//   * k_riccati_bwd_nofact_xl: step_without_factorization (:150-178) on the
+//     cached factors;
+//   * k_riccati_fwd_xl: forward_step (:181-212).
+// Workspace per problem (RiccatiArgs::xl_ws, xl_ws_doubles): V (s x n) and two
+// s x s factor buffers (this stage's, the next stage's), leading dimension s.
+#include "blk_la.hpp"
+#include "parallel.hpp"
+
+namespace pdplqr {
+
+namespace {
+constexpr int XL_S = 256;  // largest n + m
+}
+
+bool xl_shape(const Shape &sh) { return sh.s > 64 && sh.s <= XL_S; }
+
+// C (M x N, ld ldc) = A B + add over 64 x 64 output blocks (blk_mm; no aliasing
+// between C and A / B here)
+__device__ void xl_mm(double *C, int ldc, const double *A, int lda, bool at, const double *B, int ldb, bool bt,
+                      int M, int N, int K, const double *add, int ldadd) {
+    for (int j0 = 0; j0 < N; j0 += 64)
+        for (int i0 = 0; i0 < M; i0 += 64) {
+            const Mv av = at ? mv_t(A + (long long)i0 * lda, lda) : mv_n(A + i0, lda);
+            const Mv bv = bt ? mv_t(B + j0, ldb) : mv_n(B + (long long)j0 * ldb, ldb);
+            const Mv dv = add ? mv_n(add + i0 + (long long)j0 * ldadd, ldadd) : mv_none();
+            blk_mm(C + i0 + (long long)j0 * ldc, ldc, av, bv, min(64, M - i0), min(64, N - j0), K, 1.0, 0.0, dv, false);
+        }
+}
+
+// In-place left-looking Cholesky of the lower triangle of A (n x n, ld) with
+// Eigen's LLT stop: pivot j < m must be positive (else flagged and the
+// factorisation goes on, as the tiled kernels do), a pivot j >= m that is not
+// positive stops it, column j back at its input values (later columns were
+// never touched), flagged only when psd_bad.  col: n doubles of LDS scratch.
+// Returns the block-uniform status.
+__device__ bool xl_llt(double *A, int ld, int n, int m, double *col) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    for (int j = 0; j < n; ++j) {
+        __syncthreads();
+        for (int i = j + tid; i < n; i += 256) {
+            const double a0 = A[i + (long long)j * ld];
+            col[i] = a0;
+            double v = a0;
+            for (int p = 0; p < j; ++p) v = __builtin_fma(-A[i + (long long)p * ld], A[j + (long long)p * ld], v);
+            A[i + (long long)j * ld] = v;
+        }
+        __syncthreads();
+        const double d = A[j + (long long)j * ld];
+        const bool live = j < m || d > 0.0;
+        ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
+        __syncthreads();  // every thread read the pivot
+        if (!live) {      // Eigen's stop: column j at its input values, the rest untouched
+            for (int i = j + tid; i < n; i += 256) A[i + (long long)j * ld] = col[i];
+            __syncthreads();
+            break;
+        }
+        const double r = sqrt(d), ir = 1.0 / r;
+        for (int i = j + tid; i < n; i += 256) A[i + (long long)j * ld] = i == j ? r : A[i + (long long)j * ld] * ir;
+    }
+    __syncthreads();
+    return ok;
+}
+
+// lp (s) = h~ + E~^T (Lxx (Lxx^T c) + p): t, pb: n doubles of LDS
+__device__ void xl_linear(double *lp, const double *hk, const double *Ek, const double *ck, const double *Lxx, int ldl,
+                          const double *p, int n, int s, double *t, double *pb) {
+    const int tid = threadIdx.x;
+    __syncthreads();
+    for (int j = tid; j < n; j += 256) {  // t = Lxx^T c
+        double a = 0.0;
+        for (int i = j; i < n; ++i) a = __builtin_fma(Lxx[i + (long long)j * ldl], ck[i], a);
+        t[j] = a;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {  // pb = Lxx t + p
+        double a = p[i];
+        for (int j = 0; j <= i; ++j) a = __builtin_fma(Lxx[i + (long long)j * ldl], t[j], a);
+        pb[i] = a;
+    }
+    __syncthreads();
+    for (int j = tid; j < s; j += 256) {  // lp = h~ + E~^T pb
+        double a = hk[j];
+        for (int i = 0; i < n; ++i) a = __builtin_fma(Ek[i + (long long)j * n], pb[i], a);
+        lp[j] = a;
+    }
+    __syncthreads();
+}
+
+// lu <- Luu^{-1} lu (rows < m of lp), then p = lp_x - Lxu lu into pn (n) and
+// lp's x rows.  L (s x s, ld s).
+__device__ void xl_solve_u(double *lp, const double *L, int ld, int m, int s, double *pn) {
+    const int tid = threadIdx.x;
+    for (int i = 0; i < m; ++i) {  // forward substitution, one row per barrier
+        __syncthreads();
+        if (tid == 0) {
+            double v = lp[i];
+            for (int j = 0; j < i; ++j) v = __builtin_fma(-L[i + (long long)j * ld], lp[j], v);
+            lp[i] = v / L[i + (long long)i * ld];
+        }
+    }
+    __syncthreads();
+    for (int r = tid; r < s - m; r += 256) {
+        double a = lp[m + r];
+        for (int j = 0; j < m; ++j) a = __builtin_fma(-L[(m + r) + (long long)j * ld], lp[j], a);
+        pn[r] = a;
+    }
+    __syncthreads();
+    for (int r = tid; r < s - m; r += 256) lp[m + r] = pn[r];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
+    __shared__ double col[XL_S], lp[XL_S], pv[XL_S], t[XL_S], pb[XL_S];
+    const int tid = threadIdx.x;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, ps = sh.ps;
+    const long long b = blockIdx.x;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *Hb = A.Hw + b * sh.perHw;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.KD + b * sh.perKD;
+    double *Lcb = A.Lc ? A.Lc + b * sh.perHw : nullptr;
+    double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
+    double *W = A.xl_ws + b * xl_ws_doubles(sh);
+    double *const V = W, *const L0 = W + (long long)s * n, *const L1 = L0 + (long long)s * s;
+    auto Lb = [&](int k) { return (k & 1) ? L1 : L0; };
+    const long long frs = (long long)s * m + m;
+    int fail_stage = -1;
+    // ---- terminal: L_N = llt(H~_N) (order n, stored at (m, m) of the factor buffer), p_N = h~_N ----
+    double *Ln = Lb(N);
+    double *LxxN = Ln + m + (long long)m * s;
+    const double *HN = Hb + (long long)N * ps;
+    for (int q = tid; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        LxxN[i + (long long)j * s] = i >= j ? HN[pidx(i, j, n)] : 0.0;
+    }
+    if (!xl_llt(LxxN, s, n, 0, col)) fail_stage = N;
+    for (int q = tid; q < n; q += 256) {
+        pv[q] = hb[(long long)N * s + q];
+        if (lpb) lpb[(long long)N * s + q] = pv[q];
+    }
+    if (Lcb)
+        for (int q = tid; q < n * n; q += 256) {
+            const int i = q % n, j = q / n;
+            if (i >= j) Lcb[(long long)N * ps + pidx(i, j, n)] = LxxN[i + (long long)j * s];
+        }
+    for (int k = N - 1; k >= 0; --k) {
+        const double *Ek = Eb + (long long)k * n * s;
+        double *Lk = Lb(k);
+        const double *Lxx = Lb(k + 1) + m + (long long)m * s;  // Lxx_{k+1}, ld s
+        // V = E~^T Lxx_{k+1} (s x n): only its lower triangle is meaningful, the
+        // upper part of the factor buffer is zero
+        xl_mm(V, s, Ek, n, true, Lxx, s, false, s, n, n, nullptr, 0);
+        // M = H~ + V V^T into Lk (H~ unpacked first, then added in place)
+        __syncthreads();
+        for (int q = tid; q < s * s; q += 256) {
+            const int i = q % s, j = q / s;
+            Lk[i + (long long)j * s] = Hb[(long long)k * ps + (i >= j ? pidx(i, j, s) : pidx(j, i, s))];
+        }
+        xl_mm(Lk, s, V, s, false, V, s, true, s, s, n, Lk, s);
+        xl_linear(lp, hb + (long long)k * s, Ek, cb + (long long)k * n, Lxx, s, pv, n, s, t, pb);
+        const bool ok = xl_llt(Lk, s, s, m, col);
+        if (!ok && fail_stage < 0) fail_stage = k;
+        xl_solve_u(lp, Lk, s, m, s, pb);
+        for (int q = tid; q < n; q += 256) pv[q] = lp[m + q];
+        // records: FR_k = [L(:, 0:m) | lu'] (zeros above the diagonal), caches
+        double *FRk = FRb + (long long)k * frs;
+        for (int q = tid; q < s * m; q += 256) {
+            const int i = q % s, j = q / s;
+            FRk[(long long)j * s + i] = i >= j ? Lk[i + (long long)j * s] : 0.0;
+        }
+        for (int q = tid; q < m; q += 256) FRk[(long long)s * m + q] = lp[q];
+        if (lpb)
+            for (int q = tid; q < s; q += 256) lpb[(long long)k * s + q] = lp[q];
+        if (Lcb)
+            for (int q = tid; q < s * s; q += 256) {
+                const int i = q % s, j = q / s;
+                if (i >= j) Lcb[(long long)k * ps + pidx(i, j, s)] = Lk[i + (long long)j * s];
+            }
+        // the next stage reads Lxx of this buffer: its upper part must be zero
+        for (int q = tid; q < s * s; q += 256) {
+            const int i = q % s, j = q / s;
+            if (i < j) Lk[i + (long long)j * s] = 0.0;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) A.status[b] = fail_stage < 0 ? 0 : fail_stage + 1;
+}
+
+__global__ __launch_bounds__(256) void k_riccati_bwd_nofact_xl(RiccatiArgs A) {
+    __shared__ double lp[XL_S], pv[XL_S], t[XL_S], pb[XL_S];
+    const int tid = threadIdx.x;
+    const Shape &sh = A.sh;
+    const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, ps = sh.ps;
+    const long long b = blockIdx.x;
+    const double *Eb = A.E + b * sh.perE;
+    const double *cb = A.c + b * sh.perc;
+    const double *hb = A.hw + b * sh.perh;
+    double *FRb = A.KD + b * sh.perKD;
+    const double *Lcb = A.Lc + b * sh.perHw;
+    double *lpb = A.lpc + b * sh.perh;
+    double *W = A.xl_ws + b * xl_ws_doubles(sh);
+    double *const L0 = W + (long long)s * n, *const L1 = L0 + (long long)s * s;
+    auto Lb = [&](int k) { return (k & 1) ? L1 : L0; };
+    const long long frs = (long long)s * m + m;
+    // the cached factors unpacked into the workspace (ld s; Lxx of the
+    // terminal at (m, m)); the same products as the factorising backward
+    auto unpack = [&](double *L, int k) {
+        __syncthreads();
+        if (k == N) {
+            for (int q = tid; q < n * n; q += 256) {
+                const int i = q % n, j = q / n;
+                L[(m + i) + (long long)(m + j) * s] = i >= j ? Lcb[(long long)N * ps + pidx(i, j, n)] : 0.0;
+            }
+        } else {
+            for (int q = tid; q < s * s; q += 256) {
+                const int i = q % s, j = q / s;
+                L[i + (long long)j * s] = i >= j ? Lcb[(long long)k * ps + pidx(i, j, s)] : 0.0;
+            }
+        }
+        __syncthreads();
+    };
+    for (int q = tid; q < n; q += 256) {  // lp_N = h~_N (lqr_kernel.hpp:94-101)
+        pv[q] = hb[(long long)N * s + q];
+        lpb[(long long)N * s + q] = pv[q];
+    }
+    unpack(Lb(N), N);
+    for (int k = N - 1; k >= 0; --k) {
+        double *Lk = Lb(k);
+        unpack(Lk, k);
+        const double *Lxx = Lb(k + 1) + m + (long long)m * s;
+        xl_linear(lp, hb + (long long)k * s, Eb + (long long)k * n * s, cb + (long long)k * n, Lxx, s, pv, n, s, t, pb);
+        xl_solve_u(lp, Lk, s, m, s, pb);
+        for (int q = tid; q < n; q += 256) pv[q] = lp[m + q];
+        for (int q = tid; q < m; q += 256) FRb[(long long)k * frs + (long long)s * m + q] = lp[q];
+        for (int q = tid; q < s; q += 256) lpb[(long long)k * s + q] = lp[q];
+        __syncthreads();
+    }
+}
+
+// forward_step (lqr_kernel.hpp:181-212): u = -Luu^{-T} (lu' + Lxu^T x),
+// x+ = c + E~ [u; x]; ws[k s .. k s + s) = [u_k; x_k], ws[N s ..) = x_N
+__global__ __launch_bounds__(256) void k_riccati_fwd_xl(Shape sh, const double *__restrict__ E,
+                                                      const double *__restrict__ c, const double *__restrict__ FR,
+                                                      const double *__restrict__ x0, double *__restrict__ ws) {
+    __shared__ double w[XL_S], v[XL_S];
+    const int tid = threadIdx.x;
+    const int n = sh.n, m = sh.m, N = sh.N, s = sh.s;
+    const long long b = blockIdx.x;
+    const long long frs = (long long)s * m + m;
+    const double *Eb = E + b * sh.perE;
+    const double *cb = c + b * sh.perc;
+    const double *Fb = FR + b * sh.perKD;
+    double *wb = ws + b * sh.perh;
+    for (int q = tid; q < n; q += 256) {
+        w[m + q] = x0[b * n + q];
+        wb[(long long)(N > 0 ? m : 0) + q] = w[m + q];
+    }
+    __syncthreads();
+    for (int k = 0; k < N; ++k) {
+        const double *Fk = Fb + (long long)k * frs;
+        for (int j = tid; j < m; j += 256) {  // v = -(lu' + Lxu^T x)
+            double a = Fk[(long long)s * m + j];
+            for (int i = 0; i < n; ++i) a = __builtin_fma(Fk[(long long)j * s + m + i], w[m + i], a);
+            v[j] = -a;
+        }
+        for (int j = m - 1; j >= 0; --j) {  // u = Luu^{-T} v (back substitution)
+            __syncthreads();
+            const double uj = v[j] / Fk[(long long)j * s + j];
+            __syncthreads();
+            for (int i = tid; i < j; i += 256) v[i] = __builtin_fma(-Fk[(long long)i * s + j], uj, v[i]);
+            if (tid == 0) v[j] = uj;
+        }
+        __syncthreads();
+        for (int j = tid; j < m; j += 256) {
+            w[j] = v[j];
+            wb[(long long)k * s + j] = v[j];
+        }
+        __syncthreads();
+        const double *Ek = Eb + (long long)k * n * s;
+        double xn = 0.0;  // n < 256: one state row per thread
+        if (tid < n) {
+            xn = cb[(long long)k * n + tid];
+            for (int j = 0; j < s; ++j) xn = __builtin_fma(Ek[tid + (long long)j * n], w[j], xn);
+        }
+        __syncthreads();
+        if (tid < n) {
+            w[m + tid] = xn;
+            wb[(long long)(k + 1) * s + ((k + 1 < N) ? m : 0) + tid] = xn;
+        }
+        __syncthreads();
+    }
+}
+
+int launch_riccati_backward_xl(const RiccatiArgs &a, hipStream_t st) {
+    if (!xl_shape(a.sh) || !a.xl_ws) return PDPLQR_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_riccati_bwd_xl, dim3((unsigned)a.sh.batch), dim3(256), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_riccati_backward_nofact_xl(const RiccatiArgs &a, hipStream_t st) {
+    if (!xl_shape(a.sh) || !a.xl_ws || !a.Lc || !a.lpc) return PDPLQR_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_riccati_bwd_nofact_xl, dim3((unsigned)a.sh.batch), dim3(256), 0, st, a);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+int launch_riccati_forward_xl(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,
+                              double *ws, hipStream_t st) {
+    if (!xl_shape(sh)) return PDPLQR_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_riccati_fwd_xl, dim3((unsigned)sh.batch), dim3(256), 0, st, sh, E, c, FR, x0, ws);
+    PDPLQR_HIP_TRY(hipGetLastError());
+    return PDPLQR_OK;
+}
+
+}  // namespace pdplqr

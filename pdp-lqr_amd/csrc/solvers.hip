@@ -77,6 +77,7 @@ static RiccatiArgs riccati_args(pdplqr_handle h) {
     a.status = h->status;
     a.tab_s = h->tab_s;
     a.tab_n = h->tab_n;
+    a.xl_ws = h->xl_ws;
     return a;
 }
 
@@ -351,7 +352,8 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
 int solver_init(pdplqr_handle h) {
     switch (h->cfg.solver) {
         case PDPLQR_SOLVER_SERIAL:
-            if (h->sh.s > 64) return unsupported("SERIAL solver with n + m > 64");
+            if (h->sh.s > 256) return unsupported("SERIAL solver with n + m > 256");
+            if (xl_shape(h->sh)) return palloc(h, &h->xl_ws, (size_t)h->sh.batch * xl_ws_doubles(h->sh));
             return PDPLQR_OK;
         case PDPLQR_SOLVER_PARALLEL:
             return parallel_init(h);

@@ -6,7 +6,7 @@ dynamic-Eigen kernels (lqr_kernel.hpp:104-147).
 Covers backward with and without kept factors, forward, the value function,
 backward_without_factorization, constrained stages (rho penalty), the status
 flag of an indefinite stage, the ADMM loop over the serial solver, and the
-error for n + m > 64 and for the PARALLEL / KKT solvers past 32.  Tolerance
+shape limits of the three solvers.  Tolerance
 1e-9 relative (fp64, different summation order), as tests/test_gpu_serial.py.
 All calls go through the C ABI (libpdplqr.so).
 """
@@ -168,11 +168,17 @@ def test_big_admm_serial_matches_oracle():
 
 
 def test_big_shape_limits():
-    """n + m > 64: every solver refuses; 32 < n + m <= 64 runs on every solver
-    (kernels_big.hip, kernels_wide.hip; tests/test_gpu_wide.py)."""
+    """32 < n + m <= 64 runs on every solver (kernels_big.hip, kernels_wide.hip;
+    tests/test_gpu_wide.py); 64 < n + m <= 256 on the serial solver only
+    (kernels_xl.hip, tests/test_gpu_xl.py); past that every solver refuses."""
     from pdplqr import BatchedLQRSolver, PdplqrError
 
     for solver in ("serial", "parallel", "kkt"):
-        with pytest.raises(PdplqrError):
-            BatchedLQRSolver(50, 15, 4, 1, solver=solver, num_segments=2)
         BatchedLQRSolver(30, 10, 8, 1, solver=solver, num_segments=2).close()
+        with pytest.raises(PdplqrError):
+            BatchedLQRSolver(200, 57, 4, 1, solver=solver, num_segments=2)
+        if solver == "serial":
+            BatchedLQRSolver(50, 15, 4, 1, solver=solver).close()
+        else:
+            with pytest.raises(PdplqrError):
+                BatchedLQRSolver(50, 15, 4, 1, solver=solver, num_segments=2)

@@ -1,0 +1,128 @@
+"""GPU parity of the serial solver for stage sizes 64 < n + m <= 256
+(csrc/kernels_xl.hip: one 256-thread block per problem, the stage matrices in
+a per-problem global-memory workspace, the reference's factor form
+lqr_kernel.hpp:80-212 restated literally) against the size-generic CPU oracle.
+
+Covers backward with and without kept factors, forward, the value function,
+backward_without_factorization, rho-penalised stages, the status of an
+indefinite stage, and the refusal of admm_solve past n + m = 64 (its update
+pass covers a stage with at most 64 lanes).  Tolerance 1e-9 relative, as the
+other serial parity tests."""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from oracle.oracle import OracleSerial
+from pdplqr.model import PackedModel
+from pdplqr.problems import random_batch_arrays
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+# (n, m, N, batch): s = 65 (smallest), 70, 100 (m > n), 128, 160
+SHAPES = [(50, 15, 6, 2), (40, 30, 5, 2), (36, 64, 4, 2), (100, 28, 3, 2), (120, 40, 2, 1)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from pdplqr import device_count
+
+    assert device_count() > 0, "no HIP device visible"
+
+
+def _problem(n, m, N, batch, nc, seed):
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, seed)
+    s = n + m
+    g = np.random.default_rng(seed + 1)
+    ncs = np.full(N + 1, nc, dtype=np.int32)
+    dims = [s] * N + [n]
+    D = np.concatenate([g.standard_normal((batch, nc * dk)) for dk in dims], axis=1) if nc else np.zeros((batch, 0))
+    ny = int(ncs.sum())
+    ws = 0.1 * g.standard_normal((batch, N * s + n))
+    ys, zs = g.standard_normal((batch, ny)), g.standard_normal((batch, ny))
+    irho = 0.05 + g.random((batch, ny))
+    return dict(E=E, c=c, H=H, h=h, x0=x0, ncs=ncs, D=D, ws=ws, ys=ys, zs=zs, irho=irho, nc=nc)
+
+
+def _oracle(p, b, n, m, N, ws=None, nofact_ws=None):
+    nc = p["nc"]
+    pm = PackedModel(n, m, N, p["ncs"], p["E"][b], p["c"][b], p["H"][b], p["h"][b], p["D"][b] if nc else np.zeros(0))
+    o = OracleSerial(pm)
+    args = lambda w: (w, p["ys"][b] if nc else None, p["zs"][b] if nc else None, p["irho"][b] if nc else None, 1e-6)
+    o.update_problem_data(*args(p["ws"][b] if ws is None else ws))
+    o.backward((1.0 / p["irho"][b]) if nc else None)
+    if nofact_ws is not None:
+        o.update_problem_data(*args(nofact_ws))
+        o.backward_without_factorization((1.0 / p["irho"][b]) if nc else None)
+    return o, o.forward(p["x0"][b])
+
+
+@pytest.mark.parametrize("n,m,N,batch", SHAPES)
+@pytest.mark.parametrize("keep", [False, True])
+@pytest.mark.parametrize("nc", [0, 3])
+def test_xl_serial_matches_oracle(n, m, N, batch, keep, nc):
+    from pdplqr import BatchedLQRSolver
+
+    p = _problem(n, m, N, batch, nc, 11 * n + m + nc)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="serial", keep_factors=keep, ncs=p["ncs"])
+    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"] if nc else None)
+    rho = (1.0 / p["irho"]) if nc else None
+    bs.update_problem_data(p["ws"], p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                           sigma=1e-6)
+    bs.backward(rho)
+    out = np.zeros_like(p["ws"])
+    bs.forward(p["x0"], out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        o, ref = _oracle(p, b, n, m, N)
+        assert rel_err(out[b], ref) < TOL, b
+        if keep:
+            for k in (0, N):
+                P, pv = bs.value_function(b, k)
+                Po, po = o.value_function(k)
+                assert rel_err(P, Po) < TOL and rel_err(pv, po) < 1e-8, (b, k)
+    if keep:  # lqr_solver.hpp:65-70: new linear data on the kept factors
+        ws1 = p["ws"] + 0.2 * np.random.default_rng(n).standard_normal(p["ws"].shape)
+        bs.update_problem_data(ws1, p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                               sigma=1e-6)
+        bs.backward_without_factorization(rho)
+        out1 = np.zeros_like(out)
+        bs.forward(p["x0"], out1)
+        for b in range(batch):
+            _, ref1 = _oracle(p, b, n, m, N, nofact_ws=ws1[b])
+            assert rel_err(out1[b], ref1) < TOL, b
+    bs.close()
+
+
+@pytest.mark.parametrize("keep", [False, True])
+def test_xl_indefinite_stage_sets_status(keep):
+    """An indefinite stage matrix: the factorisation of that stage fails (a
+    control pivot), as k_riccati_bwd_big's full factor does."""
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch = 50, 20, 6, 2
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 5)
+    s = n + m
+    H = H.copy()
+    H[1, 3 * s * s:4 * s * s] = -np.eye(s).reshape(-1)  # stage 3 of problem 1
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+    bs.set_model(E, c, H, h)
+    bs.update_problem_data(np.zeros((batch, N * s + n)), sigma=0.0)
+    bs.backward()
+    st = bs.status()
+    assert st[0] == 0 and st[1] == 3 + 1
+    bs.close()
+
+
+def test_xl_admm_refused():
+    from pdplqr import BatchedLQRSolver, PdplqrError
+
+    n, m, N = 50, 20, 4
+    p = _problem(n, m, N, 1, 2, 3)
+    bs = BatchedLQRSolver(n, m, N, 1, keep_factors=True, ncs=p["ncs"])
+    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"])
+    lb, ub = -np.ones_like(p["irho"]), np.ones_like(p["irho"])
+    w, y, z = p["ws"].copy(), p["ys"].copy(), p["zs"].copy()
+    with pytest.raises(PdplqrError):
+        bs.admm_solve(p["x0"], lb, ub, 1.0 / p["irho"], w, y, z, max_iter=2)
+    bs.close()
