@@ -115,7 +115,7 @@ typedef struct {
  * block per problem / segment / element (kernels_big.hip, kernels_wide.hip);
  * KKT rows per stage <= 64 past the block LDL^T tiles.  The SERIAL solver
  * goes on to nx + nu <= 256 (kernels_xl.hip: global-memory stage matrices;
- * every protocol call, pdplqr_admm_solve excepted).  pdplqr_create returns
+ * every protocol call and pdplqr_admm_solve).  pdplqr_create returns
  * PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 

@@ -246,6 +246,121 @@ __global__ void __launch_bounds__(256) k_admm_update(AdmmArgs a) {
     }
 }
 
+// The same update for 64 < n + m <= 256 (the serial solver's kernels_xl.hip
+// shapes): a stage takes the whole wave, lane j holding entries j + 64 e
+// (e < EPL); a row of D_k w~ is the lane's partial sum over its entries, then
+// the wave butterfly.  Per entry the operations are k_admm_update's, in its
+// order (the D^T sums over the rows r in turn).
+template <bool FUSE, bool CHECK, int EPL>
+__global__ void __launch_bounds__(256) k_admm_update_xl(AdmmArgs a) {
+    const Shape &sh = a.sh;
+    const int b = blockIdx.x;
+    if (a.done[b]) return;  // block-uniform
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double al = a.alpha, bl = 1.0 - a.alpha;
+    double rp = 0.0, dwm = 0.0, zm = 0.0, rd = 0.0, dty = 0.0, act = 0.0;
+    for (int k = wv; k <= sh.N; k += 4) {  // wave-uniform
+        const int dim = k < sh.N ? sh.s : sh.n;
+        const int yo0 = a.uni ? k * a.uni : a.y_off[k];
+        const int nc = a.uni ? (k < sh.N ? a.uni : 0) : a.y_off[k + 1] - yo0;
+        const long long yo = (long long)b * sh.ny + yo0;
+        const double *Dk = a.D + (long long)b * sh.ndD + (a.uni ? (long long)k * a.uni * sh.s : a.d_off[k]);
+        bool col[EPL];
+        long long wo[EPL];
+        double wtj[EPL], wj[EPL], ag[EPL], ad[EPL], ay[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+            const int j = lane + 64 * e;
+            col[e] = j < dim;
+            wo[e] = (long long)b * sh.perh + (long long)k * sh.s + (col[e] ? j : 0);
+            wtj[e] = col[e] ? a.wt[wo[e]] : 0.0;
+            wj[e] = col[e] ? a.w[wo[e]] : 0.0;
+            ag[e] = ad[e] = ay[e] = 0.0;
+        }
+        for (int r = 0; r < nc; ++r) {
+            double d[EPL], pv = 0.0, pw = 0.0;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                d[e] = col[e] ? Dk[r + (lane + 64 * e) * nc] : 0.0;
+                pv += d[e] * wtj[e];
+                pw += d[e] * wj[e];
+            }
+            const double v = stage_sum<64>(pv), vw = stage_sum<64>(pw);
+            const double zr = a.z[yo + r], yr = a.y[yo + r], rr = a.rho[yo + r], ir = a.irho[yo + r];
+            const double vrel = al * v + bl * zr;
+            const double zn = fmin(fmax(vrel + ir * yr, a.lb[yo + r]), a.ub[yo + r]);
+            const double yn = yr + rr * (vrel - zn);
+            const double gn = zn - ir * yn;
+            if (lane == 0) {
+                a.z[yo + r] = zn;
+                a.y[yo + r] = yn;
+                if (FUSE) a.gw[yo + r] = gn;
+            }
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                if (FUSE) ag[e] += d[e] * (rr * gn);
+                if (CHECK) {
+                    ad[e] += d[e] * (rr * (zn - zr));
+                    ay[e] += d[e] * yn;
+                }
+            }
+            if (CHECK) {
+                const double dwn = al * v + bl * vw;
+                rp = fmax(rp, fabs(dwn - zn));
+                dwm = fmax(dwm, fabs(dwn));
+                zm = fmax(zm, fabs(zn));
+                if (zn <= a.lb[yo + r] || zn >= a.ub[yo + r]) act = 1.0;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+            if (col[e]) {
+                const double wn = al * wtj[e] + bl * wj[e];
+                a.w[wo[e]] = wn;
+                if (FUSE) {
+                    double hj = a.hv[wo[e]] - a.sigma * wn;
+                    if (nc > 0 && !a.no_penalty) hj -= ag[e];
+                    a.hw[wo[e]] = hj;
+                }
+            }
+            if (CHECK) {
+                rd = fmax(rd, fabs(ad[e]));
+                dty = fmax(dty, fabs(ay[e]));
+            }
+        }
+    }
+    if (CHECK) {
+        __shared__ double red[4][6];
+        rp = wave_max(rp);
+        dwm = wave_max(dwm);
+        zm = wave_max(zm);
+        rd = wave_max(rd);
+        dty = wave_max(dty);
+        act = wave_max(act);
+        if (lane == 0) {
+            red[wv][0] = rp;
+            red[wv][1] = dwm;
+            red[wv][2] = zm;
+            red[wv][3] = rd;
+            red[wv][4] = dty;
+            red[wv][5] = act;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                rp = fmax(rp, red[q][0]);
+                dwm = fmax(dwm, red[q][1]);
+                zm = fmax(zm, red[q][2]);
+                rd = fmax(rd, red[q][3]);
+                dty = fmax(dty, red[q][4]);
+                act = fmax(act, red[q][5]);
+            }
+            admm_decide(a, b, rp, dwm, zm, rd, dty, act);
+        }
+    }
+}
+
 __global__ void k_admm_init(long long ny_total, const double *__restrict__ rho, double *__restrict__ irho) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < ny_total) irho[t] = 1.0 / rho[t];
@@ -274,12 +389,22 @@ __global__ void k_admm_rescale(long long ny_total, int ny, const double *__restr
     irho[t] = 1.0 / r;
 }
 
+// lanes a stage of k_admm_update takes (past 64: k_admm_update_xl)
+static int admm_lps(const Shape &sh) { return sh.s <= 16 ? 16 : (sh.s <= 32 ? 32 : (sh.s <= 64 ? 64 : 256)); }
+
 static int launch_admm_update(const AdmmArgs &a, int lps, bool fuse, bool check, dim3 grid, dim3 blk,
                               hipStream_t S) {
 #define PDPLQR_ADMM_LAUNCH(L, F, C) hipLaunchKernelGGL((k_admm_update<L, F, C, 0>), grid, blk, 0, S, a)
 #define PDPLQR_ADMM_LAUNCH4(F, C) hipLaunchKernelGGL((k_admm_update<16, F, C, 4>), grid, blk, 0, S, a)
     const bool l16 = lps == 16;
-    if (l16 && a.max_nc <= 4) {
+    if (lps > 64) {  // kernels_xl.hip shapes: a wave per stage, up to 4 entries a lane
+#define PDPLQR_ADMM_XL(F, C) hipLaunchKernelGGL((k_admm_update_xl<F, C, 4>), grid, blk, 0, S, a)
+        if (fuse && check) PDPLQR_ADMM_XL(true, true);
+        else if (fuse) PDPLQR_ADMM_XL(true, false);
+        else if (check) PDPLQR_ADMM_XL(false, true);
+        else PDPLQR_ADMM_XL(false, false);
+#undef PDPLQR_ADMM_XL
+    } else if (l16 && a.max_nc <= 4) {
         if (fuse && check) PDPLQR_ADMM_LAUNCH4(true, true);
         else if (fuse) PDPLQR_ADMM_LAUNCH4(true, false);
         else if (check) PDPLQR_ADMM_LAUNCH4(false, true);
@@ -452,7 +577,7 @@ static int md_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const 
         const bool check = last || it % st->check_every == 0;
         a.it = it;
         if (check) PDPLQR_HIP_TRY(hipMemsetAsync(s->active, 0, 2 * sizeof(int32_t), S));
-        if ((rc = launch_admm_update(a, sh.s <= 16 ? 16 : (sh.s <= 32 ? 32 : 64), false, check, ugrid, ublk, S)))
+        if ((rc = launch_admm_update(a, admm_lps(sh), false, check, ugrid, ublk, S)))
             return rc;
         if (check) {
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
@@ -520,10 +645,6 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
         set_error("admm_solve: bad settings (max_iter >= 1, check_every >= 1, 0 < alpha < 2, sigma, eps >= 0, "
                   "adaptive_rho_tolerance >= 1)");
         return PDPLQR_ERR_INVALID;
-    }
-    if (sh.s > 64) {  // k_admm_update covers a stage's w with at most 64 lanes
-        set_error("admm_solve: n + m > 64 is not supported by this build (the protocol calls are)");
-        return PDPLQR_ERR_UNSUPPORTED;
     }
     if (h->md) return md_admm_solve(h, st, x0, lb, ub, rho, ws, ys, zs, mem);
     PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
@@ -682,7 +803,7 @@ int pdplqr_admm_solve(pdplqr_handle h, const pdplqr_admm_settings *st, const dou
             else if (rc == PDPLQR_ERR_UNSUPPORTED) can_fuse = false;
             else return rc;
         }
-        if (!fused && (rc = launch_admm_update(a, sh.s <= 16 ? 16 : (sh.s <= 32 ? 32 : 64), fuse, check, ugrid, ublk, S))) return rc;
+        if (!fused && (rc = launch_admm_update(a, admm_lps(sh), fuse, check, ugrid, ublk, S))) return rc;
         if (check) {
             PDPLQR_HIP_TRY(hipMemcpyAsync(s->active_h, s->active, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, S));
             PDPLQR_HIP_TRY(hipStreamSynchronize(S));

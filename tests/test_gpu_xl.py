@@ -5,8 +5,7 @@ lqr_kernel.hpp:80-212 restated literally) against the size-generic CPU oracle.
 
 Covers backward with and without kept factors, forward, the value function,
 backward_without_factorization, rho-penalised stages, the status of an
-indefinite stage, and the refusal of admm_solve past n + m = 64 (its update
-pass covers a stage with at most 64 lanes).  Tolerance 1e-9 relative, as the
+indefinite stage, and the ADMM loop over the serial solver (k_admm_update_xl).  Tolerance 1e-9 relative, as the
 other serial parity tests."""
 import numpy as np
 import pytest
@@ -114,15 +113,43 @@ def test_xl_indefinite_stage_sets_status(keep):
     bs.close()
 
 
-def test_xl_admm_refused():
-    from pdplqr import BatchedLQRSolver, PdplqrError
+@pytest.mark.parametrize("keep", [True, False])
+def test_xl_admm_matches_oracle(keep):
+    """The ADMM loop over the serial solver at n + m = 70 (k_admm_update_xl:
+    a wave per stage, several entries a lane) against the oracle's loop."""
+    from oracle.oracle import admm_solve as oracle_admm
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import pack_model, pack_stage_vectors
+    from pdplqr.problems import random_model
 
-    n, m, N = 50, 20, 4
-    p = _problem(n, m, N, 1, 2, 3)
-    bs = BatchedLQRSolver(n, m, N, 1, keep_factors=True, ncs=p["ncs"])
-    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"])
-    lb, ub = -np.ones_like(p["irho"]), np.ones_like(p["irho"])
-    w, y, z = p["ws"].copy(), p["ys"].copy(), p["zs"].copy()
-    with pytest.raises(PdplqrError):
-        bs.admm_solve(p["x0"], lb, ub, 1.0 / p["irho"], w, y, z, max_iter=2)
+    models, x0s = [], []
+    for b in range(2):
+        mod, x0 = random_model(50, 20, 6, seed=950 + b, nc=5, D_kind="ubox")
+        for nd in mod.nodes:
+            if nd.n_con:
+                nd.e_lb[:] = -0.3
+                nd.e_ub[:] = 0.3
+        models.append(mod)
+        x0s.append(x0)
+    pms = [pack_model(m) for m in models]
+    ncs = [int(x) for x in pms[0].ncs]
+    A = {k: np.ascontiguousarray(np.stack([getattr(p, k) for p in pms])) for k in "E c H h D".split()}
+    lb = np.stack([np.clip(pack_stage_vectors([nd.e_lb for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    ub = np.stack([np.clip(pack_stage_vectors([nd.e_ub for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    x0 = np.ascontiguousarray(np.stack(x0s))
+    g = np.random.default_rng(6)
+    W, Y = pms[0].h.size, int(sum(ncs))
+    ws, ys, zs = 0.1 * g.standard_normal((2, W)), 0.1 * g.standard_normal((2, Y)), 0.1 * g.standard_normal((2, Y))
+    rho = np.full(lb.shape, 10.0)
+    p = pms[0]
+    bs = BatchedLQRSolver(p.n, p.m, p.N, 2, keep_factors=keep, ncs=ncs)
+    bs.set_model(A["E"], A["c"], A["H"], A["h"], A["D"])
+    w, y, z = ws.copy(), ys.copy(), zs.copy()
+    info = bs.admm_solve(x0, np.ascontiguousarray(lb), np.ascontiguousarray(ub), rho, w, y, z, max_iter=15,
+                         eps_abs=0.0, eps_rel=0.0)
+    assert info["iterations"] == 15 and np.count_nonzero(bs.status()) == 0
     bs.close()
+    for b in range(2):
+        ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial",
+                                    max_iter=15, eps_abs=0.0, eps_rel=0.0)
+        assert rel_err(w[b], ow) < TOL and rel_err(y[b], oy) < TOL and rel_err(z[b], oz) < TOL, b
