@@ -125,7 +125,9 @@ int pdplqr_destroy(pdplqr_handle h);
 /* Thread-local message of the last failing call ("" if none). */
 const char *pdplqr_last_error(void);
 
-/* Stream control (hipStream_t passed as void*). NULL = the handle's own stream. */
+/* Stream control (hipStream_t passed as void*). NULL = the handle's own stream.
+   Switching makes the new stream wait (an event, no host sync) for what the
+   handle queued on the old one, e.g. set_model's upload. */
 int pdplqr_set_stream(pdplqr_handle h, void *hip_stream);
 void *pdplqr_get_stream(pdplqr_handle h);
 int pdplqr_synchronize(pdplqr_handle h);

@@ -241,6 +241,13 @@ int pdplqr_create(const pdplqr_config *cfg, pdplqr_handle *out) {
     }
     rc = solver_init(h);
     if (rc != PDPLQR_OK) goto fail;
+    // the null-stream fills of create and solver_init are complete before any
+    // (non-blocking) handle stream runs
+    if (!h->md && hipStreamSynchronize(nullptr) != hipSuccess) {
+        set_error("create: synchronize after the workspace fills failed");
+        rc = PDPLQR_ERR_HIP;
+        goto fail;
+    }
     *out = h;
     return PDPLQR_OK;
 fail:
@@ -275,7 +282,21 @@ int pdplqr_set_stream(pdplqr_handle h, void *stream) {
         set_error("set_stream: a num_devices > 1 handle runs one stream per device");
         return PDPLQR_ERR_UNSUPPORTED;
     }
-    h->stream = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
+    hipStream_t next = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
+    if (next != h->stream) {
+        // work already queued on the old stream (set_model's repack, a solve)
+        // precedes everything queued on the new one: without this a model
+        // uploaded before the switch can still be in flight when the first
+        // kernel on the new stream reads it
+        PDPLQR_HIP_TRY(hipSetDevice(h->cfg.device));
+        hipEvent_t ev;
+        PDPLQR_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, h->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(next, ev, 0);
+        (void)hipEventDestroy(ev);
+        PDPLQR_HIP_TRY(e);
+    }
+    h->stream = next;
     return PDPLQR_OK;
 }
 

@@ -74,9 +74,10 @@ struct RiccatiArgs {
     double *xl_ws = nullptr;  // 64 < n + m <= 256: per-problem workspace of kernels_xl.hip
 };
 bool xl_shape(const Shape &sh);           // 64 < n + m <= 256 (kernels_xl.hip)
-// workspace doubles per problem: V (s x n) and two s x s factor buffers
+// workspace doubles per problem: V (s x n), two s x s factor buffers and the
+// factorisation's input
 __host__ __device__ inline long long xl_ws_doubles(const Shape &sh) {
-    return (long long)sh.s * sh.n + 2LL * sh.s * sh.s;
+    return (long long)sh.s * sh.n + 3LL * sh.s * sh.s;
 }
 int launch_riccati_backward_xl(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_backward_nofact_xl(const RiccatiArgs &a, hipStream_t st);

@@ -12,15 +12,16 @@
 //         p_k = lp_x - Lxu lu
 //     with Eigen's LLT stop (a non-positive reduced pivot leaves its column
 //     and every later one at the input values, device_common.hpp
-//     chol_restore_tail; here the factorisation is left-looking, so only the
-//     failing column is restored) and the same status as every backward.
+//     chol_restore_tail; here they are copied back from the input) and the
+//     same status as every backward.
 //     Records FR_k = [L(:, 0:m) | lu'], the factor cache (packed L_k, lp_k)
 //     when it exists;
 //   * k_riccati_bwd_nofact_xl: step_without_factorization (:150-178) on the
 //     cached factors;
 //   * k_riccati_fwd_xl: forward_step (:181-212).
-// Workspace per problem (RiccatiArgs::xl_ws, xl_ws_doubles): V (s x n) and two
-// s x s factor buffers (this stage's, the next stage's), leading dimension s.
+// Workspace per problem (RiccatiArgs::xl_ws, xl_ws_doubles): V (s x n), two
+// s x s factor buffers (this stage's, the next stage's) and the factorisation's
+// input, leading dimension s.
 #include "blk_la.hpp"
 #include "parallel.hpp"
 
@@ -45,39 +46,59 @@ __device__ void xl_mm(double *C, int ldc, const double *A, int lda, bool at, con
         }
 }
 
-// In-place left-looking Cholesky of the lower triangle of A (n x n, ld) with
+// In-place right-looking Cholesky of the lower triangle of A (n x n, ld) with
 // Eigen's LLT stop: pivot j < m must be positive (else flagged and the
 // factorisation goes on, as the tiled kernels do), a pivot j >= m that is not
-// positive stops it, column j back at its input values (later columns were
-// never touched), flagged only when psd_bad.  col: n doubles of LDS scratch.
-// Returns the block-uniform status.
-__device__ bool xl_llt(double *A, int ld, int n, int m, double *col) {
+// positive stops it with column j and every later one at their input values
+// (Eigen factors left-looking, llt_inplace::unblocked, so those columns were
+// never touched there; here they are copied back from A0, the input), flagged
+// only when psd_bad.  One barrier per pivot: the trailing update with the raw
+// pivot column (a_ij a_lj / d_j) is spread over the block, and the columns are
+// scaled by 1 / sqrt(d_j) at the end (blk_chol's scheme).  sinv: n doubles of
+// LDS scratch.  Returns the block-uniform status.
+__device__ bool xl_llt(double *A, int ld, int n, int m, const double *A0, double *sinv) {
     const int tid = threadIdx.x;
     bool ok = true;
+    int jdead = n;
     for (int j = 0; j < n; ++j) {
         __syncthreads();
-        for (int i = j + tid; i < n; i += 256) {
-            const double a0 = A[i + (long long)j * ld];
-            col[i] = a0;
-            double v = a0;
-            for (int p = 0; p < j; ++p) v = __builtin_fma(-A[i + (long long)p * ld], A[j + (long long)p * ld], v);
-            A[i + (long long)j * ld] = v;
-        }
-        __syncthreads();
         const double d = A[j + (long long)j * ld];
-        const bool live = j < m || d > 0.0;
         ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
-        __syncthreads();  // every thread read the pivot
-        if (!live) {      // Eigen's stop: column j at its input values, the rest untouched
-            for (int i = j + tid; i < n; i += 256) A[i + (long long)j * ld] = col[i];
-            __syncthreads();
+        if (!(j < m || d > 0.0)) {  // block-uniform
+            jdead = j;
             break;
         }
-        const double r = sqrt(d), ir = 1.0 / r;
-        for (int i = j + tid; i < n; i += 256) A[i + (long long)j * ld] = i == j ? r : A[i + (long long)j * ld] * ir;
+        const double inv = 1.0 / d;
+        if (tid == 0) sinv[j] = rsqrt_f64(d);
+        // trailing lower triangle (i, l), j < l <= i < n, spread over the whole
+        // block (row index fastest: coalesced); the upper half of the square is skipped
+        const int r = n - j - 1;
+        for (int q = tid; q < r * r; q += 256) {
+            const int i = j + 1 + q % r, l = j + 1 + q / r;
+            if (l > i) continue;
+            A[i + (long long)l * ld] =
+                __builtin_fma(-A[i + (long long)j * ld] * inv, A[l + (long long)j * ld], A[i + (long long)l * ld]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i < j) continue;
+        if (j < jdead) A[i + (long long)j * ld] *= sinv[j];
+        else A[i + (long long)j * ld] = A0[i + (long long)j * ld];  // Eigen's stop: the input values
     }
     __syncthreads();
     return ok;
+}
+
+// dst <- src (lower triangle of an n x n block, ld)
+__device__ void xl_copy_lower(double *dst, const double *src, int ld, int n) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i >= j) dst[i + (long long)j * ld] = src[i + (long long)j * ld];
+    }
+    __syncthreads();
 }
 
 // lp (s) = h~ + E~^T (Lxx (Lxx^T c) + p): t, pb: n doubles of LDS
@@ -129,7 +150,7 @@ __device__ void xl_solve_u(double *lp, const double *L, int ld, int m, int s, do
 }
 
 __global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
-    __shared__ double col[XL_S], lp[XL_S], pv[XL_S], t[XL_S], pb[XL_S];
+    __shared__ double sinv[XL_S], lp[XL_S], pv[XL_S], t[XL_S], pb[XL_S];
     const int tid = threadIdx.x;
     const Shape &sh = A.sh;
     const int n = sh.n, m = sh.m, s = sh.s, N = sh.N, ps = sh.ps;
@@ -143,6 +164,7 @@ __global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
     double *lpb = A.lpc ? A.lpc + b * sh.perh : nullptr;
     double *W = A.xl_ws + b * xl_ws_doubles(sh);
     double *const V = W, *const L0 = W + (long long)s * n, *const L1 = L0 + (long long)s * s;
+    double *const M0 = L1 + (long long)s * s;  // the factorisation's input (Eigen's stop)
     auto Lb = [&](int k) { return (k & 1) ? L1 : L0; };
     const long long frs = (long long)s * m + m;
     int fail_stage = -1;
@@ -154,7 +176,8 @@ __global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
         const int i = q % n, j = q / n;
         LxxN[i + (long long)j * s] = i >= j ? HN[pidx(i, j, n)] : 0.0;
     }
-    if (!xl_llt(LxxN, s, n, 0, col)) fail_stage = N;
+    xl_copy_lower(M0, LxxN, s, n);
+    if (!xl_llt(LxxN, s, n, 0, M0, sinv)) fail_stage = N;
     for (int q = tid; q < n; q += 256) {
         pv[q] = hb[(long long)N * s + q];
         if (lpb) lpb[(long long)N * s + q] = pv[q];
@@ -179,7 +202,8 @@ __global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
         }
         xl_mm(Lk, s, V, s, false, V, s, true, s, s, n, Lk, s);
         xl_linear(lp, hb + (long long)k * s, Ek, cb + (long long)k * n, Lxx, s, pv, n, s, t, pb);
-        const bool ok = xl_llt(Lk, s, s, m, col);
+        xl_copy_lower(M0, Lk, s, s);
+        const bool ok = xl_llt(Lk, s, s, m, M0, sinv);
         if (!ok && fail_stage < 0) fail_stage = k;
         xl_solve_u(lp, Lk, s, m, s, pb);
         for (int q = tid; q < n; q += 256) pv[q] = lp[m + q];

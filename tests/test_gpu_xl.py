@@ -153,3 +153,37 @@ def test_xl_admm_matches_oracle(keep):
         ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial",
                                     max_iter=15, eps_abs=0.0, eps_rel=0.0)
         assert rel_err(w[b], ow) < TOL and rel_err(y[b], oy) < TOL and rel_err(z[b], oz) < TOL, b
+
+
+def test_set_stream_orders_the_model_upload():
+    """pdplqr_set_stream: work queued on the old stream (set_model's upload and
+    repack) precedes the first launch on the new one.  Before the ordering, a
+    solve switched to a fresh stream right after set_model could read a model
+    still in flight (seen as spurious failed stages at n + m = 128)."""
+    import torch
+
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch = 96, 32, 8, 64
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 31)
+    dev = torch.device("cuda", 0)
+    T = {k: torch.from_numpy(v).to(dev) for k, v in dict(E=E, c=c, H=H, h=h, x0=x0).items()}
+    ws0 = torch.zeros(batch, N * s + n, dtype=torch.float64, device=dev)
+    outs = []
+    for switch in (False, True):
+        bs = BatchedLQRSolver(n, m, N, batch, keep_factors=True)
+        bs.set_model(T["E"], T["c"], T["H"], T["h"])
+        st = torch.cuda.Stream(device=dev)
+        if switch:
+            bs.handle.set_stream(st.cuda_stream)
+        out = torch.full_like(ws0, float("nan"))
+        with torch.cuda.stream(st):
+            bs.update_problem_data(ws0, sigma=1e-6)
+            bs.backward()
+            bs.forward(T["x0"], out)
+        torch.cuda.synchronize()
+        assert np.count_nonzero(bs.status()) == 0, switch
+        outs.append(out.cpu().numpy())
+        bs.close()
+    assert np.isfinite(outs[1]).all() and np.array_equal(outs[0], outs[1])
