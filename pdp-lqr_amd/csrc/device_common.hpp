@@ -204,6 +204,14 @@ __device__ __forceinline__ double sum_row16(double v) {
 #ifndef PDPLQR_PSD_TOL
 #define PDPLQR_PSD_TOL 1e-8
 #endif
+// Bound below which the Neumann series P~ = sum_{j<8} (-rho_dyn P)^j P is used:
+// with e = rho_dyn ||P||_F (>= the spectral radius of rho_dyn P for ANY
+// symmetric P) the truncation after J terms is <= e^(J+1) / (1 - e) of ||P~||,
+// so at e <= 0.015 eight terms leave < 4e-17.  Above it P~ is formed exactly.
+#ifndef PDPLQR_KKT_NEUMANN_MAX
+#define PDPLQR_KKT_NEUMANN_MAX 0.015
+#endif
+
 __device__ __forceinline__ bool psd_bad(double v) { return !(v >= -PDPLQR_PSD_TOL && v < 1.0e300); }
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {

@@ -79,6 +79,11 @@ bool xl_shape(const Shape &sh);           // 64 < n + m <= 256 (kernels_xl.hip)
 __host__ __device__ inline long long xl_ws_doubles(const Shape &sh) {
     return (long long)sh.s * sh.n + 3LL * sh.s * sh.s;
 }
+// KKT_RIC_XL (kernels_xl.hip k_kkt_ric_bwd_xl): XA (n x s), Pt, T0 (n x n), Mb (s x s)
+__host__ __device__ inline long long kkt_xl_ws_doubles(const Shape &sh) {
+    return (long long)sh.n * sh.s + 2LL * sh.n * sh.n + (long long)sh.s * sh.s;
+}
+
 int launch_riccati_backward_xl(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_backward_nofact_xl(const RiccatiArgs &a, hipStream_t st);
 int launch_riccati_forward_xl(const Shape &sh, const double *E, const double *c, const double *FR, const double *x0,

@@ -1169,6 +1169,7 @@ struct KKTState {
     double *x0acc = nullptr;  // sum of the x0s since update_problem_data [b][n]
     double *Ef = nullptr, *Df = nullptr;  // frozen E, D once set_model re-runs (else the model's)
     double *ncache = nullptr;  // factor cache of the linear-only pass (ADMM), allocated on first use
+    double *xlw = nullptr;     // KKT_RIC_XL: per-problem workspace (kernels_xl.hip)
 };
 
 template <typename X>
@@ -1243,12 +1244,15 @@ int kkt_init(pdplqr_handle h) {
     int rc;
     ks->ric = kkt_ric_nc(sh, h->ncs, dmax <= 32);
     if (ks->ric >= 0) {  // Riccati-ordered path: no tile buffers
-        if ((rc = kalloc(h, &ks->rec, B * kkt_ric_rec_doubles(sh, ks->ric))) || (rc = kalloc(h, &ks->x0acc, B * n))) return rc;
+        if ((rc = kalloc(h, &ks->rec, B * kkt_ric_rec_doubles(sh, ks->ric))) || (rc = kalloc(h, &ks->x0acc, B * n)) ||
+            (ks->ric == KKT_RIC_XL && (rc = kalloc(h, &ks->xlw, B * kkt_xl_ws_doubles(sh)))))
+            return rc;
         PDPLQR_HIP_TRY(hipMemset(ks->x0acc, 0, B * n * sizeof(double)));
         return PDPLQR_OK;
     }
     if (dmax > 32) {
-        set_error("KKT solver with n + m > 64 is not supported by this build");
+        set_error(sh.s > 64 ? "KKT solver: n + m > 256, or more than 256 constraint rows on a stage"
+                            : "KKT solver: more than 64 constraint rows on a stage with n + m > 32");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     // P = 16 also needs stage 0's y columns beside the lambda_1 columns of G_0 (PPK)
@@ -1368,7 +1372,7 @@ int kkt_backward(pdplqr_handle h, const double *inv_rho) {
     if (ks->ric >= 0) {
         const int rc = launch_kkt_ric_backward(sh, ks->ric, ks->Ef ? ks->Ef : h->E, h->c, ks->Df ? ks->Df : h->D, h->Hw,
                                                h->hw, h->gw, inv_rho, h->d_off, h->y_off, h->ncs[sh.N], h->cfg.rho_dyn,
-                                               ks->rec, h->status, h->stream);
+                                               ks->rec, h->status, h->stream, ks->xlw);
         if (rc != PDPLQR_ERR_UNSUPPORTED) return rc;
         set_error("KKT backward: unaligned buffers for the Riccati-ordered path");
         return rc;

@@ -138,13 +138,7 @@ struct KBwdShape {
 // sum of a value over the whole wave (every lane gets it)
 __device__ __forceinline__ double wave_sum(double v) { return sum_groups(sum_row16(v)); }
 
-// Bound below which the Neumann series P~ = sum_{j<8} (-rho_dyn P)^j P is used:
-// with e = rho_dyn ||P||_F (>= the spectral radius of rho_dyn P for ANY
-// symmetric P) the truncation after J terms is <= e^(J+1) / (1 - e) of ||P~||,
-// so at e <= 0.015 eight terms leave < 4e-17.  Above it P~ is formed exactly.
-#ifndef PDPLQR_KKT_NEUMANN_MAX
-#define PDPLQR_KKT_NEUMANN_MAX 0.015
-#endif
+// PDPLQR_KKT_NEUMANN_MAX (device_common.hpp): the Neumann / exact P~ switch
 
 // Exact P~ = (I + rho_dyn P)^{-1} P of the x block (tile indices 4..15) of a
 // 16 x 16 C/D-layout tile: in-place Gauss-Jordan inversion of S = I + rho_dyn P
@@ -1190,6 +1184,11 @@ static bool kric_al(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15
 // LDS kernels where the block LDL^T tiles do not fit (n + m or n + nc_k > 32,
 // ldl_fits false) up to n + m <= 64, any ncs.
 int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs, bool ldl_fits) {
+    if (xl_shape(sh)) {
+        for (int k = 0; k <= sh.N; ++k)
+            if (ncs[k] > 256) return -1;  // the per-stage rho / g slots of k_kkt_ric_bwd_xl
+        return KKT_RIC_XL;
+    }
     if (!ldl_fits && sh.s <= 64) {
         for (int k = 0; k <= sh.N; ++k)
             if (ncs[k] > 64) return -1;  // the per-stage rho / g slots of k_kkt_ric_bwd_wide
@@ -1206,7 +1205,7 @@ int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs, bool ldl_fits) 
 }
 
 size_t kkt_ric_rec_doubles(const Shape &sh, int ric) {
-    if (ric == KKT_RIC_WIDE) return (size_t)sh.N * ((size_t)sh.s * sh.m + sh.m + sh.n + (size_t)sh.n * sh.n);
+    if (ric == KKT_RIC_WIDE || ric == KKT_RIC_XL) return (size_t)sh.N * ((size_t)sh.s * sh.m + sh.m + sh.n + (size_t)sh.n * sh.n);
     return (size_t)sh.N * KRecShape<12, 4>::FS;
 }
 
@@ -1214,6 +1213,8 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
                             int32_t *status, hipStream_t st, double *cache) {
+    if (nc == KKT_RIC_XL)
+        return launch_kkt_xl_backward(sh, E, c, D, Hw, hw, gw, irho, d_off, y_off, rho_dyn, rec, status, cache, st);
     if (nc == KKT_RIC_WIDE) {
         KKTRicArgs a;
         a.sh = sh;
@@ -1267,7 +1268,7 @@ int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const doub
     return PDPLQR_OK;
 }
 
-bool kkt_ric_rec_ehat(int ric) { return ric != KKT_RIC_WIDE; }
+bool kkt_ric_rec_ehat(int ric) { return ric == 0 || ric == 4; }
 
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric) {
     return ric == 0 || ric == 4 ? (size_t)sh.N * KKT_CF : 0;
@@ -1302,6 +1303,7 @@ int launch_kkt_ric_nofact(const Shape &sh, int nc, const double *D, const double
 
 int launch_kkt_ric_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
                            double *x0acc, double *ws, double rho_dyn, hipStream_t st, int ric, bool ehat) {
+    if (ric == KKT_RIC_XL) return launch_kkt_xl_forward(sh, E, c, rec, x0, x0acc, ws, rho_dyn, st);
     if (ric == KKT_RIC_WIDE) {
         hipLaunchKernelGGL(k_kkt_ric_fwd_wide, dim3((unsigned)sh.batch), dim3(64), 0, st, sh, E, c, rec, x0, x0acc,
                            ws, rho_dyn);

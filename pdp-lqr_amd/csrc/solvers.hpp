@@ -41,14 +41,24 @@ int kkt_before_model(pdplqr_handle h);  // set_model on a formed KKT handle: kee
 bool kkt_ric_active(pdplqr_handle h);  // the Riccati-ordered path serves this handle
 bool kkt_plain_rec_ehat(pdplqr_handle h);  // a plain KKT backward leaves the E^ record (kept in rec_gain)
 // Riccati-ordered KKT path (kkt_riccati.hip): nc of the uniform 12/4 row
-// layout, KKT_RIC_WIDE for the LDS kernels (any ncs, n + m <= 64), or -1
+// layout, KKT_RIC_WIDE for the LDS kernels (any ncs, n + m <= 64),
+// KKT_RIC_XL for the global-workspace kernels (kernels_xl.hip: 64 < n + m <= 256,
+// per-stage rows <= 256), or -1
 constexpr int KKT_RIC_WIDE = 1000;
+constexpr int KKT_RIC_XL = 1001;
+int launch_kkt_xl_backward(const Shape &sh, const double *E, const double *c, const double *D, const double *Hw,
+                           const double *hw, const double *gw, const double *irho, const int32_t *d_off,
+                           const int32_t *y_off, double rho_dyn, double *rec, int32_t *status, double *xws,
+                           hipStream_t st);
+int launch_kkt_xl_forward(const Shape &sh, const double *E, const double *c, const double *rec, const double *x0,
+                          double *x0acc, double *ws, double rho_dyn, hipStream_t st);
 int kkt_ric_nc(const Shape &sh, const std::vector<int32_t> &ncs, bool ldl_fits);
 size_t kkt_ric_rec_doubles(const Shape &sh, int ric);  // rollout record doubles per problem
 int launch_kkt_ric_backward(const Shape &sh, int nc, const double *E, const double *c, const double *D,
                             const double *Hw, const double *hw, const double *gw, const double *irho,
                             const int32_t *d_off, const int32_t *y_off, int nc_last, double rho_dyn, double *rec,
                             int32_t *status, hipStream_t st, double *cache = nullptr);
+// (KKT_RIC_XL: `cache` is the per-problem workspace, kkt_xl_ws_doubles)
 // linear-only pass on the factor cache the backward wrote (ric 0 / 4 only)
 size_t kkt_ric_cache_doubles(const Shape &sh, int ric);  // per problem; 0 where unsupported
 bool kkt_ric_rec_ehat(int ric);  // a plain backward of this path leaves the E^ record

@@ -6,7 +6,9 @@ lqr_kernel.hpp:80-212 restated literally) against the size-generic CPU oracle.
 Covers backward with and without kept factors, forward, the value function,
 backward_without_factorization, rho-penalised stages, the status of an
 indefinite stage, and the ADMM loop over the serial solver (k_admm_update_xl).  Tolerance 1e-9 relative, as the
-other serial parity tests."""
+other serial parity tests.  The KKT solver (QDLDLSolver, k_kkt_ric_bwd_xl /
+k_kkt_ric_fwd_xl) against OracleKKT's QDLDL at 1e-8, as the other KKT tests,
+on both sides of the Neumann / exact P~ switch, and its ADMM loop."""
 import numpy as np
 import pytest
 
@@ -113,6 +115,66 @@ def test_xl_indefinite_stage_sets_status(keep):
     bs.close()
 
 
+KKT_SHAPES = [(50, 15, 6, 2), (36, 64, 4, 2), (100, 28, 3, 2)]
+
+
+@pytest.mark.parametrize("n,m,N,batch", KKT_SHAPES)
+@pytest.mark.parametrize("nc", [0, 3])
+@pytest.mark.parametrize("rho_dyn", [1e-6, 0.3])
+def test_xl_kkt_matches_oracle(n, m, N, batch, nc, rho_dyn):
+    """QDLDLSolver past n + m = 64: rho_dyn 1e-6 keeps rho_dyn ||P||_F inside
+    the Neumann range, 0.3 puts every stage past it (the Cholesky of
+    I + rho_dyn P with both triangular solves)."""
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+
+    p = _problem(n, m, N, batch, nc, 7 * n + m + nc)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt", ncs=p["ncs"], rho_dyn=rho_dyn)
+    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"] if nc else None)
+    bs.update_problem_data(p["ws"], p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                           sigma=1e-6)
+    bs.backward(p["irho"] if nc else None)
+    out = np.zeros_like(p["ws"])
+    bs.forward(p["x0"], out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, p["ncs"], p["E"][b], p["c"][b], p["H"][b], p["h"][b],
+                         p["D"][b] if nc else np.zeros(0))
+        o = OracleKKT(pm, rho_dyn=rho_dyn)
+        o.update_problem_data(p["ws"][b], p["ys"][b], p["zs"][b], p["irho"][b], 1e-6)
+        o.backward(p["irho"][b])
+        assert rel_err(out[b], o.forward(p["x0"][b])) < 1e-8, b
+    bs.close()
+
+
+def test_xl_kkt_x0_accumulates():
+    """update_rhs_initial_stage accumulates -S0 x0 on every forward
+    (kkt.hpp:207-222): two forwards after one update solve with x0 + x0' and
+    report the second call's x0 in ws[0]; the oracle does the same."""
+    from oracle.oracle import OracleKKT
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch = 60, 20, 4, 2
+    p = _problem(n, m, N, batch, 0, 3)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="kkt")
+    bs.set_model(p["E"], p["c"], p["H"], p["h"])
+    bs.update_problem_data(p["ws"], sigma=1e-6)
+    bs.backward()
+    x1 = 0.5 * p["x0"]
+    out0, out1 = np.zeros_like(p["ws"]), np.zeros_like(p["ws"])
+    bs.forward(p["x0"], out0)
+    bs.forward(x1, out1)
+    for b in range(batch):
+        pm = PackedModel(n, m, N, p["ncs"], p["E"][b], p["c"][b], p["H"][b], p["h"][b], np.zeros(0))
+        o = OracleKKT(pm)
+        o.update_problem_data(p["ws"][b], None, None, None, 1e-6)
+        o.backward(None)
+        r0 = o.forward(p["x0"][b])
+        r1 = o.forward(x1[b])
+        assert rel_err(out0[b], r0) < 1e-8 and rel_err(out1[b], r1) < 1e-8, b
+    bs.close()
+
+
 @pytest.mark.parametrize("keep", [True, False])
 def test_xl_admm_matches_oracle(keep):
     """The ADMM loop over the serial solver at n + m = 70 (k_admm_update_xl:
@@ -153,6 +215,47 @@ def test_xl_admm_matches_oracle(keep):
         ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="serial",
                                     max_iter=15, eps_abs=0.0, eps_rel=0.0)
         assert rel_err(w[b], ow) < TOL and rel_err(y[b], oy) < TOL and rel_err(z[b], oz) < TOL, b
+
+
+def test_xl_kkt_admm_matches_oracle():
+    """The ADMM loop over the KKT solver at n + m = 70 (the whole backward every
+    iteration: no linear-only pass past 12/4) against the oracle's loop."""
+    from oracle.oracle import admm_solve as oracle_admm
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import pack_model, pack_stage_vectors
+    from pdplqr.problems import random_model
+
+    models, x0s = [], []
+    for b in range(2):
+        mod, x0 = random_model(50, 20, 5, seed=970 + b, nc=5, D_kind="ubox")
+        for nd in mod.nodes:
+            if nd.n_con:
+                nd.e_lb[:] = -0.3
+                nd.e_ub[:] = 0.3
+        models.append(mod)
+        x0s.append(x0)
+    pms = [pack_model(m) for m in models]
+    ncs = [int(x) for x in pms[0].ncs]
+    A = {k: np.ascontiguousarray(np.stack([getattr(p, k) for p in pms])) for k in "E c H h D".split()}
+    lb = np.stack([np.clip(pack_stage_vectors([nd.e_lb for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    ub = np.stack([np.clip(pack_stage_vectors([nd.e_ub for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    x0 = np.ascontiguousarray(np.stack(x0s))
+    g = np.random.default_rng(8)
+    W, Y = pms[0].h.size, int(sum(ncs))
+    ws, ys, zs = 0.1 * g.standard_normal((2, W)), 0.1 * g.standard_normal((2, Y)), 0.1 * g.standard_normal((2, Y))
+    rho = np.full(lb.shape, 10.0)
+    p = pms[0]
+    bs = BatchedLQRSolver(p.n, p.m, p.N, 2, solver="kkt", ncs=ncs)
+    bs.set_model(A["E"], A["c"], A["H"], A["h"], A["D"])
+    w, y, z = ws.copy(), ys.copy(), zs.copy()
+    info = bs.admm_solve(x0, np.ascontiguousarray(lb), np.ascontiguousarray(ub), rho, w, y, z, max_iter=12,
+                         eps_abs=0.0, eps_rel=0.0)
+    assert info["iterations"] == 12 and np.count_nonzero(bs.status()) == 0
+    bs.close()
+    for b in range(2):
+        ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="kkt",
+                                    max_iter=12, eps_abs=0.0, eps_rel=0.0)
+        assert rel_err(w[b], ow) < 1e-8 and rel_err(y[b], oy) < 1e-8 and rel_err(z[b], oz) < 1e-8, b
 
 
 def test_set_stream_orders_the_model_upload():
