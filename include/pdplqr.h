@@ -113,10 +113,10 @@ typedef struct {
  * nx + nu <= 64 for every solver: up to 32 on MFMA tiles in one wavefront,
  * 33..64 on register tiles or LDS-resident stage matrices, one 256-thread
  * block per problem / segment / element (kernels_big.hip, kernels_wide.hip);
- * KKT rows per stage <= 64 past the block LDL^T tiles.  The SERIAL and KKT
- * solvers go on to nx + nu <= 256 (kernels_xl.hip: global-memory stage
- * matrices; every protocol call and pdplqr_admm_solve; KKT rows per stage
- * <= 256 there).  pdplqr_create returns
+ * KKT rows per stage <= 64 past the block LDL^T tiles.  Every solver goes
+ * on to nx + nu <= 256 (kernels_xl.hip, kernels_xl_par.hip: global-memory
+ * stage and element matrices; every protocol call, pdplqr_admm_solve and the
+ * horizon-shard calls; KKT rows per stage <= 256 there).  pdplqr_create returns
  * PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 

@@ -89,7 +89,7 @@ static void model_destroy(orc_model *md) {
 /* Dense helpers (Eigen semantics)                                          */
 /* ------------------------------------------------------------------------ */
 
-/* Largest stage size of the serial restatement (the parallel one keeps 64). */
+/* Largest stage size of the restatement. */
 #define ORC_SMAX 256
 
 /* Eigen llt_inplace<Lower>::unblocked (Eigen/src/Cholesky/LLT.h), used by
@@ -431,7 +431,7 @@ static void pk_step(const orc_model *md, int k, const double *rho, const orc_sta
     int n = md->n, m = md->m, s = n + m, i, j, t;
     const double *E = md->E + (size_t)k * n * s;
     const double *c = md->c + (size_t)k * n;
-    double tmp[64 * 64], ftmp[64];
+    double *tmp, ftmp[ORC_SMAX];
     if (fact) k_step_fact(md, k, rho, nx_, st);
     else k_step_nofact(md, k, rho, nx_, st);
     if (last) return;
@@ -450,16 +450,17 @@ static void pk_step(const orc_model *md, int k, const double *rho, const orc_sta
         st->f[i] = a + nx_->f[i];
     }
     if (!fact) return;
+    tmp = (double *)xcalloc((size_t)n * n, sizeof(double));
     /* K = -Luu^{-T} Lxu^T (:105,107) ; K is m x n */
     for (j = 0; j < n; ++j) {
-        double col[64];
+        double col[ORC_SMAX];
         for (i = 0; i < m; ++i) col[i] = -st->L[IX(m + j, i, s)];
         trsv_lower_t(st->L, s, m, col);
         for (i = 0; i < m; ++i) st->K[IX(i, j, m)] = col[i];
     }
     /* G = -Luu^{-1} B^T F_next^T (:126-128) ; G is m x n */
     for (j = 0; j < n; ++j) {
-        double col[64];
+        double col[ORC_SMAX];
         for (i = 0; i < m; ++i) {
             double a = 0.0;
             for (t = 0; t < n; ++t) a += E[IX(t, i, n)] * nx_->F[IX(j, t, n)];
@@ -488,6 +489,7 @@ static void pk_step(const orc_model *md, int k, const double *rho, const orc_sta
             for (t = 0; t < m; ++t) a += st->G[IX(t, i, m)] * st->G[IX(t, j, m)];
             st->C[IX(i, j, n)] = nx_->C[IX(i, j, n)] + a;
         }
+    free(tmp);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -629,7 +631,7 @@ static int cond_lu_backward(orc_condensed *cs) {
         memcpy(g->LU, g->PC, sizeof(double) * n * n);
         lu_factor(g->LU, g->piv, n);
         for (j = 0; j < n; ++j) {
-            double col[64];
+            double col[ORC_SMAX];
             for (a = 0; a < n; ++a) col[a] = g->A[IX(a, j, n)];
             lu_solve(g->LU, g->piv, n, col);
             for (a = 0; a < n; ++a) g->D[IX(a, j, n)] = col[a];
@@ -647,7 +649,7 @@ static int cond_lu_backward(orc_condensed *cs) {
 /* CondensedSystemLUSolver::forward (condensed_system.hpp:105-138) */
 static void cond_lu_forward(orc_condensed *cs, const double *x0) {
     int n = cs->n, i, a, t;
-    double cbar[64];
+    double cbar[ORC_SMAX];
     for (i = cs->ns - 2; i >= 0; --i) {
         orc_cseg *g = &cs->seg[i], *nx_ = &cs->seg[i + 1];
         for (a = 0; a < n; ++a) {
@@ -691,7 +693,7 @@ static int chol_inv_step(orc_condensed *cs, int i) {
     orc_cseg *g = &cs->seg[i], *nx_ = &cs->seg[i + 1];
     if (llt_lower(nx_->P, nx_->Lp, n) >= 0) return 0;
     for (j = 0; j < n; ++j) {
-        double col[64];
+        double col[ORC_SMAX];
         for (a = 0; a < n; ++a) col[a] = nx_->Pinv[IX(a, j, n)];
         llt_solve(nx_->Lp, n, col);
         for (a = 0; a < n; ++a) nx_->Pinv[IX(a, j, n)] = col[a];
@@ -708,7 +710,7 @@ static int cond_chol_backward(orc_condensed *cs) {
         orc_cseg *g = &cs->seg[i];
         if (!chol_inv_step(cs, i)) return 0;
         for (j = 0; j < n; ++j) { /* A_i <- C_i^{-1} A_i */
-            double col[64];
+            double col[ORC_SMAX];
             for (a = 0; a < n; ++a) col[a] = g->A[IX(a, j, n)];
             llt_solve(g->Lc, n, col);
             for (a = 0; a < n; ++a) g->A[IX(a, j, n)] = col[a];
@@ -789,7 +791,7 @@ void *orc_parallel_create(int n, int m, int N, const int *nc, const double *E, c
                           const double *h, const double *D, int ns, int load_balancing, int type) {
     orc_parallel *o;
     int i, k;
-    if (N < 1 || ns < 1 || n < 1 || m < 1 || n + m > 64) return NULL;
+    if (N < 1 || ns < 1 || n < 1 || m < 1 || n + m > ORC_SMAX) return NULL; /* s <= 256 here */
     if (type == 1 && ns < 2) return NULL; /* CHOLESKY with ns=1 reads out of bounds (condensed_system.hpp:230) */
     o = (orc_parallel *)xcalloc(1, sizeof(orc_parallel));
     o->md = model_create(n, m, N, nc, E, c, H, h, D);
@@ -920,7 +922,7 @@ void orc_parallel_forward(void *p, const double *x0, double *ws) { /* :213-238 *
         memcpy(ws + (size_t)N0 * s + m, o->cs->seg[i].xhat, sizeof(double) * n);
         for (k = N0; k < N1; ++k) {
             orc_stage *st = &o->data[i][k - N0];
-            double Gu[64];
+            double Gu[ORC_SMAX];
             if (!last)
                 for (a = 0; a < m; ++a) {
                     double acc = 0.0;

@@ -179,8 +179,9 @@ __global__ __launch_bounds__(64) void k_seg_bwd_nofact(SegArgs A) {
 }
 
 int launch_seg_backward_nofact(const SegArgs &a, hipStream_t st) {
+    if (xl_shape(a.sh)) return launch_seg_backward_nofact_xl(a, st);
     if (a.sh.s > 64 || !a.Lc) {
-        set_error("PARALLEL backward_without_factorization needs keep_factors = 1 and n + m <= 64");
+        set_error("PARALLEL backward_without_factorization needs keep_factors = 1");
         return PDPLQR_ERR_UNSUPPORTED;
     }
     if (a.sh.s <= 32) hipLaunchKernelGGL(k_seg_bwd_nofact<32>, dim3((unsigned)(a.sh.batch * a.S)), dim3(64), 0, st, a);
@@ -850,6 +851,7 @@ bool seg_scan_mw(int n, bool lu, int mw) {
 
 // Resident scan combines the device holds for this shape.
 int seg_scan_slots(const Shape &sh, int device) {
+    if (xl_state(sh.n)) return xl_par_slots(device);
     if (wide_state(sh.n)) return wide_scan_slots(sh.n, device);
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
@@ -885,6 +887,7 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
+    if (xl_state(a.n)) return launch_seg_scan_xl(a, batch, st);
     if (wide_state(a.n)) {
         if (a.sk) return PDPLQR_ERR_UNSUPPORTED;  // the wide combine reads its operands from HBM
         return launch_seg_scan_wide(a, batch, st);
@@ -911,6 +914,7 @@ int launch_seg_scan(const ScanArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
+    if (xl_state(a.n)) return launch_seg_maps_xl(a, batch, st);
     if (wide_state(a.n)) return launch_seg_maps_wide(a, batch, st);
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
@@ -935,6 +939,7 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st) {
 }
 
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
+    if (xl_state(a.n)) return launch_map_scan_xl(a, batch, st);
     if (wide_state(a.n)) {
         static_assert(PDPLQR_MAP_RADIX == 4, "k_map_scan_wide composes radix-4 rounds");
         return launch_map_scan_wide(a, batch, st);
@@ -1103,8 +1108,11 @@ __global__ __launch_bounds__(64) void k_rank_chain(const double *maps, const dou
 }
 
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
-                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st) {
+                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st, double *xlw,
+                          int xl_grid) {
     if (r <= 0) return PDPLQR_OK;
+    if (xl_state(n))
+        return launch_rank_fold_maps_xl(elems, suf, x0, R, r, n, batch, maps, out_pre, flag, lu, xlw, xl_grid, st);
     if (wide_state(n)) return launch_rank_fold_maps_wide(elems, suf, x0, R, r, n, batch, maps, out_pre, flag, lu, st);
     const int T = tile_order(n);
     const dim3 gm(batch * r), blk(64);

@@ -1333,6 +1333,7 @@ int launch_riccati_forward(const Shape &sh, const double *E, const double *c, co
 
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st) {
+    if (xl_shape(sh)) return launch_riccati_forward_seg_xl(sh, E, c, FR, sf, ws, st);
     if (sh.n == 24 && sh.m == 8 && segfwd_aligned(sh, E, c, FR, sf)) {
         hipLaunchKernelGGL((k_seg_fwd_dma<24, 8, 3>), dim3((unsigned)(sh.batch * sf.S)), dim3(64), 0, st, sh, E, c,
                            FR, ws, sf);

@@ -860,6 +860,7 @@ static const void *aug_kernel(const Shape &sh) {
 static bool aug_mw(const Shape &sh) { return sh.mw && sh.n == 24 && sh.m == 8; }
 
 int seg_backward_slots(const Shape &sh, int device) {
+    if (xl_shape(sh)) return xl_par_slots(device);
     if (wide_stage(sh)) return wide_seg_backward_slots(sh, device);
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
@@ -874,6 +875,7 @@ int seg_backward_slots(const Shape &sh, int device) {
 }
 
 int launch_seg_backward(const SegArgs &a, hipStream_t st) {
+    if (xl_shape(a.sh)) return launch_seg_backward_xl(a, st);
     if (wide_stage(a.sh)) return launch_seg_backward_wide(a, st);
     if (aug_mw(a.sh) && a.sh.N >= 1) {
         hipLaunchKernelGGL((k_seg_bwd_aug_mw<24, 8>), dim3((unsigned)(a.sh.batch * a.S)), dim3(256), 0, st, a);

@@ -19,6 +19,8 @@ struct SegArgs {
                                // no element, status per problem (seg_start / seg_len unused)
     int *flag = nullptr;       // [b] the scans' / maps' failure flag: zeroed by segment 0's block
                                // (the later kernels of the solve set it; no memset launch)
+    double *xlw = nullptr;     // n + m > 64 (kernels_xl_par.hip): xl_grid workspace slots of
+    int xl_grid = 0;           // xl_par_slot_doubles each, the blocks striding over the items
 };
 
 struct ScanArgs {
@@ -38,6 +40,8 @@ struct ScanArgs {
     // entry i in the lower half of its 2 dist block combines with the first
     // entry j of the upper half, which already holds [j, j + dist - 1].
     int sk = 0;
+    double *xlw = nullptr;     // n > 64: workspace slots (SegArgs::xlw)
+    int xl_grid = 0;
 };
 
 // Blocks per problem of one scan round.
@@ -76,6 +80,8 @@ struct MapArgs {
     int *flag;
     int lu = 0;                // LU form of the combine
     int mw = 1;                // the 4-wave kernels may run (Shape::mw)
+    double *xlw = nullptr;     // n > 64: workspace slots (SegArgs::xlw)
+    int xl_grid = 0;
 };
 
 struct MapScanArgs {
@@ -84,6 +90,8 @@ struct MapScanArgs {
     double *out;
     const double *vfun;
     double *xhat, *lam;
+    double *xlw = nullptr;     // n > 64: workspace slots (SegArgs::xlw)
+    int xl_grid = 0;
 };
 
 // Rank fold of a horizon shard as two pairwise reduction trees over the
@@ -167,7 +175,8 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, bool lu, hipStream_t st);
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
-                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st);
+                          double *maps, double *out_pre, int *flag, bool lu, hipStream_t st, double *xlw = nullptr,
+                          int xl_grid = 0);
 int launch_rank_tree(const RankTreeArgs &a, int batch, hipStream_t st);
 // wide shapes (kernels_wide.hip): 32 < n + m <= 64 stage kernels, 32 < n element kernels
 bool wide_state(int n);
@@ -185,5 +194,28 @@ int launch_riccati_forward_seg_big(const Shape &sh, const double *E, const doubl
                                    const SegFwd &sf, double *ws, hipStream_t st);
 int launch_riccati_forward_seg(const Shape &sh, const double *E, const double *c, const double *FR, const SegFwd &sf,
                                double *ws, hipStream_t st);
+// n + m > 64 stage kernels, n > 64 element kernels (kernels_xl_par.hip): global
+// workspace slots, each block striding over the items
+__host__ __device__ inline bool xl_state(int n) { return n > 64; }
+// doubles of one workspace slot: the stage kernels' P, F, C (n x n), P E~, F E~
+// (n x s), M (s x s); the element kernels' five n x n buffers
+__host__ __device__ inline long long xl_par_slot_doubles(const Shape &sh) {
+    const long long n = sh.n, s = sh.s;
+    long long d = 0;
+    if (sh.s > 64) d = 3 * n * n + 2 * n * s + s * s;
+    if (sh.n > 64) d = d > 5 * n * n ? d : 5 * n * n;
+    return d;
+}
+int xl_par_slots(int device);  // workspace slots (blocks) of the XL parallel kernels
+int launch_seg_backward_xl(const SegArgs &a, hipStream_t st);
+int launch_seg_backward_nofact_xl(const SegArgs &a, hipStream_t st);
+int launch_seg_scan_xl(const ScanArgs &a, int batch, hipStream_t st);
+int launch_seg_maps_xl(const MapArgs &a, int batch, hipStream_t st);
+int launch_map_scan_xl(const MapScanArgs &a, int batch, hipStream_t st);
+int launch_rank_fold_maps_xl(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,
+                             double *maps, double *out_pre, int *flag, bool lu, double *xlw, int xl_grid,
+                             hipStream_t st);
+int launch_riccati_forward_seg_xl(const Shape &sh, const double *E, const double *c, const double *FR,
+                                  const SegFwd &sf, double *ws, hipStream_t st);
 
 }  // namespace pdplqr

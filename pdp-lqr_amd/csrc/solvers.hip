@@ -27,6 +27,7 @@ struct ParallelState {
     double *mapA = nullptr, *mapB = nullptr, *vfun = nullptr;  // boundary maps (ping-pong), value functions
     const double *suf_final = nullptr;
     int *flag = nullptr;
+    int xl_grid = 0;  // n + m > 64 or n > 64: workspace slots in h->xl_ws (kernels_xl_par.hip)
     // horizon shards
     double *left = nullptr, *right = nullptr, *gathered = nullptr;
     int gathered_cap = 0;
@@ -86,7 +87,7 @@ static bool scan_sklansky(const Shape &sh);
 static int parallel_init(pdplqr_handle h) {
     h->sh.mw = 1;
     const Shape &sh = h->sh;
-    if (sh.s > 64) return unsupported("PARALLEL solver with n + m > 64");
+    if (sh.s > 256) return unsupported("PARALLEL solver with n + m > 256");
     ParallelState *ps = new ParallelState();
     h->par = ps;
     const int ns = h->cfg.num_segments;
@@ -207,6 +208,10 @@ static int parallel_init(pdplqr_handle h) {
         (rc = palloc(h, &ps->left, B * es)) || (rc = palloc(h, &ps->right, B * es)) ||
         (rc = palloc(h, &ps->has_suf, 1)))
         return rc;
+    if (xl_shape(sh) || xl_state(sh.n)) {  // the XL kernels' workspace slots
+        ps->xl_grid = xl_par_slots(h->cfg.device);
+        if ((rc = palloc(h, &h->xl_ws, (long long)ps->xl_grid * xl_par_slot_doubles(sh)))) return rc;
+    }
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_start, ps->seg_start_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemcpy(ps->seg_len, ps->seg_len_h.data(), S * sizeof(int32_t), hipMemcpyHostToDevice));
     PDPLQR_HIP_TRY(hipMemset(ps->flag, 0, B * sizeof(int)));
@@ -222,7 +227,7 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal);
 // round, same depth) on the shapes whose combine kernels stage their operands
 // before storing (n <= 32) and that do not take the two-round k_seg_scan4
 // launches (n <= 16: radix-4 Hillis-Steele).
-static bool scan_sklansky(const Shape &sh) { return !wide_state(sh.n) && !seg_scan4_supported(sh.n); }
+static bool scan_sklansky(const Shape &sh) { return sh.n <= 32 && !seg_scan4_supported(sh.n); }
 void graph_release(pdplqr_handle h);
 
 static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = true) {
@@ -245,6 +250,8 @@ static int parallel_backward(pdplqr_handle h, int last_is_terminal, bool fact = 
     a.elem = ps->elem;
     a.seg_status = ps->seg_status;
     a.flag = ps->flag;  // reset by the segment backward itself
+    a.xlw = h->xl_ws;
+    a.xl_grid = ps->xl_grid;
     int rc = fact ? launch_seg_backward(a, h->stream) : launch_seg_backward_nofact(a, h->stream);
     if (rc) return rc;
     return parallel_scans(h, last_is_terminal);
@@ -273,6 +280,8 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
             s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
             s.mw = sh.mw;
             s.sk = d == 1 ? 1 : 2;
+            s.xlw = h->xl_ws;
+            s.xl_grid = ps->xl_grid;
             int rc = launch_seg_scan(s, sh.batch, h->stream);
             if (rc) return rc;
         }
@@ -291,6 +300,8 @@ static int parallel_scans(pdplqr_handle h, int last_is_terminal) {
         s.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
         s.scratch = ps->scan4;
         s.mw = sh.mw;
+        s.xlw = h->xl_ws;
+        s.xl_grid = ps->xl_grid;
         int rc = r4 ? launch_seg_scan4(s, sh.batch, h->stream) : launch_seg_scan(s, sh.batch, h->stream);
         if (rc) return rc;
         sin = s.out;
@@ -321,6 +332,8 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     ma.flag = ps->flag;
     ma.lu = h->cfg.condensed_type == PDPLQR_CONDENSED_LU;
     ma.mw = sh.mw;
+    ma.xlw = h->xl_ws;
+    ma.xl_grid = ps->xl_grid;
     int rc = launch_seg_maps(ma, sh.batch, h->stream);
     if (rc) return rc;
     double *mb[2] = {ps->mapA, ps->mapB};
@@ -335,6 +348,8 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
         ms.vfun = ps->vfun;
         ms.xhat = ps->xhat;
         ms.lam = ps->lam;
+        ms.xlw = h->xl_ws;
+        ms.xl_grid = ps->xl_grid;
         if ((rc = launch_map_scan(ms, sh.batch, h->stream))) return rc;
     }
     SegFwd sf;
@@ -720,7 +735,7 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
         use_tree = use_tree && f[0] == 't';
         use_scan = R > 1 && f[0] == 's';
     }
-    if (wide_state(sh.n)) use_scan = R > 1;  // the n > 32 element kernels fold by the scan form only
+    if (sh.n > 32) use_scan = R > 1;  // the n > 32 element kernels fold by the scan form only
     int rc;
     const double *left = nullptr, *right = nullptr;
     long long rstride = 0;
@@ -776,6 +791,8 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
             sa.out = ps->rscan[round & 1];
             sa.flag = ps->flag;
             sa.lu = lu;
+            sa.xlw = h->xl_ws;
+            sa.xl_grid = ps->xl_grid;
             if ((rc = launch_seg_scan(sa, sh.batch, h->stream))) return rc;
             sin = sa.out;
         }
@@ -785,7 +802,8 @@ int pdplqr_shard_forward(pdplqr_handle h, const double *x0, const double *elems_
         }
         if (r > 0) {
             if ((rc = launch_rank_fold_maps(delems, sin, dx0, R, r, sh.n, sh.batch, ps->rmaps, ps->left, ps->flag,
-                                            h->cfg.condensed_type == PDPLQR_CONDENSED_LU, h->stream)))
+                                            h->cfg.condensed_type == PDPLQR_CONDENSED_LU, h->stream, h->xl_ws,
+                                            ps->xl_grid)))
                 return rc;
             left = ps->left;
         }

@@ -1,0 +1,223 @@
+// xl_la.hpp -- block-wide (256-thread) linear algebra on global-memory
+// matrices of order up to 256 (the size-generic kernels_xl*.hip paths): the
+// products by blk_mm on 64 x 64 output blocks, one barrier per pivot for the
+// factorisations and triangular solves.  Every routine is bracketed by
+// barriers, as blk_la.hpp's.
+#pragma once
+#include "blk_la.hpp"
+
+namespace pdplqr {
+
+constexpr int XL_S = 256;  // largest n + m of the XL paths
+
+// C (M x N, ld ldc) = alpha A B + diag I + add over 64 x 64 output blocks
+// (blk_mm per block; C must not alias A or B, add may be C itself)
+__device__ __noinline__ void xl_mm(double *C, int ldc, const double *A, int lda, bool at, const double *B, int ldb,
+                                   bool bt, int M, int N, int K, const double *add, int ldadd, double alpha = 1.0,
+                                   double diag = 0.0) {
+    for (int j0 = 0; j0 < N; j0 += 64)
+        for (int i0 = 0; i0 < M; i0 += 64) {
+            const Mv av = at ? mv_t(A + (long long)i0 * lda, lda) : mv_n(A + i0, lda);
+            const Mv bv = bt ? mv_t(B + j0, ldb) : mv_n(B + (long long)j0 * ldb, ldb);
+            const Mv dv = add ? mv_n(add + i0 + (long long)j0 * ldadd, ldadd) : mv_none();
+            blk_mm(C + i0 + (long long)j0 * ldc, ldc, av, bv, min(64, M - i0), min(64, N - j0), K, alpha,
+                   i0 == j0 ? diag : 0.0, dv, false);
+        }
+}
+
+// In-place right-looking Cholesky of the lower triangle of A (n x n, ld) with
+// Eigen's LLT stop: pivot j < m must be positive (else flagged and the
+// factorisation goes on, as the tiled kernels do), a pivot j >= m that is not
+// positive stops it with column j and every later one at their input values
+// (Eigen factors left-looking, llt_inplace::unblocked, so those columns were
+// never touched there; here they are copied back from A0, the input), flagged
+// only when psd_bad.  One barrier per pivot: the trailing update with the raw
+// pivot column (a_ij a_lj / d_j) is spread over the block, and the columns are
+// scaled by 1 / sqrt(d_j) at the end (blk_chol's scheme).  sinv: n doubles of
+// LDS scratch.  Returns the block-uniform status.
+__device__ __noinline__ bool xl_llt(double *A, int ld, int n, int m, const double *A0, double *sinv) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    int jdead = n;
+    for (int j = 0; j < n; ++j) {
+        __syncthreads();
+        const double d = A[j + (long long)j * ld];
+        ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
+        if (!(j < m || d > 0.0)) {  // block-uniform
+            jdead = j;
+            break;
+        }
+        const double inv = 1.0 / d;
+        if (tid == 0) sinv[j] = rsqrt_f64(d);
+        // trailing lower triangle (i, l), j < l <= i < n, spread over the whole
+        // block (row index fastest: coalesced); the upper half of the square is skipped
+        const int r = n - j - 1;
+        for (int q = tid; q < r * r; q += 256) {
+            const int i = j + 1 + q % r, l = j + 1 + q / r;
+            if (l > i) continue;
+            A[i + (long long)l * ld] =
+                __builtin_fma(-A[i + (long long)j * ld] * inv, A[l + (long long)j * ld], A[i + (long long)l * ld]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i < j) continue;
+        if (j < jdead) A[i + (long long)j * ld] *= sinv[j];
+        else A[i + (long long)j * ld] = A0[i + (long long)j * ld];  // Eigen's stop: the input values
+    }
+    __syncthreads();
+    return ok;
+}
+
+// dst <- src (lower triangle of an n x n block, ld)
+__device__ __noinline__ void xl_copy_lower(double *dst, const double *src, int ld, int n) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i >= j) dst[i + (long long)j * ld] = src[i + (long long)j * ld];
+    }
+    __syncthreads();
+}
+
+// B (n x nb, ld ldb) <- L^{-1} B, L lower (ld): one barrier per pivot, the
+// row updates spread over the block with the unscaled pivot row, the rows
+// scaled at the end
+__device__ __noinline__ void xl_fsub(const double *L, int ld, int n, double *B, int ldb, int nb) {
+    const int tid = threadIdx.x;
+    for (int j = 0; j < n; ++j) {
+        __syncthreads();
+        const double inv = 1.0 / L[j + (long long)j * ld];
+        const int r = n - j - 1;
+        for (int q = tid; q < r * nb; q += 256) {
+            const int i = j + 1 + q % r, c = q / r;
+            B[i + (long long)c * ldb] =
+                __builtin_fma(-L[i + (long long)j * ld], B[j + (long long)c * ldb] * inv, B[i + (long long)c * ldb]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * nb; q += 256) {
+        const int i = q % n, c = q / n;
+        B[i + (long long)c * ldb] /= L[i + (long long)i * ld];
+    }
+    __syncthreads();
+}
+
+// B <- L^{-T} B (back substitution on L^T), the same scheme
+__device__ __noinline__ void xl_bsub_t(const double *L, int ld, int n, double *B, int ldb, int nb) {
+    const int tid = threadIdx.x;
+    for (int j = n - 1; j >= 0; --j) {
+        __syncthreads();
+        const double inv = 1.0 / L[j + (long long)j * ld];
+        for (int q = tid; q < j * nb; q += 256) {
+            const int i = q % j, c = q / j;
+            B[i + (long long)c * ldb] =
+                __builtin_fma(-L[j + (long long)i * ld], B[j + (long long)c * ldb] * inv, B[i + (long long)c * ldb]);
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n * nb; q += 256) {
+        const int i = q % n, c = q / n;
+        B[i + (long long)c * ldb] /= L[i + (long long)i * ld];
+    }
+    __syncthreads();
+}
+
+__device__ __noinline__ double xl_block_sum(double f, double *s_red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = f;
+    __syncthreads();
+    return (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// lu <- Luu^{-1} lu (rows < m of lp), then p = lp_x - Lxu lu into pn (n) and
+// lp's x rows.  L (s x s, ld s).
+__device__ __noinline__ void xl_solve_u(double *lp, const double *L, int ld, int m, int s, double *pn) {
+    const int tid = threadIdx.x;
+    for (int i = 0; i < m; ++i) {  // forward substitution, one row per barrier
+        __syncthreads();
+        if (tid == 0) {
+            double v = lp[i];
+            for (int j = 0; j < i; ++j) v = __builtin_fma(-L[i + (long long)j * ld], lp[j], v);
+            lp[i] = v / L[i + (long long)i * ld];
+        }
+    }
+    __syncthreads();
+    for (int r = tid; r < s - m; r += 256) {
+        double a = lp[m + r];
+        for (int j = 0; j < m; ++j) a = __builtin_fma(-L[(m + r) + (long long)j * ld], lp[j], a);
+        pn[r] = a;
+    }
+    __syncthreads();
+    for (int r = tid; r < s - m; r += 256) lp[m + r] = pn[r];
+    __syncthreads();
+}
+
+// In-place Cholesky with every pivot required positive (m = n; flagged
+// otherwise) and zeros above the diagonal, blk_chol's output form for orders
+// past 64
+__device__ __noinline__ bool xl_chol(double *A, int ld, int n, double *sinv) {
+    const bool ok = xl_llt(A, ld, n, n, A, sinv);
+    for (int q = threadIdx.x; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i < j) A[i + (long long)j * ld] = 0.0;
+    }
+    __syncthreads();
+    return ok;
+}
+
+// blk_gauss_jordan for n <= 256: W = [A | R] (n x ncol, ld n) with partial
+// (row) pivoting, the same pivot choice (largest |a| among the unused rows,
+// lowest row on ties; thread i owns row i in the search), kept in place: row
+// piv[k] of the right part holds row k of A^{-1} R on return.  prow: ncol,
+// mul: n doubles, piv: n ints, red: 8 doubles + 8 ints of LDS scratch.
+__device__ __noinline__ bool xl_gauss_jordan(double *W, int n, int *piv, double *prow, double *mul, int ncol,
+                                             double *rv, int *ra) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    bool used = false, ok = true;  // thread tid: row tid
+    for (int k = 0; k < n; ++k) {
+        __syncthreads();
+        double v = (tid < n && !used) ? fabs(W[tid + (long long)k * n]) : -1.0;
+        int arg = tid;
+#pragma unroll
+        for (int mk = 1; mk < 64; mk <<= 1) {
+            const double ov = shfl_xor_f64(v, mk);
+            const int oa = __shfl_xor(arg, mk, 64);
+            if (ov > v || (ov == v && oa < arg)) {
+                v = ov;
+                arg = oa;
+            }
+        }
+        if (lane == 0) {
+            rv[wv] = v;
+            ra[wv] = arg;
+        }
+        __syncthreads();
+        double bv = rv[0];
+        int ba = ra[0];
+        for (int w = 1; w < 4; ++w)
+            if (rv[w] > bv || (rv[w] == bv && ra[w] < ba)) {
+                bv = rv[w];
+                ba = ra[w];
+            }
+        used = used || (tid == ba);
+        if (tid == 0) piv[k] = ba;
+        const int p = ba;
+        const double pv = W[p + (long long)k * n];
+        ok = ok && pv != 0.0 && fabs(pv) <= 1.7976931348623157e308;
+        const double inv = 1.0 / pv;
+        for (int j = tid; j < ncol; j += 256) prow[j] = W[p + (long long)j * n];
+        for (int i = tid; i < n; i += 256) mul[i] = W[i + (long long)k * n] * inv;
+        __syncthreads();
+        for (int q = tid; q < ncol * n; q += 256) {
+            const int i = q % n, j = q / n;
+            W[q] = (i == p) ? prow[j] * inv : __builtin_fma(-mul[i], prow[j], W[q]);
+        }
+    }
+    __syncthreads();
+    return ok;
+}
+
+}  // namespace pdplqr

@@ -169,16 +169,12 @@ def test_big_admm_serial_matches_oracle():
 
 def test_big_shape_limits():
     """32 < n + m <= 64 runs on every solver (kernels_big.hip, kernels_wide.hip;
-    tests/test_gpu_wide.py); 64 < n + m <= 256 on the serial and KKT solvers
-    (kernels_xl.hip, tests/test_gpu_xl.py); past that every solver refuses."""
+    tests/test_gpu_wide.py); 64 < n + m <= 256 as well (kernels_xl.hip,
+    kernels_xl_par.hip, tests/test_gpu_xl.py); past that every solver refuses."""
     from pdplqr import BatchedLQRSolver, PdplqrError
 
     for solver in ("serial", "parallel", "kkt"):
         BatchedLQRSolver(30, 10, 8, 1, solver=solver, num_segments=2).close()
         with pytest.raises(PdplqrError):
             BatchedLQRSolver(200, 57, 4, 1, solver=solver, num_segments=2)
-        if solver in ("serial", "kkt"):
-            BatchedLQRSolver(50, 15, 4, 1, solver=solver).close()
-        else:
-            with pytest.raises(PdplqrError):
-                BatchedLQRSolver(50, 15, 4, 1, solver=solver, num_segments=2)
+        BatchedLQRSolver(50, 15, 4, 1, solver=solver, num_segments=2).close()

@@ -8,7 +8,10 @@ backward_without_factorization, rho-penalised stages, the status of an
 indefinite stage, and the ADMM loop over the serial solver (k_admm_update_xl).  Tolerance 1e-9 relative, as the
 other serial parity tests.  The KKT solver (QDLDLSolver, k_kkt_ric_bwd_xl /
 k_kkt_ric_fwd_xl) against OracleKKT's QDLDL at 1e-8, as the other KKT tests,
-on both sides of the Neumann / exact P~ switch, and its ADMM loop."""
+on both sides of the Neumann / exact P~ switch, and its ADMM loop.  The
+PARALLEL solver (kernels_xl_par.hip: stage kernels past n + m = 64, element
+kernels past n = 64) against OracleParallel and OracleSerial at 1e-9, both
+condensed forms, backward_without_factorization and horizon shards."""
 import numpy as np
 import pytest
 
@@ -290,3 +293,62 @@ def test_set_stream_orders_the_model_upload():
         outs.append(out.cpu().numpy())
         bs.close()
     assert np.isfinite(outs[1]).all() and np.array_equal(outs[0], outs[1])
+
+
+# (n, m, N, batch): element kernels on tiles (n = 20), LDS (n = 50) and the XL
+# workspace (n = 80, 100); stage kernels XL throughout
+PAR_SHAPES = [(20, 60, 16, 2), (50, 15, 16, 2), (80, 20, 12, 2), (100, 28, 10, 1)]
+
+
+@pytest.mark.parametrize("n,m,N,batch", PAR_SHAPES)
+@pytest.mark.parametrize("condensed", ["CHOLESKY", "LU"])
+@pytest.mark.parametrize("ns,seglen", [(3, 0), (2, 2)])
+@pytest.mark.parametrize("nc", [0, 3])
+def test_xl_parallel_matches_oracle(n, m, N, batch, condensed, ns, seglen, nc):
+    from oracle.oracle import OracleParallel
+    from pdplqr import BatchedLQRSolver
+
+    p = _problem(n, m, N, batch, nc, 5 * n + m + nc + ns)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=ns, keep_factors=True, condensed=condensed,
+                          segment_len=seglen, ncs=p["ncs"])
+    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"] if nc else None)
+    rho = (1.0 / p["irho"]) if nc else None
+    bs.update_problem_data(p["ws"], p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                           sigma=1e-6)
+    bs.backward(rho)
+    out = np.zeros_like(p["ws"])
+    bs.forward(p["x0"], out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        _, ref = _oracle(p, b, n, m, N)
+        assert rel_err(out[b], ref) < TOL, b
+        pm = PackedModel(n, m, N, p["ncs"], p["E"][b], p["c"][b], p["H"][b], p["h"][b],
+                         p["D"][b] if nc else np.zeros(0))
+        o = OracleParallel(pm, ns, True, condensed)
+        o.update_problem_data(p["ws"][b], p["ys"][b] if nc else None, p["zs"][b] if nc else None,
+                              p["irho"][b] if nc else None, 1e-6)
+        o.backward(rho[b] if nc else None)
+        assert rel_err(out[b], o.forward(p["x0"][b])) < TOL, b
+    # backward_without_factorization (lqr_solver_parallel.hpp:148-154): new linear data
+    ws1 = p["ws"] + 0.2 * np.random.default_rng(n).standard_normal(p["ws"].shape)
+    bs.update_problem_data(ws1, p["ys"] if nc else None, p["zs"] if nc else None, p["irho"] if nc else None,
+                           sigma=1e-6)
+    bs.backward_without_factorization(rho)
+    out1 = np.zeros_like(out)
+    bs.forward(p["x0"], out1)
+    for b in range(batch):
+        _, ref1 = _oracle(p, b, n, m, N, ws=ws1[b])
+        assert rel_err(out1[b], ref1) < TOL, b
+    bs.close()
+
+
+@pytest.mark.parametrize("n,m,N,batch,R,seglen", [(70, 20, 24, 2, 3, 3), (40, 30, 20, 1, 4, 2)])
+def test_xl_horizon_shards_match_oracle(n, m, N, batch, R, seglen):
+    """Horizon shards (pdplqr_shard_backward / shard_forward) past n + m = 64:
+    virtual ranks in one process against the serial oracle (the rank fold by
+    the scan form, k_rank_maps_xl for n > 64)."""
+    from test_gpu_horizon import _run_virtual
+
+    got, ref = _run_virtual(n, m, N, batch, R, seglen)
+    for b in range(batch):
+        assert rel_err(got[b], ref[b]) < TOL, b
