@@ -83,6 +83,10 @@ __global__ __launch_bounds__(256) void k_riccati_bwd_xl(RiccatiArgs A) {
     }
     xl_copy_lower(M0, LxxN, s, n);
     if (!xl_llt(LxxN, s, n, 0, M0, sinv)) fail_stage = N;
+    for (int q = tid; q < n * n; q += 256) {  // V reads Lxx as a full matrix: zeros above the diagonal
+        const int i = q % n, j = q / n;
+        if (i < j) LxxN[i + (long long)j * s] = 0.0;
+    }
     for (int q = tid; q < n; q += 256) {
         pv[q] = hb[(long long)N * s + q];
         if (lpb) lpb[(long long)N * s + q] = pv[q];

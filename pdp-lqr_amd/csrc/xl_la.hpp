@@ -11,12 +11,14 @@ namespace pdplqr {
 constexpr int XL_S = 256;  // largest n + m of the XL paths
 
 // C (M x N, ld ldc) = alpha A B + diag I + add over 64 x 64 output blocks
-// (blk_mm per block; C must not alias A or B, add may be C itself)
+// (blk_mm per block; C must not alias A or B, add may be C itself).
+// lower_blocks: only the blocks on or below the block diagonal (a symmetric
+// update of which only the lower triangle is read)
 __device__ __noinline__ void xl_mm(double *C, int ldc, const double *A, int lda, bool at, const double *B, int ldb,
                                    bool bt, int M, int N, int K, const double *add, int ldadd, double alpha = 1.0,
-                                   double diag = 0.0) {
+                                   double diag = 0.0, bool lower_blocks = false) {
     for (int j0 = 0; j0 < N; j0 += 64)
-        for (int i0 = 0; i0 < M; i0 += 64) {
+        for (int i0 = lower_blocks ? j0 : 0; i0 < M; i0 += 64) {
             const Mv av = at ? mv_t(A + (long long)i0 * lda, lda) : mv_n(A + i0, lda);
             const Mv bv = bt ? mv_t(B + j0, ldb) : mv_n(B + (long long)j0 * ldb, ldb);
             const Mv dv = add ? mv_n(add + i0 + (long long)j0 * ldadd, ldadd) : mv_none();
@@ -25,48 +27,72 @@ __device__ __noinline__ void xl_mm(double *C, int ldc, const double *A, int lda,
         }
 }
 
-// In-place right-looking Cholesky of the lower triangle of A (n x n, ld) with
-// Eigen's LLT stop: pivot j < m must be positive (else flagged and the
+constexpr int XL_PW = 16;  // panel width of xl_llt
+
+// In-place blocked right-looking Cholesky of the lower triangle of A (n x n,
+// ld) with Eigen's LLT stop: pivot j < m must be positive (else flagged and the
 // factorisation goes on, as the tiled kernels do), a pivot j >= m that is not
 // positive stops it with column j and every later one at their input values
 // (Eigen factors left-looking, llt_inplace::unblocked, so those columns were
 // never touched there; here they are copied back from A0, the input), flagged
-// only when psd_bad.  One barrier per pivot: the trailing update with the raw
-// pivot column (a_ij a_lj / d_j) is spread over the block, and the columns are
-// scaled by 1 / sqrt(d_j) at the end (blk_chol's scheme).  sinv: n doubles of
-// LDS scratch.  Returns the block-uniform status.
+// only when psd_bad.  Per panel of XL_PW columns: the panel (every row below
+// its top) is factored in LDS, one barrier per pivot (the update with the raw
+// pivot column a_ij a_lj / d_j, the columns scaled when written back), then
+// the trailing lower triangle takes the panel's rank-XL_PW update on MFMA
+// (xl_mm, lower blocks).  Entries above the diagonal may be overwritten.
+// sinv: n doubles of LDS scratch.  Returns the block-uniform status.
 __device__ __noinline__ bool xl_llt(double *A, int ld, int n, int m, const double *A0, double *sinv) {
+    __shared__ double pan[XL_S * XL_PW];
     const int tid = threadIdx.x;
     bool ok = true;
     int jdead = n;
-    for (int j = 0; j < n; ++j) {
+    for (int j0 = 0; j0 < n; j0 += XL_PW) {
+        const int w = min(XL_PW, n - j0), rows = n - j0;
         __syncthreads();
-        const double d = A[j + (long long)j * ld];
-        ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
-        if (!(j < m || d > 0.0)) {  // block-uniform
-            jdead = j;
-            break;
+        for (int q = tid; q < rows * w; q += 256) {
+            const int i = q % rows, l = q / rows;
+            if (i >= l) pan[i + l * XL_S] = A[(j0 + i) + (long long)(j0 + l) * ld];
         }
-        const double inv = 1.0 / d;
-        if (tid == 0) sinv[j] = rsqrt_f64(d);
-        // trailing lower triangle (i, l), j < l <= i < n, spread over the whole
-        // block (row index fastest: coalesced); the upper half of the square is skipped
-        const int r = n - j - 1;
-        for (int q = tid; q < r * r; q += 256) {
-            const int i = j + 1 + q % r, l = j + 1 + q / r;
-            if (l > i) continue;
-            A[i + (long long)l * ld] =
-                __builtin_fma(-A[i + (long long)j * ld] * inv, A[l + (long long)j * ld], A[i + (long long)l * ld]);
+        int wl = w;  // live columns of the panel
+        for (int jj = 0; jj < w; ++jj) {
+            __syncthreads();
+            const int j = j0 + jj;
+            const double d = pan[jj + jj * XL_S];
+            ok = ok && (j < m ? d > 0.0 : !psd_bad(d));
+            if (!(j < m || d > 0.0)) {  // block-uniform
+                jdead = j;
+                wl = jj;
+                break;
+            }
+            const double inv = 1.0 / d;
+            if (tid == 0) sinv[j] = rsqrt_f64(d);
+            const int r = rows - jj - 1, c = w - jj - 1;  // rows below the pivot, panel columns right of it
+            for (int q = tid; q < r * c; q += 256) {
+                const int i = jj + 1 + q % r, l = jj + 1 + q / r;
+                if (l > i) continue;
+                pan[i + l * XL_S] = __builtin_fma(-pan[i + jj * XL_S] * inv, pan[l + jj * XL_S], pan[i + l * XL_S]);
+            }
+        }
+        __syncthreads();
+        for (int q = tid; q < rows * wl; q += 256) {
+            const int i = q % rows, l = q / rows;
+            if (i >= l) A[(j0 + i) + (long long)(j0 + l) * ld] = pan[i + l * XL_S] * sinv[j0 + l];
+        }
+        if (jdead < n) break;  // block-uniform
+        const int t = j0 + w;
+        if (t < n) {  // trailing update A(t:, t:) -= L(t:, j0:t) L(t:, j0:t)^T
+            double *Lp = A + t + (long long)j0 * ld, *Ct = A + t + (long long)t * ld;
+            xl_mm(Ct, ld, Lp, ld, false, Lp, ld, true, n - t, n - t, w, Ct, ld, -1.0, 0.0, true);
         }
     }
     __syncthreads();
-    for (int q = tid; q < n * n; q += 256) {
-        const int i = q % n, j = q / n;
-        if (i < j) continue;
-        if (j < jdead) A[i + (long long)j * ld] *= sinv[j];
-        else A[i + (long long)j * ld] = A0[i + (long long)j * ld];  // Eigen's stop: the input values
+    if (jdead < n) {  // Eigen's stop: the input values from column jdead on
+        for (int q = tid; q < n * n; q += 256) {
+            const int i = q % n, j = q / n;
+            if (i >= j && j >= jdead) A[i + (long long)j * ld] = A0[i + (long long)j * ld];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     return ok;
 }
 
@@ -132,26 +158,21 @@ __device__ __noinline__ double xl_block_sum(double f, double *s_red) {
     return (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
-// lu <- Luu^{-1} lu (rows < m of lp), then p = lp_x - Lxu lu into pn (n) and
-// lp's x rows.  L (s x s, ld s).
+// lu <- Luu^{-1} lu (rows < m of lp) and p = lp_x - Lxu lu (lp's x rows), L
+// (s x s, ld): column-oriented forward substitution, one barrier per pivot --
+// step j subtracts L(i, j) lu_j from every row below j (lp[j] itself is final
+// before step j and divided by L(j, j) at the end), the same operation order
+// per row as a row-by-row substitution.  pn: unused (kept for the callers).
 __device__ __noinline__ void xl_solve_u(double *lp, const double *L, int ld, int m, int s, double *pn) {
     const int tid = threadIdx.x;
-    for (int i = 0; i < m; ++i) {  // forward substitution, one row per barrier
+    (void)pn;
+    for (int j = 0; j < m; ++j) {
         __syncthreads();
-        if (tid == 0) {
-            double v = lp[i];
-            for (int j = 0; j < i; ++j) v = __builtin_fma(-L[i + (long long)j * ld], lp[j], v);
-            lp[i] = v / L[i + (long long)i * ld];
-        }
+        const double xj = lp[j] / L[j + (long long)j * ld];
+        for (int i = j + 1 + tid; i < s; i += 256) lp[i] = __builtin_fma(-L[i + (long long)j * ld], xj, lp[i]);
     }
     __syncthreads();
-    for (int r = tid; r < s - m; r += 256) {
-        double a = lp[m + r];
-        for (int j = 0; j < m; ++j) a = __builtin_fma(-L[(m + r) + (long long)j * ld], lp[j], a);
-        pn[r] = a;
-    }
-    __syncthreads();
-    for (int r = tid; r < s - m; r += 256) lp[m + r] = pn[r];
+    for (int j = tid; j < m; j += 256) lp[j] /= L[j + (long long)j * ld];
     __syncthreads();
 }
 
