@@ -352,3 +352,76 @@ def test_xl_horizon_shards_match_oracle(n, m, N, batch, R, seglen):
     got, ref = _run_virtual(n, m, N, batch, R, seglen)
     for b in range(batch):
         assert rel_err(got[b], ref[b]) < TOL, b
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_xl_multidev_matches_oracle(devices):
+    """A num_devices split past n + m = 64 (n = 70: the rank maps on the XL
+    element kernels): factorising backward, then backward_without_factorization
+    on new linear data, against the serial oracle."""
+    from pdplqr import BatchedLQRSolver
+
+    n, m, N, batch, nc = 70, 20, 18, 2, 3
+    p = _problem(n, m, N, batch, nc, 41)
+    rho = 1.0 / p["irho"]
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=2, keep_factors=True, ncs=p["ncs"],
+                          devices=devices)
+    bs.set_model(p["E"], p["c"], p["H"], p["h"], p["D"])
+    bs.update_problem_data(p["ws"], p["ys"], p["zs"], p["irho"], sigma=1e-6)
+    bs.backward(rho)
+    out = np.zeros_like(p["ws"])
+    bs.forward(p["x0"], out)
+    assert np.all(bs.status() == 0)
+    for b in range(batch):
+        assert rel_err(out[b], _oracle(p, b, n, m, N)[1]) < TOL, b
+    ws1 = p["ws"] + 0.2 * np.random.default_rng(3).standard_normal(p["ws"].shape)
+    bs.update_problem_data(ws1, p["ys"], p["zs"], p["irho"], sigma=1e-6)
+    bs.backward_without_factorization(rho)
+    out1 = np.zeros_like(out)
+    bs.forward(p["x0"], out1)
+    for b in range(batch):
+        assert rel_err(out1[b], _oracle(p, b, n, m, N, ws=ws1[b])[1]) < TOL, b
+    bs.close()
+
+
+def test_xl_parallel_admm_matches_oracle():
+    """The ADMM loop over the PARALLEL solver at n + m = 70 (segment kernels on
+    the XL workspace, backward_without_factorization from iteration 2 on)
+    against the oracle's loop over its parallel restatement."""
+    from oracle.oracle import admm_solve as oracle_admm
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import pack_model, pack_stage_vectors
+    from pdplqr.problems import random_model
+
+    models, x0s = [], []
+    for b in range(2):
+        mod, x0 = random_model(50, 20, 12, seed=990 + b, nc=5, D_kind="ubox")
+        for nd in mod.nodes:
+            if nd.n_con:
+                nd.e_lb[:] = -0.3
+                nd.e_ub[:] = 0.3
+        models.append(mod)
+        x0s.append(x0)
+    pms = [pack_model(m) for m in models]
+    ncs = [int(x) for x in pms[0].ncs]
+    A = {k: np.ascontiguousarray(np.stack([getattr(p, k) for p in pms])) for k in "E c H h D".split()}
+    lb = np.stack([np.clip(pack_stage_vectors([nd.e_lb for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    ub = np.stack([np.clip(pack_stage_vectors([nd.e_ub for nd in m.nodes], ncs), -1e20, 1e20) for m in models])
+    x0 = np.ascontiguousarray(np.stack(x0s))
+    g = np.random.default_rng(12)
+    W, Y = pms[0].h.size, int(sum(ncs))
+    ws, ys, zs = 0.1 * g.standard_normal((2, W)), 0.1 * g.standard_normal((2, Y)), 0.1 * g.standard_normal((2, Y))
+    rho = np.full(lb.shape, 10.0)
+    p = pms[0]
+    bs = BatchedLQRSolver(p.n, p.m, p.N, 2, solver="parallel", num_segments=3, condensed="CHOLESKY",
+                          keep_factors=True, ncs=ncs)
+    bs.set_model(A["E"], A["c"], A["H"], A["h"], A["D"])
+    w, y, z = ws.copy(), ys.copy(), zs.copy()
+    info = bs.admm_solve(x0, np.ascontiguousarray(lb), np.ascontiguousarray(ub), rho, w, y, z, max_iter=12,
+                         eps_abs=0.0, eps_rel=0.0)
+    assert info["iterations"] == 12 and np.count_nonzero(bs.status()) == 0
+    bs.close()
+    for b in range(2):
+        ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="parallel",
+                                    num_segments=3, condensed="CHOLESKY", max_iter=12, eps_abs=0.0, eps_rel=0.0)
+        assert rel_err(w[b], ow) < TOL and rel_err(y[b], oy) < TOL and rel_err(z[b], oz) < TOL, b
