@@ -93,16 +93,19 @@ __device__ __forceinline__ void big_in_load(BigIn &in, const double *Ek, const d
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        const int i = tid + q * BT;
-        in.E[q] = i < n * s ? Ek[i] : 0.0;
+        const int i = tid + q * BT, ic = i < n * s ? i : n * s - 1;  // unconditional load (clamped, then a select):
+        const double v = Ek[ic];                                          // a guarded load is an exec-mask region with its own wait
+        in.E[q] = i < n * s ? v : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
-        const int i = tid + q * BT;
-        in.H[q] = i < ps ? Hk[i] : 0.0;
+        const int i = tid + q * BT, ic = i < ps ? i : ps - 1;
+        const double v = Hk[ic];
+        in.H[q] = i < ps ? v : 0.0;
     }
-    in.c = tid < n ? ck[tid] : 0.0;
-    in.h = tid < s ? hk[tid] : 0.0;
+    const double cvl = ck[tid < n ? tid : n - 1], hvl = hk[tid < s ? tid : s - 1];
+    in.c = tid < n ? cvl : 0.0;
+    in.h = tid < s ? hvl : 0.0;
 }
 
 // E~ into Es (ld BLD), H~ packed into Hs, c, h~

@@ -398,16 +398,19 @@ __device__ __forceinline__ void wide_in_load(WideIn &in, const double *Ek, const
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        const int i = tid + q * BLK_THREADS;
-        in.E[q] = i < n * s ? Ek[i] : 0.0;
+        const int i = tid + q * BLK_THREADS, ic = i < n * s ? i : n * s - 1;  // unconditional load (clamped, then a select):
+        const double v = Ek[ic];                                          // a guarded load is an exec-mask region with its own wait
+        in.E[q] = i < n * s ? v : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
-        const int i = tid + q * BLK_THREADS;
-        in.H[q] = i < ps ? Hk[i] : 0.0;
+        const int i = tid + q * BLK_THREADS, ic = i < ps ? i : ps - 1;
+        const double v = Hk[ic];
+        in.H[q] = i < ps ? v : 0.0;
     }
-    in.c = tid < n ? ck[tid] : 0.0;
-    in.h = tid < s ? hk[tid] : 0.0;
+    const double cvl = ck[tid < n ? tid : n - 1], hvl = hk[tid < s ? tid : s - 1];
+    in.c = tid < n ? cvl : 0.0;
+    in.h = tid < s ? hvl : 0.0;
 }
 
 __device__ __forceinline__ void wide_in_store(const WideIn &in, double *Es, double *Hs, double *cv, double *hv, int n,
@@ -426,6 +429,21 @@ __device__ __forceinline__ void wide_in_store(const WideIn &in, double *Es, doub
     if (tid < n) cv[tid] = in.c;
     if (tid < s) hv[tid] = in.h;
 }
+
+#if PDPLQR_SEGW_PROFILE
+__device__ unsigned long long g_segw[16];
+#define SEGW_T(ph)                                                              \
+    {                                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+        segw_acc[ph] += t_ - segw_prev;                                         \
+        segw_prev = t_;                                                         \
+    }
+extern "C" int pdplqr_debug_segw(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_segw), sizeof(g_segw)) == hipSuccess ? 0 : -2;
+}
+#else
+#define SEGW_T(ph)
+#endif
 
 __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     extern __shared__ __attribute__((aligned(16))) double wbuf[];
@@ -453,6 +471,9 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
            *fy = vec + 5 * VL, *lp = vec + 6 * VL, *sinv = vec + 7 * VL;
     __shared__ int s_bad;
     int fail_stage = -1;
+#if PDPLQR_SEGW_PROFILE
+    unsigned long long segw_prev = __builtin_amdgcn_s_memtime(), segw_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     WideIn nxt;
     if (N1 > N0)  // stage N1 - 1's inputs, in flight during the terminal
         wide_in_load(nxt, Eb + (long long)(N1 - 1) * n * s, Hb + (long long)(N1 - 1) * ps, cb + (long long)(N1 - 1) * n,
@@ -489,22 +510,28 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     const bool yon = !last;  // the y block (F, C, f) is identically zero on the last segment
     for (int k = N1 - 1; k >= N0; --k) {
         // Mb = E~_k, Hs = H~_k (packed), cv = c_k, hv = h~_k (written at the end of stage k + 1)
+        SEGW_T(8);
         blk_mv(pc, mv_n(XA, n), cv, n, n, 1.0, pv);  // P c + p
         if (tid == 0) s_bad = 0;  // every thread has read the previous stage's flag (blk_mv's barrier)
         if (yon) blk_mv(fy, mv_n(Fp, n), cv, n, n, 1.0, fv);  // F c + f
+        SEGW_T(0);
         blk_mm(XA, n, mv_n(XA, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // P E~
         if (yon) blk_mm(XB, n, mv_n(Fp, n), mv_n(Mb, n), n, s, n, 1.0, 0.0, mv_none(), false);  // F E~
+        SEGW_T(1);
         blk_mv(lp, mv_t(Mb, n), pc, s, n, 1.0, hv);  // h~ + E~^T (P c + p)
+        SEGW_T(2);
         blk_mm(Mb, s, mv_t(Mb, n), mv_n(XA, n), s, s, n, 1.0, 0.0, mv_pk(Hs, s), true);
         // stage k - 1's inputs in flight during the pivots
+        SEGW_T(3);
         if (k > N0)
             wide_in_load(nxt, Eb + (long long)(k - 1) * n * s, Hb + (long long)(k - 1) * ps, cb + (long long)(k - 1) * n,
                          hb + (long long)(k - 1) * s, n, s, ps);
         // ---- eliminate the u pivots of [[M, YE^T], [YE, -C]] (one barrier per pivot) ----
         double *FRk = FRb + (long long)k * frs;
         double *Gk = Gb + (long long)k * m * n;
-        const int rr = tid & 127, hh = tid >> 7;
+        const int ri = tid & 63, cg = tid >> 6;  // row, column group (s, n <= 64)
         bool ok = true;
+        SEGW_T(4);
         for (int j = 0; j < m; ++j) {
             const double d = Mb[j + j * s];
             ok = ok && d > 0.0;
@@ -517,22 +544,21 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
                 FRk[(long long)s * m + j] = lpj * invs;
                 sinv[j] = invs;
             }
-            if (rr < s) {
-                const int i = rr;
-                if (i > j) {
-                    const double lij = Mb[i + j * s] * inv2;
-                    for (int l = j + 1 + hh; l <= i; l += 2) Mb[i + l * s] = __builtin_fma(-lij, Mb[l + j * s], Mb[i + l * s]);
-                    if (hh == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
-                }
-            } else if (yon && rr < s + n) {
-                const int r = rr - s;
-                const double yrj = XB[r + j * n] * inv2;
-                for (int l = j + 1 + hh; l < s; l += 2) XB[r + l * n] = __builtin_fma(-yrj, Mb[l + j * s], XB[r + l * n]);
-                for (int q = hh; q <= r; q += 2) Cm[r + q * n] = __builtin_fma(yrj, XB[q + j * n], Cm[r + q * n]);
-                if (hh == 0) fy[r] = __builtin_fma(-yrj, lpj, fy[r]);
+            // row ri, columns l = cg (mod 4): M's trailing rows, then the y block's
+            if (ri > j && ri < s) {
+                const double lij = Mb[ri + j * s] * inv2;
+                lds_axpy_strided(Mb + ri, s, Mb + j * s, lij, j + 1 + cg, ri, 4);
+                if (cg == 0) lp[ri] = __builtin_fma(-lij, lpj, lp[ri]);
+            }
+            if (yon && ri < n) {
+                const double yrj = XB[ri + j * n] * inv2;
+                lds_axpy_strided(XB + ri, n, Mb + j * s, yrj, j + 1 + cg, s - 1, 4);
+                lds_axpy_strided(Cm + ri, n, XB + j * n, -yrj, cg, ri, 4);
+                if (cg == 0) fy[ri] = __builtin_fma(-yrj, lpj, fy[ri]);
             }
             __syncthreads();
         }
+        SEGW_T(5);
         // ---- P_k (lower block, symmetric by construction), p_k, f_k; F_k stays in XB at column m ----
         for (int q = tid; q < n * n; q += BLK_THREADS) {
             const int i = q % n, j = q / n;
@@ -550,13 +576,19 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         if (yon)
             for (int q = tid; q < n; q += BLK_THREADS) fv[q] = fy[q];
         Fp = XB + m * n;
+        SEGW_T(6);
         if (k > N0) {
             __syncthreads();  // every read of M is done
             wide_in_store(nxt, Mb, Hs, cv, hv, n, s, ps);
         }
         __syncthreads();
+        SEGW_T(7);
         if ((!ok || s_bad) && fail_stage < 0) fail_stage = k;
     }
+#if PDPLQR_SEGW_PROFILE
+    if (blockIdx.x == 0 && tid == 0)
+        for (int q = 0; q < 9; ++q) g_segw[q] = segw_acc[q];
+#endif
     if (A.serial) {
         if (tid == 0) A.seg_status[bi] = fail_stage < 0 ? 0 : fail_stage + 1;
         return;
