@@ -382,8 +382,11 @@ int launch_rank_fold_maps_wide(const double *elems, const double *suf, const dou
 // LDS: XA (n x s: P, then P E~), XB (n x s: F at column offset 0 or m, then
 // F E~), Mb (s x s: E~, then the stage matrix), Cm (n x n), vectors.
 // ---------------------------------------------------------------------------
-static size_t wide_seg_smem_bytes(int n, int s) {
-    return (size_t)(2 * n * s + s * s + n * n + s * (s + 1) / 2 + 8 * VL) * sizeof(double);
+// serial (the value-form serial backward, SegArgs::serial): no y block (XB,
+// Cm), so more blocks fit a CU (50/10: 115 -> 71 KB, two blocks a CU)
+static size_t wide_seg_smem_bytes(int n, int s, bool serial = false) {
+    return (size_t)((serial ? 1 : 2) * n * s + s * s + (serial ? 0 : n * n) + s * (s + 1) / 2 + 8 * VL) *
+           sizeof(double);
 }
 
 // Stage inputs of stage k in flight in registers (issued before the pivot
@@ -465,8 +468,11 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
     double *Gb = A.G ? A.G + bi * (long long)sh.N * m * n : nullptr;
     double *Lcb = A.Lc ? A.Lc + bi * sh.perHw : nullptr;
     double *lpb = A.lpc ? A.lpc + bi * sh.perh : nullptr;
-    double *XA = wbuf, *XB = XA + n * s, *Mb = XB + n * s, *Cm = Mb + s * s, *Hs = Cm + n * n,
-           *vec = Hs + s * (s + 1) / 2;
+    const bool ser = A.serial != 0;  // no y block (wide_seg_smem_bytes)
+    double *XA = wbuf, *XB = ser ? nullptr : XA + n * s;
+    double *Mb = ser ? XA + n * s : XB + n * s;
+    double *Cm = ser ? nullptr : Mb + s * s;
+    double *Hs = ser ? Mb + s * s : Cm + n * n, *vec = Hs + s * (s + 1) / 2;
     double *pv = vec, *fv = vec + VL, *cv = vec + 2 * VL, *hv = vec + 3 * VL, *pc = vec + 4 * VL,
            *fy = vec + 5 * VL, *lp = vec + 6 * VL, *sinv = vec + 7 * VL;
     __shared__ int s_bad;
@@ -487,8 +493,10 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         for (int q = tid; q < n * n; q += BLK_THREADS) {
             const int i = q % n, j = q / n;
             XA[q] = last ? HN[i >= j ? pidx(i, j, n) : pidx(j, i, n)] : 0.0;
-            XB[q] = (!last && i == j) ? 1.0 : 0.0;
-            Cm[q] = 0.0;
+            if (!ser) {
+                XB[q] = (!last && i == j) ? 1.0 : 0.0;
+                Cm[q] = 0.0;
+            }
             if (last && i == j && psd_bad(XA[q])) s_bad = 1;
         }
         for (int q = tid; q < n; q += BLK_THREADS) {
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         }
         if (yon)
             for (int q = tid; q < n; q += BLK_THREADS) fv[q] = fy[q];
-        Fp = XB + m * n;
+        if (yon) Fp = XB + m * n;
         SEGW_T(6);
         if (k > N0) {
             __syncthreads();  // every read of M is done
@@ -660,7 +668,7 @@ int launch_riccati_backward_value_wide(const RiccatiArgs &r, hipStream_t st) {
     a.elem = nullptr;
     a.seg_status = r.status;
     a.serial = 1;
-    const size_t sm = wide_seg_smem_bytes(a.sh.n, a.sh.s);
+    const size_t sm = wide_seg_smem_bytes(a.sh.n, a.sh.s, true);
     if (!wide_attr_set(reinterpret_cast<const void *>(&k_seg_bwd_wide), sm)) {
         set_error("backward (n + m > 32): LDS request too large");
         return PDPLQR_ERR_UNSUPPORTED;
