@@ -115,11 +115,23 @@ __device__ __noinline__ void blk_mm(double *C, int ldc, Mv A, Mv B, int M, int N
     __syncthreads();
 }
 
-// y (M) = alpha A x + add (vectors in LDS or global; y must not alias x)
+// y (M) = alpha A x + add (vectors in LDS or global; y must not alias x).
+// M <= 64: the rows on the lanes and K split over the four waves (k = w mod 4),
+// the partial sums added through LDS -- a quarter of the dependent chain of one
+// row per thread
 __device__ __noinline__ void blk_mv(double *y, Mv A, const double *x, int M, int K, double alpha, const double *add) {
+    __shared__ double part[4][64];
     const int tid = threadIdx.x;
     __syncthreads();
-    if (tid < M) {
+    if (M <= 64) {
+        const int i = tid & 63, w = tid >> 6;
+        double a = 0.0;
+        if (i < M)
+            for (int k = w; k < K; k += 4) a = __builtin_fma(A.at(i, k), x[k], a);
+        part[w][i] = a;
+        __syncthreads();
+        if (tid < M) y[tid] = alpha * ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid])) + (add ? add[tid] : 0.0);
+    } else if (tid < M) {
         double a = 0.0;
         for (int k = 0; k < K; ++k) a = __builtin_fma(A.at(tid, k), x[k], a);
         y[tid] = alpha * a + (add ? add[tid] : 0.0);
