@@ -189,8 +189,8 @@ __device__ __noinline__ bool blk_chol(double *M, int ld, int n, int m, double *s
         const int i = ri;
         if (live && i > j && i < n) {  // live: block-uniform
             const double lij = M[i + j * ld] * inv2;
-            for (int l = j + 1 + cg; l <= i; l += 4) M[i + l * ld] = __builtin_fma(-lij, M[l + j * ld], M[i + l * ld]);
-            for (int l = cg; l < nb; l += 4) B[i + l * ldb] = __builtin_fma(-lij, B[j + l * ldb], B[i + l * ldb]);
+            lds_axpy_strided(M + i, ld, M + j * ld, lij, j + 1 + cg, i, 4);  // loads before stores, four at a time
+            if (nb > 0) lds_axpy_strided(B + i, ldb, B + j, lij, cg, nb - 1, 4, ldb);
         }
     }
     __syncthreads();

@@ -217,20 +217,20 @@ __device__ __forceinline__ double sum_row16(double v) {
 // of one LDS array may alias as far as the compiler knows, so written one at a
 // time each waits for the previous store (two LDS round trips per entry).
 __device__ __forceinline__ void lds_axpy_strided(double *dst, int ldc, const double *src, double f, int l0, int lend,
-                                                 int st) {
+                                                 int st, int lds = 1) {
     constexpr int G = 4;
     int l = l0;
     for (; l + (G - 1) * st <= lend; l += G * st) {
         double sv[G], dv[G];
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-            sv[u] = src[l + u * st];
+            sv[u] = src[(l + u * st) * lds];
             dv[u] = dst[(l + u * st) * ldc];
         }
 #pragma unroll
         for (int u = 0; u < G; ++u) dst[(l + u * st) * ldc] = __builtin_fma(-f, sv[u], dv[u]);
     }
-    for (; l <= lend; l += st) dst[l * ldc] = __builtin_fma(-f, src[l], dst[l * ldc]);
+    for (; l <= lend; l += st) dst[l * ldc] = __builtin_fma(-f, src[l * lds], dst[l * ldc]);
 }
 
 __device__ __forceinline__ bool psd_bad(double v) { return !(v >= -PDPLQR_PSD_TOL && v < 1.0e300); }

@@ -55,7 +55,7 @@ __device__ __forceinline__ bool chol_big(double *M, double *sinv, int j0, int j1
         const int i = ri;
         if (i > j && i < j1) {
             const double lij = M[i + j * BLD] * inv2;
-            for (int l = j + 1 + cg; l <= i; l += 4) M[i + l * BLD] = __builtin_fma(-lij, M[l + j * BLD], M[i + l * BLD]);
+            lds_axpy_strided(M + i, BLD, M + j * BLD, lij, j + 1 + cg, i, 4);  // loads before stores, four at a time
         }
     }
     __syncthreads();

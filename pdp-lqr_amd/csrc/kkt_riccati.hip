@@ -1092,11 +1092,11 @@ __global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
             const double lpj = lp[j];
             if (tid < s) Rk[j * s + tid] = tid >= j ? Mb[tid + j * s] * invs : 0.0;
             if (tid == 255) Rk[s * m + j] = lpj * invs;
-            const int i = tid & 127, hh = tid >> 7;
+            const int i = tid & 63, cg = tid >> 6;  // row, column group (s <= 64; k_seg_bwd_wide's scheme)
             if (i > j && i < s) {
                 const double lij = Mb[i + j * s] * inv2;
-                for (int l = j + 1 + hh; l <= i; l += 2) Mb[i + l * s] = __builtin_fma(-lij, Mb[l + j * s], Mb[i + l * s]);
-                if (hh == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
+                lds_axpy_strided(Mb + i, s, Mb + j * s, lij, j + 1 + cg, i, 4);
+                if (cg == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
             }
             __syncthreads();
         }

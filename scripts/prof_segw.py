@@ -35,8 +35,9 @@ def main():
     torch.cuda.synchronize()
     out = (ctypes.c_ulonglong * 16)()
     _lib.lib().pdplqr_debug_segw(out)
-    names = ["blk_mm PE", "blk_mv lp", "blk_mm M", "issue next loads", "pivots", "P_k out", "store next",
-             "loop tail", "blk_mv pc"]
+    # g_segw[i]: the time up to marker i (kernels_wide.hip SEGW_T)
+    names = ["blk_mv pc", "blk_mm PE", "blk_mv lp", "blk_mm M", "issue next loads", "pivots", "P_k out",
+             "store next + tail", "loop head"]
     tot = sum(out[i] for i in range(9))
     print(f"{n}/{m}: backward {t0.elapsed_time(t1):.3f} ms; block 0 stage-loop s_memtime ticks {tot} "
           f"({tot / N:.0f} per stage)")
