@@ -55,7 +55,14 @@ __device__ __forceinline__ int mv_off(int i, int j, int si, int sj, int ld) {
 // kind is hoisted out of the loop (a runtime switch per element cost a scalar
 // branch per load) and the loads are branch-free (clamped indices and a
 // select: a guarded load compiles to an exec-mask region with its own wait).
-template <bool PA, bool PB>
+// LDS pointer of a generic one known to address LDS (ds_read instead of the
+// flat path, which takes the vector-memory pipeline and both wait counters)
+typedef const __attribute__((address_space(3))) double *lds_cptr;
+__device__ __forceinline__ bool in_lds(const void *p) {
+    return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void *)p);
+}
+
+template <bool PA, bool PB, bool SH>
 __device__ __forceinline__ void blk_mm_loop(d4 (&acc)[4], const int (&ti)[4], const int (&tj)[4], const bool (&on)[4],
                                             const Mv &A, const Mv &B, int M, int N, int K, int g, int c) {
     const int sai = A.kind == 1 ? A.ld : 1, saj = A.kind == 1 ? 1 : A.ld;
@@ -68,8 +75,14 @@ __device__ __forceinline__ void blk_mm_loop(d4 (&acc)[4], const int (&ti)[4], co
             if (!on[t]) continue;  // wave-uniform
             const int i = 16 * ti[t] + c, j = 16 * tj[t] + c;
             const int ic = i < M ? i : M - 1, jc = j < N ? j : N - 1;
-            const double av = A.p[mv_off<PA>(ic, kc, sai, saj, A.ld)];
-            const double bv = B.p[mv_off<PB>(kc, jc, sbi, sbj, B.ld)];
+            double av, bv;
+            if constexpr (SH) {
+                av = ((lds_cptr)A.p)[mv_off<PA>(ic, kc, sai, saj, A.ld)];
+                bv = ((lds_cptr)B.p)[mv_off<PB>(kc, jc, sbi, sbj, B.ld)];
+            } else {
+                av = A.p[mv_off<PA>(ic, kc, sai, saj, A.ld)];
+                bv = B.p[mv_off<PB>(kc, jc, sbi, sbj, B.ld)];
+            }
             const double a = (k < K && i < M) ? av : 0.0;
             const double b = (k < K && j < N) ? bv : 0.0;
             acc[t] = mfma_f64(a, b, acc[t]);
@@ -93,10 +106,18 @@ __device__ __noinline__ void blk_mm(double *C, int ldc, Mv A, Mv B, int M, int N
         acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     }
     __syncthreads();  // the operands are complete
-    if (A.kind != 2 && B.kind != 2) blk_mm_loop<false, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
-    else if (A.kind == 2 && B.kind != 2) blk_mm_loop<true, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
-    else if (A.kind != 2) blk_mm_loop<false, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
-    else blk_mm_loop<true, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    const bool sh = in_lds(A.p) && in_lds(B.p);  // wave-uniform
+    if (sh) {
+        if (A.kind != 2 && B.kind != 2) blk_mm_loop<false, false, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else if (A.kind == 2 && B.kind != 2) blk_mm_loop<true, false, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else if (A.kind != 2) blk_mm_loop<false, true, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else blk_mm_loop<true, true, true>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    } else {
+        if (A.kind != 2 && B.kind != 2) blk_mm_loop<false, false, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else if (A.kind == 2 && B.kind != 2) blk_mm_loop<true, false, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else if (A.kind != 2) blk_mm_loop<false, true, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+        else blk_mm_loop<true, true, false>(acc, ti, tj, on, A, B, M, N, K, g, c);
+    }
     __syncthreads();  // every read of the operands is done: C may overwrite them
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -126,7 +147,12 @@ __device__ __noinline__ void blk_mv(double *y, Mv A, const double *x, int M, int
     if (M <= 64) {
         const int i = tid & 63, w = tid >> 6;
         double a = 0.0;
-        if (i < M)
+        if (A.kind != 2 && in_lds(A.p) && in_lds(x)) {  // LDS operands
+            const int si = A.kind == 1 ? A.ld : 1, sk = A.kind == 1 ? 1 : A.ld;
+            const lds_cptr ap = (lds_cptr)A.p, xp = (lds_cptr)x;
+            if (i < M)
+                for (int k = w; k < K; k += 4) a = __builtin_fma(ap[i * si + k * sk], xp[k], a);
+        } else if (i < M)
             for (int k = w; k < K; k += 4) a = __builtin_fma(A.at(i, k), x[k], a);
         part[w][i] = a;
         __syncthreads();
