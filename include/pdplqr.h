@@ -110,13 +110,13 @@ typedef struct {
 /* Fill `cfg` with the reference defaults (keep_factors = 1, load_balancing = 1,
  * CHOLESKY, rho_dyn = kkt_sigma = 1e-6).
  * Shape limits of this build (the reference is size-generic, lqr_kernel.hpp:104-147):
- * nx + nu <= 64 for every solver: up to 32 on MFMA tiles in one wavefront,
+ * nx + nu <= 256 for every solver: up to 32 on MFMA tiles in one wavefront,
  * 33..64 on register tiles or LDS-resident stage matrices, one 256-thread
  * block per problem / segment / element (kernels_big.hip, kernels_wide.hip);
- * KKT rows per stage <= 64 past the block LDL^T tiles.  Every solver goes
- * on to nx + nu <= 256 (kernels_xl.hip, kernels_xl_par.hip: global-memory
- * stage and element matrices; every protocol call, pdplqr_admm_solve and the
- * horizon-shard calls; KKT rows per stage <= 256 there).  pdplqr_create returns
+ * KKT rows per stage <= 64 past the block LDL^T tiles; 65..256 on
+ * global-memory stage and element matrices (kernels_xl.hip, kernels_xl_par.hip:
+ * every protocol call, pdplqr_admm_solve and the horizon-shard calls; KKT rows
+ * per stage <= 256 there).  pdplqr_create returns
  * PDPLQR_ERR_UNSUPPORTED past them. */
 void pdplqr_config_init(pdplqr_config *cfg);
 
