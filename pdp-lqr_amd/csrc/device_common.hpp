@@ -233,6 +233,40 @@ __device__ __forceinline__ void lds_axpy_strided(double *dst, int ldc, const dou
     for (; l <= lend; l += st) dst[l * ldc] = __builtin_fma(-f, src[l * lds], dst[l * ldc]);
 }
 
+// Two pivots (j, j + 1) of a right-looking elimination in one pass over row
+// dst (entries l = l0, l0 + st, ... <= lend, ld ldc): with c0 = column j and
+// c1 = column j + 1 before either pivot, a1j = M(j + 1, j), f0 = M(i, j) / d_j
+// and f1 = M'(i, j + 1) / d'_{j + 1},
+//     t = M(i, l) - f0 M(l, j),  M'(l, j + 1) = M(l, j + 1) - (M(l, j) / d_j) M(j + 1, j),
+//     M(i, l) = t - f1 M'(l, j + 1)
+// -- the fmas of the two sequential steps, in their order (bit-identical),
+// loads of four entries before their stores.
+__device__ __forceinline__ void lds_axpy2_strided(double *dst, int ldc, const double *c0, const double *c1, double f0,
+                                                  double f1, double inv0, double a1j, int l0, int lend, int st) {
+    constexpr int G = 4;
+    int l = l0;
+    for (; l + (G - 1) * st <= lend; l += G * st) {
+        double x0[G], x1[G], dv[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            x0[u] = c0[l + u * st];
+            x1[u] = c1[l + u * st];
+            dv[u] = dst[(l + u * st) * ldc];
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const double t = __builtin_fma(-f0, x0[u], dv[u]);
+            const double al = __builtin_fma(-(x0[u] * inv0), a1j, x1[u]);
+            dst[(l + u * st) * ldc] = __builtin_fma(-f1, al, t);
+        }
+    }
+    for (; l <= lend; l += st) {
+        const double t = __builtin_fma(-f0, c0[l], dst[l * ldc]);
+        const double al = __builtin_fma(-(c0[l] * inv0), a1j, c1[l]);
+        dst[l * ldc] = __builtin_fma(-f1, al, t);
+    }
+}
+
 __device__ __forceinline__ bool psd_bad(double v) { return !(v >= -PDPLQR_PSD_TOL && v < 1.0e300); }
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {

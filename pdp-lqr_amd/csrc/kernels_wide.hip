@@ -540,7 +540,40 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
         const int ri = tid & 63, cg = tid >> 6;  // row, column group (s, n <= 64)
         bool ok = true;
         SEGW_T(4);
-        for (int j = 0; j < m; ++j) {
+        double *luq = fy;  // lu' (no y block: fy is free)
+        for (int j = 0; j < m;) {
+            if (!yon && j + 1 < m) {
+                // two pivots per barrier (lds_axpy2_strided: the same fmas as two steps)
+                const double d0 = Mb[j + j * s], a1j = Mb[(j + 1) + j * s];
+                const double inv0 = 1.0 / d0, invs0 = rsqrt_f64(d0);
+                const double d1 = __builtin_fma(-(a1j * inv0), a1j, Mb[(j + 1) + (j + 1) * s]);
+                ok = ok && d0 > 0.0 && d1 > 0.0;
+                const double inv1 = 1.0 / d1, invs1 = rsqrt_f64(d1);
+                const double lpj = lp[j], lp1 = __builtin_fma(-(a1j * inv0), lpj, lp[j + 1]);
+                if (tid < s) {
+                    const double c0 = Mb[tid + j * s];
+                    FRk[(long long)j * s + tid] = tid >= j ? c0 * invs0 : 0.0;
+                    const double a1 = __builtin_fma(-(c0 * inv0), a1j, Mb[tid + (j + 1) * s]);
+                    FRk[(long long)(j + 1) * s + tid] = tid >= j + 1 ? a1 * invs1 : 0.0;
+                }
+                if (tid == 255) {
+                    FRk[(long long)s * m + j] = lpj * invs0;
+                    FRk[(long long)s * m + j + 1] = lp1 * invs1;
+                    sinv[j] = invs0;
+                    sinv[j + 1] = invs1;
+                    luq[j] = lpj * invs0;
+                    luq[j + 1] = lp1 * invs1;
+                }
+                if (ri >= j + 2 && ri < s) {
+                    const double f0 = Mb[ri + j * s] * inv0;
+                    const double f1 = __builtin_fma(-f0, a1j, Mb[ri + (j + 1) * s]) * inv1;
+                    lds_axpy2_strided(Mb + ri, s, Mb + j * s, Mb + (j + 1) * s, f0, f1, inv0, a1j, j + 2 + cg, ri, 4);
+                    if (cg == 0) lp[ri] = __builtin_fma(-f1, lp1, __builtin_fma(-f0, lpj, lp[ri]));
+                }
+                __syncthreads();
+                j += 2;
+                continue;
+            }
             const double d = Mb[j + j * s];
             ok = ok && d > 0.0;
             const double inv2 = 1.0 / d, invs = rsqrt_f64(d);
@@ -551,6 +584,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
             if (tid == 255) {
                 FRk[(long long)s * m + j] = lpj * invs;
                 sinv[j] = invs;
+                if (!yon) luq[j] = lpj * invs;
             }
             // row ri, columns l = cg (mod 4): M's trailing rows, then the y block's
             if (ri > j && ri < s) {
@@ -565,6 +599,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
                 if (cg == 0) fy[ri] = __builtin_fma(-yrj, lpj, fy[ri]);
             }
             __syncthreads();
+            ++j;
         }
         SEGW_T(5);
         // ---- P_k (lower block, symmetric by construction), p_k, f_k; F_k stays in XB at column m ----
@@ -577,7 +612,7 @@ __global__ __launch_bounds__(256) void k_seg_bwd_wide(SegArgs A) {
             if (Lcb && i >= j) Lcb[(long long)k * ps + pidx(i, j, n)] = v;
         }
         for (int q = tid; q < s; q += BLK_THREADS) {
-            const double v = q < m ? lp[q] * sinv[q] : lp[q];  // [lu'; p_k]
+            const double v = q < m ? (yon ? lp[q] * sinv[q] : luq[q]) : lp[q];  // [lu'; p_k]
             if (lpb) lpb[(long long)k * s + q] = v;
             if (q >= m) pv[q - m] = v;
         }
