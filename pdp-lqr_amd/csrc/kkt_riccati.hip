@@ -1085,20 +1085,48 @@ __global__ __launch_bounds__(256) void k_kkt_ric_bwd_wide(KKTRicArgs A) {
         // ---- the m u-pivots (one barrier per pivot), L-form record ----
         bool ok = true;
         if (tid == 0) s_bad = 0;
-        for (int j = 0; j < m; ++j) {
+        const int i = tid & 63, cg = tid >> 6;  // row, column group (s <= 64; k_seg_bwd_wide's scheme)
+        for (int j = 0; j < m;) {
+            if (j + 1 < m) {  // two pivots per barrier (lds_axpy2_strided: the two steps' fmas, in order)
+                const double d0 = Mb[j + j * s], a1j = Mb[(j + 1) + j * s];
+                const double inv0 = 1.0 / d0, invs0 = rsqrt_f64(d0);
+                const double d1 = __builtin_fma(-(a1j * inv0), a1j, Mb[(j + 1) + (j + 1) * s]);
+                ok = ok && d0 > 0.0 && d1 > 0.0;
+                const double inv1 = 1.0 / d1, invs1 = rsqrt_f64(d1);
+                const double lpj = lp[j], lp1 = __builtin_fma(-(a1j * inv0), lpj, lp[j + 1]);
+                if (tid < s) {
+                    const double c0 = Mb[tid + j * s];
+                    Rk[j * s + tid] = tid >= j ? c0 * invs0 : 0.0;
+                    const double a1 = __builtin_fma(-(c0 * inv0), a1j, Mb[tid + (j + 1) * s]);
+                    Rk[(j + 1) * s + tid] = tid >= j + 1 ? a1 * invs1 : 0.0;
+                }
+                if (tid == 255) {
+                    Rk[s * m + j] = lpj * invs0;
+                    Rk[s * m + j + 1] = lp1 * invs1;
+                }
+                if (i >= j + 2 && i < s) {
+                    const double f0 = Mb[i + j * s] * inv0;
+                    const double f1 = __builtin_fma(-f0, a1j, Mb[i + (j + 1) * s]) * inv1;
+                    lds_axpy2_strided(Mb + i, s, Mb + j * s, Mb + (j + 1) * s, f0, f1, inv0, a1j, j + 2 + cg, i, 4);
+                    if (cg == 0) lp[i] = __builtin_fma(-f1, lp1, __builtin_fma(-f0, lpj, lp[i]));
+                }
+                __syncthreads();
+                j += 2;
+                continue;
+            }
             const double d = Mb[j + j * s];
             ok = ok && d > 0.0;
             const double inv2 = 1.0 / d, invs = rsqrt_f64(d);
             const double lpj = lp[j];
             if (tid < s) Rk[j * s + tid] = tid >= j ? Mb[tid + j * s] * invs : 0.0;
             if (tid == 255) Rk[s * m + j] = lpj * invs;
-            const int i = tid & 63, cg = tid >> 6;  // row, column group (s <= 64; k_seg_bwd_wide's scheme)
             if (i > j && i < s) {
                 const double lij = Mb[i + j * s] * inv2;
                 lds_axpy_strided(Mb + i, s, Mb + j * s, lij, j + 1 + cg, i, 4);
                 if (cg == 0) lp[i] = __builtin_fma(-lij, lpj, lp[i]);
             }
             __syncthreads();
+            ++j;
         }
         // ---- P_k, p_k ----
         for (int q = tid; q < n * n; q += BLK_THREADS) {
