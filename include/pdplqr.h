@@ -98,8 +98,9 @@ typedef struct {
                                 slices' (f, p) (2 nx doubles per problem,
                                 lqr_solver_parallel.hpp:207-210); admm_solve runs its
                                 vectors on the first device around the slices' protocol
-                                calls.  With num_devices > 1 the shard_* calls and
-                                set_stream are unsupported, and `device` is ignored.  num_devices = 1 with a non-NULL
+                                calls.  With num_devices > 1 the shard_* calls are
+                                unsupported, `device` is ignored, and set_stream takes
+                                the caller's stream on devices[0] (see below).  num_devices = 1 with a non-NULL
                                 `devices` runs the same split with one slice (RCCL
                                 communicator of one rank). */
     const int32_t *devices;  /* num_devices HIP ordinals, or NULL = 0 .. num_devices - 1.
@@ -128,7 +129,16 @@ const char *pdplqr_last_error(void);
 
 /* Stream control (hipStream_t passed as void*). NULL = the handle's own stream.
    Switching makes the new stream wait (an event, no host sync) for what the
-   handle queued on the old one, e.g. set_model's upload. */
+   handle queued on the old one, e.g. set_model's upload: the event is recorded
+   on the OLD stream, so that stream must still be alive when the handle
+   switches away from it (switch before destroying a stream the handle uses).
+   num_devices > 1: the stream is the caller's, on devices[0] (else
+   PDPLQR_ERR_INVALID); the slices keep their own streams, wait (an event) for
+   the caller's stream before reading device inputs, and the caller's stream
+   waits for the slices' work at the end of every call, forward's device
+   outputs included -- no host synchronisation.  NULL (the default): device
+   inputs are read after a drain of every slice device, and forward returns
+   with ws complete. */
 int pdplqr_set_stream(pdplqr_handle h, void *hip_stream);
 void *pdplqr_get_stream(pdplqr_handle h);
 int pdplqr_synchronize(pdplqr_handle h);

@@ -278,10 +278,7 @@ int pdplqr_destroy(pdplqr_handle h) {
 
 int pdplqr_set_stream(pdplqr_handle h, void *stream) {
     if (!h) return invalid("null handle");
-    if (h->md) {
-        set_error("set_stream: a num_devices > 1 handle runs one stream per device");
-        return PDPLQR_ERR_UNSUPPORTED;
-    }
+    if (h->md) return md_set_stream(h, stream);
     hipStream_t next = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
     if (next != h->stream) {
         // work already queued on the old stream (set_model's repack, a solve)
@@ -301,7 +298,7 @@ int pdplqr_set_stream(pdplqr_handle h, void *stream) {
 }
 
 void *pdplqr_get_stream(pdplqr_handle h) {
-    if (h && h->md) return md_stream(h);  // the first slice's device stream
+    if (h && h->md) return md_stream(h);  // the caller stream, else the first slice's device stream
     return h ? reinterpret_cast<void *>(h->stream) : nullptr;
 }
 

@@ -2,6 +2,7 @@
 // device kernels exercised directly by the GPU unit tests
 // (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
 #include "combine_mw.hpp"
+#include "combine_qd.hpp"
 #include "combine_tiles.hpp"
 #include "parallel.hpp"
 
@@ -80,6 +81,45 @@ extern "C" int pdplqr_debug_combine_mw(int n, const double *a, const double *b, 
     const size_t sm = (size_t)((mw_smem_bytes(n) + 15) / 16 * 2 + 2 * ((3 * n * n + 2 * n + 1) & ~1)) * sizeof(double);
     if (T == 1) hipLaunchKernelGGL(k_debug_combine_mw<1>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
     else hipLaunchKernelGGL(k_debug_combine_mw<2>, dim3(1), dim3(256), sm, 0, da, db, dout, n, fcf, dok);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    (void)hipFree(dok);
+    return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
+}
+
+// the n = 24 blocked-LDL^T combine of the horizon kernels (combine_qd.hpp)
+__global__ __launch_bounds__(256) void k_debug_combine_qd(const double *a, const double *b, double *out, int fcf,
+                                                          int *ok) {
+    extern __shared__ __attribute__((aligned(16))) double qbuf[];
+    constexpr int n = pdplqr::QD_N, nn = n * n, es = 3 * nn + 2 * n, slot = (es + 1) & ~1;
+    double *la = qbuf + pdplqr::qd_smem_doubles() + 2, *lb = la + slot;  // 16-byte aligned
+    for (int q = threadIdx.x; q < es; q += blockDim.x) {
+        la[q] = a[q];
+        lb[q] = b[q];
+    }
+    __syncthreads();
+    const bool good = pdplqr::qd_combine(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n,
+                                         pdplqr::elem_in(la, n), pdplqr::elem_in(lb, n), fcf != 0, qbuf);
+    if (threadIdx.x == 0) *ok = good ? 1 : 0;
+}
+
+extern "C" int pdplqr_debug_combine_qd(const double *a, const double *b, double *out, int fcf) {
+    using namespace pdplqr;
+    constexpr int n = QD_N;
+    const size_t es = (size_t)(3 * n * n + 2 * n) * sizeof(double);
+    double *d = nullptr;
+    int *dok = nullptr, okh = 0;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 3 * es));
+    PDPLQR_HIP_TRY(hipMalloc(&dok, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, a, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + 2 * es, out, es, hipMemcpyHostToDevice));  // untouched blocks kept
+    const double *da = d, *db = (const double *)((char *)d + es);
+    double *dout = (double *)((char *)d + 2 * es);
+    const size_t sm = (size_t)(qd_smem_doubles() + 2 + 2 * ((3 * n * n + 2 * n + 1) & ~1)) * sizeof(double);
+    hipLaunchKernelGGL(k_debug_combine_qd, dim3(1), dim3(256), sm, 0, da, db, dout, fcf, dok);
     PDPLQR_HIP_TRY(hipDeviceSynchronize());
     PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
     PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));

@@ -26,6 +26,7 @@
 //     (lqr_kernel_parallel.hpp:195-198), u_hat from lambda_{i+1}.
 #define PDPLQR_COMB_PROFILE_TU 1  // the combine phase marks live in this translation unit
 #include "combine_mw.hpp"
+#include "combine_qd.hpp"
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
@@ -256,6 +257,24 @@ __device__ __forceinline__ void stage_range_blk(double *dst, const double *src, 
 __host__ __device__ inline int mw_smem_doubles(int n) { return (int)((mw_smem_bytes(n) + 15) / 16 * 2); }
 __host__ __device__ inline int elem_slot(int n) { return (3 * n * n + 2 * n + 1) & ~1; }
 
+// The 4-wave combine of the n = 24 kernels: the blocked LDL^T of the junction
+// block (combine_qd.hpp) unless built with -DPDPLQR_QD_COMBINE=0 (the
+// two-Cholesky mw_combine, A/B).  Both read their operands only through ea /
+// eb (staged in LDS by every caller) and use the combine's own LDS `buf`.
+#ifndef PDPLQR_QD_COMBINE
+#define PDPLQR_QD_COMBINE 1
+#endif
+static_assert(qd_smem_doubles() <= (5 * QD_N * (QD_N + 1) + 4 * QD_N) + 2, "qd scratch fits the mw region (mw_smem_bytes)");
+template <int T, int NC>
+__device__ __forceinline__ bool mw_combine_nc(double *oF, double *oC, double *of, double *oP, double *op,
+                                              const ElemIn &ea, const ElemIn &eb, int n, bool fcf, double *buf) {
+    if constexpr (NC == QD_N && PDPLQR_QD_COMBINE) {
+        return qd_combine(oF, oC, of, oP, op, ea, eb, fcf, buf);
+    } else {
+        return mw_combine<T>(oF, oC, of, oP, op, ea, eb, n, fcf, mw_smem(buf, n));
+    }
+}
+
 template <int T, bool LU, int NC = 0>
 __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
     __shared__ CombSmem<T> sm;
@@ -386,7 +405,6 @@ __device__ __forceinline__ void mw_scan_block(const ScanArgs &A, long long blk, 
         g_comb_t[(blockIdx.x % 1024) * 32 + 22] = fcf;
     }
 #endif
-    const MwSmem sm = mw_smem(mwbuf, n);
     double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
     stage_range_blk(ea, in + (long long)i * is, es);
     stage_range_blk(eb, in + (long long)j * is, es);
@@ -394,8 +412,8 @@ __device__ __forceinline__ void mw_scan_block(const ScanArgs &A, long long blk, 
     __syncthreads();
     COMB_MARK(17);  // operands staged
     double *o = out + (long long)i * es;
-    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
-                                  elem_in(eb, n), n, fcf, sm);
+    const bool ok = mw_combine_nc<T, NC>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
+                                         elem_in(eb, n), n, fcf, mwbuf);
 #ifdef PDPLQR_COMB_PROFILE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     COMB_MARK(18);  // wave 0's stores complete
@@ -406,7 +424,7 @@ __device__ __forceinline__ void mw_scan_block(const ScanArgs &A, long long blk, 
 }
 
 template <int T, int NC = 0>
-__global__ __launch_bounds__(256) void k_seg_scan_mw(ScanArgs A) {
+__global__ __launch_bounds__(256, 2) void k_seg_scan_mw(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     mw_scan_block<T, NC>(A, blockIdx.x, mwbuf);
 }
@@ -620,7 +638,7 @@ __device__ __forceinline__ bool mw_map(const ElemIn &e, const double *vP, const 
 // mw_map's solve, with the products after the factorisations one deep and
 // split over the waves by output tile.
 template <int T, int NC = 0>
-__global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
+__global__ __launch_bounds__(256, 2) void k_seg_maps_mw(MapArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const int n = NC ? NC : A.n, S = A.S, J = S + 1, nn = n * n;
@@ -651,7 +669,8 @@ __global__ __launch_bounds__(256) void k_seg_maps_mw(MapArgs A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (vcomb) {  // block-uniform
-        ok = mw_combine<T>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(es1, n), elem_in(es2, n), n, false, sm);
+        ok = mw_combine_nc<T, NC>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(es1, n), elem_in(es2, n), n, false,
+                                  mwbuf);
         __syncthreads();  // vo (written by waves 0 and 3) is complete; es1 is free
         for (int q = threadIdx.x; q < mw; q += 256) es1[q] = vo[q];
         __syncthreads();
@@ -1149,7 +1168,7 @@ int launch_rank_fold_maps(const double *elems, const double *suf, const double *
 // max(ceil(log2 r), ceil(log2(R - 1 - r))) combines, against ceil(log2 R)
 // scan rounds plus the boundary-map round and the map chain of the scan form.
 template <int T, int NC = 0>
-__global__ __launch_bounds__(256) void k_rank_tree_mw(RankTreeArgs A) {
+__global__ __launch_bounds__(256, 2) void k_rank_tree_mw(RankTreeArgs A) {
     extern __shared__ __attribute__((aligned(16))) double mwbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, nn = n * n, es = 3 * nn + 2 * n;
@@ -1167,14 +1186,13 @@ __global__ __launch_bounds__(256) void k_rank_tree_mw(RankTreeArgs A) {
     }
     const double *ib = src(op.b);
     const bool fcf = op.fcf, suf = op.suf;
-    const MwSmem sm = mw_smem(mwbuf, n);
     double *ea = mwbuf + mw_smem_doubles(n), *eb = ea + elem_slot(n);
     stage_range_blk(ea, ia, es);
     stage_range_blk(eb, ib, es);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const bool ok = mw_combine<T>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
-                                  elem_in(eb, n), n, fcf, sm);
+    const bool ok = mw_combine_nc<T, NC>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(ea, n),
+                                         elem_in(eb, n), n, fcf, mwbuf);
     if (!fcf && wv == 1)
         for (int p = lane; p < 2 * nn + n; p += 64) o[p] = 0.0;  // [F | C | f]
     if (!ok && threadIdx.x == 0) atomicOr(A.flag + b, suf ? 8 : 4);

@@ -113,6 +113,12 @@ struct MultiDev {
     std::vector<hipStream_t> st;
     std::vector<hipEvent_t> ev;   // elem / fp ready on its shard's stream (device-copy exchange)
     std::vector<hipEvent_t> xev;  // shard r's exchange copies done (they read every other shard's buffers)
+    std::vector<hipEvent_t> tail;  // shard r's queued work (the caller stream's join)
+    // the caller's stream on devices[0] (pdplqr_set_stream): device inputs are
+    // ordered after it by an event, and it waits for the slices' work at the end
+    // of every call; NULL: the devices are drained before device inputs are read
+    hipStream_t caller = nullptr;
+    hipEvent_t cev = nullptr;     // recorded on `caller`, waited on by every slice stream
     bool xpending = false;        // a device-copy exchange was issued since the last backward
     // per shard, on its device: model staging (set_model), vectors, elements,
     // the (f, p) parts of the element and their gather (backward_without_factorization)
@@ -152,16 +158,40 @@ static int md_copy2d(double *dst, long long dp, const double *src, long long sp,
     return PDPLQR_OK;
 }
 
-// Device-memory inputs may still be in production on another stream of the
-// caller (torch's current stream, say): the driver's copies run on the slices'
-// own non-blocking streams, so every device is drained first.
+// Device-memory inputs may still be in production on a stream of the caller
+// (torch's current stream, say) while the driver's copies run on the slices'
+// own non-blocking streams.  With a caller stream set (pdplqr_set_stream) every
+// slice stream waits for an event recorded on it -- no host synchronisation;
+// without one every device is drained first.
 static int md_inputs_ready(MultiDev *md, int mem) {
     if (mem != PDPLQR_MEM_DEVICE) return PDPLQR_OK;
+    if (md->caller) {
+        PDPLQR_HIP_TRY(hipSetDevice(md->dev[0]));
+        PDPLQR_HIP_TRY(hipEventRecord(md->cev, md->caller));
+        for (int r = 0; r < md->R; ++r) {
+            PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
+            PDPLQR_HIP_TRY(hipStreamWaitEvent(md->st[r], md->cev, 0));
+        }
+        return PDPLQR_OK;
+    }
     for (int r = 0; r < md->R; ++r) {
         if (std::find(md->dev.begin(), md->dev.begin() + r, md->dev[r]) != md->dev.begin() + r) continue;
         PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
         PDPLQR_HIP_TRY(hipDeviceSynchronize());
     }
+    return PDPLQR_OK;
+}
+
+// The caller stream waits (events) for everything the slices queued so far:
+// outputs are read, inputs freed or overwritten there.  No-op without one.
+static int md_join_caller(MultiDev *md) {
+    if (!md->caller) return PDPLQR_OK;
+    for (int r = 0; r < md->R; ++r) {
+        PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
+        PDPLQR_HIP_TRY(hipEventRecord(md->tail[r], md->st[r]));
+    }
+    PDPLQR_HIP_TRY(hipSetDevice(md->dev[0]));
+    for (int r = 0; r < md->R; ++r) PDPLQR_HIP_TRY(hipStreamWaitEvent(md->caller, md->tail[r], 0));
     return PDPLQR_OK;
 }
 
@@ -183,10 +213,15 @@ void md_release(pdplqr_handle h) {
     if (md->rccl)
         for (ncclComm_t c : md->comm)
             if (c) (void)g_rccl.destroy(c);
+    if (md->cev) {
+        (void)hipSetDevice(md->dev[0]);
+        (void)hipEventDestroy(md->cev);
+    }
     for (int r = 0; r < md->R; ++r) {
         (void)hipSetDevice(md->dev[r]);
         if (r < (int)md->ev.size() && md->ev[r]) (void)hipEventDestroy(md->ev[r]);
         if (r < (int)md->xev.size() && md->xev[r]) (void)hipEventDestroy(md->xev[r]);
+        if (r < (int)md->tail.size() && md->tail[r]) (void)hipEventDestroy(md->tail[r]);
         if (r < (int)md->sh.size() && md->sh[r]) (void)pdplqr_destroy(md->sh[r]);
         for (void *p : md->allocs[r]) (void)hipFree(p);
     }
@@ -227,6 +262,7 @@ int md_create(pdplqr_handle h, const pdplqr_config &C) {
     md->st.assign(R, nullptr);
     md->ev.assign(R, nullptr);
     md->xev.assign(R, nullptr);
+    md->tail.assign(R, nullptr);
     md->fp.assign(R, nullptr);
     md->gathered_fp.assign(R, nullptr);
     md->ws.assign(R, nullptr);
@@ -270,7 +306,10 @@ int md_create(pdplqr_handle h, const pdplqr_config &C) {
         PDPLQR_HIP_TRY(hipSetDevice(md->dev[r]));
         PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->ev[r], hipEventDisableTiming));
         PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->xev[r], hipEventDisableTiming));
+        PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->tail[r], hipEventDisableTiming));
     }
+    PDPLQR_HIP_TRY(hipSetDevice(md->dev[0]));
+    PDPLQR_HIP_TRY(hipEventCreateWithFlags(&md->cev, hipEventDisableTiming));
     // admm_solve's update pass runs on the first device over the whole horizon
     {
         double *p = nullptr;
@@ -397,7 +436,7 @@ int md_set_model(pdplqr_handle h, int mask, const double *E, const double *c, co
     }
     h->model_set = true;
     if (mask & (PDPLQR_MODEL_H | PDPLQR_MODEL_HV)) h->updated = false;
-    return PDPLQR_OK;
+    return md_join_caller(md);
 }
 
 // per-stage vectors of the slice: the stage rows [a0, a1) and, for the last
@@ -443,7 +482,7 @@ int md_update(pdplqr_handle h, const double *ws, const double *ys, const double 
     }
     if (mem != PDPLQR_MEM_DEVICE && (rc = md_sync(md))) return rc;  // host inputs may be reused on return
     h->updated = true;
-    return PDPLQR_OK;
+    return md_join_caller(md);
 }
 
 // backward (fact) or backward_without_factorization: the slice backwards, then
@@ -546,7 +585,7 @@ int md_backward(pdplqr_handle h, const double *rho, int mem, bool fact) {
     }
     if (mem != PDPLQR_MEM_DEVICE && (rc = md_sync(md))) return rc;
     if (fact) h->factored = true;
-    return PDPLQR_OK;
+    return md_join_caller(md);
 }
 
 int md_forward(pdplqr_handle h, const double *x0, double *ws, int mem) {
@@ -576,7 +615,10 @@ int md_forward(pdplqr_handle h, const double *x0, double *ws, int mem) {
                                       md->st[r])))
             return rc;
     }
-    return md_sync(md);  // ws is complete when the call returns
+    // device outputs with a caller stream: ordered on it (events); otherwise
+    // ws is complete when the call returns
+    if (md->caller && mem == PDPLQR_MEM_DEVICE) return md_join_caller(md);
+    return md_sync(md);
 }
 
 int md_status(pdplqr_handle h, int32_t *flags) {
@@ -611,7 +653,29 @@ int md_clear(pdplqr_handle h) {
     return PDPLQR_OK;
 }
 
-void *md_stream(pdplqr_handle h) { return h->md->R > 0 ? reinterpret_cast<void *>(h->md->st[0]) : nullptr; }
+void *md_stream(pdplqr_handle h) {
+    MultiDev *md = h->md;
+    if (md->caller) return reinterpret_cast<void *>(md->caller);
+    return md->R > 0 ? reinterpret_cast<void *>(md->st[0]) : nullptr;
+}
+
+// pdplqr_set_stream on a split handle: the caller's stream, on devices[0]
+// (NULL: back to draining the devices before device inputs are read).  What
+// the slices queued before the switch is joined to the new stream.
+int md_set_stream(pdplqr_handle h, void *stream) {
+    MultiDev *md = h->md;
+    hipStream_t next = reinterpret_cast<hipStream_t>(stream);
+    if (next) {
+        int d = -1;
+        PDPLQR_HIP_TRY(hipStreamGetDevice(next, &d));
+        if (d != md->dev[0]) {
+            set_error("set_stream: a num_devices > 1 handle takes a stream of its first device (devices[0])");
+            return PDPLQR_ERR_INVALID;
+        }
+    }
+    md->caller = next;
+    return md_join_caller(md);
+}
 
 int md_primary_device(pdplqr_handle h) { return h->md->dev[0]; }
 

@@ -80,6 +80,7 @@ int md_status(pdplqr_handle h, int32_t *flags);
 int md_synchronize(pdplqr_handle h);
 int md_clear(pdplqr_handle h);
 void *md_stream(pdplqr_handle h);
+int md_set_stream(pdplqr_handle h, void *stream);
 int md_primary_device(pdplqr_handle h);  // the device admm_solve's vectors live on
 void md_admm_view(pdplqr_handle h, const double **D, const int32_t **d_off, const int32_t **y_off);
 }  // namespace pdplqr

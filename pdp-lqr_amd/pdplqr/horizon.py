@@ -95,19 +95,28 @@ class HorizonShard:
         self._hd = _Handle(n, m, N_local, batch, _lib.PDPLQR_SOLVER_PARALLEL, num_segments=ns,
                            condensed_type=ctype, device=device, keep_factors=True, ncs=ncs,
                            segment_len=segment_len)
+        # the full all-gather of the last factorising solve_distributed and its
+        # key (world size, rank, group): factorize=False writes the new (f, p)
+        # into it, so anything that changes F, C, P or the ranks clears it
+        self._gathered = None
+        self._gather_key = None
 
     @property
     def handle(self):
         return self._hd
 
     def set_model(self, E, c, H, h, D=None):
+        self._gathered = None  # the kept gather holds F, C, P of the old model
         self._hd.set_model(E, c, H, h, D)
 
     def update_problem_data(self, ws, ys=None, zs=None, inv_rho=None, sigma: float = 0.0):
         self._hd.update_problem_data(ws, ys, zs, inv_rho, sigma)
 
     def backward(self, elem_out, is_last: bool, rho=None):
-        """Slice backward; writes the slice element(s) [batch, 3n^2+2n] into elem_out."""
+        """Slice backward; writes the slice element(s) [batch, 3n^2+2n] into elem_out.
+        A factorising backward outside solve_distributed invalidates the gather
+        solve_distributed(factorize=False) would reuse."""
+        self._gathered = None
         pr, pe = _ptr(rho, "rho"), _ptr(elem_out, "elem")
         mem = pe[1]
         check(lib().pdplqr_shard_backward(self._hd.h, pr[0], int(bool(is_last)), pe[0], mem))
@@ -162,8 +171,14 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None, fac
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     last = rank == world - 1
-    if not factorize and getattr(shard, "_gathered", None) is None:
-        raise RuntimeError("solve_distributed(factorize=False) needs a preceding factorising solve")
+    key = (world, rank, id(group) if group is not None else None)
+    if not factorize:
+        if getattr(shard, "_gathered", None) is None:
+            raise RuntimeError("solve_distributed(factorize=False) needs a preceding factorising solve "
+                               "(set_model / a direct backward since then invalidate it)")
+        if shard._gather_key != key:
+            raise RuntimeError("solve_distributed(factorize=False): the process group or world size changed "
+                               "since the factorising solve")
     fs, ps = shard.fp_slices()
 
     def exchange(elem):
@@ -177,6 +192,7 @@ def solve_distributed(shard: HorizonShard, x0, ws_out, rho=None, group=None, fac
                 dist.all_gather(parts, elem, group=group)
                 g = torch.stack(parts).contiguous()
             shard._gathered = g
+            shard._gather_key = key
             return g
         fp = torch.cat([elem[:, fs], elem[:, ps]], dim=1).contiguous()
         gfp = torch.empty(world, shard.batch, 2 * shard.n, dtype=torch.float64, device=fp.device)

@@ -6,7 +6,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 C=$ROOT/pdp-lqr_amd/csrc
 SRCS=$(sed -n 's/^SRCS := //p' "$C/Makefile")
-mkdir -p "$ROOT/pdp-lqr_amd/build/variants"
+OUTD=${VARIANT_DIR:-$ROOT/pdp-lqr_amd/build/variants}
+mkdir -p "$OUTD"
 cd "$C"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -mllvm -amdgpu-mfma-vgpr-form \
-  "$@" -shared -o "$ROOT/pdp-lqr_amd/build/variants/libpdplqr_$NAME.so" $SRCS
+  "$@" -shared -o "$OUTD/libpdplqr_$NAME.so" $SRCS

@@ -131,3 +131,67 @@ def test_device_combine_lu_form_matches_numpy(n):
     got, ref = _unpack(out, n), combine(a, b)
     for name, x, y in zip("FCfPp", got, ref):
         assert np.linalg.norm(x - y) <= 1e-12 * max(1.0, np.linalg.norm(y)), name
+
+
+@pytest.mark.parametrize("case", ["random", "zero_b", "no_fcf", "ill_Pb", "seg_elems"])
+def test_qd_combine_matches_numpy(case):
+    """The n = 24 blocked LDL^T combine of the horizon kernels (combine_qd.hpp):
+    the same element as seg_ref.combine (1e-12; ill-conditioned P_b, where the
+    two-Cholesky form itself drifts, 1e-10), untouched F, C, f without fcf."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_qd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    n = 24
+    rng = np.random.default_rng(700 + len(case))
+    fcf = case != "no_fcf"
+    a, b = _elem(n, rng), _elem(n, rng, zero_fcf=(case in ("zero_b", "no_fcf")))
+    tol = 1e-12
+    if case == "ill_Pb":
+        w, U = np.linalg.eigh(b[3])
+        w[: n // 3] *= 1e-6
+        b = (b[0], b[1], b[2], (U * w) @ U.T, b[4])
+        tol = 1e-10
+    if case == "seg_elems":  # real segment elements (24/8, 6 stages each)
+        from seg_ref import slice_element
+
+        m, Lseg = 8, 6
+        E, c, Ht, ht = [], [], [], []
+        for _ in range(2 * Lseg):
+            A = np.eye(n) + 0.1 * rng.standard_normal((n, n))
+            E.append(np.concatenate([rng.standard_normal((n, m)), A], 1))
+            c.append(rng.standard_normal(n))
+            M = rng.standard_normal((n + m, n + m))
+            Ht.append(M @ M.T / (n + m) + np.eye(n + m))
+            ht.append(rng.standard_normal(n + m))
+        a = slice_element(E, c, Ht, ht, 0, Lseg, None)
+        b = slice_element(E, c, Ht, ht, Lseg, 2 * Lseg, None)
+    va, vb = _pack(a), _pack(b)
+    sentinel = 12345.0
+    out = np.full_like(va, sentinel)
+    assert L.pdplqr_debug_combine_qd(va.ctypes.data, vb.ctypes.data, out.ctypes.data, int(fcf)) == 0
+    got, ref = _unpack(out, n), combine(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        if not fcf and name in "FCf":
+            assert np.all(x == sentinel), name
+            continue
+        assert np.linalg.norm(x - y) <= tol * max(1.0, np.linalg.norm(y)), name
+    for M in (got[1], got[3]):
+        if fcf or M is got[3]:
+            assert np.array_equal(M, M.T)  # written symmetric
+
+
+def test_qd_combine_flags_zero_value_function():
+    """P_b = 0 (a zero state cost): the first x pivot is 0 -- flagged, as chol(P_b)
+    failing is in the Cholesky form (condensed_system.hpp:217-226)."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_qd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    n = 24
+    rng = np.random.default_rng(71)
+    a, b = _elem(n, rng), _elem(n, rng)
+    b = (b[0], b[1], b[2], np.zeros((n, n)), b[4])
+    va, vb = _pack(a), _pack(b)
+    out = np.zeros_like(va)
+    assert L.pdplqr_debug_combine_qd(va.ctypes.data, vb.ctypes.data, out.ctypes.data, 1) != 0

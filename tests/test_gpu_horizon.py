@@ -119,7 +119,28 @@ def _dist_worker(rank, world, port, q):
         sh.update_problem_data(np.zeros((1, (N1 - N0) * (n + m) + n)), sigma=1e-6)
         loc = np.zeros((1, (N1 - N0) * (n + m) + n))
         solve_distributed(sh, x0, loc)
-        q.put((rank, N0, N1, loc))
+        # the gather kept for factorize=False is invalidated by a new
+        # model and by a factorising backward outside solve_distributed
+        loc2 = np.zeros_like(loc)
+        solve_distributed(sh, x0, loc2, factorize=False)  # same data: same answer
+        stale = []
+        sh.set_model(*slice_arrays(E, c, H, h, n, m, N, N0, N1, last))
+        sh.update_problem_data(np.zeros((1, (N1 - N0) * (n + m) + n)), sigma=1e-6)
+        for act in ("set_model", "backward"):
+            if act == "backward":
+                solve_distributed(sh, x0, loc2)
+                sh.backward(np.zeros((1, sh.es)), last)
+            try:
+                solve_distributed(sh, x0, loc2, factorize=False)
+                stale.append(act)
+            except RuntimeError:
+                pass
+        q.put((rank, N0, N1, loc, bool(np.allclose(loc, loc2, rtol=1e-12, atol=1e-12)), stale))
+    except Exception as e:  # report instead of leaving the parent waiting on the queue
+        import traceback
+
+        q.put((rank, -1, -1, None, False, [traceback.format_exc()]))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -133,7 +154,9 @@ def test_two_process_gloo_exchange():
     ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(2)])
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for r in res:
+        assert r[1] >= 0, r[5]
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -142,10 +165,11 @@ def test_two_process_gloo_exchange():
     E, c, H, h, x0 = _full(n, m, N, 1, 11)
     ref = _oracle(n, m, N, E, c, H, h, x0)[0]
     full = np.zeros(N * s + n)
-    for rank, N0, N1, loc in res:
+    for rank, N0, N1, loc, same, stale in res:
         full[N0 * s:N1 * s] = loc[0, :(N1 - N0) * s]
         if N1 == N:
             full[N * s:] = loc[0, (N1 - N0) * s:]
+        assert same and stale == [], (rank, same, stale)
     assert rel_err(full, ref) < TOL
 
 

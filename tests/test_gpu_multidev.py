@@ -286,7 +286,61 @@ def test_multidev_unsupported_calls():
 
     n, m, N = 4, 2, 20
     bs = BatchedLQRSolver(n, m, N, 1, solver="parallel", num_segments=2, devices=[0, 0])
-    with pytest.raises(PdplqrError):
-        bs.handle.set_stream(0)
+    bs.handle.set_stream(0)  # NULL: the default (drain before device inputs)
     with pytest.raises(PdplqrError):  # the split needs the PARALLEL solver
         BatchedLQRSolver(n, m, N, 1, solver="serial", devices=[0, 0])
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multidev_caller_stream_orders_device_inputs(devices):
+    """a split handle given the caller's stream
+    (pdplqr_set_stream) orders its slices after that stream by events, not device
+    drains.  Inputs are produced on a side stream behind a slow chain of
+    matmuls, every protocol call is issued on it with device tensors and no host
+    synchronisation until the end; the answers match the oracle each round (a
+    slice reading its inputs early would see the previous round's data)."""
+    import torch
+
+    from oracle.oracle import OracleSerial
+    from pdplqr import BatchedLQRSolver
+    from pdplqr.model import PackedModel
+    from pdplqr.problems import random_batch_arrays
+
+    n, m, N, batch = 12, 4, 300, 16
+    s = n + m
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, 909)
+    bs = BatchedLQRSolver(n, m, N, batch, solver="parallel", num_segments=4, devices=devices)
+    side = torch.cuda.Stream()
+    bs.handle.set_stream(side.cuda_stream)
+    assert bs.handle.stream() == side.cuda_stream
+    g = np.random.default_rng(910)
+    dev = torch.device("cuda", 0)
+    with torch.cuda.stream(side):
+        bs.set_model(*(torch.from_numpy(a).to(dev) for a in (E, c, H, h)))
+        ws_d = torch.zeros(batch, N * s + n, dtype=torch.float64, device=dev)
+        x0_d = torch.from_numpy(x0).to(dev)
+        outs, refs = [], []
+        for _ in range(3):
+            ws = g.standard_normal((batch, N * s + n))
+            big = torch.randn(2048, 2048, device=dev)
+            for _ in range(8):  # ~ms of work ahead of the input write on this stream
+                big = big @ big / 45.0
+            ws_d.copy_(torch.from_numpy(ws).pin_memory(), non_blocking=True)
+            ws_d += 0.0 * big[0, 0].double()
+            bs.update_problem_data(ws_d, sigma=1e-6)
+            bs.backward(torch.zeros(batch, 0, dtype=torch.float64, device=dev))
+            out_d = torch.empty(batch, N * s + n, dtype=torch.float64, device=dev)
+            bs.forward(x0_d, out_d)
+            outs.append(out_d)
+            refs.append(ws)
+    side.synchronize()
+    assert np.all(bs.status() == 0)
+    for out_d, ws in zip(outs, refs):
+        out = out_d.cpu().numpy()
+        for b in (0, batch - 1):
+            o = OracleSerial(PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b],
+                                         np.zeros(0)))
+            o.update_problem_data(ws[b], None, None, None, 1e-6)
+            o.backward(None)
+            assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+    bs.close()
