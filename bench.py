@@ -277,10 +277,23 @@ def _timed(fn, steps, warmup, dev, dist):
     return el / steps
 
 
+def _timed_local(fn, steps, warmup, dev):
+    """This rank alone (no barrier, no max over ranks): seconds per call."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / steps
+
+
 def measured_copy_gbs(dev, nbytes=1 << 32, reps=5):
     """Achievable HBM rate, read + write bytes / time of a 4 GiB device copy:
-    {"float4": the 16-byte streaming copy kernel (csrc/probe_pattern.hip,
-    the guide's 6.29 TB/s probe; best block count of a short sweep), "blit":
+    {"float4": the 16-byte copy kernels (csrc/probe_pattern.hip, the guide's
+    6.29 TB/s probe shape: best of one element per thread and a short
+    grid-stride sweep), "blit":
     torch's copy_ (the runtime's blit kernel)}.  float4 is None without the
     probe library."""
     import ctypes
@@ -305,18 +318,22 @@ def measured_copy_gbs(dev, nbytes=1 << 32, reps=5):
     out = {"blit": rate(lambda: b.copy_(a)), "float4": None}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pdp-lqr_amd", "pdplqr", "libpdplqr_probe.so")
     if os.path.exists(path):
-        fn = ctypes.CDLL(path).pdplqr_probe_copy
+        fn = ctypes.CDLL(path).pdplqr_probe_copy_mode
         fn.restype = ctypes.c_int
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 
-        def launcher(blocks):
+        def launcher(mode, blocks=0):
             def go():
-                rc = fn(a.data_ptr(), b.data_ptr(), nbytes, blocks, ctypes.c_void_p(stream.cuda_stream))
+                rc = fn(a.data_ptr(), b.data_ptr(), nbytes, mode, blocks, ctypes.c_void_p(stream.cuda_stream))
                 if rc != 0:
-                    raise RuntimeError(f"pdplqr_probe_copy: hip error {rc}")
+                    raise RuntimeError(f"pdplqr_probe_copy_mode: hip error {rc}")
             return go
 
-        out["float4"] = max(rate(launcher(bl)) for bl in (2048, 4096, 8192, 16384))
+        # mode 1: one 16-byte element per thread over a grid covering the
+        # buffer once -- the guide's float4 copy shape (6.21 TB/s against the
+        # guide's 6.29, scripts/copy_sweep.py, profiles/r06/copy_sweep.log);
+        # the grid-stride form (mode 0) peaks near 5.2
+        out["float4"] = max([rate(launcher(1))] + [rate(launcher(0, bl)) for bl in (8192, 32768)])
     del a, b
     torch.cuda.empty_cache()
     return out
@@ -717,7 +734,57 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
         t = _timed(step, steps, warmup, dev, dist)
     torch.cuda.synchronize(dev)
     ok = bool(torch.isfinite(out).all().item())
+    # the parts of the strong-scaling ratio, measured in this run (VERDICT r5
+    # item 6): every rank's own solve without the exchange (backward + forward
+    # on the gather of the timed solves), the exchange alone (the same
+    # all-gather of 3n^2+2n doubles per rank), and rank 0 solving the whole
+    # horizon alone on its GPU while the others wait
+    scal = {"rank_ms": [t * 1e3], "max_rank_ms": t * 1e3, "exchange_ms": 0.0}
+    if dist:
+        gat = sh._gathered.to(dev).contiguous()  # the last timed solve's gather
+        el1 = torch.empty(1, sh.es, dtype=torch.float64, device=dev)
+        with torch.cuda.stream(side):
+            def solve_local():
+                sh.backward(el1, last)
+                sh.forward(x0, gat, world, rank, out)
+            tl = _timed_local(solve_local, steps, warmup, dev)
+        per = [None] * world
+        dist.all_gather_object(per, tl * 1e3)
+        ex_in = torch.zeros(1, sh.es, dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
+        ex_out = torch.empty(world, 1, sh.es, dtype=ex_in.dtype, device=ex_in.device)
+
+        def exch():
+            if BACKEND == "nccl":
+                dist.all_gather_into_tensor(ex_out, ex_in)
+            else:
+                dist.all_gather(list(ex_out.unbind(0)), ex_in)
+        scal = {"rank_ms": per, "max_rank_ms": max(per),
+                "exchange_ms": _timed(exch, max(steps, 5), warmup, dev, dist) * 1e3}
     sh.close()
+    ref_ms = t * 1e3
+    if dist:
+        ref_ms = None
+        if rank == 0:  # the 1-GPU reference of the same horizon, same run
+            Ef, cf, Hf, hf, _ = gen_batch_device(n, m, Ntot, 1, seed=4242, device=dev)
+            sh1 = HorizonShard(n, m, Ntot, 1, device=local)
+            sh1.set_model(Ef, cf, Hf, hf)
+            del Ef, Hf
+            w1 = torch.zeros(1, Ntot * s + n, dtype=torch.float64, device=dev)
+            sh1.update_problem_data(w1, sigma=1e-6)
+            e1 = torch.empty(1, 1, sh1.es, dtype=torch.float64, device=dev)
+            sh1.synchronize()
+            sh1.set_stream(side.cuda_stream)
+            with torch.cuda.stream(side):
+                def one():
+                    sh1.backward(e1[0], True)
+                    sh1.forward(x0, e1, 1, 0, w1)
+                ref_ms = _timed_local(one, steps, warmup, dev) * 1e3
+            sh1.close()
+            del w1, e1, cf, hf
+            torch.cuda.empty_cache()
+        dist.barrier()
+    scal["ref_1rank_ms"] = ref_ms
+    scal["strong_scaling_ratio"] = (ref_ms / (t * 1e3)) if ref_ms else None
     oerr = None
     if world == 1:  # the whole horizon is this rank's: check it against the serial oracle
         oerr = _horizon_oracle_err([(E0[0], c[0], H0[0], h[0])], [out[0].cpu().numpy()], x0[0], n, m, Ntot)
@@ -740,6 +807,9 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
     return {"N": Ntot, "nx": n, "nu": m, "n_gpus": world, "ms_per_solve": t * 1e3, "stages_per_s": Ntot / t,
             "scaling": "strong", "finite": ok, "oracle_rel_err": oerr,
             "exchange": "all-gather of 3n^2+2n doubles per rank",
+            "parts": dict(scal, note="rank_ms: each rank's backward + forward without the exchange; exchange_ms: "
+                                      "the all-gather alone; ref_1rank_ms: rank 0 solving the whole horizon alone "
+                                      "in this run; strong_scaling_ratio = ref_1rank_ms / ms_per_solve"),
             "roofline": roofline_block(bst, Ntot, t * 1e3, f"C4_N{Ntot}_R{world}",
                                        ("k_seg_bwd_aug", "k_seg_scan", "k_seg_maps", "k_map_scan", "k_seg_fwd_dma"),
                                        flops_stage=103235 + 59968,

@@ -92,25 +92,80 @@ static void model_destroy(orc_model *md) {
 /* Largest stage size of the restatement. */
 #define ORC_SMAX 256
 
-/* Eigen llt_inplace<Lower>::unblocked (Eigen/src/Cholesky/LLT.h), used by
- * Eigen for sizes < 32 and restated here for every size.  Writes the lower
- * factor into L (ld = dim) with a zero upper triangle, as
- * `L = M.llt().matrixL()` does (lqr_kernel.hpp:89,126).  Returns -1 on
- * success or the failing column (the reference ignores it). */
+/* Eigen llt_inplace<Lower>::unblocked (Eigen/src/Cholesky/LLT.h) on the
+ * diagonal block [off, off + sz) of the column-major L (ld): left-looking --
+ * column k takes the products of the block's earlier columns only; on a pivot
+ * <= 0 it returns k (relative to off) with column k and the later columns of
+ * the block untouched.  Returns -1 on success. */
+static int llt_unblocked(double *L, int ld, int off, int sz) {
+    int i, k, p;
+    for (k = 0; k < sz; ++k) {
+        double x = L[IX(off + k, off + k, ld)];
+        for (p = 0; p < k; ++p) x -= L[IX(off + k, off + p, ld)] * L[IX(off + k, off + p, ld)];
+        if (x <= 0.0) return k;
+        x = sqrt(x);
+        L[IX(off + k, off + k, ld)] = x;
+        for (i = k + 1; i < sz; ++i) {
+            double a = L[IX(off + i, off + k, ld)];
+            for (p = 0; p < k; ++p) a -= L[IX(off + i, off + p, ld)] * L[IX(off + k, off + p, ld)];
+            L[IX(off + i, off + k, ld)] = a / x;
+        }
+    }
+    return -1;
+}
+
+/* Eigen's block size of llt_inplace<Lower>::blocked for a matrix of order
+ * dim (0: dim < 32, the unblocked form runs). */
+static int llt_block_size(int dim) {
+    int bs;
+    if (dim < 32) return 0;
+    bs = dim / 8;
+    bs = (bs / 16) * 16;
+    if (bs < 8) bs = 8;
+    if (bs > 128) bs = 128;
+    return bs;
+}
+
+/* `L = M.llt().matrixL()` (lqr_kernel.hpp:89,126; condensed_system.hpp:188-247):
+ * Eigen's LLT::compute runs llt_inplace<Lower>::blocked -- the unblocked form
+ * below order 32, else blocks of llt_block_size(dim) columns: the diagonal
+ * block A11 unblocked, then A21 <- A21 A11^{-T}, then A22 -= A21 A21^T.  A
+ * pivot <= 0 inside A11 ends it: the columns of the finished blocks hold L, A11
+ * its columns up to the pivot (rows inside A11), and every other entry of the
+ * later columns (A21 of the block included) the Schur complement of the
+ * finished blocks.  The reference ignores the failure and uses that lower
+ * triangle.  Writes L (ld = dim) with a zero upper triangle;
+ * returns -1 on success or the failing column. */
 static int llt_lower(const double *M, double *L, int dim) {
     int i, j, k, p, fail = -1;
+    const int bs = llt_block_size(dim);
     for (j = 0; j < dim; ++j)
         for (i = 0; i < dim; ++i) L[IX(i, j, dim)] = M[IX(i, j, dim)];
-    for (k = 0; k < dim; ++k) {
-        double x = L[IX(k, k, dim)];
-        for (p = 0; p < k; ++p) x -= L[IX(k, p, dim)] * L[IX(k, p, dim)];
-        if (x <= 0.0) { fail = k; break; }
-        x = sqrt(x);
-        L[IX(k, k, dim)] = x;
-        for (i = k + 1; i < dim; ++i) {
-            double a = L[IX(i, k, dim)];
-            for (p = 0; p < k; ++p) a -= L[IX(i, p, dim)] * L[IX(k, p, dim)];
-            L[IX(i, k, dim)] = a / x;
+    if (!bs) {
+        fail = llt_unblocked(L, dim, 0, dim);
+    } else {
+        for (k = 0; k < dim; k += bs) {
+            const int b = bs < dim - k ? bs : dim - k, rs = dim - k - b;
+            const int ret = llt_unblocked(L, dim, k, b);
+            if (ret >= 0) {
+                fail = k + ret;
+                break;
+            }
+            /* A21 <- A21 A11^{-T}: row by row, forward substitution with A11 */
+            for (i = k + b; i < dim; ++i)
+                for (j = 0; j < b; ++j) {
+                    double a = L[IX(i, k + j, dim)];
+                    for (p = 0; p < j; ++p) a -= L[IX(i, k + p, dim)] * L[IX(k + j, k + p, dim)];
+                    L[IX(i, k + j, dim)] = a / L[IX(k + j, k + j, dim)];
+                }
+            /* A22 -= A21 A21^T (lower triangle) */
+            (void)rs;
+            for (j = k + b; j < dim; ++j)
+                for (i = j; i < dim; ++i) {
+                    double a = L[IX(i, j, dim)];
+                    for (p = 0; p < b; ++p) a -= L[IX(i, k + p, dim)] * L[IX(j, k + p, dim)];
+                    L[IX(i, j, dim)] = a;
+                }
         }
     }
     for (j = 0; j < dim; ++j)

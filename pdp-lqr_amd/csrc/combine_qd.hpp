@@ -25,24 +25,22 @@
 // at cond(P_b) = 1e8; the two-Cholesky form 1e-13).
 //
 // Schedule: 48 pivots in 6 blocks of 8.  The 96 x 96 matrix (+ the linear
-// column) lives in 16 x 16 MFMA tiles, lower triangle only (21 tiles).  Per
-// block of pivots J (two barriers, no products outside the elimination):
-//   1. the owners publish the pivot rows M[J, :] to LDS (by symmetry the
-//      pivot COLUMNS of the tiles below the diagonal);            -> barrier A
-//   2. waves 2, 3 (one thread per column) factor the 8 x 8 pivot block LDL^T
-//      (wave-uniform) and form V = L^{-1} M[J, col], W = D^{-1} V;  -> barrier B
-//   3. every active tile takes the rank-8 update M[I, K] -= V[:, I]^T W[:, K]
+// column) lives in 16 x 16 MFMA tiles, lower triangle only (21 tiles).  Wave 0
+// owns the three diagonal tiles (every pivot block lives in one of them); waves
+// 1..3 own the others.  Per block t of pivots J:
+//   1. wave 0 takes block t - 1's update of the diagonal tile holding J first,
+//      publishes its rows J, factors the 8 x 8 pivot block LDL^T (wave-uniform)
+//      and publishes L, 1/d; meanwhile the owners of the tiles below it take
+//      that update and publish the pivot COLUMNS J (= rows J by symmetry), then
+//      the updates of the tiles whose pivots come later;     -> barrier A
+//   2. every thread forms V = L^{-1} M[J, col], W = D^{-1} V for one column
+//      (97 columns over the four waves);                   -> barrier B
+//   3. the linear column row by row; the tiles take M[I, K] -= V[:, I]^T W[:, K]
 //      as two MFMAs (A operand V of the tile's rows, B operand W of its
-//      columns, both read from LDS); the linear column row by row.
-// Roles: waves 0, 1 own the 15 tiles of the junction columns (and the linear
-// column, one row a thread); waves 2, 3 own the 6 tiles of the outer block and
-// do step 2.  The critical path of a block is  B -> the tiles holding the next
-// pivots (K = their tile) -> publish -> A -> LDL^T, V, W -> B;  every other
-// update of the block (the outer tiles, junction tiles whose pivots come
-// later) has its operands read before A and its MFMAs issued after it, beside
-// step 2 of the next block.  Each wave's code is specialised at compile time
-// (tile list, step), so the MFMAs of a step issue back to back without
-// branches.
+//      columns, read from LDS), the tiles of the next pivots first (step 1).
+// Two barriers a block, no products outside the elimination.  Each wave's code
+// is specialised at compile time (tile list, step), so the MFMAs of a step
+// issue back to back without branches.
 #pragma once
 
 #include "combine_tiles.hpp"
@@ -58,7 +56,7 @@ constexpr int QD_PRS = 10;                // pivot rows: [column][8] at stride 1
 constexpr int QD_VWS = 18;                // [column][V 0..7 | W 0..7] at stride 18 (odd bank step)
 constexpr int QD_STEPS = QD_NJ / 8;
 
-__host__ __device__ constexpr int qd_smem_doubles() { return QD_NCOL * QD_PRS + QD_NCOL * QD_VWS + 2; }
+__host__ __device__ constexpr int qd_smem_doubles() { return QD_NCOL * QD_PRS + QD_NCOL * QD_VWS + 36 + 2; }
 
 // Phase stamps (diagnostic builds with -DPDPLQR_COMB_PROFILE, kernels_parallel.hip):
 // shader-clock sums over the 6 blocks of one combine, by thread 0 (a junction
@@ -84,26 +82,30 @@ struct QdProf {
     } while (0)
 #endif
 
-// Tile lists of waves 1..3 (compile time; wave 0 owns no tile).  The tiles
-// whose column holds the next block's pivots (K = 0 at block 0, 1 at blocks
-// 1-2, 2 at blocks 3-4) are the critical ones: 2/2/2, 2/2/1, 1/2/1 a wave;
-// 7 tiles each in all.
+// Tile lists (compile time).  Wave 0: the diagonal tiles.  Waves 1..3: the
+// others, balanced for the tiles holding the next block's pivots (K = 0 at
+// block 0, 1 at blocks 1-2, 2 at blocks 3-4): 2/2/1, 1/2/1, 1/1/1.
 template <int W>
 struct QdTiles;
 template <>
+struct QdTiles<0> {
+    static constexpr int n = 3;
+    static constexpr int I[6] = {0, 1, 2, 0, 0, 0}, K[6] = {0, 1, 2, 0, 0, 0};
+};
+template <>
 struct QdTiles<1> {
-    static constexpr int n = 7;
-    static constexpr int I[7] = {0, 1, 1, 2, 2, 3, 4}, K[7] = {0, 0, 1, 1, 2, 3, 3};
+    static constexpr int n = 6;
+    static constexpr int I[6] = {1, 2, 2, 3, 3, 4}, K[6] = {0, 0, 1, 2, 3, 3};
 };
 template <>
 struct QdTiles<2> {
-    static constexpr int n = 7;
-    static constexpr int I[7] = {2, 3, 3, 4, 3, 4, 4}, K[7] = {0, 0, 1, 1, 2, 2, 4};
+    static constexpr int n = 6;
+    static constexpr int I[6] = {3, 4, 3, 4, 4, 4}, K[6] = {0, 0, 1, 1, 2, 4};
 };
 template <>
 struct QdTiles<3> {
-    static constexpr int n = 7;
-    static constexpr int I[7] = {4, 5, 5, 5, 5, 5, 5}, K[7] = {0, 0, 1, 2, 3, 4, 5};
+    static constexpr int n = 6;
+    static constexpr int I[6] = {5, 5, 5, 5, 5, 5}, K[6] = {0, 1, 2, 3, 4, 5};
 };
 
 // Tile (I, K) of the matrix before the elimination, branch-free: every
@@ -157,10 +159,11 @@ __device__ __forceinline__ double qd_lin_bf(const ElemIn &ea, const ElemIn &eb, 
 }
 
 template <int W>
-__device__ __forceinline__ void qd_assemble(d4 (&Q)[7], const ElemIn &ea, const ElemIn &eb, bool fcf, int g, int c) {
+__device__ __forceinline__ void qd_assemble(d4 (&Q)[6], const ElemIn &ea, const ElemIn &eb, bool fcf, int g, int c) {
     using TL = QdTiles<W>;
-#define QD_ASM(s) Q[s] = qd_tile<TL::I[s], TL::K[s]>(ea, eb, fcf, g, c);
-    QD_ASM(0) QD_ASM(1) QD_ASM(2) QD_ASM(3) QD_ASM(4) QD_ASM(5) QD_ASM(6)
+#define QD_ASM(s) \
+    if constexpr ((s) < TL::n) Q[s] = qd_tile<TL::I[s], TL::K[s]>(ea, eb, fcf, g, c);
+    QD_ASM(0) QD_ASM(1) QD_ASM(2) QD_ASM(3) QD_ASM(4) QD_ASM(5)
 #undef QD_ASM
 }
 
@@ -168,7 +171,7 @@ __device__ __forceinline__ void qd_assemble(d4 (&Q)[7], const ElemIn &ea, const 
 // block: [A0, A1, B0, B1] = V of its rows and W of its columns at the pivots
 // g and 4 + g (K chunks 0 and 1).
 template <int W, int LO, int HI>
-__device__ __forceinline__ void qd_operands(double (&op)[7][4], const double *vw, int g, int c) {
+__device__ __forceinline__ void qd_operands(double (&op)[6][4], const double *vw, int g, int c) {
     using TL = QdTiles<W>;
 #pragma unroll
     for (int s = 0; s < TL::n; ++s) {
@@ -185,9 +188,9 @@ __device__ __forceinline__ void qd_operands(double (&op)[7][4], const double *vw
 // then every second (independent MFMAs back to back).  SPLIT: the second
 // chunk on its own accumulator (one product deep; the critical tiles).
 template <int W, int LO, int HI, bool SPLIT>
-__device__ __forceinline__ void qd_update(d4 (&Q)[7], const double (&op)[7][4]) {
+__device__ __forceinline__ void qd_update(d4 (&Q)[6], const double (&op)[6][4]) {
     using TL = QdTiles<W>;
-    d4 Z[7];
+    d4 Z[6];
 #pragma unroll
     for (int s = 0; s < TL::n; ++s)
         if (TL::K[s] >= LO && TL::K[s] <= HI) Q[s] = mfma_f64(-op[s][0], op[s][2], Q[s]);
@@ -203,144 +206,177 @@ __device__ __forceinline__ void qd_update(d4 (&Q)[7], const double (&op)[7][4]) 
             if (TL::K[s] >= LO && TL::K[s] <= HI) Q[s] += Z[s];
 }
 
-// Waves 1..3: the tiles.  After barrier B of block t: the tiles holding block
-// t + 1's pivots take block t's update and publish (critical); the other
-// active tiles read their operands and take the update after barrier A of
-// block t + 1, beside wave 0's factorisation.
-template <int W>
-__device__ __forceinline__ void qd_tile_wave(d4 (&Q)[7], double *pr, const double *vw, int g, int c) {
+// Publish block T's pivot rows M[8 T .. 8 T + 7, :] from the tiles of column
+// tile T / 2 (the diagonal tile: rows J at its 16 columns; below it: the
+// columns J at its 16 rows, by symmetry).
+template <int W, int T>
+__device__ __forceinline__ void qd_publish(const d4 (&Q)[6], double *pr, int g, int c) {
     using TL = QdTiles<W>;
-    constexpr int PRS = QD_PRS;
-    double op[7][4];
-#if QD_PROF
-    QdProf prof;
-#endif
+    constexpr int pt = T >> 1, h = T & 1;
 #pragma unroll
-    for (int t = 0; t < QD_STEPS; ++t) {
-        const int pt = t >> 1, h = t & 1;
-        // ---- publish block t's pivot rows M[8 t .. 8 t + 7, :] ----
+    for (int s = 0; s < TL::n; ++s) {
+        if (TL::K[s] != pt) continue;
+        if (TL::I[s] == pt) {
 #pragma unroll
-        for (int s = 0; s < TL::n; ++s) {
-            if (TL::K[s] != pt) continue;
-            if (TL::I[s] == pt) {  // the diagonal tile: rows J at its 16 columns
+            for (int rr = 0; rr < 2; ++rr) pr[(16 * pt + c) * QD_PRS + 4 * rr + g] = Q[s][2 * h + rr];
+        } else if ((c >> 3) == h) {
 #pragma unroll
-                for (int rr = 0; rr < 2; ++rr) pr[(16 * pt + c) * PRS + 4 * rr + g] = Q[s][2 * h + rr];
-            } else if ((c >> 3) == h) {  // below it: columns J at its 16 rows (symmetry)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) pr[(16 * TL::I[s] + 4 * r + g) * PRS + (c & 7)] = Q[s][r];
-            }
+            for (int r = 0; r < 4; ++r) pr[(16 * TL::I[s] + 4 * r + g) * QD_PRS + (c & 7)] = Q[s][r];
         }
-        QD_MARK(0);
-        __syncthreads();  // A_t
-        QD_MARK(3);
-        // block t - 1's updates of the tiles whose pivots come later
-        if (t == 1) qd_update<W, 1, 5, false>(Q, op);
-        if (t == 2 || t == 3) qd_update<W, 2, 5, false>(Q, op);
-        if (t == 4 || t == 5) qd_update<W, 3, 5, false>(Q, op);
-        __syncthreads();  // B_t
-        QD_MARK(1);
-        // block t's update: the tiles of block t + 1's pivots now, the rest read
-        if (t == 0) {
-            qd_operands<W, 0, 0>(op, vw, g, c);
-            qd_update<W, 0, 0, true>(Q, op);
-            qd_operands<W, 1, 5>(op, vw, g, c);
-        } else if (t == 1 || t == 2) {
-            qd_operands<W, 1, 1>(op, vw, g, c);
-            qd_update<W, 1, 1, true>(Q, op);
-            qd_operands<W, 2, 5>(op, vw, g, c);
-        } else if (t == 3 || t == 4) {
-            qd_operands<W, 2, 2>(op, vw, g, c);
-            qd_update<W, 2, 2, true>(Q, op);
-            qd_operands<W, 3, 5>(op, vw, g, c);
-        } else {
-            qd_operands<W, 3, 5>(op, vw, g, c);
-        }
-        QD_MARK(2);
     }
-    qd_update<W, 3, 5, false>(Q, op);  // block 5
-#if QD_PROF
-    if (threadIdx.x == 64) prof.save(23);
-#endif
 }
 
-// Wave 0: per block, the LDL^T of the 8 x 8 pivot block (wave-uniform) and
-// V = L^{-1} M[J, col], W = D^{-1} V of every column (columns lane, lane + 64),
-// and the linear column (rows lane, lane + 64).
-__device__ __forceinline__ bool qd_factor_wave(double (&lin)[2], double *pr, double *vw, int lane) {
-    constexpr int PRS = QD_PRS, VWS = QD_VWS, NCOL = QD_NCOL, NT = QD_NT, AUG = QD_AUG;
+// Wave 0, block T: LDL^T of the pivot block in pr (wave-uniform), L (strict
+// lower, row-major packed) and 1/d to lb.  False if a pivot has the wrong sign.
+template <int T>
+__device__ __forceinline__ bool qd_factor(const double *pr, double *lb, int lane) {
+    constexpr int J0 = 8 * T;
+    double a[8][8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l)
+#pragma unroll
+        for (int l2 = 0; l2 <= l; ++l2) a[l][l2] = pr[(J0 + l2) * QD_PRS + l];
+    bool ok = true;
+    double inv[8], L[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const double d = a[j][j];
+        ok = ok && ((j & 1) == 0 ? d > 0.0 : d < 0.0);  // J0 even: j even is an x pivot
+        inv[j] = rcp_f64(d);
+#pragma unroll
+        for (int i = j + 1; i < 8; ++i) L[i][j] = a[i][j] * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < 8; ++i)
+#pragma unroll
+            for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-L[i][j], a[k][j], a[i][k]);
+    }
+    // wave-uniform values: one lane stores them (16-byte pairs)
+    if (lane == 0) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        double w[36];
+#pragma unroll
+        for (int i = 1; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) w[i * (i - 1) / 2 + j] = L[i][j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[28 + j] = inv[j];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) reinterpret_cast<d2 *>(lb)[q] = d2{w[2 * q], w[2 * q + 1]};
+    }
+    return ok;
+}
+
+// Every wave: the column / linear-column row of this thread (25 per wave).
+__device__ __forceinline__ int qd_col(int tid) { return 25 * (tid >> 6) + (tid & 63); }
+
+// One combine's block loop on wave W.
+template <int W>
+__device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, double *vw, double *lb, int g, int c,
+                                        int tid) {
+    constexpr int PRS = QD_PRS, VWS = QD_VWS, AUG = QD_AUG, NCOL = QD_NCOL, NT = QD_NT;
+    const int lane = tid & 63;
+    const int col = qd_col(tid);
+    const bool own = (tid & 63) < 25 && col < NCOL;  // this thread's column (and row of the linear column)
+    double op[6][4], V[8];
     bool ok = true;
 #if QD_PROF
     QdProf prof;
 #endif
-#pragma unroll 1
+    // block 0's pivot rows and (wave 0) its factorisation, from the assembled tiles
+    qd_publish<W, 0>(Q, pr, g, c);
+    if constexpr (W == 0) {
+        wave_sync();
+        ok = qd_factor<0>(pr, lb, lane);
+    }
+#pragma unroll
     for (int t = 0; t < QD_STEPS; ++t) {
         const int J0 = 8 * t;
-        // publish the linear column's rows J (rows lane and lane + 64)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int row = lane + 64 * u;
-            if (row >= J0 && row < J0 + 8) pr[AUG * PRS + (row - J0)] = lin[u];
-        }
-        __syncthreads();  // A_t
+        if (own && col >= J0 && col < J0 + 8) pr[AUG * PRS + (col - J0)] = lin;  // linear column, rows J
         QD_MARK(0);
-        double a[8][8], x[2][8];
+        __syncthreads();  // A_t
+        QD_MARK(1);
+        // ---- V, W of this thread's column ----
+        {
+            const bool act = own && col >= J0 + 8;
+            const int cc = act ? col : J0 + 8;  // clamped (branch-free reads)
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            double x[8], L[28], inv[8];
 #pragma unroll
-        for (int l = 0; l < 8; ++l)
-#pragma unroll
-            for (int l2 = 0; l2 <= l; ++l2) a[l][l2] = pr[(J0 + l2) * PRS + l];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int col = lane + 64 * u, cc = (col >= J0 + 8 && col < NCOL) ? col : J0 + 8;  // clamped
-#pragma unroll
-            for (int l = 0; l < 8; ++l) x[u][l] = pr[cc * PRS + l];
-        }
-        // right-looking LDL^T of the pivot block carrying the two columns: after
-        // pivot j, x[j] = V[j] = (L^{-1} x)[j] (the fmas of a forward
-        // substitution with L, in its order)
-        double inv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const double d = a[j][j];
-            ok = ok && ((j & 1) == 0 ? d > 0.0 : d < 0.0);  // J0 even: j even is an x pivot
-            inv[j] = rcp_f64(d);
-            double Lj[8];
-#pragma unroll
-            for (int i = j + 1; i < 8; ++i) Lj[i] = a[i][j] * inv[j];
-#pragma unroll
-            for (int i = j + 1; i < 8; ++i) {
-#pragma unroll
-                for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-Lj[i], a[k][j], a[i][k]);
-#pragma unroll
-                for (int u = 0; u < 2; ++u) x[u][i] = __builtin_fma(-Lj[i], x[u][j], x[u][i]);
+            for (int l = 0; l < 4; ++l) {
+                const d2 v = reinterpret_cast<const d2 *>(pr + cc * PRS)[l];
+                x[2 * l] = v.x;
+                x[2 * l + 1] = v.y;
             }
-        }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int col = lane + 64 * u;
-            if (col >= J0 + 8 && col < NCOL) {
+            for (int q = 0; q < 14; ++q) {
+                const d2 v = reinterpret_cast<const d2 *>(lb)[q];
+                L[2 * q] = v.x;
+                L[2 * q + 1] = v.y;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const d2 v = reinterpret_cast<const d2 *>(lb + 28)[q];
+                inv[2 * q] = v.x;
+                inv[2 * q + 1] = v.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                double v = x[j];
+#pragma unroll
+                for (int k = 0; k < j; ++k) v = __builtin_fma(-L[j * (j - 1) / 2 + k], V[k], v);
+                V[j] = v;
+            }
+            if (act) {
                 double *o = vw + col * VWS;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    o[j] = x[u][j];
-                    o[8 + j] = x[u][j] * inv[j];
+                    o[j] = V[j];
+                    o[8 + j] = V[j] * inv[j];
                 }
             }
         }
-        wave_sync();  // W of the linear column (lane 32's second column) to every lane
-        const double *w = vw + AUG * VWS + 8;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {  // linear column, row lane + 64 u: -= V[:, row]^T W[:, AUG]
-            const int row = lane + 64 * u;
-            if (row >= J0 + 8 && row < NT)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) lin[u] = __builtin_fma(-x[u][j], w[j], lin[u]);
-        }
-        QD_MARK(1);
-        __syncthreads();  // B_t
         QD_MARK(2);
+        __syncthreads();  // B_t
+        QD_MARK(3);
+        if (own && col >= J0 + 8 && col < NT) {  // linear column, row col: -= V[:, col]^T W[:, AUG]
+            const double *w = vw + AUG * VWS + 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) lin = __builtin_fma(-V[j], w[j], lin);
+        }
+        // ---- block t's update: the tiles of block t + 1's pivots first ----
+        if (t == QD_STEPS - 1) {
+            qd_operands<W, 3, 5>(op, vw, g, c);
+            qd_update<W, 3, 5, false>(Q, op);
+            break;
+        }
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int pn = (t + 1) >> 1;  // column tile of block t + 1's pivots
+#define QD_STEP(TT, PN)                                            \
+    if (t == (TT)) {                                               \
+        qd_operands<W, PN, PN>(op, vw, g, c);                      \
+        qd_update<W, PN, PN, true>(Q, op);                         \
+        qd_operands<W, PN + 1, 5>(op, vw, g, c);                   \
+        if constexpr (W == 0) qd_update<W, PN + 1, 5, false>(Q, op); \
+        qd_publish<W, (TT) + 1>(Q, pr, g, c);                      \
+        if constexpr (W == 0) {                                    \
+            wave_sync();                                           \
+            ok = qd_factor<(TT) + 1>(pr, lb, lane) && ok;          \
+        } else {                                                   \
+            qd_update<W, PN + 1, 5, false>(Q, op);                 \
+        }                                                          \
+    }
+        QD_STEP(0, 0)
+        QD_STEP(1, 1)
+        QD_STEP(2, 1)
+        QD_STEP(3, 2)
+        QD_STEP(4, 2)
+#undef QD_STEP
+        (void)pn;
     }
 #if QD_PROF
-    if (threadIdx.x == 0) prof.save(27);
+    if (tid == 0) prof.save(27);
+    if (tid == 64) prof.save(23);
 #endif
     return ok;
 }
@@ -356,27 +392,22 @@ __device__ __forceinline__ bool qd_combine(double *oF, double *oC, double *of, d
     constexpr int XS = QD_NJ, LE = QD_NJ + n;
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on the role
-    double *pr = qs, *vw = qs + NCOL * PRS;
-    int *okw = reinterpret_cast<int *>(vw + NCOL * VWS);
+    double *pr = qs, *vw = qs + NCOL * PRS, *lb = vw + NCOL * VWS;
+    int *okw = reinterpret_cast<int *>(lb + 36);
     COMB_MARK(0);
-    d4 Q[7];
-    double lin[2] = {0.0, 0.0};
-    bool ok = true;
-    if (wv == 0) {
-        lin[0] = qd_lin_bf(ea, eb, fcf, lane);
-        lin[1] = qd_lin_bf(ea, eb, fcf, lane < 32 ? lane + 64 : 0);
-    } else if (wv == 1) {
-        qd_assemble<1>(Q, ea, eb, fcf, g, c);
-    } else if (wv == 2) {
-        qd_assemble<2>(Q, ea, eb, fcf, g, c);
-    } else {
-        qd_assemble<3>(Q, ea, eb, fcf, g, c);
-    }
+    d4 Q[6];
+    const int col = qd_col(tid);
+    double lin = qd_lin_bf(ea, eb, fcf, (lane < 25 && col < NT) ? col : 0);  // row col of the linear column
+    if (wv == 0) qd_assemble<0>(Q, ea, eb, fcf, g, c);
+    else if (wv == 1) qd_assemble<1>(Q, ea, eb, fcf, g, c);
+    else if (wv == 2) qd_assemble<2>(Q, ea, eb, fcf, g, c);
+    else qd_assemble<3>(Q, ea, eb, fcf, g, c);
     COMB_MARK(1);
-    if (wv == 0) ok = qd_factor_wave(lin, pr, vw, lane);
-    else if (wv == 1) qd_tile_wave<1>(Q, pr, vw, g, c);
-    else if (wv == 2) qd_tile_wave<2>(Q, pr, vw, g, c);
-    else qd_tile_wave<3>(Q, pr, vw, g, c);
+    bool ok = true;
+    if (wv == 0) ok = qd_wave<0>(Q, lin, pr, vw, lb, g, c, tid);
+    else if (wv == 1) qd_wave<1>(Q, lin, pr, vw, lb, g, c, tid);
+    else if (wv == 2) qd_wave<2>(Q, lin, pr, vw, lb, g, c, tid);
+    else qd_wave<3>(Q, lin, pr, vw, lb, g, c, tid);
     COMB_MARK(7);
     // ---- outputs: x_s = rows / columns 48 .. 71, lam_e = 72 .. 95 ----
     auto out_tile = [&](const d4 &T, int I, int K) {
@@ -399,19 +430,19 @@ __device__ __forceinline__ bool qd_combine(double *oF, double *oC, double *of, d
             }
         }
     };
-    if (wv == 0) {
-        if (lane >= XS) op[lane - XS] = lin[0];                       // rows 48 .. 63
-        if (lane < LE - 64) op[lane + 64 - XS] = lin[1];              // rows 64 .. 71
-        if (fcf && lane >= LE - 64 && lane < NT - 64) of[lane + 64 - LE] = lin[1];  // rows 72 .. 95
-    } else if (wv == 1) {
-        out_tile(Q[5], 3, 3);
-        out_tile(Q[6], 4, 3);
+    if (wv == 1) {
+        out_tile(Q[4], 3, 3);
+        out_tile(Q[5], 4, 3);
     } else if (wv == 2) {
-        out_tile(Q[6], 4, 4);
-    } else if (fcf) {
-        out_tile(Q[4], 5, 3);
-        out_tile(Q[5], 5, 4);
-        out_tile(Q[6], 5, 5);
+        out_tile(Q[5], 4, 4);
+    } else if (wv == 3 && fcf) {
+        out_tile(Q[3], 5, 3);
+        out_tile(Q[4], 5, 4);
+        out_tile(Q[5], 5, 5);
+    }
+    if (lane < 25) {
+        if (col >= XS && col < LE) op[col - XS] = lin;
+        if (fcf && col >= LE && col < NT) of[col - LE] = lin;
     }
     if (tid == 0) okw[0] = 1;
     __syncthreads();

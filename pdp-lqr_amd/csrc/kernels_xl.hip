@@ -10,10 +10,9 @@
 //         V = E~^T Lxx_{k+1},  M = H~ + V V^T,  L = llt(M)
 //         lp = h~ + E~^T (Lxx (Lxx^T c) + p_{k+1}),  lu <- Luu^{-1} lu,
 //         p_k = lp_x - Lxu lu
-//     with Eigen's LLT stop (a non-positive reduced pivot leaves its column
-//     and every later one at the input values, device_common.hpp
-//     chol_restore_tail; here they are copied back from the input) and the
-//     same status as every backward.
+//     with Eigen's LLT stop as LLT::compute leaves it for these orders (>= 65:
+//     the blocked form, xl_la.hpp xl_llt -- the later columns at the Schur
+//     complement of the finished blocks) and the same status as every backward.
 //     Records FR_k = [L(:, 0:m) | lu'], the factor cache (packed L_k, lp_k)
 //     when it exists;
 //   * k_riccati_bwd_nofact_xl: step_without_factorization (:150-178) on the

@@ -67,7 +67,68 @@ __global__ __launch_bounds__(256) void k_probe_copy(const double2 *__restrict__ 
     for (; i < n; i += stride) b[i] = a[i];
 }
 
+// Variants of the same copy (bench.py reports the best; scripts/copy_sweep.py):
+//   mode 1: one 16-byte element per thread, a grid that covers the buffer once;
+//   mode 2: four consecutive 16-byte elements per thread (64 B), grid covers once;
+//   mode 3: mode 2 with non-temporal loads and stores (streamed once, no reuse).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_probe_copy_v(const double2 *__restrict__ a, double2 *__restrict__ b,
+                                                      size_t n) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (MODE == 1) {
+        if (t < n) b[t] = a[t];
+    } else {
+        const size_t i = 4 * t;
+        if (i + 3 < n) {
+            double2 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (MODE == 3) {
+                    v[k].x = __builtin_nontemporal_load(&a[i + k].x);
+                    v[k].y = __builtin_nontemporal_load(&a[i + k].y);
+                } else {
+                    v[k] = a[i + k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (MODE == 3) {
+                    __builtin_nontemporal_store(v[k].x, &b[i + k].x);
+                    __builtin_nontemporal_store(v[k].y, &b[i + k].y);
+                } else {
+                    b[i + k] = v[k];
+                }
+            }
+        } else {
+            for (size_t j = i; j < n; ++j) b[j] = a[j];
+        }
+    }
+}
+
 }  // namespace
+
+// The copy variants above (mode 1..3; mode 0 = pdplqr_probe_copy's grid-stride
+// form with `blocks` blocks).  Returns 0 or a hipError_t.
+extern "C" int pdplqr_probe_copy_mode(const void *src, void *dst, size_t nbytes, int mode, int blocks, void *stream) {
+    if (nbytes % 16) return (int)hipErrorInvalidValue;
+    const size_t n = nbytes / 16;
+    const hipStream_t st = (hipStream_t)stream;
+    const double2 *a = (const double2 *)src;
+    double2 *b = (double2 *)dst;
+    if (mode == 0) {
+        if (blocks < 1) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_probe_copy, dim3(blocks), dim3(256), 0, st, a, b, n);
+    } else if (mode == 1) {
+        hipLaunchKernelGGL(k_probe_copy_v<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b, n);
+    } else if (mode == 2 || mode == 3) {
+        const size_t th = (n + 3) / 4;
+        if (mode == 2) hipLaunchKernelGGL(k_probe_copy_v<2>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, a, b, n);
+        else hipLaunchKernelGGL(k_probe_copy_v<3>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, a, b, n);
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
 
 // 16-byte streaming copy of nbytes (a multiple of 16); returns 0 or a hipError_t.
 extern "C" int pdplqr_probe_copy(const void *src, void *dst, size_t nbytes, int blocks, void *stream) {

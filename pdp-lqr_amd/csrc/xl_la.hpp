@@ -27,15 +27,38 @@ __device__ __noinline__ void xl_mm(double *C, int ldc, const double *A, int lda,
         }
 }
 
+// dst <- src (lower triangle of an n x n block, ld)
+__device__ __noinline__ void xl_copy_lower(double *dst, const double *src, int ld, int n) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < n * n; q += 256) {
+        const int i = q % n, j = q / n;
+        if (i >= j) dst[i + (long long)j * ld] = src[i + (long long)j * ld];
+    }
+    __syncthreads();
+}
+
 constexpr int XL_PW = 16;  // panel width of xl_llt
+
+// Eigen's block size of llt_inplace<Lower>::blocked (Eigen/src/Cholesky/LLT.h)
+// for order n; 0 below 32 (the unblocked form).  The oracle's llt_block_size.
+__device__ __forceinline__ int xl_eigen_bs(int n) {
+    if (n < 32) return 0;
+    const int bs = (n / 8 / 16) * 16;
+    return bs < 8 ? 8 : (bs > 128 ? 128 : bs);
+}
 
 // In-place blocked right-looking Cholesky of the lower triangle of A (n x n,
 // ld) with Eigen's LLT stop: pivot j < m must be positive (else flagged and the
 // factorisation goes on, as the tiled kernels do), a pivot j >= m that is not
-// positive stops it with column j and every later one at their input values
-// (Eigen factors left-looking, llt_inplace::unblocked, so those columns were
-// never touched there; here they are copied back from A0, the input), flagged
-// only when psd_bad.  Per panel of XL_PW columns: the panel (every row below
+// positive stops it, flagged only when psd_bad.  What the stop leaves is
+// Eigen's: LLT::compute factors blocks of xl_eigen_bs(n) columns (the diagonal
+// block A11 left-looking, then A21 <- A21 A11^{-T}, A22 -= A21 A21^T), so when
+// pivot j in the block starting at k0 is not positive, the columns before k0
+// hold L, A11's columns k0 .. j - 1 their factor (rows inside A11), and every
+// other entry of the columns >= k0 the Schur complement of the columns < k0:
+// recomputed from A0 (the input) as A0 - L(:, :k0) L(:, :k0)^T, with A11's
+// factored columns kept (the oracle's llt_lower; below order 32 -- unblocked,
+// k0 = j -- the input values from column j on).  Per panel of XL_PW columns: the panel (every row below
 // its top) is factored in LDS, one barrier per pivot (the update with the raw
 // pivot column a_ij a_lj / d_j, the columns scaled when written back), then
 // the trailing lower triangle takes the panel's rank-XL_PW update on MFMA
@@ -86,25 +109,32 @@ __device__ __noinline__ bool xl_llt(double *A, int ld, int n, int m, const doubl
         }
     }
     __syncthreads();
-    if (jdead < n) {  // Eigen's stop: the input values from column jdead on
-        for (int q = tid; q < n * n; q += 256) {
-            const int i = q % n, j = q / n;
-            if (i >= j && j >= jdead) A[i + (long long)j * ld] = A0[i + (long long)j * ld];
+    if (jdead < n) {  // Eigen's stop (block-uniform, rare)
+        const int bs = xl_eigen_bs(n);
+        const int k0 = bs ? (jdead / bs) * bs : jdead, b = bs ? min(bs, n - k0) : 0;
+        // A11's factored columns k0 .. jdead - 1 (rows k0 .. k0 + b - 1) aside
+        for (int q = tid; q < b * b; q += 256) {
+            const int i = q % b, l = q / b;
+            if (k0 + l < jdead && i >= l) pan[i + l * XL_S] = A[(k0 + i) + (long long)(k0 + l) * ld];
+        }
+        __syncthreads();
+        if (k0 > 0) {  // A(k0:, k0:) = A0(k0:, k0:) - L(k0:, :k0) L(k0:, :k0)^T (lower blocks)
+            const double *Lp = A + k0;
+            xl_mm(A + k0 + (long long)k0 * ld, ld, Lp, ld, false, Lp, ld, true, n - k0, n - k0, k0,
+                  A0 + k0 + (long long)k0 * ld, ld, -1.0, 0.0, true);
+        } else {
+            xl_copy_lower(A, A0, ld, n);
+        }
+        __syncthreads();
+        for (int q = tid; q < b * b; q += 256) {
+            const int i = q % b, l = q / b;
+            if (k0 + l < jdead && i >= l) A[(k0 + i) + (long long)(k0 + l) * ld] = pan[i + l * XL_S];
         }
         __syncthreads();
     }
     return ok;
 }
 
-// dst <- src (lower triangle of an n x n block, ld)
-__device__ __noinline__ void xl_copy_lower(double *dst, const double *src, int ld, int n) {
-    __syncthreads();
-    for (int q = threadIdx.x; q < n * n; q += 256) {
-        const int i = q % n, j = q / n;
-        if (i >= j) dst[i + (long long)j * ld] = src[i + (long long)j * ld];
-    }
-    __syncthreads();
-}
 
 // B (n x nb, ld ldb) <- L^{-1} B, L lower (ld): one barrier per pivot, the
 // row updates spread over the block with the unscaled pivot row, the rows

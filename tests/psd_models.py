@@ -47,3 +47,34 @@ def eigen_stop_factor(Q):
         L[k, k] = np.sqrt(x)
         L[k + 1:, k] = (Q[k + 1:, k] - L[k + 1:, :k] @ L[k, :k]) / L[k, k]
     return L
+
+
+def decoupled_dead_state(n, m, N, batch, seed, k):
+    """State k decoupled (x_{t+1}[k] = x_t[k], no input, no offset) and
+    costless in every stage and the terminal: with sigma = 0 every value
+    function has a zero pivot at state k, so Eigen's LLT stops there -- in
+    the terminal factor (order n) and at pivot m + k of every stage."""
+    from pdplqr.problems import random_batch_arrays
+
+    E, c, H, h, x0 = random_batch_arrays(n, m, N, batch, seed)
+    s = n + m
+    E, c, H, h = E.copy(), c.copy(), H.copy(), h.copy()
+    for b in range(batch):
+        for t in range(N):
+            Et = E[b, t * n * s:(t + 1) * n * s].reshape(n, s, order="F")  # [B A], column-major
+            Et[k, :] = 0.0
+            Et[:, m + k] = 0.0
+            Et[k, m + k] = 1.0
+            E[b, t * n * s:(t + 1) * n * s] = Et.ravel(order="F")
+            c[b, t * n + k] = 0.0
+            Ht = H[b, t * s * s:(t + 1) * s * s].reshape(s, s, order="F")
+            Ht[m + k, :] = 0.0
+            Ht[:, m + k] = 0.0
+            H[b, t * s * s:(t + 1) * s * s] = Ht.ravel(order="F")
+            h[b, t * s + m + k] = 0.0
+        HN = H[b, N * s * s:].reshape(n, n, order="F")
+        HN[k, :] = 0.0
+        HN[:, k] = 0.0
+        H[b, N * s * s:] = HN.ravel(order="F")
+        h[b, N * s + k] = 0.0
+    return E, c, H, h, x0

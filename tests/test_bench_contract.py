@@ -74,4 +74,10 @@ def test_bench_spawns_ranks(gpus):
     assert abs(d["value"] - gpus * 128 * 256 / (d["ms_per_step"] * 1e-3)) / d["value"] < 1e-6
     c4 = d["secondary"]["C4_horizon_sharded"]
     assert c4["n_gpus"] == gpus and c4["oracle_rel_err"] < 1e-9
+    # the strong-scaling parts of the same run
+    pt = c4["parts"]
+    assert len(pt["rank_ms"]) == gpus and all(x > 0 for x in pt["rank_ms"])
+    assert pt["max_rank_ms"] == max(pt["rank_ms"]) and pt["exchange_ms"] > 0
+    assert pt["ref_1rank_ms"] > 0 and abs(pt["strong_scaling_ratio"] - pt["ref_1rank_ms"] / c4["ms_per_solve"]) < 1e-9
+    assert d["rehearsal"]["backend"] == "gloo"
     assert d["cpu_baseline"] is not None and d["cpu_baseline"]["value"] > 0

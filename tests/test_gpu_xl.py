@@ -425,3 +425,36 @@ def test_xl_parallel_admm_matches_oracle():
         ow, oy, oz, _ = oracle_admm(pms[b], x0[b], lb[b], ub[b], rho[b], ws[b], ys[b], zs[b], solver="parallel",
                                     num_segments=3, condensed="CHOLESKY", max_iter=12, eps_abs=0.0, eps_rel=0.0)
         assert rel_err(w[b], ow) < TOL and rel_err(y[b], oy) < TOL and rel_err(z[b], oz) < TOL, b
+
+
+@pytest.mark.parametrize("keep", [False, True])
+def test_xl_state_pivot_stop_follows_eigen_blocked(keep):
+    """ADVICE r5: Eigen's LLT::compute factors orders >= 32 in blocks
+    (llt_inplace::blocked: 8 columns below order 128), so a state pivot that
+    stops it inside a later block leaves the Schur complement of the finished
+    blocks in the later columns -- not their input values.  State 20 of a
+    50 / 15 problem is dead: the terminal factor (order 50) stops at 20 (block
+    16..23), every stage factor (order 65) at 35 (block 32..39).  The XL
+    kernels (xl_llt) against the oracle's restated blocked LLT (1e-9), status
+    clean (a zero state pivot is not flagged, as the reference ignores it)."""
+    from pdplqr import BatchedLQRSolver
+    from psd_models import decoupled_dead_state
+
+    n, m, N, batch, k = 50, 15, 5, 2, 20
+    s = n + m
+    E, c, H, h, x0 = decoupled_dead_state(n, m, N, batch, 77, k)
+    bs = BatchedLQRSolver(n, m, N, batch, keep_factors=keep)
+    bs.set_model(E, c, H, h)
+    ws = 0.1 * np.random.default_rng(78).standard_normal((batch, N * s + n))
+    bs.update_problem_data(ws, sigma=0.0)
+    bs.backward()
+    out = np.zeros((batch, N * s + n))
+    bs.forward(x0, out)
+    assert np.all(bs.status() == 0)
+    assert np.all(np.isfinite(out))
+    for b in range(batch):
+        o = OracleSerial(PackedModel(n, m, N, np.zeros(N + 1, dtype=np.int32), E[b], c[b], H[b], h[b], np.zeros(0)))
+        o.update_problem_data(ws[b], None, None, None, 0.0)
+        o.backward(None)
+        assert rel_err(out[b], o.forward(x0[b])) < TOL, b
+    bs.close()
