@@ -44,7 +44,6 @@ for fl in (1, 0):
     sel = t[:, 22] == fl
     if sel.any():
         print(f"  fcf={fl}: {sel.sum()} blocks, combine {med(t[sel][:, 8] - t[sel][:, 0]):.0f} ticks")
-print("  tile wave 1 (shader cycles over the 6 blocks): publish " + f"{med(t[:, 23]):.0f}, wait at A {med(t[:, 26]):.0f}, "
-      f"deferred MFMA + wait at B {med(t[:, 24]):.0f}, critical update + operand reads {med(t[:, 25]):.0f}")
-print("  factor wave 0: publish + wait at A " + f"{med(t[:, 27]):.0f}, LDL^T + V/W + linear column {med(t[:, 28]):.0f}, "
-      f"wait at B {med(t[:, 29]):.0f}")
+for nm, off in (("wave 0 (diagonal tiles, LDL^T)", 27), ("wave 1 (tiles)", 23)):
+    print(f"  {nm}, shader cycles over the 6 blocks: after B (updates, publish, LDL^T) {med(t[:, off]):.0f}, "
+          f"wait at A {med(t[:, off + 1]):.0f}, V/W {med(t[:, off + 2]):.0f}, wait at B {med(t[:, off + 3]):.0f}")
