@@ -77,9 +77,11 @@ def _pmc_summaries():
         for f in sorted(fs):
             if f.endswith("_pmc.json"):
                 try:
-                    out.append(json.load(open(os.path.join(dp, f))))
+                    d = json.load(open(os.path.join(dp, f)))
                 except Exception:
                     continue
+                d["_path"] = os.path.relpath(os.path.join(dp, f), ROOT)
+                out.append(d)
     return out
 
 
@@ -91,6 +93,8 @@ def load_pmc_traffic(workload_tag, kernel=None):
     names = [kernel] if kernel else []
     if kernel and kernel.endswith(", 0>"):  # pre-round-4 name of the same kernel
         names.append(kernel[:-4] + ">")
+    if kernel and kernel.endswith(">"):  # round-5+ name: the one-wave-per-SIMD flag appended (false here)
+        names.append(kernel[:-1] + ", false>")
     for d in _pmc_summaries():
         if (d.get("workload") == workload_tag and "bytes_per_launch" in d
                 and (kernel is None or any(d.get("dominant_kernel", "").endswith(k) for k in names))):
@@ -126,7 +130,7 @@ def pmc_traffic(workload_tag, kernels):
         mult = c.get("dispatches", 1) / found["solves"] if found.get("solves") else 1.0
         tot += (c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024) * mult
         seen.append(ks[0])
-    return {"bytes": tot, "kernels": seen}
+    return {"bytes": tot, "kernels": seen, "path": found.get("_path", "profiles/")}
 
 
 def roofline_block(bytes_stage, stages, ms, workload_tag=None, kernels=(), flops_stage=None, kernel_desc=None):
@@ -139,8 +143,8 @@ def roofline_block(bytes_stage, stages, ms, workload_tag=None, kernels=(), flops
          "frac": achieved / HBM_PEAK_GBS, "bytes_per_stage_algorithmic": bytes_stage, "ms": ms}
     t = pmc_traffic(workload_tag, kernels) if workload_tag else None
     r["traffic"] = t["bytes"] if t else None
-    r["traffic_source"] = (f"committed PMC summary, workload {workload_tag}: {', '.join(t['kernels'])}" if t
-                           else "no committed PMC summary for this workload")
+    r["traffic_source"] = (f"committed PMC summary {t['path']}, workload {workload_tag}: {', '.join(t['kernels'])}"
+                           if t else "no committed PMC summary for this workload")
     if t:
         r["frac_moved"] = t["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
         r["traffic_over_algorithmic"] = t["bytes"] / (bytes_stage * stages)
@@ -1092,7 +1096,8 @@ def main():
         # 12/4), so it moves fewer bytes than the 3,808 B algorithmic figure and
         # `frac_of_measured_copy` (algorithmic bytes) can exceed 1
         res["roofline"]["frac_moved"] = pmc["bytes_per_launch"] / (ms_bwd * 1e-3) / 1e9 / HBM_PEAK_GBS
-        res["roofline"]["traffic_source"] = "committed PMC summary (profiles/), same workload and kernel; not this run"
+        res["roofline"]["traffic_source"] = (f"committed PMC summary {pmc.get('_path', 'profiles/')}, same workload "
+                                             "and kernel; not this run")
     copy = measured_copy_gbs(dev)
     copy_gbs = copy["float4"] or copy["blit"]
     res["roofline"]["peak_measured_copy"] = copy_gbs
