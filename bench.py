@@ -1126,7 +1126,7 @@ def main():
     del E, c, h, x0, ws0, out, Hk
     torch.cuda.empty_cache()
     if not args.no_secondary:
-        lines = [("C2", "C2_single_N1024_parallel", lambda: bench_single(local, dev, dist)),
+        lines = [("C2", "C2_single_N1024_parallel", lambda: bench_single(local, dev, dist, steps=50, warmup=5)),
                  ("C3", "C3_batched_N256", lambda: bench_batched_c3(local, dev, dist)),
                  ("wide", "wide_24x16_N256_b1024", lambda: bench_batched_c3(local, dev, dist, steps=5, warmup=2,
                                                                              N=256, batch=1024, n=24, m=16)),

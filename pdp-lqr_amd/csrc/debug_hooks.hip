@@ -3,6 +3,7 @@
 // (tests/test_gpu_combine.py).  Nothing in the solver path calls them.
 #include "combine_mw.hpp"
 #include "combine_qd.hpp"
+#include "combine_qd1.hpp"
 #include "combine_tiles.hpp"
 #include "parallel.hpp"
 
@@ -184,4 +185,64 @@ extern "C" int pdplqr_debug_rank_tree(int R, int r, int level, int q, int *out) 
         out[5] = op.dst;
     }
     return per;
+}
+
+// Test hook (CPU, no device): the suffix-scan round plan of scan_round_operands
+// (the block -> (i, j) indexing k_seg_scan / k_seg_scan_mw run): out[2] = {i, j}
+// of block q in the round of distance `dist`, form sk; returns the block count
+// of the round and -1 in out[0] when block q has nothing to do
+// (tests/test_rank_tree_plan.py simulates the Sklansky rounds with it).
+extern "C" int pdplqr_debug_scan_round(int S, int dist, int sk, int q, int *out) {
+    const int per = pdplqr::scan_round_blocks(S, dist, sk);
+    if (q >= 0 && q < per && out) {
+        int i = -1, j = -1;
+        if (!pdplqr::scan_round_operands(S, dist, sk, q, i, j)) i = -1;
+        out[0] = i;
+        out[1] = j;
+    }
+    return per;
+}
+
+// Test hook: the one-wave n <= 12 junction-LDL^T combine (combine_qd1.hpp) of
+// two elements [F | C | f | P | p] (column-major blocks); returns
+// PDPLQR_ERR_NUMERIC when a pivot has the wrong sign.
+template <int NN>
+__global__ __launch_bounds__(64) void k_debug_combine_qd1(const double *a, const double *b, double *out, int fcf,
+                                                         int *ok) {
+    __shared__ __attribute__((aligned(16))) double qs[pdplqr::Qd1<NN>::smem];
+    constexpr int n = NN, nn = n * n, es = 3 * nn + 2 * n;
+    __shared__ __attribute__((aligned(16))) double la[es + 1], lb[es + 1];
+    for (int q = threadIdx.x; q < es; q += 64) {
+        la[q] = a[q];
+        lb[q] = b[q];
+    }
+    pdplqr::wave_sync();
+    const bool good = pdplqr::qd1_combine<NN>(out, out + nn, out + 2 * nn, out + 2 * nn + n, out + 3 * nn + n,
+                                              pdplqr::elem_in(la, n), pdplqr::elem_in(lb, n), fcf != 0, qs,
+                                              threadIdx.x);
+    if (threadIdx.x == 0) *ok = good ? 1 : 0;
+}
+
+extern "C" int pdplqr_debug_combine_qd1(int n, const double *a, const double *b, double *out, int fcf) {
+    using namespace pdplqr;
+    if (n != 4 && n != 8 && n != 12) return PDPLQR_ERR_INVALID;
+    const size_t es = (size_t)(3 * n * n + 2 * n) * sizeof(double);
+    double *d = nullptr;
+    int *dok = nullptr, okh = 0;
+    PDPLQR_HIP_TRY(hipMalloc(&d, 3 * es));
+    PDPLQR_HIP_TRY(hipMalloc(&dok, sizeof(int)));
+    PDPLQR_HIP_TRY(hipMemcpy(d, a, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + es, b, es, hipMemcpyHostToDevice));
+    PDPLQR_HIP_TRY(hipMemcpy((char *)d + 2 * es, out, es, hipMemcpyHostToDevice));  // untouched blocks kept
+    const double *da = d, *db = (const double *)((char *)d + es);
+    double *dout = (double *)((char *)d + 2 * es);
+    if (n == 4) hipLaunchKernelGGL(k_debug_combine_qd1<4>, dim3(1), dim3(64), 0, 0, da, db, dout, fcf, dok);
+    else if (n == 8) hipLaunchKernelGGL(k_debug_combine_qd1<8>, dim3(1), dim3(64), 0, 0, da, db, dout, fcf, dok);
+    else hipLaunchKernelGGL(k_debug_combine_qd1<12>, dim3(1), dim3(64), 0, 0, da, db, dout, fcf, dok);
+    PDPLQR_HIP_TRY(hipDeviceSynchronize());
+    PDPLQR_HIP_TRY(hipMemcpy(out, dout, es, hipMemcpyDeviceToHost));
+    PDPLQR_HIP_TRY(hipMemcpy(&okh, dok, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    (void)hipFree(dok);
+    return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
 }

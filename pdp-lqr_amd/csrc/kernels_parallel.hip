@@ -27,6 +27,7 @@
 #define PDPLQR_COMB_PROFILE_TU 1  // the combine phase marks live in this translation unit
 #include "combine_mw.hpp"
 #include "combine_qd.hpp"
+#include "combine_qd1.hpp"
 #include "combine_tiles.hpp"
 #include "device_common.hpp"
 #include "parallel.hpp"
@@ -321,8 +322,18 @@ __global__ __launch_bounds__(64) void k_seg_scan(ScanArgs A) {
 // latencies but one dispatch, operand fetch and write-back less.  Each
 // combine's right operand covers [first, min(first + span - 1, S - 1)]; when
 // that range holds the real terminal, F = C = f = 0 (see k_seg_scan).
+// The n = 12 CHOLESKY combines of the two-round scan run the one-wave blocked
+// LDL^T of the junction block (combine_qd1.hpp) unless built with
+// -DPDPLQR_QD1_COMBINE=0 (the Cholesky form tcombine_parts, A/B).
+#ifndef PDPLQR_QD1_COMBINE
+#define PDPLQR_QD1_COMBINE 1
+#endif
+template <int NC, bool LU>
+constexpr bool use_qd1() { return PDPLQR_QD1_COMBINE && !LU && NC == 12; }
+
 template <int T, bool LU, int NC = 0>
-__device__ __forceinline__ void seg_scan4_block(const ScanArgs &A, long long blk, CombSmem<T> (&smv)[2], double *ebuf) {
+__device__ __forceinline__ void seg_scan4_block(const ScanArgs &A, long long blk, CombSmem<T> (&smv)[2], double *ebuf,
+                                                double *qd1s = nullptr) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = NC ? NC : A.n, S = A.S, d = A.dist;
     const int es = 3 * n * n + 2 * n, nn = n * n, ol = op_stage_len(n);
@@ -332,15 +343,28 @@ __device__ __forceinline__ void seg_scan4_block(const ScanArgs &A, long long blk
     const double *in = A.in + b * (A.bstride ? A.bstride : (long long)S * es);
     double *out = A.out + b * (long long)S * es;
     double *scr = A.scratch + (b * S + i) * 2LL * es;
-    double *eb = ebuf + wv * 2 * ol;
+    constexpr bool QD1 = use_qd1<NC, LU>();
+    // per wave: two operand images (QD1: the whole elements, so the assembly
+    // reads LDS only -- one memory latency per combine)
+    double *eb = ebuf + wv * 2 * (QD1 ? elem_slot(n) : ol);
     CombSmem<T> &sm = smv[wv];
     auto combine = [&](double *o, const double *left, const double *right, bool fcf) {
-        const ElemIn ea = stage_left(eb, left, n, lane);
-        const ElemIn er = stage_right(eb + ol, right, n, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wave_sync();
-        const bool ok = tcombine_parts<T, LU>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, er, n, fcf,
-                                              true, sm, lane);
+        bool ok;
+        if constexpr (QD1) {
+            stage_range(eb, left, es, lane);
+            stage_range(eb + elem_slot(n), right, es, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            ok = qd1_combine<12>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, elem_in(eb, n),
+                                 elem_in(eb + elem_slot(n), n), fcf, qd1s + wv * Qd1<12>::smem, lane);
+        } else {
+            const ElemIn ea = stage_left(eb, left, n, lane);
+            const ElemIn er = stage_right(eb + ol, right, n, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            ok = tcombine_parts<T, LU>(o, o + nn, o + 2 * nn, o + 2 * nn + n, o + 3 * nn + n, ea, er, n, fcf, true, sm,
+                                       lane);
+        }
         if (!fcf)
             for (int q = lane; q < 2 * nn + n; q += 64) o[q] = 0.0;  // [F | C | f]
         return ok;
@@ -371,8 +395,9 @@ __device__ __forceinline__ void seg_scan4_block(const ScanArgs &A, long long blk
 template <int T, bool LU, int NC = 0>
 __global__ __launch_bounds__(128) void k_seg_scan4(ScanArgs A) {
     __shared__ CombSmem<T> smv[2];
+    __shared__ __attribute__((aligned(16))) double qd1s[use_qd1<NC, LU>() ? 2 * Qd1<12>::smem : 2];
     extern __shared__ __attribute__((aligned(16))) double ebuf[];  // per wave: 2 operand images
-    seg_scan4_block<T, LU, NC>(A, blockIdx.x, smv, ebuf);
+    seg_scan4_block<T, LU, NC>(A, blockIdx.x, smv, ebuf, qd1s);
 }
 
 
@@ -684,7 +709,33 @@ __global__ __launch_bounds__(256, 2) void k_seg_maps_mw(MapArgs A) {
     const double *src = src_g ? es0 : nullptr;
     WV<T> phi, x;
     bool have_x = false;  // j = 0: x_0 formed (wave 0)
-    if (src && vP) {
+    if (src && vP && NC == QD_N && PDPLQR_QD_COMBINE) {
+        // n = 24: the map as ONE junction elimination (combine_qd.hpp).  The
+        // element b_V = (I, 0, 0, P_j, p_j) -- no stages, value function V_j --
+        // composed after e: its junction is (I + C P_j) x_j = F x + f - C p_j,
+        // so (e (x) b_V).F = Phi_j and .f = phi_j.
+        const int es = 3 * nn + 2 * n;
+        for (int q = threadIdx.x; q < es; q += 256)
+            es2[q] = q < nn ? ((q % (n + 1)) == 0 ? 1.0 : 0.0) : q < 2 * nn + n ? 0.0 : es1[q - (2 * nn + n)];
+        __syncthreads();
+        ok = qd_combine(es1, es1 + nn, es1 + 2 * nn, es1 + 2 * nn + n, es1 + 3 * nn + n, elem_in(src, n),
+                        elem_in(es2, n), true, mwbuf) && ok;  // ends with a block barrier: es1 complete
+        if (j > 0) {
+            for (int q = threadIdx.x; q < mw; q += 256) mo[q] = q < nn ? es1[q] : es1[2 * nn + (q - nn)];
+        } else if (wv == 0) {
+            WM<T> PhiT;
+            WV<T> x0v;
+            wm_load(PhiT, es1, n, n, true, 0.0, g, c);
+            wv_load(phi, es1 + 2 * nn, n, g, c);
+            wv_load(x0v, A.x0 + b * (long long)n, n, g, c);
+            wv_tn(x, PhiT, x0v, n, 1.0, &phi);
+            have_x = true;
+        }
+        if (wv == 0) {  // x_0's lambda below reads P_0 from es2 (es1 now holds the map)
+            vP = es2 + 2 * nn + n;
+            vp = es2 + 3 * nn + n;
+        }
+    } else if (src && vP) {
         WM<T> Phi;
         ok = mw_map<T>(elem_in(src, n), vP, vp, n, sm, j == 0, Phi, phi) && ok;
         if (wv == 0) {
@@ -777,16 +828,19 @@ __global__ __launch_bounds__(64) void k_map_scan(MapScanArgs A) {
     wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
 }
 
-// Radix-4 form of the same composition (PDPLQR_MAP_RADIX = 4): one round of
-// distance d composes m_j with m_{j-d}, m_{j-2d}, m_{j-3d} in turn, stopping at
-// the first anchored partner (index < d), so after the round the entries
-// j < 4 d are anchored: ceil(log4 (S + 1)) launches instead of
-// ceil(log2 (S + 1)), each at most three products in sequence.  The running
-// map is kept transposed (Phi^T), the form the matrix-vector product reads.
-template <int T, int NC = 0>
-__device__ __forceinline__ void map_scan4_block(const MapScanArgs &A, long long blk) {
+// Radix-R form of the same composition: one round of distance d composes m_j
+// with m_{j-d}, m_{j-2d}, ..., m_{j-(R-1)d} in turn, stopping at the first
+// anchored partner (index < d), so after the round the entries j < R d are
+// anchored: ceil(log_R (S + 1)) launches instead of ceil(log2 (S + 1)), each at
+// most R - 1 products in sequence.  The radix is chosen per solve (map_radix:
+// the fewest rounds, then the smallest R for them) up to the compile-time RM
+// the partner registers are sized for.  The running map is kept transposed
+// (Phi^T), the form the matrix-vector product reads.
+template <int T, int NC = 0, int RM = 4>
+__device__ __forceinline__ void map_scan_block(const MapScanArgs &A, long long blk) {
     const int lane = wave_lane(), g = lane >> 4, c = lane & 15;
     const int n = NC ? NC : A.n, J = A.S + 1, d = A.dist, nn = n * n, mw = nn + n;
+    const int R = A.radix;  // <= RM (launch_map_scan)
     const long long b = blk / J;
     const int j = (int)(blk % J);
     const double *in = A.in + b * (long long)J * mw;
@@ -795,17 +849,17 @@ __device__ __forceinline__ void map_scan4_block(const MapScanArgs &A, long long 
         for (int q = lane; q < n; q += 64) out[(long long)j * mw + nn + q] = in[(long long)j * mw + nn + q];
         return;
     }
-    // partners j - d, ..., j - K d; the K-th is anchored (index < d) when j / d <= 3.
+    // partners j - d, ..., j - K d; the K-th is anchored (index < d) when j / d <= R - 1.
     // Every operand is loaded up front (none depends on the running map), so
     // the round pays one memory latency, not one per partner.
-    const int K = j / d < 3 ? j / d : 3;
-    const bool anch = j / d <= 3;
-    WM<T> PaccT, Pa[3];
-    WV<T> pacc, pa[3];
+    const int K = j / d < R - 1 ? j / d : R - 1;
+    const bool anch = j / d <= R - 1;
+    WM<T> PaccT, Pa[RM - 1];
+    WV<T> pacc, pa[RM - 1];
     wm_load(PaccT, in + (long long)j * mw, n, n, true, 0.0, g, c);
     wv_load(pacc, in + (long long)j * mw + nn, n, g, c);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < RM - 1; ++k) {
         const double *ea = in + (long long)(j - (k + 1) * d) * mw;
         if (k < K) wv_load(pa[k], ea + nn, n, g, c);
         if (k < K - (anch ? 1 : 0)) wm_load(Pa[k], ea, n, n, false, 0.0, g, c);
@@ -817,33 +871,64 @@ __device__ __forceinline__ void map_scan4_block(const MapScanArgs &A, long long 
         wm_load(Pv, v, n, n, false, 0.0, g, c);
         wv_load(pv, v + nn, n, g, c);
     }
+    // (guards, no break / return inside: the loop must unroll, or the partner
+    // arrays go to scratch)
+    const int KM = anch ? K - 1 : K;  // matrix products before the anchored partner's vector one
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (k >= K) break;
-        WV<T> po;
-        wv_tn(po, PaccT, pa[k], n, 1.0, &pacc);  // Phi_acc phi_a + phi_acc
-        if (anch && k == K - 1) {  // anchored partner: po = x_j
-            wv_store(po, out + (long long)j * mw + nn, n, g, c);
-            wv_store(po, A.xhat + (b * J + j) * (long long)n, n, g, c);
-            WV<T> lam;
-            wv_tn(lam, Pv, po, n, 1.0, &pv);
-            wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
-            return;
+    for (int k = 0; k < RM - 1; ++k) {
+        if (k < KM) {
+            WV<T> po;
+            wv_tn(po, PaccT, pa[k], n, 1.0, &pacc);  // Phi_acc phi_a + phi_acc
+            WM<T> Pn;
+            wm_tn(Pn, Pa[k], PaccT, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi_a^T Phi_acc^T = (Phi_acc Phi_a)^T
+            PaccT = Pn;
+            pacc = po;
         }
-        WM<T> Pn;
-        wm_tn(Pn, Pa[k], PaccT, n, 1.0, 0.0, (const WM<T> *)nullptr, g, c);  // Phi_a^T Phi_acc^T = (Phi_acc Phi_a)^T
-        PaccT = Pn;
-        pacc = po;
+    }
+    if (anch) {  // anchored partner K - 1: x_j = Phi_acc x_a + phi_acc
+        WV<T> po, xa;
+#pragma unroll
+        for (int k = 0; k < RM - 1; ++k)
+            if (k == K - 1) xa = pa[k];
+        wv_tn(po, PaccT, xa, n, 1.0, &pacc);
+        wv_store(po, out + (long long)j * mw + nn, n, g, c);
+        wv_store(po, A.xhat + (b * J + j) * (long long)n, n, g, c);
+        WV<T> lam;
+        wv_tn(lam, Pv, po, n, 1.0, &pv);
+        wv_store(lam, A.lam + (b * J + j) * (long long)n, n, g, c);
+        return;
     }
     wm_store_t(PaccT, out + (long long)j * mw, n, g, c);  // Phi_acc (natural) from its transpose
     wv_store(pacc, out + (long long)j * mw + nn, n, g, c);
 }
 
-template <int T, int NC = 0>
-__global__ __launch_bounds__(64) void k_map_scan4(MapScanArgs A) {
-    map_scan4_block<T, NC>(A, blockIdx.x);
+template <int T, int NC = 0, int RM = 4>
+__global__ __launch_bounds__(64) void k_map_scanR(MapScanArgs A) {
+    map_scan_block<T, NC, RM>(A, blockIdx.x);
 }
 
+// Largest radix of the one-wave composition kernels: the partners' registers
+// (RM - 1 maps of WM<T>) and R - 1 products in sequence per round.  12 x 12
+// maps (T = 1): 2 rounds of radix 17 take 7.0 + 7.4 us against 4 radix-4
+// rounds of 4.7 us (C2, gpurun r6e).  24 x 24 (T = 2): a product in the chain
+// costs ~1.5 us, so radix 8 (3 rounds of 11.4-14.1 us, the C4 rank, r6f) loses
+// to radix 4 (5 rounds of ~6.9 us).
+static inline int map_radix_max(int n) { return n <= 16 ? 17 : 4; }
+
+int map_radix(int n, int J) {
+    if (PDPLQR_MAP_RADIX != 4) return PDPLQR_MAP_RADIX;
+    if (xl_state(n) || wide_state(n)) return 4;  // (k_map_scan_wide / _xl: radix-4 rounds)
+    const int RM = map_radix_max(n);
+    auto rounds = [&](int R) {
+        int r = 0;
+        for (long long d = 1; d < J; d *= R) ++r;
+        return r;
+    };
+    const int best = rounds(RM);
+    int R = 2;
+    while (rounds(R) > best) ++R;
+    return R;
+}
 
 static int tile_order(int n);
 
@@ -898,8 +983,10 @@ int launch_seg_scan4(const ScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * a.S)), blk(128);
     const size_t smem = 2 * op_stage_bytes(a.n);
     if (!seg_scan4_supported(a.n) || !a.scratch) return PDPLQR_ERR_UNSUPPORTED;
+    const size_t smem_qd1 = 2 * 2 * (size_t)elem_slot(a.n) * sizeof(double);  // whole operand elements (QD1)
     if (a.lu) hipLaunchKernelGGL((k_seg_scan4<1, true>), grid, blk, smem, st, a);
-    else if (ct_n12(a.n)) hipLaunchKernelGGL((k_seg_scan4<1, false, 12>), grid, blk, smem, st, a);
+    else if (ct_n12(a.n)) hipLaunchKernelGGL((k_seg_scan4<1, false, 12>), grid, blk, (use_qd1<12, false>() ? smem_qd1 : smem),
+                                             st, a);
     else hipLaunchKernelGGL((k_seg_scan4<1, false>), grid, blk, smem, st, a);
     PDPLQR_HIP_TRY(hipGetLastError());
     return PDPLQR_OK;
@@ -966,10 +1053,11 @@ int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st) {
     const dim3 grid((unsigned)(batch * (a.S + 1))), blk(64);
     const int T = tile_order(a.n);
     if (PDPLQR_MAP_RADIX == 4) {
-        if (T == 1 && ct_n12(a.n)) hipLaunchKernelGGL((k_map_scan4<1, 12>), grid, blk, 0, st, a);
-        else if (T == 1) hipLaunchKernelGGL(k_map_scan4<1>, grid, blk, 0, st, a);
-        else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_map_scan4<2, 24>), grid, blk, 0, st, a);
-        else if (T == 2) hipLaunchKernelGGL(k_map_scan4<2>, grid, blk, 0, st, a);
+        if (a.radix < 2 || a.radix > map_radix_max(a.n)) return PDPLQR_ERR_INVALID;
+        if (T == 1 && ct_n12(a.n)) hipLaunchKernelGGL((k_map_scanR<1, 12, 17>), grid, blk, 0, st, a);
+        else if (T == 1) hipLaunchKernelGGL((k_map_scanR<1, 0, 17>), grid, blk, 0, st, a);
+        else if (T == 2 && ct_n24(a.n)) hipLaunchKernelGGL((k_map_scanR<2, 24, 4>), grid, blk, 0, st, a);
+        else if (T == 2) hipLaunchKernelGGL((k_map_scanR<2, 0, 4>), grid, blk, 0, st, a);
         else return PDPLQR_ERR_UNSUPPORTED;
     } else if (T == 1) hipLaunchKernelGGL(k_map_scan<1>, grid, blk, 0, st, a);
     else if (T == 2) hipLaunchKernelGGL(k_map_scan<2>, grid, blk, 0, st, a);

@@ -60,9 +60,24 @@ __host__ __device__ inline bool scan_round_operands(int S, int dist, int sk, int
         j = blk * 2 * dist + dist;
         return j < S;
     }
+    if (sk == 1) {
+        // the S / 2 combines (2 k, 2 k + 1) take the first blocks, the copies of
+        // the unpaired entries the rest: the dispatcher hands consecutive blocks
+        // to different CUs, so the combines -- the round's critical path -- get
+        // a CU each before any copy block lands next to one
+        const int nc = S >> 1;
+        if (q < nc) {
+            i = 2 * q;
+            j = i + 1;
+        } else {
+            const int k = q - nc;
+            i = 2 * k + 1 < S ? 2 * k + 1 : S - 1;  // odd entries, then the last one of an odd S
+            j = -1;
+        }
+        return true;
+    }
     i = q;
-    if (sk == 1) j = ((i & 1) || i + 1 >= S) ? -1 : i + 1;
-    else j = i + dist < S ? i + dist : -1;
+    j = i + dist < S ? i + dist : -1;
     return true;
 }
 
@@ -86,6 +101,7 @@ struct MapArgs {
 
 struct MapScanArgs {
     int n, S, dist;
+    int radix = 4;             // this solve's composition radix (map_radix; 4 for the wide / XL kernels)
     const double *in;          // [b][S+1][n^2 + n]
     double *out;
     const double *vfun;
@@ -172,6 +188,8 @@ int launch_seg_maps(const MapArgs &a, int batch, hipStream_t st);
 #define PDPLQR_MAP_RADIX 4
 #endif
 int launch_map_scan(const MapScanArgs &a, int batch, hipStream_t st);
+// radix of the boundary-map composition for n-state maps over J = S + 1 entries
+int map_radix(int n, int J);
 int launch_fold_shards(const double *elems, int R, int r, int n, int batch, double *out_pre, double *out_suf,
                        int *has_suf, int *flag, bool lu, hipStream_t st);
 int launch_rank_fold_maps(const double *elems, const double *suf, const double *x0, int R, int r, int n, int batch,

@@ -338,11 +338,13 @@ static int parallel_forward(pdplqr_handle h, const double *x0, double *ws, const
     if (rc) return rc;
     double *mb[2] = {ps->mapA, ps->mapB};
     int round = 0;
-    for (int d = 1; d < ps->S + 1; d *= PDPLQR_MAP_RADIX, ++round) {
+    const int radix = map_radix(sh.n, ps->S + 1);
+    for (int d = 1; d < ps->S + 1; d *= radix, ++round) {
         MapScanArgs ms;
         ms.n = sh.n;
         ms.S = ps->S;
         ms.dist = d;
+        ms.radix = radix;
         ms.in = mb[round & 1];
         ms.out = mb[(round + 1) & 1];
         ms.vfun = ps->vfun;

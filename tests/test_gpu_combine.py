@@ -195,3 +195,66 @@ def test_qd_combine_flags_zero_value_function():
     va, vb = _pack(a), _pack(b)
     out = np.zeros_like(va)
     assert L.pdplqr_debug_combine_qd(va.ctypes.data, vb.ctypes.data, out.ctypes.data, 1) != 0
+
+
+@pytest.mark.parametrize("n", [4, 8, 12])
+@pytest.mark.parametrize("case", ["random", "zero_b", "no_fcf", "ill_Pb", "seg_elems"])
+def test_qd1_combine_matches_numpy(n, case):
+    """The one-wave blocked LDL^T combine of the n <= 12 scans (combine_qd1.hpp):
+    the same element as seg_ref.combine (1e-12; ill-conditioned P_b 1e-10),
+    untouched F, C, f without fcf, P and C written symmetric."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_qd1.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(900 + 7 * n + len(case))
+    fcf = case != "no_fcf"
+    a, b = _elem(n, rng), _elem(n, rng, zero_fcf=(case in ("zero_b", "no_fcf")))
+    tol = 1e-12
+    if case == "ill_Pb":
+        w, U = np.linalg.eigh(b[3])
+        w[: max(1, n // 3)] *= 1e-6
+        b = (b[0], b[1], b[2], (U * w) @ U.T, b[4])
+        tol = 1e-10
+    if case == "seg_elems":  # real segment elements (n/(n/3), 5 stages each)
+        from seg_ref import slice_element
+
+        m, Lseg = max(1, n // 3), 5
+        E, c, Ht, ht = [], [], [], []
+        for _ in range(2 * Lseg):
+            A = np.eye(n) + 0.1 * rng.standard_normal((n, n))
+            E.append(np.concatenate([rng.standard_normal((n, m)), A], 1))
+            c.append(rng.standard_normal(n))
+            M = rng.standard_normal((n + m, n + m))
+            Ht.append(M @ M.T / (n + m) + np.eye(n + m))
+            ht.append(rng.standard_normal(n + m))
+        a = slice_element(E, c, Ht, ht, 0, Lseg, None)
+        b = slice_element(E, c, Ht, ht, Lseg, 2 * Lseg, None)
+    va, vb = _pack(a), _pack(b)
+    sentinel = 12345.0
+    out = np.full_like(va, sentinel)
+    assert L.pdplqr_debug_combine_qd1(n, va.ctypes.data, vb.ctypes.data, out.ctypes.data, int(fcf)) == 0
+    got, ref = _unpack(out, n), combine(a, b)
+    for name, x, y in zip("FCfPp", got, ref):
+        if not fcf and name in "FCf":
+            assert np.all(x == sentinel), name
+            continue
+        assert np.linalg.norm(x - y) <= tol * max(1.0, np.linalg.norm(y)), (name, np.linalg.norm(x - y))
+    assert np.array_equal(got[3], got[3].T)
+    if fcf:
+        assert np.array_equal(got[1], got[1].T)
+
+
+@pytest.mark.parametrize("n", [4, 12])
+def test_qd1_combine_flags_zero_value_function(n):
+    """P_b = 0: the first x pivot is 0 -- flagged, as chol(P_b) failing is in the
+    Cholesky form (condensed_system.hpp:217-226)."""
+    from pdplqr import _lib
+
+    L = _lib.lib()
+    L.pdplqr_debug_combine_qd1.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(72)
+    a, b = _elem(n, rng), _elem(n, rng)
+    b = (b[0], b[1], b[2], np.zeros((n, n)), b[4])
+    out = np.zeros_like(_pack(a))
+    assert L.pdplqr_debug_combine_qd1(n, _pack(a).ctypes.data, _pack(b).ctypes.data, out.ctypes.data, 1) != 0

@@ -73,3 +73,43 @@ def test_rank_tree_plan_reduces_prefix_and_suffix(R):
             assert final["right"] == (r + 1, R - 1)
         else:
             assert "right" not in final
+
+
+@pytest.mark.parametrize("S", list(range(2, 70)))
+def test_sklansky_scan_plan_builds_every_suffix(S):
+    """The suffix scan's Sklansky rounds (scan_round_operands through the hook
+    pdplqr_debug_scan_round): the first round (sk = 1, elements -> buffer)
+    writes every entry once -- the pair combines in the first S // 2 blocks,
+    the copies after them -- and each later round (sk = 2, in place) combines
+    entry i with an entry j holding the adjacent range, so after ceil(log2 S)
+    rounds entry i covers segments [i, S - 1]."""
+    L = _lib()
+    L.pdplqr_debug_scan_round.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+    L.pdplqr_debug_scan_round.restype = C.c_int
+    out = (C.c_int * 2)()
+    cov = {}
+    per = L.pdplqr_debug_scan_round(S, 1, 1, 0, out)
+    assert per == S
+    for q in range(per):
+        L.pdplqr_debug_scan_round(S, 1, 1, q, out)
+        i, j = out[0], out[1]
+        assert i not in cov
+        assert (j >= 0) == (q < S // 2)  # combines first
+        cov[i] = (i, i) if j < 0 else (i, j)
+        if j >= 0:
+            assert j == i + 1
+    assert sorted(cov) == list(range(S))
+    d = 2
+    while d < S:
+        per = L.pdplqr_debug_scan_round(S, d, 2, 0, out)
+        new = dict(cov)
+        for q in range(per):
+            L.pdplqr_debug_scan_round(S, d, 2, q, out)
+            i, j = out[0], out[1]
+            if i < 0:
+                continue
+            assert cov[i][1] + 1 == j, (S, d, q)  # adjacent ranges, earlier operand first
+            new[i] = (cov[i][0], cov[j][1])
+        cov = new
+        d *= 2
+    assert all(cov[i] == (i, S - 1) for i in range(S)), S
