@@ -1132,7 +1132,7 @@ def main():
                                                                              N=256, batch=1024, n=24, m=16)),
                  ("reuse", "factor_reuse", lambda: bench_factor_reuse(local, dev, dist, N=N, batch=B)),
                  ("C5", "C5_conic_kkt", lambda: bench_conic(local, dev, dist)),
-                 ("C4", "C4_horizon_sharded", lambda: bench_horizon(local, dev, dist, world, rank, args.c4_N))]
+                 ("C4", "C4_horizon_sharded", lambda: bench_horizon(local, dev, dist, world, rank, args.c4_N, steps=10, warmup=2))]
         pick = None if args.secondary == "all" else set(args.secondary.split(","))
         res["secondary"] = {key: fn() for tag, key, fn in lines if pick is None or tag in pick}
     if rank == 0 and not args.no_cpu:

@@ -2,7 +2,10 @@
 virtual ranks (each rank's slice solved in turn on the same device): prints,
 per rank, the slice backward and the shard forward (fold of the gathered
 elements + boundary maps + rollout) in ms, and the slowest rank's total -- what
-an R-GPU run takes per solve, less the all-gather.
+an R-GPU run takes per solve, less the all-gather.  bwd_ms / fwd_ms are event
+times of single calls on an idle GPU (they include the host's launch latency);
+pipelined_ms is the rank's backward + forward issued back to back, wall clock
+per solve (bench.py's per-rank figure).
 usage: python scripts/prof_shards.py [Ntot=65536] [R=8] [reps=5] [segment_len=0 (automatic)]"""
 import json
 import os
@@ -66,10 +69,27 @@ def main():
             torch.cuda.synchronize()
             if it:
                 res["bwd"][r].append(ev[0].elapsed_time(ev[1]))
+    # pipelined: each rank's backward + forward issued `reps` times back to back
+    # on its stream and timed by the wall clock around them (as bench.py's C4
+    # line times a rank): the host's launch latency overlaps the GPU work, as in
+    # a distributed solve where the forward is queued behind the all-gather
+    import time
+    pipe = []
+    for r, sh in enumerate(shards):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps * 4):
+            sh.backward(elems[r], r == R - 1)
+            sh.forward(x0, gathered, R, r, outs[r])
+        torch.cuda.synchronize()
+        pipe.append((time.perf_counter() - t0) / (reps * 4) * 1e3)
     med = lambda v: sorted(v)[len(v) // 2]
     per = [{"rank": r, "bwd_ms": med(res["bwd"][r]), "fwd_ms": med(res["fwd"][r])} for r in range(R)]
     ok = all(bool(torch.isfinite(o).all().item()) for o in outs)
+    for r, p in enumerate(per):
+        p["pipelined_ms"] = pipe[r]
     print(json.dumps({"Ntot": Ntot, "R": R, "ranks": per, "max_rank_ms": max(p["bwd_ms"] + p["fwd_ms"] for p in per),
+                      "max_rank_ms_pipelined": max(pipe),
                       "finite": ok, "segment_len": seglen, "fold": os.environ.get("PDPLQR_SHARD_FOLD", "auto"), "lib": os.environ.get("PDPLQR_LIB", "in-tree")}), flush=True)
     for sh in shards:
         sh.close()
