@@ -693,7 +693,13 @@ __global__ __launch_bounds__(256, 2) void k_seg_maps_mw(MapArgs A) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (vcomb) {  // block-uniform
+    if (vcomb && NC == QD_N && PDPLQR_QD_COMBINE) {  // block-uniform
+        // the junction elimination reads its operands only while assembling, long
+        // before its (barrier-ordered) output stores: [P | p] goes straight into
+        // es1 (V_j for the map below, no global round trip) and then to vfun
+        ok = qd_combine(nullptr, nullptr, nullptr, es1, es1 + nn, elem_in(es1, n), elem_in(es2, n), false, mwbuf);
+        for (int q = threadIdx.x; q < mw; q += 256) vo[q] = es1[q];
+    } else if (vcomb) {
         ok = mw_combine_nc<T, NC>(nullptr, nullptr, nullptr, vo, vo + nn, elem_in(es1, n), elem_in(es2, n), n, false,
                                   mwbuf);
         __syncthreads();  // vo (written by waves 0 and 3) is complete; es1 is free
