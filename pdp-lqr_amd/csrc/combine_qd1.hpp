@@ -213,22 +213,28 @@ __device__ __forceinline__ bool qd1_combine(double *oF, double *oC, double *of, 
                 o[2] = vb[g];
                 o[3] = vb[4 + g];
             }
+        // the tiles of column KT first (they hold the next block's pivot rows, which
+        // the next publish waits for), then the rest; within each group every
+        // first K chunk before every second (independent MFMAs back to back)
 #pragma unroll
-        for (int I = 0; I < TN; ++I)
+        for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-            for (int K = 0; K <= I; ++K) {
-                if (K < KT) continue;
-                const double *o = op4[qd1_tile(I, K)];
-                Q[qd1_tile(I, K)] = mfma_f64(-o[0], o[2], Q[qd1_tile(I, K)]);
-            }
+            for (int I = 0; I < TN; ++I)
 #pragma unroll
-        for (int I = 0; I < TN; ++I)
+                for (int K = 0; K <= I; ++K) {
+                    if (K < KT || (pass == 0) != (K == KT)) continue;
+                    const double *o = op4[qd1_tile(I, K)];
+                    Q[qd1_tile(I, K)] = mfma_f64(-o[0], o[2], Q[qd1_tile(I, K)]);
+                }
 #pragma unroll
-            for (int K = 0; K <= I; ++K) {
-                if (K < KT) continue;
-                const double *o = op4[qd1_tile(I, K)];
-                Q[qd1_tile(I, K)] = mfma_f64(-o[1], o[3], Q[qd1_tile(I, K)]);
-            }
+            for (int I = 0; I < TN; ++I)
+#pragma unroll
+                for (int K = 0; K <= I; ++K) {
+                    if (K < KT || (pass == 0) != (K == KT)) continue;
+                    const double *o = op4[qd1_tile(I, K)];
+                    Q[qd1_tile(I, K)] = mfma_f64(-o[1], o[3], Q[qd1_tile(I, K)]);
+                }
+        }
         wave_sync();  // this block's LDS reads retire before the next block's writes
     }
     // ---- outputs: x_s = rows / columns NJ .. XE - 1, lam_e = XE .. NT - 1 ----
