@@ -17,7 +17,7 @@
 //     combine_tiles.hpp (Y = P_b (I + C_a P_b)^{-1}, Z = I - C_a Y).
 //   * k_seg_scan_wide / k_seg_maps_wide / k_map_scan_wide: one scan round,
 //     the boundary maps and one radix-4 composition round, as k_seg_scan,
-//     k_seg_maps, k_map_scan4.
+//     k_seg_maps, k_map_scanR.
 // Every blk_* call is a block-wide step bracketed by barriers (blk_la.hpp).
 #include "blk_la.hpp"
 #include "combine_tiles.hpp"  // ElemIn, elem_in
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_seg_maps_wide(MapArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// one radix-4 round of the prefix composition of the boundary maps (k_map_scan4)
+// one radix-4 round of the prefix composition of the boundary maps (k_map_scanR at radix 4)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_map_scan_wide(MapScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) double wbuf[];
