@@ -246,3 +246,7 @@ extern "C" int pdplqr_debug_combine_qd1(int n, const double *a, const double *b,
     (void)hipFree(dok);
     return okh ? PDPLQR_OK : PDPLQR_ERR_NUMERIC;
 }
+
+// Test hook (CPU, no device): the boundary-map composition radix map_radix
+// picks for n-state maps over J = S + 1 entries (tests/test_rank_tree_plan.py).
+extern "C" int pdplqr_debug_map_radix(int n, int J) { return pdplqr::map_radix(n, J); }

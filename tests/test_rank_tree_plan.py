@@ -113,3 +113,31 @@ def test_sklansky_scan_plan_builds_every_suffix(S):
         cov = new
         d *= 2
     assert all(cov[i] == (i, S - 1) for i in range(S)), S
+
+
+@pytest.mark.parametrize("n", [4, 12, 16, 24, 32, 40, 100])
+def test_map_radix_takes_the_fewest_rounds(n):
+    """map_radix (the per-solve radix of the boundary-map composition,
+    k_map_scanR): the fewest rounds its kernel's largest radix allows (17 for
+    n <= 16, 4 for 24 x 24 maps and the wide / XL kernels), then the smallest
+    radix with that many rounds; every round count covers J entries."""
+    L = _lib()
+    L.pdplqr_debug_map_radix.argtypes = [C.c_int, C.c_int]
+    L.pdplqr_debug_map_radix.restype = C.c_int
+    rmax = 17 if n <= 16 else 4
+
+    def rounds(R, J):
+        r, d = 0, 1
+        while d < J:
+            d *= R
+            r += 1
+        return r
+
+    for J in list(range(2, 300)) + [411, 513, 1025, 4097]:
+        R = L.pdplqr_debug_map_radix(n, J)
+        if n > 32:  # the wide / XL composition kernels run radix-4 rounds only
+            assert R == 4, (n, J, R)
+            continue
+        assert 2 <= R <= rmax, (n, J, R)
+        assert rounds(R, J) == rounds(rmax, J), (n, J, R)
+        assert R == 2 or rounds(R - 1, J) > rounds(R, J), (n, J, R)
