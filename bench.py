@@ -789,6 +789,8 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
         dist.barrier()
     scal["ref_1rank_ms"] = ref_ms
     scal["strong_scaling_ratio"] = (ref_ms / (t * 1e3)) if ref_ms else None
+    if not dist:
+        scal["rehearsal_R8"] = _horizon_rehearsal(local, dev, Ntot, 8, x0)
     oerr = None
     if world == 1:  # the whole horizon is this rank's: check it against the serial oracle
         oerr = _horizon_oracle_err([(E0[0], c[0], H0[0], h[0])], [out[0].cpu().numpy()], x0[0], n, m, Ntot)
@@ -818,6 +820,53 @@ def bench_horizon(local, dev, dist, world, rank, Ntot, steps=3, warmup=1):
                                        ("k_seg_bwd_aug", "k_seg_scan", "k_seg_maps", "k_map_scan", "k_seg_fwd_dma"),
                                        flops_stage=103235 + 59968,
                                        kernel_desc="whole horizon solve (latency-bound: see DESIGN.md section 6)")}
+
+
+def _horizon_rehearsal(local, dev, Ntot, R, x0, reps=10):
+    """The R-GPU split rehearsed on this one GPU (scripts/prof_shards.py's
+    method): the R slices solved in turn as R virtual ranks, each rank's
+    backward + forward issued `reps` times back to back on its stream (the
+    rank's own critical path, as an R-GPU run would see it less the all-gather;
+    the gather is the slices' elements of one untimed pass).  Not a multi-GPU
+    measurement: the per-rank kernels run alone on the device here."""
+    from pdplqr.horizon import HorizonShard, split_horizon
+
+    n, m = 24, 8
+    s = n + m
+    side = torch.cuda.Stream(device=dev)
+    shards, elems, outs = [], [], []
+    for r, (N0, N1) in enumerate(split_horizon(Ntot, R)):
+        Nl = N1 - N0
+        E, c, H, h, _ = gen_batch_device(n, m, Nl, 1, seed=4242 + r, device=dev)
+        if r < R - 1:
+            H[:, Nl * s * s:] = 0.0
+            h[:, Nl * s:] = 0.0
+        sh = HorizonShard(n, m, Nl, 1, device=local)
+        sh.set_model(E, c, H, h)
+        sh.update_problem_data(torch.zeros(1, Nl * s + n, dtype=torch.float64, device=dev), sigma=1e-6)
+        sh.synchronize()
+        sh.set_stream(side.cuda_stream)
+        shards.append(sh)
+        elems.append(torch.empty(1, sh.es, dtype=torch.float64, device=dev))
+        outs.append(torch.empty(1, Nl * s + n, dtype=torch.float64, device=dev))
+        del E, H
+    gathered = torch.empty(R, 1, shards[0].es, dtype=torch.float64, device=dev)
+    with torch.cuda.stream(side):
+        for r, sh in enumerate(shards):
+            sh.backward(elems[r], r == R - 1)
+            gathered[r].copy_(elems[r])
+        per = []
+        for r, sh in enumerate(shards):
+            def one():
+                sh.backward(elems[r], r == R - 1)
+                sh.forward(x0, gathered, R, r, outs[r])
+            per.append(_timed_local(one, reps, 2, dev) * 1e3)
+    ok = all(bool(torch.isfinite(o).all().item()) for o in outs)
+    for sh in shards:
+        sh.close()
+    return {"R": R, "rank_ms": per, "max_rank_ms": max(per), "finite": ok,
+            "note": "one-GPU rehearsal of the R-rank split (virtual ranks solved in turn, each rank's calls "
+                    "back to back): the per-rank critical path less the all-gather"}
 
 
 def _horizon_oracle_err(parts, outs, x0, n, m, Ntot):
