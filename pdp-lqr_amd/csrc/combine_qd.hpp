@@ -226,10 +226,13 @@ __device__ __forceinline__ void qd_publish(const d4 (&Q)[6], double *pr, int g, 
     }
 }
 
-// Wave 0, block T: LDL^T of the pivot block in pr (wave-uniform), L (strict
-// lower, row-major packed) and 1/d to lb.  False if a pivot has the wrong sign.
+// Block T: LDL^T of the pivot block in pr (wave-uniform values, every wave
+// after barrier A): L (strict lower) and 1/d in registers.  False if a pivot
+// has the wrong sign.  (Round 6: wave 0 factored before barrier A and broadcast
+// L, 1/d through LDS; every wave factoring for itself drops the store, the 22
+// LDS reads per thread and wave 0's factor from ahead of the barrier.)
 template <int T>
-__device__ __forceinline__ bool qd_factor(const double *pr, double *lb, int lane) {
+__device__ __forceinline__ bool qd_factor_regs(const double *pr, double (&L)[8][8], double (&inv)[8]) {
     constexpr int J0 = 8 * T;
     double a[8][8];
 #pragma unroll
@@ -237,7 +240,6 @@ __device__ __forceinline__ bool qd_factor(const double *pr, double *lb, int lane
 #pragma unroll
         for (int l2 = 0; l2 <= l; ++l2) a[l][l2] = pr[(J0 + l2) * QD_PRS + l];
     bool ok = true;
-    double inv[8], L[8][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const double d = a[j][j];
@@ -249,19 +251,6 @@ __device__ __forceinline__ bool qd_factor(const double *pr, double *lb, int lane
         for (int i = j + 1; i < 8; ++i)
 #pragma unroll
             for (int k = j + 1; k <= i; ++k) a[i][k] = __builtin_fma(-L[i][j], a[k][j], a[i][k]);
-    }
-    // wave-uniform values: one lane stores them (16-byte pairs)
-    if (lane == 0) {
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        double w[36];
-#pragma unroll
-        for (int i = 1; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < i; ++j) w[i * (i - 1) / 2 + j] = L[i][j];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w[28 + j] = inv[j];
-#pragma unroll
-        for (int q = 0; q < 18; ++q) reinterpret_cast<d2 *>(lb)[q] = d2{w[2 * q], w[2 * q + 1]};
     }
     return ok;
 }
@@ -282,12 +271,10 @@ __device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, dou
 #if QD_PROF
     QdProf prof;
 #endif
-    // block 0's pivot rows and (wave 0) its factorisation, from the assembled tiles
+    // block 0's pivot rows, from the assembled tiles
     qd_publish<W, 0>(Q, pr, g, c);
-    if constexpr (W == 0) {
-        wave_sync();
-        ok = qd_factor<0>(pr, lb, lane);
-    }
+    (void)lb;
+    (void)lane;
 #pragma unroll
     for (int t = 0; t < QD_STEPS; ++t) {
         const int J0 = 8 * t;
@@ -295,35 +282,29 @@ __device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, dou
         QD_MARK(0);
         __syncthreads();  // A_t
         QD_MARK(1);
-        // ---- V, W of this thread's column ----
+        // ---- the pivot block's LDL^T (every wave), V, W of this thread's column ----
         {
             const bool act = own && col >= J0 + 8;
             const int cc = act ? col : J0 + 8;  // clamped (branch-free reads)
             typedef double d2 __attribute__((ext_vector_type(2)));
-            double x[8], L[28], inv[8];
+            double x[8], L[8][8], inv[8];
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
                 const d2 v = reinterpret_cast<const d2 *>(pr + cc * PRS)[l];
                 x[2 * l] = v.x;
                 x[2 * l + 1] = v.y;
             }
-#pragma unroll
-            for (int q = 0; q < 14; ++q) {
-                const d2 v = reinterpret_cast<const d2 *>(lb)[q];
-                L[2 * q] = v.x;
-                L[2 * q + 1] = v.y;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const d2 v = reinterpret_cast<const d2 *>(lb + 28)[q];
-                inv[2 * q] = v.x;
-                inv[2 * q + 1] = v.y;
-            }
+            bool okt = true;
+#define QD_FAC(TT) \
+    if (t == (TT)) okt = qd_factor_regs<TT>(pr, L, inv);
+            QD_FAC(0) QD_FAC(1) QD_FAC(2) QD_FAC(3) QD_FAC(4) QD_FAC(5)
+#undef QD_FAC
+            ok = ok && okt;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 double v = x[j];
 #pragma unroll
-                for (int k = 0; k < j; ++k) v = __builtin_fma(-L[j * (j - 1) / 2 + k], V[k], v);
+                for (int k = 0; k < j; ++k) v = __builtin_fma(-L[j][k], V[k], v);
                 V[j] = v;
             }
             if (act) {
@@ -357,14 +338,8 @@ __device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, dou
         qd_operands<W, PN, PN>(op, vw, g, c);                      \
         qd_update<W, PN, PN, true>(Q, op);                         \
         qd_operands<W, PN + 1, 5>(op, vw, g, c);                   \
-        if constexpr (W == 0) qd_update<W, PN + 1, 5, false>(Q, op); \
         qd_publish<W, (TT) + 1>(Q, pr, g, c);                      \
-        if constexpr (W == 0) {                                    \
-            wave_sync();                                           \
-            ok = qd_factor<(TT) + 1>(pr, lb, lane) && ok;          \
-        } else {                                                   \
-            qd_update<W, PN + 1, 5, false>(Q, op);                 \
-        }                                                          \
+        qd_update<W, PN + 1, 5, false>(Q, op);                     \
     }
         QD_STEP(0, 0)
         QD_STEP(1, 1)
