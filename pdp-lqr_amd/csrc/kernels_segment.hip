@@ -452,10 +452,15 @@ __global__ __launch_bounds__(64) void k_seg_bwd_aug(SegArgs A) {
 // m % 4 == 0, m <= 16.
 // ---------------------------------------------------------------------------
 #ifdef PDPLQR_COMB_PROFILE
-__device__ unsigned long long g_aug_t[1024 * 8];
-#define AUG_MARK(q)                                                                             \
-    do {                                                                                        \
-        if (tid == 0 && k == N1 - 2) g_aug_t[(blockIdx.x % 1024) * 8 + (q)] = wall_clock64(); \
+__device__ unsigned long long g_aug_t[1024 * 16];
+// slots 0-7 the stage phases, 8-13 three marks per pivot block, 14 / 15 the
+// shader clock (clock64) at marks 0 / 7
+#define AUG_MARK(q)                                                                              \
+    do {                                                                                         \
+        if (tid == 0 && k == N1 - 2) {                                                           \
+            g_aug_t[(blockIdx.x % 1024) * 16 + (q)] = wall_clock64();                            \
+            if ((q) == 0 || (q) == 7) g_aug_t[(blockIdx.x % 1024) * 16 + 14 + ((q) == 7)] = clock64(); \
+        }                                                                                        \
     } while (0)
 #else
 #define AUG_MARK(q) \
@@ -467,6 +472,9 @@ template <int NN, int MM>
 // PDPLQR_AUG_MW_OCC: resident blocks per CU the register allocation targets
 // (2: 215 VGPRs, no spill; 3: 168 VGPRs with 19 spill ops per stage -- the
 // N = 8192 slice 0.49 -> 0.62 ms, forced 4-wave N = 65536 1.32 -> 1.54 ms)
+#ifndef PDPLQR_AUG_PIV8
+#define PDPLQR_AUG_PIV8 0
+#endif
 #ifndef PDPLQR_AUG_MW_OCC
 #define PDPLQR_AUG_MW_OCC 2
 #endif
@@ -478,9 +486,12 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
     constexpr int INQ = (IN + 255) / 256;            // per thread
     constexpr int K0 = m / 4, K1 = s / 4;            // K chunks of the x rows
     static_assert(s <= 32 && D < 64 && m % 4 == 0 && m <= 16 && n % 4 == 0, "4-wave aug shape");
+    // u-pivots per elimination block: 8 when m allows (one publish / barrier /
+    // factor round for m = 8 instead of two), else 4 (PDPLQR_AUG_PIV8=0: 4 always)
+    constexpr int PIVB = (PDPLQR_AUG_PIV8 && m % 8 == 0) ? 8 : 4;
     __shared__ double Xq[n * XLD];                   // P_{k+1} (x rows, x cols)
     __shared__ double In[IN];                        // E~ (n x s) | H~ packed | c | h~ of this stage
-    __shared__ double Pr[2][4 * 64];                 // pivot rows of block 0 / 1 at every column
+    __shared__ double Pr[2][PIVB * 64];              // pivot rows of block 0 / 1 at every column
     __shared__ double lpa[32], fcv[32];              // h~ + G^T c per [u; x] column, F c per y column
     __shared__ int s_bad;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
@@ -691,12 +702,109 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
         double *FRk = FRb + (long long)k * frs;
         double *Gk = Gb + (long long)k * m * n;
         bool ok = true;
+        if constexpr (PIVB == 8) {
+#pragma unroll
+        for (int blk = 0; blk < m / 8; ++blk) {
+            const int j0 = 8 * blk;
+            double *P8 = Pr[blk & 1];
+            P8[g * 64 + col] = Q[0][2 * blk];            // row j0 + g at this column
+            P8[(4 + g) * 64 + col] = Q[0][2 * blk + 1];  // row j0 + 4 + g
+            __syncthreads();
+            AUG_MARK(8 + 3 * blk);
+            // every LDS read of the block up front, then the arithmetic
+            double L[8][8], pr[8], avv[4][2], mi[8], lu[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) L[i][j] = P8[i * 64 + j0 + j];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) pr[l] = P8[l * 64 + col];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)  // M[16 a + c][j0 + 4 h + g] by symmetry (aug / padding: not rows)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) avv[a][h] = (16 * a + c < D ? 1.0 : 0.0) * P8[(4 * h + g) * 64 + 16 * a + c];
+            // Cholesky of the 8 x 8 pivot block in place (wave-uniform); the
+            // diagonal keeps 1 / L_jj
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ok = ok && (L[j][j] > 0.0);
+                const double iv = rsqrt_f64(L[j][j]);
+                L[j][j] = iv;
+#pragma unroll
+                for (int i = j + 1; i < 8; ++i) L[i][j] *= iv;
+#pragma unroll
+                for (int i = j + 1; i < 8; ++i)
+#pragma unroll
+                    for (int kq = j + 1; kq <= i; ++kq) L[i][kq] = __builtin_fma(-L[i][j], L[kq][j], L[i][kq]);
+            }
+            // forward substitution L^{-1} v (in place)
+            auto fsub = [&](double (&v)[8]) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    double t = v[i];
+#pragma unroll
+                    for (int l = 0; l < i; ++l) t = __builtin_fma(-L[i][l], v[l], t);
+                    v[i] = t * L[i][i];
+                }
+            };
+            // X[J][col] = Muu^{-1} M[J, col] = L^{-T} (L^{-1} pr)
+            fsub(pr);
+#pragma unroll
+            for (int i = 7; i >= 0; --i) {
+                double t = pr[i];
+#pragma unroll
+                for (int l = i + 1; l < 8; ++l) t = __builtin_fma(-L[l][i], pr[l], t);
+                pr[i] = t * L[i][i];
+            }
+            double xg0 = 0.0, xg1 = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xg0 = (g == i) ? pr[i] : xg0;
+                xg1 = (g == i) ? pr[4 + i] : xg1;
+            }
+            // rank-8 update of every row tile (two K = 4 MFMAs)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                if (wv < 2 && a >= 2) continue;  // rows y of the [u; x] columns are never read
+                Q[a] = mfma_f64(-avv[a][0], xg0, Q[a]);
+                Q[a] = mfma_f64(-avv[a][1], xg1, Q[a]);
+            }
+            AUG_MARK(9 + 3 * blk);
+            // records: L(i, J) = M[i][J] L_JJ^{-T}  (row i: forward substitution);
+            // their operands are read after the update is issued (registers)
+            const int ir = (wv == 0) ? lane : s + lane;
+            const bool rec = (wv == 0 && ir < s) || (wv == 1 && !last && lane < n);
+            const int irc = ir < 64 ? ir : 0;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) mi[l] = P8[l * 64 + irc];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) lu[l] = P8[l * 64 + AUG];
+            if (rec) {
+                fsub(mi);
+#pragma unroll
+                for (int l = 0; l < 8; ++l) {
+                    if (wv == 0) gstore(FRk + (long long)(j0 + l) * s + ir, ir >= j0 + l ? mi[l] : 0.0);
+                    else gstore(Gk + (j0 + l) + lane * m, -mi[l]);
+                }
+            }
+            if (tid == 2 * 64) {  // lu' = L^{-1} lu, lu = M[J][aug]
+                fsub(lu);
+#pragma unroll
+                for (int l = 0; l < 8; ++l) {
+                    gstore(FRk + (long long)s * m + j0 + l, lu[l]);
+                    if (lpb) gstore(lpb + (long long)k * s + j0 + l, lu[l]);
+                }
+            }
+            AUG_MARK(10 + 3 * blk);
+        }
+        } else {
 #pragma unroll
         for (int blk = 0; blk < m / 4; ++blk) {
             const int j0 = 4 * blk;
             double *P4 = Pr[blk & 1];
             P4[g * 64 + col] = Q[0][blk];  // row j0 + g at this column
             __syncthreads();
+            AUG_MARK(8 + 3 * blk);
             // every LDS read of the block up front (one wait), then the arithmetic
             double a4[4][4], L[4][4], T4[4][4], inv[4], pr[4], avv[4], mi[4], lu[4];
 #pragma unroll
@@ -762,6 +870,7 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                 if (wv < 2 && a >= 2) continue;  // rows y of the [u; x] columns are never read
                 Q[a] = mfma_f64(-avv[a], xg, Q[a]);
             }
+            AUG_MARK(9 + 3 * blk);
             // records: L(i, j0 + l) = sum_l' M[i][j0 + l'] T4[l][l']
             if (rec) {
 #pragma unroll
@@ -783,6 +892,8 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                     if (lpb) gstore(lpb + (long long)k * s + j0 + l, v);
                 }
             }
+            AUG_MARK(10 + 3 * blk);
+        }
         }
         AUG_MARK(5);
         // ---- P_k diagonal check, factor cache (P_k packed lower, p_k) ----
@@ -896,6 +1007,6 @@ int launch_seg_backward(const SegArgs &a, hipStream_t st) {
 
 #ifdef PDPLQR_COMB_PROFILE
 extern "C" int pdplqr_debug_aug_times(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_aug_t), sizeof(unsigned long long) * 1024 * 8) == hipSuccess ? 0 : -2;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pdplqr::g_aug_t), sizeof(unsigned long long) * 1024 * 16) == hipSuccess ? 0 : -2;
 }
 #endif

@@ -76,12 +76,14 @@ if len(seg):
           f"riccati {np.median(seg[:, 10] / st):.0f}  element {np.median(seg[:, 11] / st):.0f}")
 # stage phases of the 4-wave segment backward (k_seg_bwd_aug_mw, second stage of each segment)
 if hasattr(L, "pdplqr_debug_aug_times"):
-    ab = np.zeros(1024 * 8, dtype=np.uint64)
+    ab = np.zeros(1024 * 16, dtype=np.uint64)
     L.pdplqr_debug_aug_times.argtypes = [C.c_void_p]
     if L.pdplqr_debug_aug_times(C.c_void_p(ab.ctypes.data)) == 0:
-        a = ab.reshape(1024, 8).astype(np.int64)
+        a16 = ab.reshape(1024, 16).astype(np.int64)
+        a = a16[:, :8]
         ok = (a[:, 0] > 0) & np.all(np.diff(a, axis=1) >= 0, axis=1)
         a = a[ok]
+        a16 = a16[ok]
         if len(a):
             an = ["B1 (publish, barrier)", "G = P E~", "rows [u;x] + aug", "B2", "u-pivot blocks", "checks, cache",
                   "inputs, B_end"]
@@ -89,3 +91,15 @@ if hasattr(L, "pdplqr_debug_aug_times"):
             print(f"aug stage ({len(a)} blocks): total median {np.median(a[:, 7] - a[:, 0]):.0f} ticks")
             for k, nm in enumerate(an):
                 print(f"  {nm:24s} {np.median(da[:, k]):8.0f}")
+            # inside the two u-pivot blocks: barrier passed, factor + update issued, records issued
+            two = len(a16) and (a16[:, 11] > 0).all()  # 4-pivot blocks (else one 8-pivot block)
+            pb = a16[:, [4, 8, 9, 10, 11, 12, 13, 5] if two else [4, 8, 9, 10, 5]]
+            if len(pb) and (np.diff(pb, axis=1) >= 0).all():
+                dp = np.diff(pb, axis=1)
+                nms = ["blk0: publish + barrier", "blk0: factor, X, MFMA issue", "blk0: records"]
+                nms += ["blk1: publish + barrier", "blk1: factor, X, MFMA issue", "blk1: records"] if two else []
+                for k, nm in enumerate(nms + ["-> end of pivots"]):
+                    print(f"    {nm:30s} {np.median(dp[:, k]):8.0f}")
+            wt, ct = a16[:, 7] - a16[:, 0], a16[:, 15] - a16[:, 14]
+            if (wt > 0).all():
+                print(f"  shader clock over the stage: {np.median(ct / wt) * 100:.0f} MHz")
