@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
     __shared__ double Xq[n * XLD];                   // P_{k+1} (x rows, x cols)
     __shared__ double In[IN];                        // E~ (n x s) | H~ packed | c | h~ of this stage
     __shared__ double Pr[2][PIVB * 64];              // pivot rows of block 0 / 1 at every column
-    __shared__ double lpa[32], fcv[32];              // h~ + G^T c per [u; x] column, F c per y column
+    __shared__ double augr[64];                      // per row of the aug column: h~ + G^T c ([u; x]), F c (y), 0
     __shared__ int s_bad;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
     const int col = 16 * wv + c;
@@ -565,6 +565,7 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
                 Q[a][r] = v;
             }
         if (tid == 0) s_bad = 0;
+        if (tid >= D && tid < 64) augr[tid] = 0.0;  // padding rows (never written again)
         __syncthreads();
         if (bad) s_bad = 1;
         if (last) {
@@ -603,6 +604,12 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
         double bvE[NK];  // E~[kx - m][col] (B operand of G)
 #pragma unroll
         for (int q = 0; q < NK; ++q) bvE[q] = fux * Es[(4 * (K0 + q) + g - m) + colc * n];
+        // the aug pieces' operands (c rows of this lane group, h~[col]), read here so
+        // their LDS latency hides under the products instead of chaining before B2
+        double cxv[NK];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) cxv[q] = cs[4 * (K0 + q) + g - m];
+        const double hcol = hs[colc];
         d4 G[2] = {d4{0.0, 0.0, 0.0, 0.0}, d4{0.0, 0.0, 0.0, 0.0}};
         if (wv < 2) {
             double avP[2][NK];  // P_sym[16 a + c][kx]
@@ -670,18 +677,15 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
 #pragma unroll
             for (int a = 0; a < 2; ++a) Mu[a] += Mo[a];
         }
-        // ---- aug pieces: lpa[col] = h~ + G^T c ([u; x] columns), fcv = F c (y columns) ----
+        // ---- aug pieces: augr[col] = h~ + G^T c ([u; x] columns), F c (y columns) ----
         {
             double part = 0.0;
 #pragma unroll
-            for (int kk = K0; kk < K1; ++kk) {
-                const double cx = cs[4 * kk + g - m];
-                part = __builtin_fma(cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3], cx, part);
-            }
+            for (int kk = K0; kk < K1; ++kk)
+                part = __builtin_fma(cux ? G[kk >> 2][kk & 3] : Q[kk >> 2][kk & 3], cxv[kk - K0], part);
             part = sum_groups(part);
             if (g == 0) {
-                if (cux) lpa[col] = hs[col] + part;
-                else if (cy) fcv[col - s] = part;
+                if (cux || cy) augr[col] = (cux ? hcol : 0.0) + part;
             }
         }
 #pragma unroll
@@ -689,15 +693,20 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
         AUG_MARK(3);
         __syncthreads();  // B2
         AUG_MARK(4);
-        if (caug)  // aug column: rows [u; x] += h~ + G^T c (E~^T p is already in), rows y += F c
+        if (caug) {  // aug column: rows [u; x] += h~ + G^T c (E~^T p is already in), rows y += F c
+            // every read issued before the first add (the default schedule waited on each pair)
+            double av[4][4];
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * a + 4 * r + g;
-                    if (i < s) Q[a][r] += lpa[i];
-                    else if (i < D) Q[a][r] += fcv[i - s];
-                }
+                for (int r = 0; r < 4; ++r) av[a][r] = augr[16 * a + 4 * r + g];
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the DS reads
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0); // then the adds
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Q[a][r] += av[a][r];
+        }
         // ---- the m u-pivots, 4 per block ----
         double *FRk = FRb + (long long)k * frs;
         double *Gk = Gb + (long long)k * m * n;
