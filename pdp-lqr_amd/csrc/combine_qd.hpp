@@ -55,6 +55,14 @@ constexpr int QD_NCOL = QD_NT + 1;
 constexpr int QD_PRS = 10;                // pivot rows: [column][8] at stride 10 (16-byte rows)
 constexpr int QD_VWS = 18;                // [column][V 0..7 | W 0..7] at stride 18 (odd bank step)
 constexpr int QD_STEPS = QD_NJ / 8;
+// The right-of-panel update of block t is issued after barrier A_{t+1}, so
+// its MFMAs run under block t + 1's factor (VALU) instead of ahead of the
+// barrier: C4 rank 0.364 -> 0.356 ms pipelined (profiles/r06/qd_defer_ab/).
+// PDPLQR_QD_DEFER=0: the old order (A/B switch)
+#ifndef PDPLQR_QD_DEFER
+#define PDPLQR_QD_DEFER 1
+#endif
+#define QD_DEFER PDPLQR_QD_DEFER
 
 __host__ __device__ constexpr int qd_smem_doubles() { return QD_NCOL * QD_PRS + QD_NCOL * QD_VWS + 36 + 2; }
 
@@ -282,6 +290,15 @@ __device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, dou
         QD_MARK(0);
         __syncthreads();  // A_t
         QD_MARK(1);
+#if QD_DEFER
+        // block t - 1's update of the tiles right of block t's panel (operands
+        // read before A_t): issued here so the matrix pipe runs it under the
+        // factor's VALU chain instead of ahead of the barrier
+#define QD_REST(TT, PN) \
+    if (t == (TT) + 1) qd_update<W, PN + 1, 5, false>(Q, op);
+        QD_REST(0, 0) QD_REST(1, 1) QD_REST(2, 1) QD_REST(3, 2) QD_REST(4, 2)
+#undef QD_REST
+#endif
         // ---- the pivot block's LDL^T (every wave), V, W of this thread's column ----
         {
             const bool act = own && col >= J0 + 8;
@@ -339,7 +356,7 @@ __device__ __forceinline__ bool qd_wave(d4 (&Q)[6], double &lin, double *pr, dou
         qd_update<W, PN, PN, true>(Q, op);                         \
         qd_operands<W, PN + 1, 5>(op, vw, g, c);                   \
         qd_publish<W, (TT) + 1>(Q, pr, g, c);                      \
-        qd_update<W, PN + 1, 5, false>(Q, op);                     \
+        if (!QD_DEFER) qd_update<W, PN + 1, 5, false>(Q, op);      \
     }
         QD_STEP(0, 0)
         QD_STEP(1, 1)
