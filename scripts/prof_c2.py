@@ -13,4 +13,5 @@ import bench  # noqa: E402
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    print(json.dumps(bench.bench_single(0, dev, None, steps=5, warmup=2)), flush=True)
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5  # more for an A/B timing
+    print(json.dumps(bench.bench_single(0, dev, None, steps=steps, warmup=2)), flush=True)
