@@ -825,6 +825,9 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
 #pragma unroll
             for (int a = 0; a < 4; ++a)  // M[16 a + c][j0 + g] = M[j0 + g][16 a + c] (symmetry;
                 avv[a] = (16 * a + c < D ? 1.0 : 0.0) * P4[g * 64 + 16 * a + c];  // aug / padding: not rows)
+#pragma unroll
+            for (int a = 2; a < 4; ++a)  // keep the row-tile 2, 3 reads here, with the others (the
+                asm volatile("" ::"v"(avv[a]));  // compiler sank them into the wave-2/3 branch: one LDS wait each)
             // records: wave 0 the FR rows i < s, wave 1 the coupling rows s + lane
             const int ir = (wv == 0) ? lane : s + lane;
             const bool rec = (wv == 0 && ir < s) || (wv == 1 && !last && lane < n);
@@ -833,6 +836,7 @@ __global__ __launch_bounds__(256, PDPLQR_AUG_MW_OCC) void k_seg_bwd_aug_mw(SegAr
             for (int l = 0; l < 4; ++l) mi[l] = P4[l * 64 + irc];
 #pragma unroll
             for (int l = 0; l < 4; ++l) lu[l] = P4[l * 64 + AUG];
+            __builtin_amdgcn_sched_barrier(0);  // every LDS read above issues before the factor
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 ok = ok && (a4[j][j] > 0.0);
